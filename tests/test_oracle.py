@@ -1,0 +1,125 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import agents, replay, spec
+from oracle import nets as N
+
+torch.set_num_threads(1)
+
+
+def _close(a, b, rtol=1e-5, atol=1e-6):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol)
+
+
+def test_lap_sampler_law():
+    g = load_golden("lap_sampler")
+    for n, seed in ((65536, 11), (1000000, 12), (1, 13), (4097, 14)):
+        p = spec.init_priorities(n, seed)
+        ind = replay.lap_indices(p, n, g[f"n{n}_u"])
+        np.testing.assert_array_equal(ind, g[f"n{n}_ind"])
+
+
+def test_lap_scatter_last_writer_wins():
+    g = load_golden("lap_sampler")
+    r = replay.Replay(64, 1, 1, np.ones(1, np.float32), np.zeros(1, np.float32), True)
+    r.priority[:] = g["scatter_base"]
+    r.size = 64
+    r.ind = g["scatter_ind"]
+    r.update_priority(g["scatter_new"])
+    np.testing.assert_array_equal(r.priority, g["scatter_out"])
+    assert r.max_priority == max(1.0, float(g["scatter_new"].max()))
+
+
+def test_uniform_sampler_law():
+    g = load_golden("uniform_sampler")
+    for size in (1, 7, 25000, 1000000):
+        ind = replay.uniform_indices(size, g[f"s{size}_u"])
+        np.testing.assert_array_equal(ind, g[f"s{size}_ind"])
+        assert ind.min() >= 0 and ind.max() <= size - 1
+
+
+def test_sac_rsample():
+    g = load_golden("sac_rsample")
+    a, lp = N.gaussian_tanh(torch.from_numpy(g["mean"]), torch.from_numpy(g["log_std"]),
+                            torch.from_numpy(g["eps"]))
+    np.testing.assert_array_equal(a.numpy(), g["action"])
+    np.testing.assert_array_equal(lp.numpy(), g["log_pi"])
+
+
+def build_from_golden(g):
+    alg = str(g["meta_alg"])
+    env = str(g["meta_env"])
+    H, B, Ncap, n_fill, n_steps, use_lap, seed = (int(x) for x in g["meta"])
+    S, A, hi = spec.TASKS[env]
+    extra = dict(zip([str(k) for k in g["meta_extra_keys"]], g["meta_extra_vals"].tolist()))
+    extra = {k: (int(v) if k in ("target_update_rate", "policy_freq") else v) for k, v in extra.items()}
+    nets = spec.agent_params(alg, S, A, H, seed)
+    orc = agents.make_oracle(alg, nets, A, bool(use_lap), **extra)
+    scale = np.full(A, hi, np.float32)
+    bias = np.zeros(A, np.float32)
+    rep = replay.Replay(Ncap, S, A, (scale - (-scale)) / 2.0, bias, bool(use_lap))
+    data = spec.replay_data(S, A, n_fill, seed + 1, hi)
+    for i in range(n_fill):
+        rep.append(data["state"][i], data["action"][i], float(data["reward"][i]),
+                   data["next_state"][i], float(data["done"][i]))
+    if use_lap:
+        p0 = spec.init_priorities(Ncap, seed + 2)
+        p0[rep.size:] = 0.0
+        rep.priority[:] = p0
+        rep.max_priority = float(p0.max())
+    tp = {k[5:]: v for k, v in g.items() if k.startswith("tape_")}
+    return alg, orc, rep, tp, n_steps, B
+
+
+TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny"]
+FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid"]
+
+
+@pytest.mark.parametrize("name", TINY + FULL)
+def test_oracle_matches_reference(name):
+    g = load_golden(name)
+    alg, orc, rep, tp, n_steps, B = build_from_golden(g)
+    keys = [str(k) for k in g["info_keys"]]
+    infos, inds = [], []
+    for t in range(n_steps):
+        i1, n1 = agents.run_steps(orc, alg, rep, {k: v[t:t + 1] for k, v in tp.items()}, 1, B)
+        infos += i1
+        inds += n1
+        np.testing.assert_array_equal(inds[t], g["ind"][t])
+        got = [np.nan if infos[t][k] is None else infos[t][k] for k in keys]
+        _close(got, g["info"][t], rtol=1e-5, atol=1e-6)
+        if f"prio_{t}" in g:
+            _close(rep.priority, g[f"prio_{t}"], rtol=1e-6, atol=0)
+        if f"vbounds_{t}" in g:
+            _close([orc.value_max, orc.value_min, orc.vt_max, orc.vt_min], g[f"vbounds_{t}"])
+    nets = orc.nets()
+    for key in g:
+        if not key.startswith("out_") or key == "out_log_alpha":
+            continue
+        net, rest = key[4:].split(".", 1)
+        if rest.endswith(":digest"):
+            pname = rest[: -len(":digest")]
+            v = nets[net][pname].detach().numpy().ravel()
+            _close(v[g[key[: -len(':digest')] + ':pos']], g[key[: -len(':digest')] + ':vals'],
+                   rtol=1e-5, atol=1e-6)
+        elif ":" not in rest:
+            _close(nets[net][rest].detach().numpy(), g[key], rtol=1e-5, atol=1e-6)
+    if "out_log_alpha" in g:
+        _close(orc.log_alpha.detach().numpy(), g["out_log_alpha"])
+
+
+@pytest.mark.parametrize("name", TINY)
+def test_oracle_bitwise_on_this_host(name):
+    """Same torch-CPU ops in the same order => bitwise equal infos/params here."""
+    g = load_golden(name)
+    alg, orc, rep, tp, n_steps, B = build_from_golden(g)
+    infos, _ = agents.run_steps(orc, alg, rep, tp, n_steps, B)
+    keys = [str(k) for k in g["info_keys"]]
+    got = np.array([[np.nan if infos[t][k] is None else infos[t][k] for k in keys]
+                    for t in range(n_steps)])
+    np.testing.assert_array_equal(got, g["info"])
