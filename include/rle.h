@@ -1,0 +1,136 @@
+/*
+ * rle.h — C ABI of the MI355X off-policy update engine (librle.so).
+ *
+ * The reference (seungju-k1m/sac-td3-td7) has no FFI: its hot path is the
+ * Python method Agent.train_ops(batch, replay_buffer) (rl/agent/abc.py:23-28)
+ * driven by run_train_ops (rl/runner/run.py:87-96).  This ABI sits UNDER the
+ * Python classes that mirror that interface (sac-td3-td7_amd/rl); each entry
+ * point below names the reference interface it replaces.
+ *
+ * Conventions: every function returns 0 on success or a negative error code;
+ * rle_last_error() returns a thread-local message for the last failure.  All
+ * pointers are host pointers borrowed for the duration of the call; the
+ * engine owns all device memory.  A handle is bound to one device and one
+ * HIP stream and is not thread-safe.  Plain C types only (no torch types).
+ */
+#ifndef RLE_H
+#define RLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RLE_TD7 0
+#define RLE_TD3 1
+#define RLE_SAC 2
+
+#define RLE_INFO_MAX 8
+
+#define RLE_OK 0
+#define RLE_EINVAL (-1)
+#define RLE_EHIP (-2)
+#define RLE_ESTATE (-3)
+
+typedef struct rle_replay rle_replay;
+typedef struct rle_engine rle_engine;
+
+typedef struct rle_config {
+  int algo;                 /* RLE_TD7 / RLE_TD3 / RLE_SAC */
+  int state_dim, action_dim;
+  int hidden;               /* hidden width (TD7: hdim = zs_dim) */
+  int batch;                /* B (multiple of 4, <= 1024) */
+  int use_lap;              /* TD7/TD3: LAP Huber + priority update */
+  float discount;           /* td7.py:37 / td3.py:36 / sac.py:30 */
+  float policy_lr, critic_lr;
+  float tau;                /* TD3/SAC Polyak */
+  float target_policy_noise, noise_clip;
+  int policy_freq;          /* TD7/TD3 */
+  int target_update_rate;   /* TD7 hard update period */
+  float min_log_std, max_log_std;  /* SAC */
+  float tmp;                /* SAC: < 0 => auto temperature (sac.py:36,55) */
+  unsigned long long seed;  /* Philox stream for sampling / noise */
+  int device;
+} rle_config;
+
+/* ---- replay memory: rl/replay_memory/{lap,simple}.py ---------------------- */
+
+/* LAPReplayMemory.__init__ (lap.py:15-29) / SimpleReplayMemory.__init__ (simple.py:15-27). */
+int rle_replay_create(int device, long long capacity, int state_dim, int action_dim, int lap,
+                      rle_replay** out);
+int rle_replay_destroy(rle_replay* r);
+/* append (lap.py:31-43): rows of fp32 state[S], action[A] (already a/scale - bias), reward,
+ * next_state[S], notdone (1 - terminated).  count rows, host pointers. */
+int rle_replay_append(rle_replay* r, const float* state, const float* action, const float* reward,
+                      const float* next_state, const float* notdone, long long count);
+/* ptr / size / max_priority (lap.py:18-29, len = ptr Q6). */
+int rle_replay_state(rle_replay* r, long long* ptr, long long* size, float* max_priority);
+/* Test / bench hooks. */
+int rle_replay_fill_random(rle_replay* r, long long count, unsigned long long seed);
+int rle_replay_get_priority(rle_replay* r, float* out, long long n);
+int rle_replay_set_priority(rle_replay* r, const float* p, long long n, float max_priority);
+/* Device LAP/uniform index search with given uniforms (lap.py:47-54, simple.py:45-54). */
+int rle_replay_sample_indices(rle_replay* r, int n, const float* u, long long* ind_out);
+/* LAPReplayMemory.update_priority (lap.py:66-69) with explicit indices. */
+int rle_replay_update_priority(rle_replay* r, int n, const long long* ind, const float* p);
+/* LAPReplayMemory.reset_max_priority (lap.py:71-73). */
+int rle_replay_reset_max_priority(rle_replay* r);
+/* Gather rows (state, action, reward, next_state, notdone) for indices (lap.py:55-60). */
+int rle_replay_gather(rle_replay* r, int n, const long long* ind, float* state, float* action,
+                      float* reward, float* next_state, float* notdone);
+
+/* ---- agent: rl/agent/{td7,td3,sac}.py ------------------------------------- */
+
+/* TD7.__init__ (td7.py:34-87) / TD3.__init__ (td3.py:33-74) / SAC.__init__ (sac.py:27-77). */
+int rle_create(const rle_config* cfg, rle_engine** out);
+int rle_destroy(rle_engine* e);
+/* Bind the replay the step samples from (the replay_buffer arg of train_ops). */
+int rle_bind_replay(rle_engine* e, rle_replay* r);
+/* Parameter import/export in the reference's state_dict layout (Agent.load_state_dict,
+ * td7.py:114-125; deepcopy / pickle, abc.py:38-55).  net: "policy", "q1", "q2", "target_q1",
+ * "target_q2", "encoder", "fixed_encoder", "fixed_encoder_target"; name: e.g. "q01.weight",
+ * "mlp.2.bias"; SAC temperature: net "tmp", name "log_alpha". */
+int rle_param_numel(rle_engine* e, const char* net, const char* name, long long* numel);
+int rle_get_param(rle_engine* e, const char* net, const char* name, float* out, long long n);
+int rle_set_param(rle_engine* e, const char* net, const char* name, const float* in, long long n);
+/* Optimizer state: which = 0 (m) / 1 (v) of the param's Adam; step counter per optimizer. */
+int rle_get_adam(rle_engine* e, const char* net, const char* name, int which, float* out, long long n);
+int rle_set_adam(rle_engine* e, const char* net, const char* name, int which, const float* in,
+                 long long n);
+/* Device counters: [0] critic Adam t, [1] policy Adam t, [2] encoder Adam t, [3] n_runs,
+ * [4] rng step, [5] SAC temperature Adam t. */
+int rle_get_counters(rle_engine* e, long long* out6);
+int rle_set_counters(rle_engine* e, const long long* in6);
+/* TD7 value clipping state [value_max, value_min, value_target_max, value_target_min]. */
+int rle_get_value_bounds(rle_engine* e, float* out4);
+int rle_set_value_bounds(rle_engine* e, const float* in4);
+
+/* n_steps x Agent.train_ops(replay.sample(B), replay) (run_train_ops, run.py:87-96), fully on
+ * device incl. sampling and LAP priority update.  info_out: [n_steps][RLE_INFO_MAX] (per-agent
+ * key order; NaN = None).  One host sync per call. */
+int rle_step(rle_engine* e, int n_steps, float* info_out);
+/* Parity mode: replace the Philox draws of the next n_steps with tapes.
+ * u [n][B] (torch.rand in sample), eps [n][B][A] (randn_like target noise, or SAC next-state
+ * rsample noise), eps_pi [n][B][A] (SAC policy rsample noise, may be NULL), ind [n][B]
+ * (optional explicit indices; overrides u).  Pass n_steps = 0 to return to Philox. */
+int rle_set_tapes(rle_engine* e, int n_steps, const float* u, const float* eps, const float* eps_pi,
+                  const long long* ind);
+/* Last sampled indices (LAPReplayMemory.ind) [B]. */
+int rle_last_indices(rle_engine* e, long long* ind_out);
+/* Agent.sample / _inference_action forward (td7.py:158-162, td3.py:131-135, sac.py:154-159):
+ * obs [n][S] (n <= 1024) -> out [n][W]: TD7 tanh actor output (W = A); TD3 actor MLP output
+ * before tanh (W = A); SAC raw (mean | log_std) head (W = 2A).  Exploration noise, clipping and
+ * scale/bias stay on the host as in the reference. */
+int rle_act(rle_engine* e, const float* obs, int n, float* out);
+/* Launches per gradient step of each captured graph kind (for roofline accounting). */
+int rle_graph_stats(rle_engine* e, int* levels_policy_step, int* levels_plain_step);
+/* Copy all weights/optimizer state/counters of src into dst (checkpoint agent,
+ * ckpt_agent.load_state_dict(agent), run_w_checkpoint.py:140). Same config required. */
+int rle_copy_state(rle_engine* dst, rle_engine* src);
+int rle_synchronize(rle_engine* e);
+
+const char* rle_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RLE_H */

@@ -1,0 +1,2015 @@
+// Host side of the MI355X off-policy update engine: device memory, the
+// per-agent step programs (built as op DAGs), the level scheduler, hipGraph
+// capture and the C ABI declared in include/rle.h.
+//
+// A step program is written in the reference's order (td7.py:287-332,
+// td3.py:206-242, sac.py:251-295) as a list of ops with read/write resource
+// sets.  `Prog::schedule` assigns every op the lowest dependency level that
+// respects RAW, WAR and WAW hazards; each level becomes one launch of the
+// device dispatch kernel, and the whole step is captured into a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ops.h"
+#include "rle.h"
+
+namespace rle {
+hipError_t launch_level(const Op* d_ops, int nops, int nwg, hipStream_t st);
+hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
+                         float* priority, const float* st_s, const float* st_ns, const float* st_a,
+                         const float* st_r, const float* st_d, long long ptr, long long cap, int count,
+                         int Sp, int Ap, const float* max_priority, int lap, hipStream_t st);
+hipError_t launch_fill(float* state, float* next_state, float* action, float* reward, float* notdone,
+                       float* priority, long long n, int S, int Sp, int A, int Ap, unsigned long long seed,
+                       hipStream_t st);
+
+static thread_local std::string g_err;
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+#define HIPCHK(x)                                                                               \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) throw Error{RLE_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+#define REQUIRE(c, m)                              \
+  do {                                                \
+    if (!(c)) throw Error{RLE_EINVAL, std::string(m)}; \
+  } while (0)
+
+static inline int r4(int x) { return (x + 3) & ~3; }
+static inline int r16(int x) { return (x + 15) & ~15; }
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+static int host_fkey(float f) {
+  int i;
+  std::memcpy(&i, &f, 4);
+  return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+static float host_unkey(int k) {
+  int i = k >= 0 ? k : k ^ 0x7FFFFFFF;
+  float f;
+  std::memcpy(&f, &i, 4);
+  return f;
+}
+
+struct DevMem {
+  std::vector<void*> ptrs;
+  void* alloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0) bytes = 16;
+    HIPCHK(hipMalloc(&p, bytes));
+    HIPCHK(hipMemset(p, 0, bytes));
+    // hipMemset runs on the null stream, which does not order against our
+    // non-blocking streams: finish it before any stream touches the buffer.
+    HIPCHK(hipDeviceSynchronize());
+    ptrs.push_back(p);
+    return p;
+  }
+  template <class T>
+  T* make(size_t n) {
+    return reinterpret_cast<T*>(alloc(n * sizeof(T)));
+  }
+  ~DevMem() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+};
+
+// ------------------------------------------------------------------ replay
+
+struct Replay {
+  int device;
+  long long cap;
+  int S, Sp, A, Ap, lap;
+  long long ptr = 0, size = 0;
+  float *state, *next_state, *action, *reward, *notdone, *priority;
+  long long* size_d;
+  float* maxp_d;
+  double* bsum;
+  int nblk;
+  float* maxred_part;
+  int maxred_nwg = 256;
+  hipStream_t stream = nullptr;
+  DevMem mem;
+  // append staging
+  float* stage = nullptr;
+  long long stage_rows = 0;
+};
+
+// ------------------------------------------------------------------ programs
+
+struct View {
+  float* p = nullptr;
+  int ld = 0, rows = 0, cols = 0;
+  int id = -1;
+  const float* norm = nullptr;  // AvgL1Norm partials (producer |x| column-tile sums)
+  int norm_ld = 0, norm_row0 = 0, nparts = 0, width = 0, norm_id = -1;
+  View sub(int r0, int n) const {
+    View v = *this;
+    v.p = p + (size_t)r0 * ld;
+    v.rows = n;
+    v.norm_row0 += r0;
+    return v;
+  }
+};
+
+struct Prog {
+  struct Item {
+    Op op;
+    std::vector<int> rd, wr;
+    int level = 0;
+  };
+  std::vector<Item> items;
+  void add(const Op& op, std::vector<int> rd, std::vector<int> wr) {
+    Item it;
+    it.op = op;
+    it.rd = std::move(rd);
+    it.wr = std::move(wr);
+    items.push_back(std::move(it));
+  }
+  // Lowest level respecting RAW / WAR / WAW against all earlier ops.
+  std::vector<std::vector<Op>> schedule() {
+    std::map<int, int> lw, lr;
+    int maxl = -1;
+    for (auto& it : items) {
+      int l = 0;
+      for (int r : it.rd)
+        if (r >= 0 && lw.count(r)) l = std::max(l, lw[r] + 1);
+      for (int w : it.wr) {
+        if (w < 0) continue;
+        if (lw.count(w)) l = std::max(l, lw[w] + 1);
+        if (lr.count(w)) l = std::max(l, lr[w] + 1);
+      }
+      it.level = l;
+      for (int w : it.wr)
+        if (w >= 0) lw[w] = l;
+      for (int r : it.rd)
+        if (r >= 0) lr[r] = std::max(lr.count(r) ? lr[r] : -1, l);
+      maxl = std::max(maxl, l);
+    }
+    std::vector<std::vector<Op>> levels(maxl + 1);
+    for (auto& it : items) levels[it.level].push_back(it.op);
+    for (auto& lv : levels) {
+      int wg = 0;
+      for (auto& op : lv) {
+        op.wg_begin = wg;
+        wg += op.wg_count;
+      }
+    }
+    return levels;
+  }
+};
+
+struct Graph {
+  hipGraph_t g = nullptr;
+  hipGraphExec_t x = nullptr;
+  Op* d_ops = nullptr;
+  std::vector<int> nops, nwg, off;
+  int levels() const { return (int)nops.size(); }
+};
+
+struct Layer {
+  std::string wname, bname;
+  int out = 0, K = 0;
+  std::vector<int> seg_w, seg_p;  // logical / padded widths of input segments
+  size_t w_off = 0, b_off = 0;
+  int res = -1;
+};
+
+struct Net {
+  std::string name, kind;  // kind: sale_enc / sale_actor / sale_critic / mlp
+  std::vector<Layer> layers;
+  size_t off = 0, size = 0;
+  int res = -1;  // whole-net resource (polyak / copy)
+};
+
+enum Res : int {
+  R_CNT = 1,
+  R_VKEYS,
+  R_VT,
+  R_INFO,
+  R_LA,
+  R_PRIO,
+  R_MAXP,
+  R_REPLAY,
+  R_FIRST_DYNAMIC = 100,
+};
+
+struct Engine {
+  rle_config cfg;
+  int S, Sp, A, Ap, H, Hp, B;
+  int algo;
+  hipStream_t stream = nullptr;
+  DevMem mem;
+  float* P = nullptr;
+  size_t nP = 0;
+  std::vector<Net> nets;
+  Ctrl* ctrl = nullptr;
+  float* info = nullptr;
+  int info_cap = 4096;
+  std::vector<float> info_host;
+  Replay* replay = nullptr;
+  int next_id = R_FIRST_DYNAMIC;
+  Graph g_policy, g_plain, g_hard;
+  bool built = false;
+  long long n_runs = 0;  // host mirror of the agent's step counter
+  // step buffers
+  View ss, act_in, rw, nd, eps, eps2;
+  long long* ind = nullptr;
+  float* u_buf = nullptr;
+  double* bsum = nullptr;
+  // tapes
+  float *t_u = nullptr, *t_eps = nullptr, *t_eps2 = nullptr;
+  long long* t_ind = nullptr;
+  long long tape_cap = 0, tape_left = 0;
+  // act programs (cached per n)
+  std::map<int, std::pair<Graph, View>> act_graphs;  // n -> graph, output view
+  std::map<int, View> act_inputs;
+
+  // ---------------------------------------------------------------- params
+  Net& net(const std::string& name) {
+    for (auto& n : nets)
+      if (n.name == name) return n;
+    throw Error{RLE_EINVAL, "unknown net '" + name + "'"};
+  }
+
+  void add_layer(Net& n, const std::string& pre, int out, std::vector<int> segw) {
+    Layer L;
+    L.wname = pre + ".weight";
+    L.bname = pre + ".bias";
+    L.out = out;
+    L.seg_w = segw;
+    for (int w : segw) L.seg_p.push_back(r4(w));
+    L.K = 0;
+    for (int p : L.seg_p) L.K += p;
+    L.res = next_id++;
+    n.layers.push_back(L);
+  }
+
+  Net make_net(const std::string& name, const std::string& kind) {
+    Net n;
+    n.name = name;
+    n.kind = kind;
+    n.res = next_id++;
+    if (kind == "sale_enc") {  // rl/nn/sale.py:16-55
+      add_layer(n, "zs1", H, {S});
+      add_layer(n, "zs2", H, {H});
+      add_layer(n, "zs3", H, {H});
+      add_layer(n, "zsa1", H, {H, A});
+      add_layer(n, "zsa2", H, {H});
+      add_layer(n, "zsa3", H, {H});
+    } else if (kind == "sale_actor") {  // sale.py:58-83
+      add_layer(n, "l0", H, {S});
+      add_layer(n, "l1", H, {H, H});
+      add_layer(n, "l2", H, {H});
+      add_layer(n, "l3", A, {H});
+    } else if (kind == "sale_critic") {  // sale.py:86-121
+      add_layer(n, "q01", H, {S, A});
+      add_layer(n, "q1", H, {H, H, H});
+      add_layer(n, "q2", H, {H});
+      add_layer(n, "q3", 1, {H});
+    } else if (kind == "mlp_actor") {  // mlp.py:38-55
+      add_layer(n, "mlp.0", H, {S});
+      add_layer(n, "mlp.2", H, {H});
+      add_layer(n, "mlp.4", algo == RLE_SAC ? 2 * A : A, {H});
+    } else {  // mlp_critic, mlp.py:75-101
+      add_layer(n, "mlp.0", H, {S, A});
+      add_layer(n, "mlp.2", H, {H});
+      add_layer(n, "mlp.4", 1, {H});
+    }
+    return n;
+  }
+
+  void layout_params() {
+    size_t off = 0;
+    for (auto& n : nets) {
+      n.off = off;
+      for (auto& L : n.layers) {
+        L.w_off = off;
+        off += (size_t)L.out * L.K;
+        off = (off + 3) & ~(size_t)3;
+        L.b_off = off;
+        off += (size_t)r4(L.out);
+      }
+      n.size = off - n.off;
+    }
+    nP = off + 4;  // + SAC log_alpha slot
+    P = mem.make<float>(3 * nP);  // params | m | v
+  }
+
+  float* param(const Layer& L) { return P + L.w_off; }
+  float* bias(const Layer& L) { return P + L.b_off; }
+
+  // locate (net, torch param name) -> (layer, is_bias)
+  std::pair<Layer*, bool> find_param(const std::string& netn, const std::string& name) {
+    Net& n = net(netn);
+    for (auto& L : n.layers) {
+      if (L.wname == name) return {&L, false};
+      if (L.bname == name) return {&L, true};
+    }
+    throw Error{RLE_EINVAL, "unknown param '" + netn + "." + name + "'"};
+  }
+
+  long long numel(const std::string& netn, const std::string& name) {
+    if (netn == "tmp") return 1;
+    auto pr = find_param(netn, name);
+    const Layer& L = *pr.first;
+    if (pr.second) return L.out;
+    long long k = 0;
+    for (int w : L.seg_w) k += w;
+    return (long long)L.out * k;
+  }
+
+  // copy between logical [out][sum seg_w] host layout and padded device layout
+  void xfer_param(const std::string& netn, const std::string& name, float* host, long long n, bool to_dev,
+                  int which) {
+    REQUIRE(n == numel(netn, name), "size mismatch for " + netn + "." + name);
+    const size_t base = (size_t)which * nP;
+    HIPCHK(hipStreamSynchronize(stream));
+    if (netn == "tmp") {
+      float* d = P + base + (nP - 4);
+      if (to_dev) HIPCHK(hipMemcpy(d, host, 4, hipMemcpyHostToDevice));
+      else HIPCHK(hipMemcpy(host, d, 4, hipMemcpyDeviceToHost));
+      return;
+    }
+    auto pr = find_param(netn, name);
+    const Layer& L = *pr.first;
+    if (pr.second) {
+      float* d = P + base + L.b_off;
+      if (to_dev) HIPCHK(hipMemcpy(d, host, sizeof(float) * L.out, hipMemcpyHostToDevice));
+      else HIPCHK(hipMemcpy(host, d, sizeof(float) * L.out, hipMemcpyDeviceToHost));
+      return;
+    }
+    std::vector<float> pad((size_t)L.out * L.K, 0.f);
+    float* d = P + base + L.w_off;
+    int klog = 0;
+    for (int w : L.seg_w) klog += w;
+    if (!to_dev) HIPCHK(hipMemcpy(pad.data(), d, pad.size() * 4, hipMemcpyDeviceToHost));
+    for (int o = 0; o < L.out; ++o) {
+      int lc = 0, pc = 0;
+      for (size_t s = 0; s < L.seg_w.size(); ++s) {
+        for (int c = 0; c < L.seg_w[s]; ++c) {
+          float& dv = pad[(size_t)o * L.K + pc + c];
+          float& hv = host[(size_t)o * klog + lc + c];
+          if (to_dev) dv = hv; else hv = dv;
+        }
+        lc += L.seg_w[s];
+        pc += L.seg_p[s];
+      }
+    }
+    if (to_dev) HIPCHK(hipMemcpy(d, pad.data(), pad.size() * 4, hipMemcpyHostToDevice));
+  }
+
+  // ---------------------------------------------------------------- buffers
+  // Zero-initialised activation buffer; feature dims padded to 4 (16-B rows),
+  // single-column vectors kept dense (ld 1).
+  View buf(int rows, int cols) {
+    View v;
+    v.ld = cols == 1 ? 1 : r4(cols);
+    v.rows = rows;
+    v.cols = v.ld;
+    v.p = mem.make<float>((size_t)rows * v.ld + 4);
+    v.id = next_id++;
+    return v;
+  }
+
+  // ---------------------------------------------------------------- op builders
+  static Seg seg_contig(const View& v, int x0, int r0, int r1) {
+    Seg s{};
+    s.p = v.p;
+    s.ld = v.ld;
+    s.x0 = x0;
+    s.x1 = x0 + v.rows;
+    s.r0 = r0;
+    s.r1 = r1;
+    s.strided = 0;
+    if (v.norm) {
+      s.norm = v.norm;
+      s.norm_ld = v.norm_ld;
+      s.norm_row0 = v.norm_row0;
+      s.norm_nparts = v.nparts;
+      s.norm_width = v.width;
+    }
+    return s;
+  }
+
+  // Y = act(X W^T + b) over concatenated input segments (each a list of row pieces).
+  View fwd(Prog& pg, const Layer& L, const std::vector<std::vector<View>>& ins, int M, int act, View* pre_out,
+           bool normed, const View* noise = nullptr, int noise_row0 = 0) {
+    REQUIRE(ins.size() == L.seg_p.size(), "fwd: input segment count mismatch for " + L.wname);
+    Op op{};
+    op.kind = OP_GEMM;
+    GemmArgs& g = op.gemm;
+    std::vector<int> rd{L.res}, wr;
+    int koff = 0, ns = 0;
+    for (size_t s = 0; s < ins.size(); ++s) {
+      int xo = 0;
+      for (const View& v : ins[s]) {
+        REQUIRE(v.cols == L.seg_p[s], "fwd: segment width mismatch for " + L.wname);
+        REQUIRE(ns < kMaxSeg, "fwd: too many operand segments");
+        g.A.seg[ns++] = seg_contig(v, xo, koff, koff + L.seg_p[s]);
+        xo += v.rows;
+        rd.push_back(v.id);
+        if (v.norm) rd.push_back(v.norm_id);
+      }
+      REQUIRE(xo >= M, "fwd: input rows < M");
+      koff += L.seg_p[s];
+    }
+    g.A.nseg = ns;
+    Seg w{};
+    w.p = param(L);
+    w.ld = L.K;
+    w.x0 = 0;
+    w.x1 = L.out;
+    w.r0 = 0;
+    w.r1 = L.K;
+    g.B.seg[0] = w;
+    g.B.nseg = 1;
+    g.M = M;
+    g.N = L.out;
+    g.R = L.K;
+    g.tiles_m = cdiv(M, kTile);
+    g.tiles_n = cdiv(L.out, kTile);
+    g.epi = EPI_STORE;
+    g.act = act;
+    View out = buf(M, L.out);
+    g.out = out.p;
+    g.ldo = out.ld;
+    g.bias = bias(L);
+    wr.push_back(out.id);
+    if (pre_out) {
+      *pre_out = buf(M, L.out);
+      g.pre = pre_out->p;
+      g.ldpre = pre_out->ld;
+      wr.push_back(pre_out->id);
+    }
+    if (normed) {
+      float* part = mem.make<float>((size_t)g.tiles_n * M);
+      g.norm_out = part;
+      g.norm_ld = M;
+      out.norm = part;
+      out.norm_ld = M;
+      out.norm_row0 = 0;
+      out.nparts = g.tiles_n;
+      out.width = L.out;
+      out.norm_id = next_id++;
+      wr.push_back(out.norm_id);
+    }
+    if (noise) {
+      g.noise = noise->p;
+      g.ldnoise = noise->ld;
+      g.noise_row0 = noise_row0;
+      g.noise_sigma = cfg.target_policy_noise;
+      g.noise_clip = cfg.noise_clip;
+      rd.push_back(noise->id);
+    }
+    op.wg_count = g.tiles_m * g.tiles_n;
+    pg.add(op, rd, wr);
+    return out;
+  }
+
+  struct DxTerm {
+    View dz;
+    const Layer* L;
+    int col0;
+  };
+
+  // dX[:, 0:ncols] = sum_t dZ_t W_t[:, col0_t : col0_t + ncols]  (* act'(saved))
+  View dx(Prog& pg, const std::vector<DxTerm>& terms, int ncols, int M, int dact, const View* saved) {
+    Op op{};
+    op.kind = OP_GEMM;
+    GemmArgs& g = op.gemm;
+    std::vector<int> rd, wr;
+    REQUIRE((int)terms.size() <= kMaxSeg, "dx: too many terms");
+    int roff = 0;
+    for (size_t t = 0; t < terms.size(); ++t) {
+      const DxTerm& tm = terms[t];
+      Seg a{};
+      a.p = tm.dz.p;
+      a.ld = tm.dz.ld;
+      a.x0 = 0;
+      a.x1 = M;
+      a.r0 = roff;
+      a.r1 = roff + tm.L->out;
+      g.A.seg[t] = a;
+      Seg b{};
+      b.p = param(*tm.L) + tm.col0;
+      b.ld = tm.L->K;
+      b.x0 = 0;
+      b.x1 = ncols;
+      b.r0 = roff;
+      b.r1 = roff + tm.L->out;
+      b.strided = 1;
+      g.B.seg[t] = b;
+      roff += r4(tm.L->out);
+      rd.push_back(tm.dz.id);
+      rd.push_back(tm.L->res);
+    }
+    g.A.nseg = g.B.nseg = (int)terms.size();
+    g.M = M;
+    g.N = ncols;
+    g.R = roff;
+    g.tiles_m = cdiv(M, kTile);
+    g.tiles_n = cdiv(ncols, kTile);
+    g.epi = EPI_STORE;
+    g.act = ACT_NONE;
+    View out = buf(M, ncols);
+    g.out = out.p;
+    g.ldo = out.ld;
+    if (saved) {
+      g.dact = dact;
+      g.dsrc = saved->p;
+      g.lddact = saved->ld;
+      rd.push_back(saved->id);
+    }
+    wr.push_back(out.id);
+    op.wg_count = g.tiles_m * g.tiles_n;
+    pg.add(op, rd, wr);
+    return out;
+  }
+
+  // dW = dZ^T [X], db = sum dZ, fused Adam (torch.optim.Adam law).
+  void dw(Prog& pg, const Layer& L, const View& dz, const std::vector<View>& X, int Brows, int cnt, float lr,
+          float* gsq = nullptr, float* gsq_b = nullptr) {
+    REQUIRE(X.size() == L.seg_p.size(), "dw: input count mismatch for " + L.wname);
+    Op op{};
+    op.kind = OP_GEMM;
+    GemmArgs& g = op.gemm;
+    std::vector<int> rd{dz.id, L.res, R_CNT}, wr{L.res};
+    Seg a{};
+    a.p = dz.p;
+    a.ld = dz.ld;
+    a.x0 = 0;
+    a.x1 = L.out;
+    a.r0 = 0;
+    a.r1 = Brows;
+    a.strided = 1;
+    g.A.seg[0] = a;
+    g.A.nseg = 1;
+    int koff = 0;
+    for (size_t s = 0; s < X.size(); ++s) {
+      const View& v = X[s];
+      REQUIRE(v.cols == L.seg_p[s] && v.rows >= Brows, "dw: input view mismatch for " + L.wname);
+      Seg b{};
+      b.p = v.p;
+      b.ld = v.ld;
+      b.x0 = koff;
+      b.x1 = koff + L.seg_p[s];
+      b.r0 = 0;
+      b.r1 = Brows;
+      b.strided = 1;
+      if (v.norm) {
+        b.norm = v.norm;
+        b.norm_ld = v.norm_ld;
+        b.norm_row0 = v.norm_row0;
+        b.norm_nparts = v.nparts;
+        b.norm_width = v.width;
+        rd.push_back(v.norm_id);
+      }
+      g.B.seg[s] = b;
+      rd.push_back(v.id);
+      koff += L.seg_p[s];
+    }
+    g.B.nseg = (int)X.size();
+    g.M = L.out;
+    g.N = L.K;
+    g.R = Brows;
+    g.tiles_m = cdiv(L.out, kTile);
+    g.tiles_n = cdiv(L.K, kTile) + 1;
+    g.epi = EPI_ADAM;
+    AdamArgs& ad = g.adam;
+    ad.w = param(L);
+    ad.b = bias(L);
+    ad.mo = (long long)nP;
+    ad.vo = 2LL * (long long)nP;
+    ad.t = &ctrl->counters[cnt];
+    ad.lr = lr;
+    ad.beta1 = 0.9f;
+    ad.beta2 = 0.999f;
+    ad.eps = 1e-8f;
+    ad.ldw = L.K;
+    ad.bias_col = r16(L.K);
+    ad.gsq = gsq;
+    ad.gsq_b = gsq_b;
+    op.wg_count = g.tiles_m * g.tiles_n;
+    pg.add(op, rd, wr);
+  }
+
+  View normbwd(Prog& pg, const View& gv, const View& x) {
+    REQUIRE(x.norm, "normbwd: x is not a normed view");
+    Op op{};
+    op.kind = OP_NORMBWD;
+    NormBwdArgs& a = op.nb;
+    View out = buf(gv.rows, x.width);
+    a.g = gv.p;
+    a.ldg = gv.ld;
+    a.x = x.p;
+    a.ldx = x.ld;
+    a.dx = out.p;
+    a.lddx = out.ld;
+    a.rows = gv.rows;
+    a.width = x.width;
+    a.norm = x.norm;
+    a.norm_ld = x.norm_ld;
+    a.norm_row0 = x.norm_row0;
+    a.norm_nparts = x.nparts;
+    op.wg_count = cdiv(gv.rows, 4);
+    pg.add(op, {gv.id, x.id, x.norm_id}, {out.id});
+    View o = out;
+    return o;
+  }
+
+  // polyak / copy over a whole net range
+  void flat(Prog& pg, int kind, Net& dst, Net* src, float tau, bool self_alias) {
+    Op op{};
+    op.kind = kind;
+    FlatArgs& f = op.flat;
+    f.dst = P + dst.off;
+    f.src = src ? P + src->off : P + dst.off;
+    f.n = (long long)dst.size;
+    f.tau = tau;
+    f.omt = 1.f - tau;  // fp32(1 - tau) as torch casts the python scalar (Q2)
+    f.self_alias = self_alias ? 1 : 0;
+    op.wg_count = cdiv(f.n, (long long)kThreads * 4);
+    std::vector<int> rd{dst.res}, wr{dst.res};
+    for (auto& L : dst.layers) {
+      rd.push_back(L.res);
+      wr.push_back(L.res);
+    }
+    if (src) {
+      rd.push_back(src->res);
+      for (auto& L : src->layers) rd.push_back(L.res);
+    }
+    pg.add(op, rd, wr);
+  }
+
+  // ---------------------------------------------------------------- step programs
+  void add_sampling(Prog& pg, bool sac) {
+    Replay& rp = *replay;
+    if (rp.lap) {
+      Op op{};
+      op.kind = OP_SAMPLE_REDUCE;
+      fill_sample_args(op.sample, sac);
+      op.wg_count = rp.nblk;
+      pg.add(op, {R_PRIO}, {bsum_id});
+    }
+    Op op{};
+    op.kind = OP_SAMPLE_GATHER;
+    fill_sample_args(op.sample, sac);
+    op.wg_count = B;
+    // reads the RNG step / tape position counters -> ordered before STEP_END (WAR)
+    pg.add(op, {bsum_id, R_PRIO, R_REPLAY, R_CNT},
+           {ss.id, act_in.id, rw.id, nd.id, eps.id, ind_id, sac ? eps2.id : -1});
+  }
+  int bsum_id = -1, ind_id = -1;
+
+  void fill_sample_args(SampleArgs& s, bool sac) {
+    Replay& rp = *replay;
+    s.state = rp.state;
+    s.next_state = rp.next_state;
+    s.action = rp.action;
+    s.reward = rp.reward;
+    s.notdone = rp.notdone;
+    s.priority = rp.priority;
+    s.S = S;
+    s.Sp = Sp;
+    s.A = A;
+    s.Ap = Ap;
+    s.size = rp.size_d;
+    s.lap = rp.lap;
+    s.B = B;
+    s.bsum = rp.bsum;
+    s.nblk = rp.nblk;
+    s.ss = ss.p;
+    s.ldss = ss.ld;
+    s.a = act_in.p;
+    s.lda = act_in.ld;
+    s.r = rw.p;
+    s.nd = nd.p;
+    s.ind = ind;
+    s.u_out = u_buf;
+    s.eps = eps.p;
+    s.ldeps = eps.ld;
+    s.eps2 = sac ? eps2.p : nullptr;
+    s.ctrl_rng = &ctrl->counters[4];
+    s.seed = cfg.seed;
+    s.tape_mode = &ctrl->tape_mode;
+    s.tape_pos = &ctrl->counters[5];
+    s.tape_u = t_u;
+    s.tape_eps = t_eps;
+    s.tape_eps2 = t_eps2;
+    s.tape_ind = t_ind;
+  }
+
+  Op head_op(int mode, int rows) {
+    Op op{};
+    op.kind = OP_HEAD;
+    HeadArgs& h = op.head;
+    h.mode = mode;
+    h.rows = rows;
+    h.H = H;
+    h.gamma = cfg.discount;
+    h.inv_b = 1.f / (float)B;
+    op.wg_count = cdiv(rows, 4);
+    return op;
+  }
+
+  void set_head_twin(HeadArgs& h, const View& h1, const View& h2, const Layer& l1, const Layer& l2) {
+    h.h[0] = h1.p;
+    h.h[1] = h2.p;
+    h.ldh = h1.ld;
+    h.w[0] = param(l1);
+    h.w[1] = param(l2);
+    h.b[0] = bias(l1);
+    h.b[1] = bias(l2);
+  }
+
+  Op step_end_op() {
+    Op op{};
+    op.kind = OP_STEP_END;
+    StepEndArgs& a = op.end;
+    a.counters = ctrl->counters;
+    a.info_slot = &ctrl->info_slot;
+    a.info = info;
+    a.info_cap = info_cap;
+    a.inv_b = 1.f / (float)B;
+    op.wg_count = 1;
+    return op;
+  }
+
+  void info_sum(StepEndArgs& a, int k, const float* part, int n, int stride, float scale) {
+    a.part[k] = part;
+    a.npart[k] = n;
+    a.stride[k] = stride;
+    a.scale[k] = scale;
+    a.kind[k] = INFO_SUM;
+  }
+
+  // STEP_END writes the info row and bumps the step counters; every reader of a
+  // counter (Adam t, RNG step, tape position) is therefore scheduled before it.
+  void add_step_end(Prog& pg, Op op, std::vector<int> rd, const std::vector<int>& counters) {
+    StepEndArgs& a = op.end;
+    a.cmask = 0;
+    for (int c : counters) a.cmask |= 1 << c;
+    rd.push_back(R_CNT);
+    std::vector<int> wr{R_INFO, R_CNT};
+    if (a.log_alpha) wr.push_back(R_LA);
+    pg.add(op, rd, wr);
+  }
+
+  // TD7 (td7.py:287-332)
+  void build_td7(Prog& pg, bool policy) {
+    const int B2 = 2 * B;
+    Net& enc = net("encoder");
+    Net& fe = net("fixed_encoder");
+    Net& fet = net("fixed_encoder_target");
+    Net& pi = net("policy");
+    Net* q[2] = {&net("q1"), &net("q2")};
+    Net* tq[2] = {&net("target_q1"), &net("target_q2")};
+    const bool lap = cfg.use_lap;
+    add_sampling(pg, false);
+    View s = ss.sub(0, B), s2 = ss.sub(B, B);
+    // ---- encoder phase (td7.py:246-257): online encoder on [s; s'] (one GEMM per layer)
+    View ez1, ez2;
+    View eh1 = fwd(pg, enc.layers[0], {{ss}}, B2, ACT_ELU, &ez1, false);
+    View eh2 = fwd(pg, enc.layers[1], {{eh1}}, B2, ACT_ELU, &ez2, false);
+    View ex3 = fwd(pg, enc.layers[2], {{eh2}}, B2, ACT_NONE, nullptr, true);
+    View ezs = ex3.sub(0, B), ezs2 = ex3.sub(B, B);
+    View ea1z, ea2z;
+    View ea1 = fwd(pg, enc.layers[3], {{ezs}, {act_in}}, B, ACT_ELU, &ea1z, false);
+    View ea2 = fwd(pg, enc.layers[4], {{ea1}}, B, ACT_ELU, &ea2z, false);
+    // zsa3 + MSE gradient vs zs_next (normed) fused
+    View ed3;
+    float* enc_loss = nullptr;
+    int enc_tiles = 0;
+    {
+      const Layer& L = enc.layers[5];
+      Op op{};
+      op.kind = OP_GEMM;
+      GemmArgs& g = op.gemm;
+      g.A.seg[0] = seg_contig(ea2, 0, 0, L.K);
+      g.A.nseg = 1;
+      Seg w{};
+      w.p = param(L);
+      w.ld = L.K;
+      w.x1 = L.out;
+      w.r1 = L.K;
+      g.B.seg[0] = w;
+      g.B.nseg = 1;
+      g.M = B;
+      g.N = L.out;
+      g.R = L.K;
+      g.tiles_m = cdiv(B, kTile);
+      g.tiles_n = cdiv(L.out, kTile);
+      g.epi = EPI_MSE;
+      g.bias = bias(L);
+      ed3 = buf(B, L.out);
+      g.out = ed3.p;
+      g.ldo = ed3.ld;
+      g.tgt = seg_contig(ezs2, 0, 0, L.out);
+      enc_tiles = g.tiles_m * g.tiles_n;
+      enc_loss = mem.make<float>(enc_tiles);
+      g.loss_part = enc_loss;
+      g.mse_scale = 1.f / (float)((long long)B * H);
+      op.wg_count = enc_tiles;
+      pg.add(op, {ea2.id, L.res, ezs2.id, ezs2.norm_id}, {ed3.id, loss_id_enc = next_id++});
+    }
+    // encoder backward + Adam (optim_encoder, lr = policy_lr)
+    {
+      View d2 = dx(pg, {{ed3, &enc.layers[5], 0}}, H, B, ACT_ELU, &ea2z);
+      dw(pg, enc.layers[5], ed3, {ea2}, B, CNT_ADAM_ENC, cfg.policy_lr);
+      View d1 = dx(pg, {{d2, &enc.layers[4], 0}}, H, B, ACT_ELU, &ea1z);
+      dw(pg, enc.layers[4], d2, {ea1}, B, CNT_ADAM_ENC, cfg.policy_lr);
+      View gzs = dx(pg, {{d1, &enc.layers[3], 0}}, H, B, ACT_NONE, nullptr);
+      dw(pg, enc.layers[3], d1, {ezs, act_in}, B, CNT_ADAM_ENC, cfg.policy_lr);
+      View dx3 = normbwd(pg, gzs, ex3.sub(0, B));
+      View ez2s = ez2.sub(0, B), ez1s = ez1.sub(0, B);
+      View dh2 = dx(pg, {{dx3, &enc.layers[2], 0}}, H, B, ACT_ELU, &ez2s);
+      dw(pg, enc.layers[2], dx3, {eh2.sub(0, B)}, B, CNT_ADAM_ENC, cfg.policy_lr);
+      View dh1 = dx(pg, {{dh2, &enc.layers[1], 0}}, H, B, ACT_ELU, &ez1s);
+      dw(pg, enc.layers[1], dh2, {eh1.sub(0, B)}, B, CNT_ADAM_ENC, cfg.policy_lr);
+      dw(pg, enc.layers[0], dh1, {s}, B, CNT_ADAM_ENC, cfg.policy_lr);
+    }
+    // ---- fixed encoder on s, fixed target encoder on s'
+    View fh1 = fwd(pg, fe.layers[0], {{s}}, B, ACT_ELU, nullptr, false);
+    View fh2 = fwd(pg, fe.layers[1], {{fh1}}, B, ACT_ELU, nullptr, false);
+    View fzs = fwd(pg, fe.layers[2], {{fh2}}, B, ACT_NONE, nullptr, true);
+    View th1 = fwd(pg, fet.layers[0], {{s2}}, B, ACT_ELU, nullptr, false);
+    View th2 = fwd(pg, fet.layers[1], {{th1}}, B, ACT_ELU, nullptr, false);
+    View tzs = fwd(pg, fet.layers[2], {{th2}}, B, ACT_NONE, nullptr, true);
+    View fa1 = fwd(pg, fe.layers[3], {{fzs}, {act_in}}, B, ACT_ELU, nullptr, false);
+    View fa2 = fwd(pg, fe.layers[4], {{fa1}}, B, ACT_ELU, nullptr, false);
+    View fzsa = fwd(pg, fe.layers[5], {{fa2}}, B, ACT_NONE, nullptr, false);
+    // ---- actor on [s; s'] (target policy aliases the policy, Q1)
+    View ap0 = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_NONE, nullptr, true);
+    View ap1 = fwd(pg, pi.layers[1], {{ap0}, {fzs, tzs}}, B2, ACT_RELU, nullptr, false);
+    View ap2 = fwd(pg, pi.layers[2], {{ap1}}, B2, ACT_RELU, nullptr, false);
+    View actv = fwd(pg, pi.layers[3], {{ap2}}, B2, ACT_TANH, nullptr, false, &eps, B);
+    View a_pi = actv.sub(0, B), a_next = actv.sub(B, B);
+    // ---- target: zsa' and target critics
+    View ta1 = fwd(pg, fet.layers[3], {{tzs}, {a_next}}, B, ACT_ELU, nullptr, false);
+    View ta2 = fwd(pg, fet.layers[4], {{ta1}}, B, ACT_ELU, nullptr, false);
+    View tzsa = fwd(pg, fet.layers[5], {{ta2}}, B, ACT_NONE, nullptr, false);
+    View th[2];
+    for (int n = 0; n < 2; ++n) {
+      View t01 = fwd(pg, tq[n]->layers[0], {{s2}, {a_next}}, B, ACT_NONE, nullptr, true);
+      View t1 = fwd(pg, tq[n]->layers[1], {{t01}, {tzsa}, {tzs}}, B, ACT_ELU, nullptr, false);
+      th[n] = fwd(pg, tq[n]->layers[2], {{t1}}, B, ACT_ELU, nullptr, false);
+    }
+    View y = buf(B, 1);
+    {
+      Op op = head_op(HEAD_TD7_TARGET, B);
+      HeadArgs& h = op.head;
+      set_head_twin(h, th[0], th[1], tq[0]->layers[3], tq[1]->layers[3]);
+      h.reward = rw.p;
+      h.notdone = nd.p;
+      h.y = y.p;
+      h.vmax_key = &ctrl->vmax_key;
+      h.vmin_key = &ctrl->vmin_key;
+      h.vt = ctrl->vt;
+      pg.add(op, {th[0].id, th[1].id, tq[0]->layers[3].res, tq[1]->layers[3].res, rw.id, nd.id, R_VT},
+             {y.id, R_VKEYS});
+    }
+    // ---- online critics on (s, a, zsa_f, zs_f)
+    View c01[2], c1[2], c2[2], c1z[2], c2z[2];
+    for (int n = 0; n < 2; ++n) {
+      c01[n] = fwd(pg, q[n]->layers[0], {{s}, {act_in}}, B, ACT_NONE, nullptr, true);
+      c1[n] = fwd(pg, q[n]->layers[1], {{c01[n]}, {fzsa}, {fzs}}, B, ACT_ELU, &c1z[n], false);
+      c2[n] = fwd(pg, q[n]->layers[2], {{c1[n]}}, B, ACT_ELU, &c2z[n], false);
+    }
+    View dz2[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1), buf(B, 1)};
+    View prio = buf(B, 1);
+    const int hw = cdiv(B, 4);
+    qloss_part = mem.make<float>((size_t)hw * 4);
+    {
+      Op op = head_op(HEAD_TD7_LOSS, B);
+      HeadArgs& h = op.head;
+      set_head_twin(h, c2[0], c2[1], q[0]->layers[3], q[1]->layers[3]);
+      h.dsrc[0] = c2z[0].p;
+      h.dsrc[1] = c2z[1].p;
+      h.ldd = c2z[0].ld;
+      h.dact = ACT_ELU;
+      h.lap = lap;
+      h.y = y.p;
+      h.dz[0] = dz2[0].p;
+      h.dz[1] = dz2[1].p;
+      h.lddz = dz2[0].ld;
+      h.dq[0] = dq[0].p;
+      h.dq[1] = dq[1].p;
+      h.loss_part = qloss_part;
+      h.prio = prio.p;
+      pg.add(op, {c2[0].id, c2[1].id, c2z[0].id, c2z[1].id, q[0]->layers[3].res, q[1]->layers[3].res, y.id},
+             {dz2[0].id, dz2[1].id, dq[0].id, dq[1].id, prio.id, qloss_id = next_id++});
+    }
+    if (lap) {
+      Op op{};
+      op.kind = OP_PRIORITY;
+      op.prio.priority = replay->priority;
+      op.prio.ind = ind;
+      op.prio.p = prio.p;
+      op.prio.B = B;
+      op.prio.max_priority = replay->maxp_d;
+      op.wg_count = 1;
+      pg.add(op, {prio.id, ind_id, bsum_id}, {R_PRIO, R_MAXP});
+    }
+    for (int n = 0; n < 2; ++n) {  // critic backward + Adam (optim_q_fns spans q1 + q2)
+      Net& Q = *q[n];
+      dw(pg, Q.layers[3], dq[n], {c2[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
+      View d1 = dx(pg, {{dz2[n], &Q.layers[2], 0}}, H, B, ACT_ELU, &c1z[n]);
+      dw(pg, Q.layers[2], dz2[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
+      View g01 = dx(pg, {{d1, &Q.layers[1], 0}}, H, B, ACT_NONE, nullptr);
+      dw(pg, Q.layers[1], d1, {c01[n], fzsa, fzs}, B, CNT_ADAM_Q, cfg.critic_lr);
+      View dx01 = normbwd(pg, g01, c01[n]);
+      dw(pg, Q.layers[0], dx01, {s, act_in}, B, CNT_ADAM_Q, cfg.critic_lr);
+    }
+    ploss_part = nullptr;
+    if (policy) {  // td7.py:259-276 with the updated critics
+      View pa1z, pa2z;
+      View pa1 = fwd(pg, fe.layers[3], {{fzs}, {a_pi}}, B, ACT_ELU, &pa1z, false);
+      View pa2 = fwd(pg, fe.layers[4], {{pa1}}, B, ACT_ELU, &pa2z, false);
+      View pzsa = fwd(pg, fe.layers[5], {{pa2}}, B, ACT_NONE, nullptr, false);
+      View p01[2], p1[2], p2[2], p1z[2], p2z[2];
+      for (int n = 0; n < 2; ++n) {
+        p01[n] = fwd(pg, q[n]->layers[0], {{s}, {a_pi}}, B, ACT_NONE, nullptr, true);
+        p1[n] = fwd(pg, q[n]->layers[1], {{p01[n]}, {pzsa}, {fzs}}, B, ACT_ELU, &p1z[n], false);
+        p2[n] = fwd(pg, q[n]->layers[2], {{p1[n]}}, B, ACT_ELU, &p2z[n], false);
+      }
+      View dzp2[2] = {buf(B, H), buf(B, H)};
+      ploss_part = mem.make<float>((size_t)hw * 4);
+      {
+        Op op = head_op(HEAD_TD7_POLICY, B);
+        HeadArgs& h = op.head;
+        set_head_twin(h, p2[0], p2[1], q[0]->layers[3], q[1]->layers[3]);
+        h.dsrc[0] = p2z[0].p;
+        h.dsrc[1] = p2z[1].p;
+        h.ldd = p2z[0].ld;
+        h.dact = ACT_ELU;
+        h.dz[0] = dzp2[0].p;
+        h.dz[1] = dzp2[1].p;
+        h.lddz = dzp2[0].ld;
+        h.loss_part = ploss_part;
+        pg.add(op, {p2[0].id, p2[1].id, p2z[0].id, p2z[1].id, q[0]->layers[3].res, q[1]->layers[3].res},
+               {dzp2[0].id, dzp2[1].id, ploss_id = next_id++});
+      }
+      View dzp1[2], dxp01[2];
+      for (int n = 0; n < 2; ++n) {
+        dzp1[n] = dx(pg, {{dzp2[n], &q[n]->layers[2], 0}}, H, B, ACT_ELU, &p1z[n]);
+        View g = dx(pg, {{dzp1[n], &q[n]->layers[1], 0}}, H, B, ACT_NONE, nullptr);
+        dxp01[n] = normbwd(pg, g, p01[n]);
+      }
+      // grad wrt zsa from both critics (q1 input columns [H, 2H))
+      View gzsa = dx(pg, {{dzp1[0], &q[0]->layers[1], Hp}, {dzp1[1], &q[1]->layers[1], Hp}}, H, B, ACT_NONE,
+                     nullptr);
+      View dpa2 = dx(pg, {{gzsa, &fe.layers[5], 0}}, H, B, ACT_ELU, &pa2z);
+      View dpa1 = dx(pg, {{dpa2, &fe.layers[4], 0}}, H, B, ACT_ELU, &pa1z);
+      // d action = sum of three paths, then tanh' (actor output)
+      View dl3 = dx(pg,
+                    {{dxp01[0], &q[0]->layers[0], Sp}, {dxp01[1], &q[1]->layers[0], Sp},
+                     {dpa1, &fe.layers[3], Hp}},
+                    A, B, ACT_TANH, &a_pi);
+      // input-grads through a layer are emitted BEFORE its Adam update so the
+      // scheduler orders them against the pre-update weights (as autograd does)
+      View ap2s = ap2.sub(0, B), ap1s = ap1.sub(0, B);
+      View dl2 = dx(pg, {{dl3, &pi.layers[3], 0}}, H, B, ACT_RELU, &ap2s);
+      dw(pg, pi.layers[3], dl3, {ap2s}, B, CNT_ADAM_PI, cfg.policy_lr);
+      View dl1 = dx(pg, {{dl2, &pi.layers[2], 0}}, H, B, ACT_RELU, &ap1s);
+      dw(pg, pi.layers[2], dl2, {ap1s}, B, CNT_ADAM_PI, cfg.policy_lr);
+      View gl0 = dx(pg, {{dl1, &pi.layers[1], 0}}, H, B, ACT_NONE, nullptr);
+      dw(pg, pi.layers[1], dl1, {ap0.sub(0, B), fzs}, B, CNT_ADAM_PI, cfg.policy_lr);
+      View dl0 = normbwd(pg, gl0, ap0.sub(0, B));
+      dw(pg, pi.layers[0], dl0, {s}, B, CNT_ADAM_PI, cfg.policy_lr);
+    }
+    // ---- step end: info row [encoder, q_fn, policy]
+    Op op = step_end_op();
+    StepEndArgs& a = op.end;
+    info_sum(a, 0, enc_loss, enc_tiles, 1, 1.f / (float)((long long)B * H));
+    info_sum(a, 1, qloss_part, hw * 4, 1, (lap ? 1.f : 0.5f) / (float)B);
+    if (policy) info_sum(a, 2, ploss_part, hw, 4, -0.5f / (float)B);
+    else a.kind[2] = INFO_NAN;
+    a.ninfo = 3;
+    std::vector<int> rd{loss_id_enc, qloss_id};
+    if (policy) rd.push_back(ploss_id);
+    std::vector<int> cn{CNT_ADAM_Q, CNT_ADAM_ENC, 3, CNT_RNG, CNT_TAPE};
+    if (policy) cn.push_back(CNT_ADAM_PI);
+    add_step_end(pg, op, rd, cn);
+  }
+  int loss_id_enc = -1, qloss_id = -1, ploss_id = -1;
+  float* qloss_part = nullptr;
+  float* ploss_part = nullptr;
+
+  void build_td7_hard(Prog& pg) {  // td7.py:278-285, 325-331
+    flat(pg, OP_COPY, net("target_q1"), &net("q1"), 0.f, false);
+    flat(pg, OP_COPY, net("target_q2"), &net("q2"), 0.f, false);
+    flat(pg, OP_COPY, net("fixed_encoder_target"), &net("fixed_encoder"), 0.f, false);
+    flat(pg, OP_COPY, net("fixed_encoder"), &net("encoder"), 0.f, false);
+    Op c{};
+    c.kind = OP_CTRL;
+    c.ctrl.vmax_key = &ctrl->vmax_key;
+    c.ctrl.vmin_key = &ctrl->vmin_key;
+    c.ctrl.vt = ctrl->vt;
+    c.wg_count = 1;
+    pg.add(c, {R_VKEYS}, {R_VT});
+    if (cfg.use_lap) add_reset_maxp(pg);
+  }
+
+  void add_reset_maxp(Prog& pg) {
+    Replay& rp = *replay;
+    Op a{};
+    a.kind = OP_MAXRED;
+    a.flat.src = rp.priority;
+    a.flat.size = rp.size_d;
+    a.flat.partial = rp.maxred_part;
+    a.flat.nwg = rp.maxred_nwg;
+    a.flat.stage = 0;
+    a.wg_count = rp.maxred_nwg;
+    int pid = next_id++;
+    pg.add(a, {R_PRIO}, {pid});
+    Op b = a;
+    b.flat.stage = 1;
+    b.flat.out = rp.maxp_d;
+    b.wg_count = 1;
+    pg.add(b, {pid}, {R_MAXP});
+  }
+
+  // MLP critic stack forward: returns (h0, h1)
+  void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, View& h0, View& h1) {
+    h0 = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false);
+    h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false);
+  }
+
+  // TD3 (td3.py:206-242) and SAC (sac.py:251-295)
+  void build_mlp(Prog& pg, bool policy) {
+    const bool sac = algo == RLE_SAC;
+    const int B2 = 2 * B;
+    Net& pi = net("policy");
+    Net* q[2] = {&net("q1"), &net("q2")};
+    Net* tq[2] = {&net("target_q1"), &net("target_q2")};
+    const bool lap = cfg.use_lap && !sac;
+    add_sampling(pg, sac);
+    View s = ss.sub(0, B), s2 = ss.sub(B, B);
+    // actor on [s; s'] (target policy aliases the policy, Q1; SAC policy unchanged until its step)
+    View h0 = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_RELU, nullptr, false);
+    View h1 = fwd(pg, pi.layers[1], {{h0}}, B2, ACT_RELU, nullptr, false);
+    View actv, raw, logpi;
+    if (!sac) {
+      actv = fwd(pg, pi.layers[2], {{h1}}, B2, ACT_TANH, nullptr, false, &eps, B);
+    } else {
+      raw = fwd(pg, pi.layers[2], {{h1}}, B2, ACT_NONE, nullptr, false);
+      actv = buf(B2, A);
+      logpi = buf(B2, 1);
+      Op op{};
+      op.kind = OP_SAC_ACTOR;
+      SacActorArgs& a = op.sac;
+      a.out = raw.p;
+      a.ldo = raw.ld;
+      a.A = A;
+      a.rows = B2;
+      a.eps = eps.p;
+      a.eps2 = eps2.p;
+      a.ldeps = eps.ld;
+      a.eps_row_split = B;
+      a.act = actv.p;
+      a.ldact = actv.ld;
+      a.logpi = logpi.p;
+      a.min_log_std = cfg.min_log_std;
+      a.max_log_std = cfg.max_log_std;
+      a.mean_off = 0;
+      a.ls_off = A;
+      op.wg_count = cdiv(B2, kThreads);
+      pg.add(op, {raw.id, eps.id, eps2.id}, {actv.id, logpi.id});
+    }
+    View a_pi = actv.sub(0, B), a_next = actv.sub(B, B);
+    // target critics + y
+    View th0[2], th1[2];
+    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n]);
+    View y = buf(B, 1);
+    {
+      Op op = head_op(HEAD_MLP_TARGET, B);
+      HeadArgs& h = op.head;
+      set_head_twin(h, th1[0], th1[1], tq[0]->layers[2], tq[1]->layers[2]);
+      h.reward = rw.p;
+      h.notdone = nd.p;
+      h.y = y.p;
+      std::vector<int> rd{th1[0].id, th1[1].id, tq[0]->layers[2].res, tq[1]->layers[2].res, rw.id, nd.id};
+      if (sac) {
+        h.sac = 1;
+        h.logpi = logpi.p + B;
+        h.log_alpha = P + (nP - 4);
+        rd.push_back(logpi.id);
+        rd.push_back(R_LA);
+      }
+      pg.add(op, rd, {y.id});
+    }
+    // online critics
+    View c0[2], c1[2];
+    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c0[n], c1[n]);
+    View dz1[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1), buf(B, 1)};
+    View prio = buf(B, 1);
+    const int hw = cdiv(B, 4);
+    qloss_part = mem.make<float>((size_t)hw * 4);
+    {
+      Op op = head_op(HEAD_MLP_LOSS, B);
+      HeadArgs& h = op.head;
+      set_head_twin(h, c1[0], c1[1], q[0]->layers[2], q[1]->layers[2]);
+      h.dsrc[0] = c1[0].p;
+      h.dsrc[1] = c1[1].p;
+      h.ldd = c1[0].ld;
+      h.dact = ACT_RELU;
+      h.lap = lap;
+      h.y = y.p;
+      h.dz[0] = dz1[0].p;
+      h.dz[1] = dz1[1].p;
+      h.lddz = dz1[0].ld;
+      h.dq[0] = dq[0].p;
+      h.dq[1] = dq[1].p;
+      h.loss_part = qloss_part;
+      h.prio = prio.p;
+      pg.add(op, {c1[0].id, c1[1].id, q[0]->layers[2].res, q[1]->layers[2].res, y.id},
+             {dz1[0].id, dz1[1].id, dq[0].id, dq[1].id, prio.id, qloss_id = next_id++});
+    }
+    if (lap) {
+      Op op{};
+      op.kind = OP_PRIORITY;
+      op.prio.priority = replay->priority;
+      op.prio.ind = ind;
+      op.prio.p = prio.p;
+      op.prio.B = B;
+      op.prio.max_priority = replay->maxp_d;
+      op.wg_count = 1;
+      pg.add(op, {prio.id, ind_id, bsum_id}, {R_PRIO, R_MAXP});
+    }
+    for (int n = 0; n < 2; ++n) {
+      Net& Q = *q[n];
+      dw(pg, Q.layers[2], dq[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
+      View d0 = dx(pg, {{dz1[n], &Q.layers[1], 0}}, H, B, ACT_RELU, &c0[n]);
+      dw(pg, Q.layers[1], dz1[n], {c0[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
+      dw(pg, Q.layers[0], d0, {s, act_in}, B, CNT_ADAM_Q, cfg.critic_lr);
+    }
+    ploss_part = nullptr;
+    float* gsq = nullptr;
+    int ngsq = 0;
+    if (policy) {
+      View p0[2], p1[2];
+      for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, a_pi, p0[n], p1[n]);
+      View dzp1[2] = {buf(B, H), buf(B, H)};
+      ploss_part = mem.make<float>((size_t)hw * 4);
+      {
+        Op op = head_op(HEAD_MLP_POLICY, B);
+        HeadArgs& h = op.head;
+        set_head_twin(h, p1[0], p1[1], q[0]->layers[2], q[1]->layers[2]);
+        h.dsrc[0] = p1[0].p;
+        h.dsrc[1] = p1[1].p;
+        h.ldd = p1[0].ld;
+        h.dact = ACT_RELU;
+        h.dz[0] = dzp1[0].p;
+        h.dz[1] = dzp1[1].p;
+        h.lddz = dzp1[0].ld;
+        h.loss_part = ploss_part;
+        std::vector<int> rd{p1[0].id, p1[1].id, q[0]->layers[2].res, q[1]->layers[2].res};
+        if (sac) {
+          h.sac = 1;
+          h.logpi = logpi.p;
+          h.log_alpha = P + (nP - 4);
+          rd.push_back(logpi.id);
+          rd.push_back(R_LA);
+        }
+        pg.add(op, rd, {dzp1[0].id, dzp1[1].id, ploss_id = next_id++});
+      }
+      View dzp0[2];
+      for (int n = 0; n < 2; ++n) dzp0[n] = dx(pg, {{dzp1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &p0[n]);
+      View dout;
+      if (!sac) {
+        dout = dx(pg, {{dzp0[0], &q[0]->layers[0], Sp}, {dzp0[1], &q[1]->layers[0], Sp}}, A, B, ACT_TANH, &a_pi);
+      } else {
+        View da = dx(pg, {{dzp0[0], &q[0]->layers[0], Sp}, {dzp0[1], &q[1]->layers[0], Sp}}, A, B, ACT_NONE,
+                     nullptr);
+        dout = buf(B, 2 * A);
+        Op op{};
+        op.kind = OP_SAC_ACTOR_BWD;
+        SacActorArgs& a = op.sac;
+        a.out = raw.p;
+        a.ldo = raw.ld;
+        a.A = A;
+        a.rows = B;
+        a.eps2 = eps2.p;
+        a.ldeps = eps2.ld;
+        a.min_log_std = cfg.min_log_std;
+        a.max_log_std = cfg.max_log_std;
+        a.mean_off = 0;
+        a.ls_off = A;
+        a.da = da.p;
+        a.ldda = da.ld;
+        a.dout = dout.p;
+        a.lddout = dout.ld;
+        a.log_alpha = P + (nP - 4);
+        a.inv_b = 1.f / (float)B;
+        op.wg_count = cdiv(B, kThreads);
+        pg.add(op, {raw.id, eps2.id, da.id, R_LA}, {dout.id});
+      }
+      if (!sac) {
+        // per-tile grad-square partials for norm/policy (rl/nn/utils.py:13-19)
+        for (auto& L : pi.layers) ngsq += cdiv(L.out, kTile) * cdiv(L.K, kTile) + cdiv(L.out, kTile);
+        gsq = mem.make<float>(ngsq);
+      }
+      std::vector<int> tens;
+      float* gp = gsq;
+      auto gsq_for = [&](const Layer& L, int t_w, int t_b) -> std::pair<float*, float*> {
+        if (!gsq) return {nullptr, nullptr};
+        int nw = cdiv(L.out, kTile) * cdiv(L.K, kTile), nb = cdiv(L.out, kTile);
+        float* w = gp;
+        float* b = gp + nw;
+        gp += nw + nb;
+        for (int i = 0; i < nw; ++i) tens.push_back(t_w);
+        for (int i = 0; i < nb; ++i) tens.push_back(t_b);
+        return {w, b};
+      };
+      // actor backward: tensors in parameters() order mlp.0.w, mlp.0.b, mlp.2.w, ...
+      auto g0 = gsq_for(pi.layers[0], 0, 1);
+      auto g1 = gsq_for(pi.layers[1], 2, 3);
+      auto g2 = gsq_for(pi.layers[2], 4, 5);
+      View h1s = h1.sub(0, B), h0s = h0.sub(0, B);
+      View d1 = dx(pg, {{dout, &pi.layers[2], 0}}, H, B, ACT_RELU, &h1s);
+      dw(pg, pi.layers[2], dout, {h1s}, B, CNT_ADAM_PI, cfg.policy_lr, g2.first, g2.second);
+      View d0 = dx(pg, {{d1, &pi.layers[1], 0}}, H, B, ACT_RELU, &h0s);
+      dw(pg, pi.layers[1], d1, {h0s}, B, CNT_ADAM_PI, cfg.policy_lr, g1.first, g1.second);
+      dw(pg, pi.layers[0], d0, {s}, B, CNT_ADAM_PI, cfg.policy_lr, g0.first, g0.second);
+      if (gsq) {
+        gsq_tensor_d = mem.make<int>(tens.size());
+        HIPCHK(hipMemcpy(gsq_tensor_d, tens.data(), tens.size() * 4, hipMemcpyHostToDevice));
+        gsq_id = next_id++;
+      }
+    }
+    // Polyak (td3.py:194-204 on policy steps incl. aliased policy Q2; sac.py:243-249 every step)
+    if (!sac && policy) {
+      flat(pg, OP_POLYAK, *tq[0], q[0], cfg.tau, false);
+      flat(pg, OP_POLYAK, *tq[1], q[1], cfg.tau, false);
+      flat(pg, OP_POLYAK, pi, nullptr, cfg.tau, true);
+    }
+    if (sac) {
+      flat(pg, OP_POLYAK, *tq[0], q[0], cfg.tau, false);
+      flat(pg, OP_POLYAK, *tq[1], q[1], cfg.tau, false);
+    }
+    // step end
+    Op op = step_end_op();
+    StepEndArgs& a = op.end;
+    std::vector<int> rd{qloss_id};
+    if (policy) rd.push_back(ploss_id);
+    if (!sac) {  // [train/q_fn, train/policy, norm/policy]
+      info_sum(a, 0, qloss_part, hw * 4, 1, (lap ? 1.f : 0.5f) / (float)B);
+      if (policy) {
+        info_sum(a, 1, ploss_part, hw, 4, -1.f / (float)B);
+        a.kind[2] = INFO_GNORM;
+        a.gsq = gsq;
+        a.ngsq = ngsq;
+        a.gsq_tensor = gsq_tensor_d;
+        for (auto& L : pi.layers) rd.push_back(L.res);
+      } else {
+        a.kind[1] = INFO_NAN;
+        a.kind[2] = INFO_NAN;
+      }
+      a.ninfo = 3;
+    } else if (cfg.tmp < 0.f) {  // [train/q_fn, tmp, norm/tmp, train/policy, train/tmp, entropy]
+      info_sum(a, 0, qloss_part, hw * 4, 1, 0.5f / (float)B);
+      a.kind[1] = INFO_SAC_TMP;
+      a.kind[2] = INFO_SAC_NTMP;
+      info_sum(a, 3, ploss_part, hw, 4, 1.f / (float)B);
+      a.kind[3] = INFO_SAC_POL;
+      a.kind[4] = INFO_SAC_TMPL;
+      a.kind[5] = INFO_SAC_ENT;
+      a.ninfo = 6;
+      a.log_alpha = P + (nP - 4);
+      a.la_m = P + nP + (nP - 4);
+      a.la_v = P + 2 * nP + (nP - 4);
+      a.la_t = &ctrl->la_t;
+      a.la_lr = cfg.policy_lr;
+      a.target_entropy = -(float)A;
+      a.logpi_part = ploss_part;
+      a.nlogpi = hw;
+    } else {  // fixed temperature: [train/q_fn, train/policy, entropy]
+      info_sum(a, 0, qloss_part, hw * 4, 1, 0.5f / (float)B);
+      info_sum(a, 1, ploss_part, hw, 4, 1.f / (float)B);
+      a.kind[2] = INFO_SAC_ENT;
+      a.ninfo = 3;
+      a.logpi_part = ploss_part;
+      a.nlogpi = hw;
+    }
+    std::vector<int> cn{CNT_ADAM_Q, 3, CNT_RNG, CNT_TAPE};
+    if (policy) cn.push_back(CNT_ADAM_PI);
+    add_step_end(pg, op, rd, cn);
+  }
+  int* gsq_tensor_d = nullptr;
+  int gsq_id = -1;
+
+  // ---------------------------------------------------------------- graphs
+  Graph capture(Prog& pg) {
+    auto levels = pg.schedule();
+    Graph G;
+    size_t total = 0;
+    for (auto& lv : levels) {
+      G.off.push_back((int)total);
+      G.nops.push_back((int)lv.size());
+      int wg = 0;
+      for (auto& op : lv) wg += op.wg_count;
+      G.nwg.push_back(wg);
+      total += lv.size();
+    }
+    std::vector<Op> flat_ops;
+    flat_ops.reserve(total);
+    for (auto& lv : levels)
+      for (auto& op : lv) flat_ops.push_back(op);
+    G.d_ops = mem.make<Op>(total);
+    HIPCHK(hipMemcpy(G.d_ops, flat_ops.data(), total * sizeof(Op), hipMemcpyHostToDevice));
+    HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    for (size_t l = 0; l < levels.size(); ++l) {
+      hipError_t e = launch_level(G.d_ops + G.off[l], G.nops[l], G.nwg[l], stream);
+      if (e != hipSuccess) {
+        hipGraph_t tmp;
+        (void)hipStreamEndCapture(stream, &tmp);
+        throw Error{RLE_EHIP, std::string("launch during capture: ") + hipGetErrorString(e)};
+      }
+    }
+    HIPCHK(hipStreamEndCapture(stream, &G.g));
+    HIPCHK(hipGraphInstantiate(&G.x, G.g, nullptr, nullptr, 0));
+    return G;
+  }
+
+  void alloc_step_buffers() {
+    ss = buf(2 * B, S);
+    act_in = buf(B, A);
+    rw = buf(B, 1);
+    nd = buf(B, 1);
+    eps = buf(B, A);
+    eps2 = buf(B, A);
+    ind = mem.make<long long>(B);
+    u_buf = mem.make<float>(B);
+    ind_id = next_id++;
+    bsum_id = next_id++;
+  }
+
+  void ensure_tapes(long long n) {
+    if (n <= tape_cap) return;
+    // tapes are referenced by captured graphs: allocate once at a generous size
+    REQUIRE(!built || n <= tape_cap, "tape larger than the capacity fixed at first use");
+    tape_cap = std::max<long long>(n, 1024);
+    t_u = mem.make<float>((size_t)tape_cap * B);
+    t_eps = mem.make<float>((size_t)tape_cap * B * A);
+    t_eps2 = mem.make<float>((size_t)tape_cap * B * A);
+    t_ind = mem.make<long long>((size_t)tape_cap * B);
+  }
+
+  void build() {
+    REQUIRE(replay, "no replay bound");
+    ensure_tapes(1024);
+    Prog p1, p2;
+    if (algo == RLE_TD7) {
+      build_td7(p1, true);
+      g_policy = capture(p1);
+      build_td7(p2, false);
+      g_plain = capture(p2);
+      Prog ph;
+      build_td7_hard(ph);
+      g_hard = capture(ph);
+    } else if (algo == RLE_TD3) {
+      build_mlp(p1, true);
+      g_policy = capture(p1);
+      build_mlp(p2, false);
+      g_plain = capture(p2);
+    } else {
+      build_mlp(p1, true);
+      g_policy = capture(p1);
+      g_plain = g_policy;
+    }
+    built = true;
+  }
+
+  // ---------------------------------------------------------------- run
+  void step(int n, float* info_out) {
+    REQUIRE(replay, "no replay bound");
+    REQUIRE(replay->size > 0, "replay is empty");
+    if (!built) build();
+    const int pf = std::max(1, cfg.policy_freq);
+    int done = 0;
+    while (done < n) {
+      const int chunk = std::min(n - done, info_cap);
+      int zero = 0;
+      HIPCHK(hipMemcpyAsync(&ctrl->info_slot, &zero, sizeof(int), hipMemcpyHostToDevice, stream));
+      for (int i = 0; i < chunk; ++i) {
+        if (ctrl_tape_mode_host) {
+          REQUIRE(tape_left > 0, "tape exhausted");
+          --tape_left;
+        }
+        if (algo == RLE_TD7) {
+          ++n_runs;  // td7.py:295 (increment first)
+          HIPCHK(hipGraphLaunch((n_runs % pf == 0) ? g_policy.x : g_plain.x, stream));
+          if (n_runs % std::max(1, cfg.target_update_rate) == 0) HIPCHK(hipGraphLaunch(g_hard.x, stream));
+        } else if (algo == RLE_TD3) {
+          HIPCHK(hipGraphLaunch((n_runs % pf == 0) ? g_policy.x : g_plain.x, stream));  // td3.py:231
+          ++n_runs;
+        } else {
+          HIPCHK(hipGraphLaunch(g_policy.x, stream));
+          ++n_runs;
+        }
+      }
+      if (info_out) {
+        HIPCHK(hipMemcpyAsync(info_out + (size_t)done * kInfoMax, info, (size_t)chunk * kInfoMax * sizeof(float),
+                              hipMemcpyDeviceToHost, stream));
+      }
+      HIPCHK(hipStreamSynchronize(stream));
+      done += chunk;
+    }
+  }
+  int ctrl_tape_mode_host = 0;
+};
+
+}  // namespace rle
+
+// ====================================================================== C ABI
+
+using rle::Engine;
+using rle::Error;
+using rle::Replay;
+
+struct rle_replay {
+  Replay r;
+};
+struct rle_engine {
+  std::unique_ptr<Engine> e;
+};
+
+template <class F>
+static int guard(F&& f) {
+  try {
+    f();
+    return RLE_OK;
+  } catch (const Error& err) {
+    rle::g_err = err.msg;
+    return err.code;
+  } catch (const std::exception& ex) {
+    rle::g_err = ex.what();
+    return RLE_ESTATE;
+  }
+}
+
+extern "C" {
+
+const char* rle_last_error(void) { return rle::g_err.c_str(); }
+
+int rle_replay_create(int device, long long capacity, int state_dim, int action_dim, int lap, rle_replay** out) {
+  return guard([&] {
+    REQUIRE(out && capacity > 0 && state_dim > 0 && action_dim > 0, "rle_replay_create: bad args");
+    REQUIRE(capacity <= 2048LL * 4096, "rle_replay_create: capacity > 8M transitions");
+    HIPCHK(hipSetDevice(device));
+    auto* h = new rle_replay();
+    Replay& r = h->r;
+    r.device = device;
+    r.cap = capacity;
+    r.S = state_dim;
+    r.Sp = rle::r4(state_dim);
+    r.A = action_dim;
+    r.Ap = rle::r4(action_dim);
+    r.lap = lap ? 1 : 0;
+    try {
+      HIPCHK(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+      r.state = r.mem.make<float>((size_t)capacity * r.Sp);
+      r.next_state = r.mem.make<float>((size_t)capacity * r.Sp);
+      r.action = r.mem.make<float>((size_t)capacity * r.Ap);
+      r.reward = r.mem.make<float>(capacity);
+      r.notdone = r.mem.make<float>(capacity);
+      r.priority = r.mem.make<float>(capacity);
+      r.size_d = r.mem.make<long long>(1);
+      r.maxp_d = r.mem.make<float>(1);
+      const float one = 1.f;  // lap.py:29 max_priority = 1
+      HIPCHK(hipMemcpy(r.maxp_d, &one, 4, hipMemcpyHostToDevice));
+      r.nblk = rle::cdiv(capacity, 4096);
+      r.bsum = r.mem.make<double>(r.nblk);
+      r.maxred_part = r.mem.make<float>(r.maxred_nwg);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int rle_replay_destroy(rle_replay* r) {
+  return guard([&] {
+    if (!r) return;
+    (void)hipStreamSynchronize(r->r.stream);
+    (void)hipStreamDestroy(r->r.stream);
+    delete r;
+  });
+}
+
+int rle_replay_append(rle_replay* h, const float* state, const float* action, const float* reward,
+                      const float* next_state, const float* notdone, long long count) {
+  return guard([&] {
+    REQUIRE(h && count >= 0, "append: bad args");
+    Replay& r = h->r;
+    HIPCHK(hipSetDevice(r.device));
+    long long done = 0;
+    // a chunk never wraps onto itself (rows i and i+cap would race; the later must win)
+    const long long chunk_max = std::min<long long>(65536, r.cap);
+    while (done < count) {
+      const long long c = std::min(chunk_max, count - done);
+      const size_t per = 2 * (size_t)r.Sp + r.Ap + 2;
+      if (c > r.stage_rows) {
+        r.stage = r.mem.make<float>((size_t)c * per);
+        r.stage_rows = c;
+      }
+      std::vector<float> host((size_t)c * per, 0.f);
+      float* hs = host.data();
+      float* hns = hs + (size_t)c * r.Sp;
+      float* ha = hns + (size_t)c * r.Sp;
+      float* hr = ha + (size_t)c * r.Ap;
+      float* hd = hr + c;
+      for (long long i = 0; i < c; ++i) {
+        const long long k = done + i;
+        std::memcpy(hs + i * r.Sp, state + k * r.S, sizeof(float) * r.S);
+        std::memcpy(hns + i * r.Sp, next_state + k * r.S, sizeof(float) * r.S);
+        std::memcpy(ha + i * r.Ap, action + k * r.A, sizeof(float) * r.A);
+        hr[i] = reward[k];
+        hd[i] = notdone[k];
+      }
+      float* ds = r.stage;
+      HIPCHK(hipMemcpyAsync(ds, hs, host.size() * sizeof(float), hipMemcpyHostToDevice, r.stream));
+      HIPCHK(rle::launch_append(r.state, r.next_state, r.action, r.reward, r.notdone, r.priority, ds,
+                                ds + (size_t)c * r.Sp, ds + 2 * (size_t)c * r.Sp, ds + 2 * (size_t)c * r.Sp + c * r.Ap,
+                                ds + 2 * (size_t)c * r.Sp + c * r.Ap + c, r.ptr, r.cap, (int)c, r.Sp, r.Ap, r.maxp_d,
+                                r.lap, r.stream));
+      r.ptr = (r.ptr + c) % r.cap;
+      r.size = std::min(r.size + c, r.cap);
+      HIPCHK(hipMemcpyAsync(r.size_d, &r.size, sizeof(long long), hipMemcpyHostToDevice, r.stream));
+      HIPCHK(hipStreamSynchronize(r.stream));
+      done += c;
+    }
+  });
+}
+
+int rle_replay_state(rle_replay* h, long long* ptr, long long* size, float* max_priority) {
+  return guard([&] {
+    REQUIRE(h, "state: null");
+    Replay& r = h->r;
+    if (ptr) *ptr = r.ptr;
+    if (size) *size = r.size;
+    if (max_priority) {
+      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipMemcpy(max_priority, r.maxp_d, 4, hipMemcpyDeviceToHost));
+    }
+  });
+}
+
+int rle_replay_fill_random(rle_replay* h, long long count, unsigned long long seed) {
+  return guard([&] {
+    Replay& r = h->r;
+    REQUIRE(count > 0 && count <= r.cap, "fill: bad count");
+    HIPCHK(hipSetDevice(r.device));
+    HIPCHK(rle::launch_fill(r.state, r.next_state, r.action, r.reward, r.notdone, r.priority, count, r.S, r.Sp, r.A,
+                            r.Ap, seed, r.stream));
+    r.size = std::max(r.size, count);
+    r.ptr = count % r.cap;
+    HIPCHK(hipMemcpyAsync(r.size_d, &r.size, sizeof(long long), hipMemcpyHostToDevice, r.stream));
+    HIPCHK(hipStreamSynchronize(r.stream));
+  });
+}
+
+int rle_replay_get_priority(rle_replay* h, float* out, long long n) {
+  return guard([&] {
+    REQUIRE(n <= h->r.cap, "get_priority: n > capacity");
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, h->r.priority, n * 4, hipMemcpyDeviceToHost));
+  });
+}
+
+int rle_replay_set_priority(rle_replay* h, const float* p, long long n, float max_priority) {
+  return guard([&] {
+    REQUIRE(n <= h->r.cap, "set_priority: n > capacity");
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(h->r.priority, p, n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->r.maxp_d, &max_priority, 4, hipMemcpyHostToDevice));
+  });
+}
+
+// Runs a small op program eagerly on the replay's stream (test hooks).
+static void run_eager(Replay& r, rle::DevMem& tmp, std::vector<std::vector<rle::Op>> levels) {
+  for (auto& lv : levels) {
+    int wg = 0;
+    for (auto& op : lv) {
+      op.wg_begin = wg;
+      wg += op.wg_count;
+    }
+    rle::Op* d = tmp.make<rle::Op>(lv.size());
+    HIPCHK(hipMemcpy(d, lv.data(), lv.size() * sizeof(rle::Op), hipMemcpyHostToDevice));
+    HIPCHK(rle::launch_level(d, (int)lv.size(), wg, r.stream));
+  }
+  HIPCHK(hipStreamSynchronize(r.stream));
+}
+
+int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* ind_out) {
+  return guard([&] {
+    Replay& r = h->r;
+    REQUIRE(n > 0 && r.size > 0, "sample_indices: bad args / empty replay");
+    HIPCHK(hipSetDevice(r.device));
+    rle::DevMem tmp;
+    rle::SampleArgs s{};
+    s.state = r.state;
+    s.next_state = r.next_state;
+    s.action = r.action;
+    s.reward = r.reward;
+    s.notdone = r.notdone;
+    s.priority = r.priority;
+    s.S = r.S;
+    s.Sp = r.Sp;
+    s.A = r.A;
+    s.Ap = r.Ap;
+    s.size = r.size_d;
+    s.lap = r.lap;
+    s.B = n;
+    s.bsum = r.bsum;
+    s.nblk = r.nblk;
+    s.ss = tmp.make<float>((size_t)2 * n * r.Sp);
+    s.ldss = r.Sp;
+    s.a = tmp.make<float>((size_t)n * r.Ap);
+    s.lda = r.Ap;
+    s.r = tmp.make<float>(n);
+    s.nd = tmp.make<float>(n);
+    long long* dind = tmp.make<long long>(n);
+    s.ind = dind;
+    s.u_out = tmp.make<float>(n);
+    s.eps = tmp.make<float>((size_t)n * r.Ap);
+    s.ldeps = r.Ap;
+    long long* cnt = tmp.make<long long>(2);
+    int* mode = tmp.make<int>(1);
+    const int one = 1;
+    HIPCHK(hipMemcpy(mode, &one, 4, hipMemcpyHostToDevice));
+    s.ctrl_rng = cnt;
+    s.tape_mode = mode;
+    s.tape_pos = cnt + 1;
+    float* du = tmp.make<float>(n);
+    HIPCHK(hipMemcpy(du, u, n * 4, hipMemcpyHostToDevice));
+    s.tape_u = du;
+    s.tape_eps = tmp.make<float>((size_t)n * r.A);
+    std::vector<std::vector<rle::Op>> lv;
+    if (r.lap) {
+      rle::Op a{};
+      a.kind = rle::OP_SAMPLE_REDUCE;
+      a.sample = s;
+      a.wg_count = r.nblk;
+      lv.push_back({a});
+    }
+    rle::Op b{};
+    b.kind = rle::OP_SAMPLE_GATHER;
+    b.sample = s;
+    b.wg_count = n;
+    lv.push_back({b});
+    run_eager(r, tmp, lv);
+    HIPCHK(hipMemcpy(ind_out, dind, n * sizeof(long long), hipMemcpyDeviceToHost));
+  });
+}
+
+int rle_replay_update_priority(rle_replay* h, int n, const long long* ind, const float* p) {
+  return guard([&] {
+    Replay& r = h->r;
+    REQUIRE(n > 0 && n <= 1024, "update_priority: 0 < n <= 1024");
+    rle::DevMem tmp;
+    long long* di = tmp.make<long long>(n);
+    float* dp = tmp.make<float>(n);
+    HIPCHK(hipMemcpy(di, ind, n * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dp, p, n * 4, hipMemcpyHostToDevice));
+    rle::Op op{};
+    op.kind = rle::OP_PRIORITY;
+    op.prio.priority = r.priority;
+    op.prio.ind = di;
+    op.prio.p = dp;
+    op.prio.B = n;
+    op.prio.max_priority = r.maxp_d;
+    op.wg_count = 1;
+    run_eager(r, tmp, {{op}});
+  });
+}
+
+int rle_replay_reset_max_priority(rle_replay* h) {
+  return guard([&] {
+    Replay& r = h->r;
+    REQUIRE(r.size > 0, "reset_max_priority: empty");
+    rle::DevMem tmp;
+    rle::Op a{};
+    a.kind = rle::OP_MAXRED;
+    a.flat.src = r.priority;
+    a.flat.size = r.size_d;
+    a.flat.partial = r.maxred_part;
+    a.flat.nwg = r.maxred_nwg;
+    a.flat.stage = 0;
+    a.wg_count = r.maxred_nwg;
+    rle::Op b = a;
+    b.flat.stage = 1;
+    b.flat.out = r.maxp_d;
+    b.wg_count = 1;
+    run_eager(r, tmp, {{a}, {b}});
+  });
+}
+
+int rle_replay_gather(rle_replay* h, int n, const long long* ind, float* state, float* action, float* reward,
+                      float* next_state, float* notdone) {
+  return guard([&] {
+    Replay& r = h->r;
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<float> row(r.Sp);
+    for (int i = 0; i < n; ++i) {
+      const long long k = ind[i];
+      REQUIRE(k >= 0 && k < r.cap, "gather: index out of range");
+      if (state) {
+        HIPCHK(hipMemcpy(row.data(), r.state + k * r.Sp, r.Sp * 4, hipMemcpyDeviceToHost));
+        std::memcpy(state + (size_t)i * r.S, row.data(), r.S * 4);
+      }
+      if (next_state) {
+        HIPCHK(hipMemcpy(row.data(), r.next_state + k * r.Sp, r.Sp * 4, hipMemcpyDeviceToHost));
+        std::memcpy(next_state + (size_t)i * r.S, row.data(), r.S * 4);
+      }
+      if (action) {
+        HIPCHK(hipMemcpy(row.data(), r.action + k * r.Ap, r.Ap * 4, hipMemcpyDeviceToHost));
+        std::memcpy(action + (size_t)i * r.A, row.data(), r.A * 4);
+      }
+      if (reward) HIPCHK(hipMemcpy(reward + i, r.reward + k, 4, hipMemcpyDeviceToHost));
+      if (notdone) HIPCHK(hipMemcpy(notdone + i, r.notdone + k, 4, hipMemcpyDeviceToHost));
+    }
+  });
+}
+
+int rle_create(const rle_config* cfg, rle_engine** out) {
+  return guard([&] {
+    REQUIRE(cfg && out, "create: null");
+    REQUIRE(cfg->algo >= 0 && cfg->algo <= 2, "create: bad algo");
+    REQUIRE(cfg->batch > 0 && cfg->batch % 4 == 0 && cfg->batch <= 1024, "create: batch must be a multiple of 4, <= 1024");
+    REQUIRE(cfg->state_dim > 0 && cfg->action_dim > 0 && cfg->hidden > 0 && cfg->hidden % 4 == 0,
+            "create: bad dims (hidden must be a multiple of 4)");
+    HIPCHK(hipSetDevice(cfg->device));
+    auto h = std::make_unique<rle_engine>();
+    h->e = std::make_unique<Engine>();
+    Engine& e = *h->e;
+    e.cfg = *cfg;
+    e.algo = cfg->algo;
+    e.S = cfg->state_dim;
+    e.Sp = rle::r4(e.S);
+    e.A = cfg->action_dim;
+    e.Ap = rle::r4(e.A);
+    e.H = cfg->hidden;
+    e.Hp = rle::r4(e.H);
+    e.B = cfg->batch;
+    HIPCHK(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
+    if (e.algo == RLE_TD7) {
+      for (const char* n : {"encoder", "fixed_encoder", "fixed_encoder_target"}) e.nets.push_back(e.make_net(n, "sale_enc"));
+      e.nets.push_back(e.make_net("policy", "sale_actor"));
+      for (const char* n : {"q1", "q2", "target_q1", "target_q2"}) e.nets.push_back(e.make_net(n, "sale_critic"));
+    } else {
+      e.nets.push_back(e.make_net("policy", "mlp_actor"));
+      for (const char* n : {"q1", "q2", "target_q1", "target_q2"}) e.nets.push_back(e.make_net(n, "mlp_critic"));
+    }
+    e.layout_params();
+    e.ctrl = e.mem.make<rle::Ctrl>(1);
+    rle::Ctrl c{};
+    c.vmax_key = rle::host_fkey(-1e8f);  // td7.py:84-87
+    c.vmin_key = rle::host_fkey(1e8f);
+    c.vt[0] = c.vt[1] = 0.f;
+    c.max_priority = 1.f;
+    HIPCHK(hipMemcpy(e.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
+    if (e.algo == RLE_SAC) {
+      const float la = cfg->tmp < 0.f ? 0.f : std::log(cfg->tmp);  // sac.py:56-60
+      HIPCHK(hipMemcpy(e.P + (e.nP - 4), &la, 4, hipMemcpyHostToDevice));
+    }
+    e.info = e.mem.make<float>((size_t)e.info_cap * rle::kInfoMax);
+    e.alloc_step_buffers();
+    *out = h.release();
+  });
+}
+
+int rle_destroy(rle_engine* h) {
+  return guard([&] {
+    if (!h) return;
+    Engine& e = *h->e;
+    (void)hipStreamSynchronize(e.stream);
+    for (rle::Graph* g : {&e.g_policy, &e.g_plain, &e.g_hard}) {
+      if (g->x && !(g == &e.g_plain && e.algo == RLE_SAC)) (void)hipGraphExecDestroy(g->x);
+      if (g->g && !(g == &e.g_plain && e.algo == RLE_SAC)) (void)hipGraphDestroy(g->g);
+    }
+    for (auto& kv : e.act_graphs) {
+      if (kv.second.first.x) (void)hipGraphExecDestroy(kv.second.first.x);
+      if (kv.second.first.g) (void)hipGraphDestroy(kv.second.first.g);
+    }
+    (void)hipStreamDestroy(e.stream);
+    delete h;
+  });
+}
+
+int rle_bind_replay(rle_engine* h, rle_replay* r) {
+  return guard([&] {
+    Engine& e = *h->e;
+    REQUIRE(r, "bind: null replay");
+    REQUIRE(r->r.S == e.S && r->r.A == e.A, "bind: replay dims differ from agent dims");
+    if (e.replay == &r->r) return;
+    REQUIRE(!e.built, "bind: engine already bound to another replay");
+    e.replay = &r->r;
+  });
+}
+
+int rle_param_numel(rle_engine* h, const char* net, const char* name, long long* numel) {
+  return guard([&] { *numel = h->e->numel(net, name); });
+}
+int rle_get_param(rle_engine* h, const char* net, const char* name, float* out, long long n) {
+  return guard([&] { h->e->xfer_param(net, name, out, n, false, 0); });
+}
+int rle_set_param(rle_engine* h, const char* net, const char* name, const float* in, long long n) {
+  return guard([&] { h->e->xfer_param(net, name, const_cast<float*>(in), n, true, 0); });
+}
+int rle_get_adam(rle_engine* h, const char* net, const char* name, int which, float* out, long long n) {
+  return guard([&] {
+    REQUIRE(which == 0 || which == 1, "adam: which in {0,1}");
+    h->e->xfer_param(net, name, out, n, false, 1 + which);
+  });
+}
+int rle_set_adam(rle_engine* h, const char* net, const char* name, int which, const float* in, long long n) {
+  return guard([&] {
+    REQUIRE(which == 0 || which == 1, "adam: which in {0,1}");
+    h->e->xfer_param(net, name, const_cast<float*>(in), n, true, 1 + which);
+  });
+}
+
+int rle_get_counters(rle_engine* h, long long* out6) {
+  return guard([&] {
+    Engine& e = *h->e;
+    HIPCHK(hipStreamSynchronize(e.stream));
+    rle::Ctrl c;
+    HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 5; ++i) out6[i] = c.counters[i];
+    out6[3] = e.n_runs;
+    out6[5] = c.la_t;
+  });
+}
+
+int rle_set_counters(rle_engine* h, const long long* in6) {
+  return guard([&] {
+    Engine& e = *h->e;
+    HIPCHK(hipStreamSynchronize(e.stream));
+    rle::Ctrl c;
+    HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 5; ++i) c.counters[i] = in6[i];
+    c.la_t = in6[5];
+    e.n_runs = in6[3];
+    HIPCHK(hipMemcpy(e.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
+  });
+}
+
+int rle_get_value_bounds(rle_engine* h, float* out4) {
+  return guard([&] {
+    Engine& e = *h->e;
+    HIPCHK(hipStreamSynchronize(e.stream));
+    rle::Ctrl c;
+    HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    out4[0] = rle::host_unkey(c.vmax_key);
+    out4[1] = rle::host_unkey(c.vmin_key);
+    out4[2] = c.vt[0];
+    out4[3] = c.vt[1];
+  });
+}
+
+int rle_set_value_bounds(rle_engine* h, const float* in4) {
+  return guard([&] {
+    Engine& e = *h->e;
+    HIPCHK(hipStreamSynchronize(e.stream));
+    rle::Ctrl c;
+    HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    c.vmax_key = rle::host_fkey(in4[0]);
+    c.vmin_key = rle::host_fkey(in4[1]);
+    c.vt[0] = in4[2];
+    c.vt[1] = in4[3];
+    HIPCHK(hipMemcpy(e.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
+  });
+}
+
+int rle_step(rle_engine* h, int n_steps, float* info_out) {
+  return guard([&] {
+    REQUIRE(n_steps >= 0, "step: n < 0");
+    Engine& e = *h->e;
+    HIPCHK(hipSetDevice(e.cfg.device));
+    if (e.replay) HIPCHK(hipStreamSynchronize(e.replay->stream));
+    e.step(n_steps, info_out);
+  });
+}
+
+int rle_set_tapes(rle_engine* h, int n, const float* u, const float* eps, const float* eps_pi, const long long* ind) {
+  return guard([&] {
+    Engine& e = *h->e;
+    HIPCHK(hipStreamSynchronize(e.stream));
+    int mode = 0;
+    if (n > 0) {
+      REQUIRE(n <= 1024, "set_tapes: at most 1024 steps per tape");
+      e.ensure_tapes(n);
+      const size_t nb = (size_t)n * e.B, na = nb * e.A;
+      if (u) HIPCHK(hipMemcpy(e.t_u, u, nb * 4, hipMemcpyHostToDevice));
+      if (eps) HIPCHK(hipMemcpy(e.t_eps, eps, na * 4, hipMemcpyHostToDevice));
+      if (eps_pi) HIPCHK(hipMemcpy(e.t_eps2, eps_pi, na * 4, hipMemcpyHostToDevice));
+      if (ind) HIPCHK(hipMemcpy(e.t_ind, ind, nb * 8, hipMemcpyHostToDevice));
+      REQUIRE(u || ind, "set_tapes: need u or ind");
+      mode = ind ? 2 : 1;
+    }
+    rle::Ctrl c;
+    HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    c.tape_mode = mode;
+    c.counters[5] = 0;
+    HIPCHK(hipMemcpy(e.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
+    e.ctrl_tape_mode_host = mode;
+    e.tape_left = n;
+  });
+}
+
+int rle_last_indices(rle_engine* h, long long* out) {
+  return guard([&] {
+    Engine& e = *h->e;
+    HIPCHK(hipStreamSynchronize(e.stream));
+    HIPCHK(hipMemcpy(out, e.ind, e.B * sizeof(long long), hipMemcpyDeviceToHost));
+  });
+}
+
+int rle_act(rle_engine* h, const float* obs, int n, float* out) {
+  return guard([&] {
+    Engine& e = *h->e;
+    REQUIRE(n > 0 && n <= 1024, "act: 0 < n <= 1024");
+    HIPCHK(hipSetDevice(e.cfg.device));
+    auto it = e.act_graphs.find(n);
+    if (it == e.act_graphs.end()) {
+      rle::Prog pg;
+      rle::View in = e.buf(n, e.S);
+      rle::View o;
+      if (e.algo == RLE_TD7) {  // td7.py:158-162
+        rle::Net& fe = e.net("fixed_encoder");
+        rle::Net& pi = e.net("policy");
+        rle::View h1 = e.fwd(pg, fe.layers[0], {{in}}, n, rle::ACT_ELU, nullptr, false);
+        rle::View h2 = e.fwd(pg, fe.layers[1], {{h1}}, n, rle::ACT_ELU, nullptr, false);
+        rle::View zs = e.fwd(pg, fe.layers[2], {{h2}}, n, rle::ACT_NONE, nullptr, true);
+        rle::View p0 = e.fwd(pg, pi.layers[0], {{in}}, n, rle::ACT_NONE, nullptr, true);
+        rle::View p1 = e.fwd(pg, pi.layers[1], {{p0}, {zs}}, n, rle::ACT_RELU, nullptr, false);
+        rle::View p2 = e.fwd(pg, pi.layers[2], {{p1}}, n, rle::ACT_RELU, nullptr, false);
+        o = e.fwd(pg, pi.layers[3], {{p2}}, n, rle::ACT_TANH, nullptr, false);
+      } else {
+        rle::Net& pi = e.net("policy");
+        rle::View h0 = e.fwd(pg, pi.layers[0], {{in}}, n, rle::ACT_RELU, nullptr, false);
+        rle::View h1 = e.fwd(pg, pi.layers[1], {{h0}}, n, rle::ACT_RELU, nullptr, false);
+        o = e.fwd(pg, pi.layers[2], {{h1}}, n, rle::ACT_NONE, nullptr, false);
+      }
+      rle::Graph G = e.capture(pg);
+      it = e.act_graphs.emplace(n, std::make_pair(G, o)).first;
+      e.act_inputs[n] = in;
+    }
+    rle::View in = e.act_inputs[n];
+    rle::View o = it->second.second;
+    const int W = e.algo == RLE_SAC ? 2 * e.A : e.A;
+    std::vector<float> pad((size_t)n * in.ld, 0.f);
+    for (int i = 0; i < n; ++i) std::memcpy(&pad[(size_t)i * in.ld], obs + (size_t)i * e.S, e.S * 4);
+    HIPCHK(hipMemcpyAsync(in.p, pad.data(), pad.size() * 4, hipMemcpyHostToDevice, e.stream));
+    HIPCHK(hipGraphLaunch(it->second.first.x, e.stream));
+    std::vector<float> res((size_t)n * o.ld);
+    HIPCHK(hipMemcpyAsync(res.data(), o.p, res.size() * 4, hipMemcpyDeviceToHost, e.stream));
+    HIPCHK(hipStreamSynchronize(e.stream));
+    for (int i = 0; i < n; ++i) std::memcpy(out + (size_t)i * W, &res[(size_t)i * o.ld], W * 4);
+  });
+}
+
+int rle_graph_stats(rle_engine* h, int* lp, int* lplain) {
+  return guard([&] {
+    Engine& e = *h->e;
+    if (!e.built) e.build();
+    if (lp) *lp = e.g_policy.levels();
+    if (lplain) *lplain = e.g_plain.levels();
+  });
+}
+
+int rle_copy_state(rle_engine* dst, rle_engine* src) {
+  return guard([&] {
+    Engine& d = *dst->e;
+    Engine& s = *src->e;
+    REQUIRE(d.nP == s.nP && d.algo == s.algo, "copy_state: config mismatch");
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(d.P, s.P, 3 * d.nP * sizeof(float), hipMemcpyDeviceToDevice));
+    rle::Ctrl c;
+    HIPCHK(hipMemcpy(&c, s.ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(d.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
+    d.n_runs = s.n_runs;
+  });
+}
+
+int rle_synchronize(rle_engine* h) {
+  return guard([&] { HIPCHK(hipStreamSynchronize(h->e->stream)); });
+}
+
+}  // extern "C"

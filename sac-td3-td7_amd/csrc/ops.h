@@ -1,0 +1,245 @@
+// Op descriptors shared by the host program builder (engine.cpp) and the
+// device dispatch kernel (kernels.hip).  Plain POD; one level of a step graph
+// is an array of Op, launched as ONE kernel whose workgroups are partitioned
+// over the ops by Op::wg_begin.
+#pragma once
+#include <stdint.h>
+
+namespace rle {
+
+constexpr int kThreads = 256;   // 4 waves per workgroup, every op kind
+constexpr int kTile = 16;       // GEMM output tile edge (v_mfma_f32_16x16x4_f32)
+constexpr int kMaxSeg = 4;
+constexpr int kInfoMax = 8;     // floats per step in the info ring
+
+enum OpKind : int {
+  OP_GEMM = 1,
+  OP_NORMBWD = 2,
+  OP_SAMPLE_REDUCE = 3,
+  OP_SAMPLE_GATHER = 4,
+  OP_HEAD = 5,
+  OP_PRIORITY = 6,
+  OP_SAC_ACTOR = 7,
+  OP_SAC_ACTOR_BWD = 8,
+  OP_STEP_END = 9,
+  OP_POLYAK = 10,
+  OP_COPY = 11,
+  OP_MAXRED = 12,
+  OP_CTRL = 13,
+};
+
+// One rectangle of a GEMM operand in (x, r) space: x = output row (operand A)
+// or output column (operand B); r = reduction index.
+//   strided == 0 : elem(x, r) = p[(x - x0) * ld + (r - r0)]   (float4 along r)
+//   strided == 1 : elem(x, r) = p[(r - r0) * ld + (x - x0)]
+// If norm != nullptr the stored values are pre-AvgL1Norm outputs x and the
+// operand value is x / m(row) with m = max(sum_p norm[p*norm_ld + row] / width, 1e-8)
+// (rl/nn/sale.py:11-13), row = (strided ? r - r0 : x - x0) + norm_row0.
+struct Seg {
+  const float* p;
+  const float* norm;
+  int ld;
+  int x0, x1, r0, r1;
+  int strided;
+  int norm_ld, norm_row0, norm_nparts, norm_width;
+  int pad_;
+};
+
+struct Operand {
+  Seg seg[kMaxSeg];
+  int nseg;
+  int pad_[3];
+};
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2, ACT_TANH = 3 };
+
+enum Epi : int {
+  EPI_STORE = 0,   // out = act(acc + bias); optional pre-act store, |y| partials, derivative mask, tanh-noise
+  EPI_ADAM = 1,    // acc is dL/dW (or dL/db on the bias tile column): Adam in place
+  EPI_MSE = 2,     // acc (+bias) = zsa; grad = 2 (zsa - tgt) / n ; loss partial sum of squares
+};
+
+struct AdamArgs {
+  float* w;              // weight base [N][ldw]
+  float* b;              // bias [N] (bias tile column j0 == bias_col)
+  long long mo, vo;      // element offsets of m / v arrays relative to params
+  const long long* t;    // completed optimizer steps (device counter)
+  float lr, beta1, beta2, eps;
+  int ldw, bias_col;     // bias_col = first padded column index of the bias tile (>= R... = padded K)
+  float* gsq;            // optional: per-tile sum of squared grads (weights), [tiles]
+  float* gsq_b;          // optional: per-tile sum of squared grads (bias), [tiles_m]
+};
+
+struct GemmArgs {
+  int M, N, R;           // output rows, output cols (x-extent of B), reduction length
+  int tiles_m, tiles_n;  // tiles_n includes the extra bias tile column for EPI_ADAM
+  int epi;
+  int act;               // forward activation (EPI_STORE)
+  Operand A, B;
+  float* out; int ldo;
+  const float* bias;
+  float* pre; int ldpre;           // pre-activation store (optional)
+  float* norm_out; int norm_ld;    // |y| partials: norm_out[jt * norm_ld + i] (optional)
+  int dact; int lddact;            // derivative mask: out *= act'(dsrc[i][j])
+  const float* dsrc;
+  const float* noise; int ldnoise; int noise_row0; float noise_sigma, noise_clip;  // tanh-noise
+  Seg tgt;                         // EPI_MSE target (normed view)
+  float* loss_part;                // EPI_MSE per-tile partial sums
+  float mse_scale;                 // 2/n
+  int pad_;
+  AdamArgs adam;
+};
+
+// AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise)
+struct NormBwdArgs {
+  const float* g; int ldg;
+  const float* x; int ldx;
+  float* dx; int lddx;
+  int rows, width;
+  const float* norm; int norm_ld, norm_row0, norm_nparts;  // partials for m (x rows)
+};
+
+enum HeadMode : int {
+  HEAD_TD7_TARGET = 0,   // tq_i, y = r + g*clamp(min, vt_min, vt_max)*nd, vmax/vmin
+  HEAD_TD7_LOSS = 1,     // q_i, LAP huber (or MSE), priority, dq, dZ
+  HEAD_TD7_POLICY = 2,   // q_i, loss = -mean(cat), dZ
+  HEAD_MLP_TARGET = 3,   // TD3 / SAC target: y = r + g*(min - alpha*logpi)*nd
+  HEAD_MLP_LOSS = 4,     // MSE (or TD3 LAP per-critic mean), priority
+  HEAD_MLP_POLICY = 5,   // TD3: -mean(min);  SAC: mean(-min + alpha*logpi)
+};
+
+struct HeadArgs {
+  int mode, rows, H, lap;
+  const float* h[2]; int ldh;        // last hidden (post-activation) of each twin
+  const float* dsrc[2]; int ldd;     // derivative source (Z for ELU, H for ReLU)
+  int dact;
+  const float* w[2];                 // last-layer weight row [H]
+  const float* b[2];                 // last-layer bias [1]
+  const float* reward; const float* notdone;
+  float* y;                          // target (written by *_TARGET, read by *_LOSS)
+  float* dz[2]; int lddz;            // grad wrt last hidden pre-activation
+  float* dq[2];                      // grad wrt q (for dW of last layer)
+  float* loss_part;                  // per-workgroup partial sums [wg][4]
+  float* prio;                       // LAP priority out [rows]
+  float gamma;
+  int sac;                           // SAC: alpha term
+  const float* logpi;                // SAC logpi [rows] (target rows / policy rows)
+  const float* log_alpha;            // SAC log alpha scalar
+  int* vmax_key; int* vmin_key;      // TD7 value tracking (ordered-int keys)
+  const float* vt;                   // TD7 [vt_max, vt_min]
+  float inv_b;                       // 1/B (policy loss scale)
+};
+
+struct SampleArgs {
+  // replay
+  const float* state; const float* next_state; const float* action;
+  const float* reward; const float* notdone;
+  float* priority;
+  int S, Sp, A, Ap;
+  const long long* size;             // device replay size
+  int lap, B;
+  double* bsum; int nblk;            // LAP block sums (fp64), 4096 priorities per block
+  // outputs
+  float* ss; int ldss;               // [2B][Sp] rows 0..B-1 state, B..2B-1 next_state
+  float* a; int lda;                 // [B][Ap]
+  float* r; float* nd;               // [B]
+  long long* ind;                    // [B]
+  float* u_out;                      // [B] uniform used (debug)
+  float* eps; int ldeps;             // [B][Ap] target smoothing / SAC next noise
+  float* eps2;                       // [B][Ap] SAC policy noise (optional)
+  // randomness
+  const long long* ctrl_rng;         // step counter for Philox
+  unsigned long long seed;
+  const int* tape_mode;              // 0: Philox, 1: tapes, 2: tapes incl. indices
+  const long long* tape_pos;
+  const float* tape_u; const float* tape_eps; const float* tape_eps2; const long long* tape_ind;
+};
+
+struct PriorityArgs {
+  float* priority; const long long* ind; const float* p; int B;
+  float* max_priority;
+};
+
+struct SacActorArgs {
+  const float* out; int ldo;         // raw head output [rows][2A(p)]: mean | log_std
+  int A, rows;                       // rows = 2B
+  const float* eps; int ldeps; int eps_row_split; const float* eps2;  // rows < split use eps2 (policy), else eps (target)
+  float* act; int ldact;             // tanh action
+  float* logpi;                      // [rows]
+  float min_log_std, max_log_std;
+  int mean_off, ls_off;              // column offsets of mean / log_std blocks
+  // backward
+  const float* da; int ldda;         // grad wrt action from critics [B][Ap]
+  float* dout; int lddout;           // grad wrt raw output [B][2A(p)]
+  const float* log_alpha; float inv_b;
+};
+
+// Step end: info ring row + counter increments + SAC temperature Adam.
+struct StepEndArgs {
+  long long* counters; int cmask;            // counters[i] += 1 for every bit i of cmask
+  int* info_slot; float* info; int info_cap;
+  // up to kInfoMax info values, each = scale * sum(parts[0..n)) (or special)
+  const float* part[kInfoMax]; int npart[kInfoMax]; int stride[kInfoMax]; float scale[kInfoMax];
+  int kind[kInfoMax]; int ninfo;
+  // SAC temperature
+  float* log_alpha; float* la_m; float* la_v; long long* la_t; float la_lr; float target_entropy;
+  const float* logpi_part; int nlogpi; float inv_b;
+  const float* gsq; int ngsq; const int* gsq_tensor;  // TD3 grad norm: per-tile sq sums -> per-tensor sqrt sum
+};
+
+enum InfoKind : int {
+  INFO_SUM = 0,       // scale * sum
+  INFO_NAN = 1,       // NaN (policy loss on a non-policy step)
+  INFO_GNORM = 2,     // sum_t sqrt(sum of tiles of tensor t)
+  INFO_SAC_TMP = 3,   // exp(log_alpha) before update
+  INFO_SAC_NTMP = 4,  // d obj / d log_alpha
+  INFO_SAC_POL = 5,   // policy_obj + tmp_obj
+  INFO_SAC_TMPL = 6,  // tmp_obj
+  INFO_SAC_ENT = 7,   // -mean(logpi)
+};
+
+struct FlatArgs {   // POLYAK / COPY / MAXRED
+  float* dst; const float* src; long long n;
+  float tau, omt; int self_alias;     // self_alias: p <- tau*p + p*(1-tau) (TD3 quirk Q2)
+  const long long* size; float* partial; int nwg; float* out;   // MAXRED
+  int stage;
+};
+
+struct CtrlArgs {   // small control-plane writes (value bounds copy at hard update)
+  const int* vmax_key; const int* vmin_key; float* vt;
+};
+
+struct Op {
+  int kind;
+  int wg_begin;     // first workgroup of this op within its level launch
+  int wg_count;
+  int pad_;
+  union {
+    GemmArgs gemm;
+    NormBwdArgs nb;
+    HeadArgs head;
+    SampleArgs sample;
+    PriorityArgs prio;
+    SacActorArgs sac;
+    StepEndArgs end;
+    FlatArgs flat;
+    CtrlArgs ctrl;
+  };
+};
+
+// Device control block.
+struct Ctrl {
+  long long counters[16];   // [0..3] adam steps per optimizer, [4] rng step, [5] tape pos
+  long long size;           // replay size (mirrors host)
+  int info_slot;
+  int tape_mode;
+  int vmax_key, vmin_key;   // ordered-int keys of value_max / value_min
+  float vt[2];              // value_target_max, value_target_min
+  float max_priority;
+  float log_alpha, la_m, la_v;
+  long long la_t;
+};
+
+enum Counter : int { CNT_ADAM_Q = 0, CNT_ADAM_PI = 1, CNT_ADAM_ENC = 2, CNT_RNG = 4, CNT_TAPE = 5 };
+
+}  // namespace rle

@@ -1,0 +1,301 @@
+"""ctypes binding of ``librle.so`` (C ABI in ``include/rle.h``).
+
+This is the only bridge between the Python mirror of the reference interface
+and the HIP engine.  There is no CPU fallback: if the library is missing or
+fails to load, every engine-backed object raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+RLE_TD7, RLE_TD3, RLE_SAC = 0, 1, 2
+INFO_MAX = 8
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librle.so")
+
+_lib = None
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i64p = ctypes.POINTER(ctypes.c_longlong)
+_vp = ctypes.c_void_p
+_cs = ctypes.c_char_p
+_int = ctypes.c_int
+_ll = ctypes.c_longlong
+
+
+class Config(ctypes.Structure):
+    """Mirror of ``rle_config`` (include/rle.h)."""
+
+    _fields_ = [
+        ("algo", _int), ("state_dim", _int), ("action_dim", _int), ("hidden", _int),
+        ("batch", _int), ("use_lap", _int), ("discount", ctypes.c_float),
+        ("policy_lr", ctypes.c_float), ("critic_lr", ctypes.c_float), ("tau", ctypes.c_float),
+        ("target_policy_noise", ctypes.c_float), ("noise_clip", ctypes.c_float),
+        ("policy_freq", _int), ("target_update_rate", _int), ("min_log_std", ctypes.c_float),
+        ("max_log_std", ctypes.c_float), ("tmp", ctypes.c_float), ("seed", ctypes.c_ulonglong),
+        ("device", _int),
+    ]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "rle_last_error": (_cs, []),
+    "rle_replay_create": (_int, [_int, _ll, _int, _int, _int, ctypes.POINTER(_vp)]),
+    "rle_replay_destroy": (_int, [_vp]),
+    "rle_replay_append": (_int, [_vp, _f32p, _f32p, _f32p, _f32p, _f32p, _ll]),
+    "rle_replay_state": (_int, [_vp, _i64p, _i64p, _f32p]),
+    "rle_replay_fill_random": (_int, [_vp, _ll, ctypes.c_ulonglong]),
+    "rle_replay_get_priority": (_int, [_vp, _f32p, _ll]),
+    "rle_replay_set_priority": (_int, [_vp, _f32p, _ll, ctypes.c_float]),
+    "rle_replay_sample_indices": (_int, [_vp, _int, _f32p, _i64p]),
+    "rle_replay_update_priority": (_int, [_vp, _int, _i64p, _f32p]),
+    "rle_replay_reset_max_priority": (_int, [_vp]),
+    "rle_replay_gather": (_int, [_vp, _int, _i64p, _f32p, _f32p, _f32p, _f32p, _f32p]),
+    "rle_create": (_int, [ctypes.POINTER(Config), ctypes.POINTER(_vp)]),
+    "rle_destroy": (_int, [_vp]),
+    "rle_bind_replay": (_int, [_vp, _vp]),
+    "rle_param_numel": (_int, [_vp, _cs, _cs, _i64p]),
+    "rle_get_param": (_int, [_vp, _cs, _cs, _f32p, _ll]),
+    "rle_set_param": (_int, [_vp, _cs, _cs, _f32p, _ll]),
+    "rle_get_adam": (_int, [_vp, _cs, _cs, _int, _f32p, _ll]),
+    "rle_set_adam": (_int, [_vp, _cs, _cs, _int, _f32p, _ll]),
+    "rle_get_counters": (_int, [_vp, _i64p]),
+    "rle_set_counters": (_int, [_vp, _i64p]),
+    "rle_get_value_bounds": (_int, [_vp, _f32p]),
+    "rle_set_value_bounds": (_int, [_vp, _f32p]),
+    "rle_step": (_int, [_vp, _int, _f32p]),
+    "rle_set_tapes": (_int, [_vp, _int, _f32p, _f32p, _f32p, _i64p]),
+    "rle_last_indices": (_int, [_vp, _i64p]),
+    "rle_act": (_int, [_vp, _f32p, _int, _f32p]),
+    "rle_graph_stats": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "rle_copy_state": (_int, [_vp, _vp]),
+    "rle_synchronize": (_int, [_vp]),
+}
+
+
+def lib():
+    """Load librle.so (fails loudly: no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"HIP engine library not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        msg = lib().rle_last_error().decode(errors="replace")
+        raise RuntimeError(f"rle error {rc}: {msg}")
+
+
+def _fp(a):
+    return None if a is None else a.ctypes.data_as(_f32p)
+
+
+def _ip(a):
+    return None if a is None else a.ctypes.data_as(_i64p)
+
+
+def _f32(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return a if shape is None else a.reshape(shape)
+
+
+class Replay:
+    """Device replay ring (HBM) with optional LAP priorities."""
+
+    def __init__(self, capacity, state_dim, action_dim, lap, device=0):
+        self.h = _vp()
+        self.S, self.A, self.capacity, self.lap = state_dim, action_dim, capacity, bool(lap)
+        _check(lib().rle_replay_create(device, capacity, state_dim, action_dim, int(lap), ctypes.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            _check(lib().rle_replay_destroy(self.h))
+            self.h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def append(self, state, action, reward, next_state, notdone):
+        n = len(reward)
+        s = _f32(state, (n, self.S))
+        a = _f32(action, (n, self.A))
+        r = _f32(reward, (n,))
+        s2 = _f32(next_state, (n, self.S))
+        d = _f32(notdone, (n,))
+        _check(lib().rle_replay_append(self.h, _fp(s), _fp(a), _fp(r), _fp(s2), _fp(d), n))
+
+    def state(self):
+        p, s, m = _ll(), _ll(), ctypes.c_float()
+        _check(lib().rle_replay_state(self.h, ctypes.byref(p), ctypes.byref(s), ctypes.byref(m)))
+        return p.value, s.value, m.value
+
+    def fill_random(self, count, seed):
+        _check(lib().rle_replay_fill_random(self.h, count, seed))
+
+    def get_priority(self, n=None):
+        n = self.capacity if n is None else n
+        out = np.empty(n, np.float32)
+        _check(lib().rle_replay_get_priority(self.h, _fp(out), n))
+        return out
+
+    def set_priority(self, p, max_priority):
+        p = _f32(p)
+        _check(lib().rle_replay_set_priority(self.h, _fp(p), p.size, float(max_priority)))
+
+    def sample_indices(self, u):
+        u = _f32(u)
+        out = np.empty(u.size, np.int64)
+        _check(lib().rle_replay_sample_indices(self.h, u.size, _fp(u), _ip(out)))
+        return out
+
+    def update_priority(self, ind, p):
+        ind = np.ascontiguousarray(ind, np.int64)
+        p = _f32(p)
+        _check(lib().rle_replay_update_priority(self.h, ind.size, _ip(ind), _fp(p)))
+
+    def reset_max_priority(self):
+        _check(lib().rle_replay_reset_max_priority(self.h))
+
+    def gather(self, ind):
+        ind = np.ascontiguousarray(ind, np.int64)
+        n = ind.size
+        s = np.empty((n, self.S), np.float32)
+        a = np.empty((n, self.A), np.float32)
+        r = np.empty(n, np.float32)
+        s2 = np.empty((n, self.S), np.float32)
+        d = np.empty(n, np.float32)
+        _check(lib().rle_replay_gather(self.h, n, _ip(ind), _fp(s), _fp(a), _fp(r), _fp(s2), _fp(d)))
+        return s, a, r, s2, d
+
+
+class Engine:
+    """One agent's device state + captured step graphs."""
+
+    def __init__(self, cfg: Config):
+        self.cfg = cfg
+        self.h = _vp()
+        _check(lib().rle_create(ctypes.byref(cfg), ctypes.byref(self.h)))
+        self.replay = None
+
+    def close(self):
+        if self.h:
+            _check(lib().rle_destroy(self.h))
+            self.h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def bind(self, replay: Replay):
+        _check(lib().rle_bind_replay(self.h, replay.h))
+        self.replay = replay
+
+    def numel(self, net, name):
+        n = _ll()
+        _check(lib().rle_param_numel(self.h, net.encode(), name.encode(), ctypes.byref(n)))
+        return n.value
+
+    def get_param(self, net, name, shape=None):
+        n = self.numel(net, name)
+        out = np.empty(n, np.float32)
+        _check(lib().rle_get_param(self.h, net.encode(), name.encode(), _fp(out), n))
+        return out if shape is None else out.reshape(shape)
+
+    def set_param(self, net, name, value):
+        v = _f32(value).ravel()
+        _check(lib().rle_set_param(self.h, net.encode(), name.encode(), _fp(v), v.size))
+
+    def get_adam(self, net, name, which, shape=None):
+        n = self.numel(net, name)
+        out = np.empty(n, np.float32)
+        _check(lib().rle_get_adam(self.h, net.encode(), name.encode(), which, _fp(out), n))
+        return out if shape is None else out.reshape(shape)
+
+    def set_adam(self, net, name, which, value):
+        v = _f32(value).ravel()
+        _check(lib().rle_set_adam(self.h, net.encode(), name.encode(), which, _fp(v), v.size))
+
+    def counters(self):
+        out = np.zeros(6, np.int64)
+        _check(lib().rle_get_counters(self.h, _ip(out)))
+        return out
+
+    def set_counters(self, c):
+        c = np.ascontiguousarray(c, np.int64)
+        _check(lib().rle_set_counters(self.h, _ip(c)))
+
+    def value_bounds(self):
+        out = np.zeros(4, np.float32)
+        _check(lib().rle_get_value_bounds(self.h, _fp(out)))
+        return out
+
+    def set_value_bounds(self, v):
+        v = _f32(v)
+        _check(lib().rle_set_value_bounds(self.h, _fp(v)))
+
+    def step(self, n, want_info=True):
+        info = np.empty((max(n, 1), INFO_MAX), np.float32) if want_info else None
+        _check(lib().rle_step(self.h, n, _fp(info)))
+        return info[:n] if want_info else None
+
+    def set_tapes(self, u=None, eps=None, eps_pi=None, ind=None):
+        if u is None and ind is None:
+            _check(lib().rle_set_tapes(self.h, 0, None, None, None, None))
+            return
+        n = (u if u is not None else ind).shape[0]
+        _check(lib().rle_set_tapes(
+            self.h, n, _fp(None if u is None else _f32(u)), _fp(None if eps is None else _f32(eps)),
+            _fp(None if eps_pi is None else _f32(eps_pi)),
+            _ip(None if ind is None else np.ascontiguousarray(ind, np.int64))))
+
+    def last_indices(self):
+        out = np.empty(self.cfg.batch, np.int64)
+        _check(lib().rle_last_indices(self.h, _ip(out)))
+        return out
+
+    def act(self, obs, width):
+        obs = _f32(obs)
+        if obs.ndim == 1:
+            obs = obs[None]
+        n = obs.shape[0]
+        out = np.empty((n, width), np.float32)
+        _check(lib().rle_act(self.h, _fp(obs), n, _fp(out)))
+        return out
+
+    def graph_stats(self):
+        a, b = _int(), _int()
+        _check(lib().rle_graph_stats(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def copy_state_from(self, other: "Engine"):
+        _check(lib().rle_copy_state(self.h, other.h))
+
+    def synchronize(self):
+        _check(lib().rle_synchronize(self.h))
+
+
+def make_config(algo, state_dim, action_dim, hidden, batch, use_lap=False, discount=0.99,
+                policy_lr=3e-4, critic_lr=3e-4, tau=0.005, target_policy_noise=0.2,
+                noise_clip=0.5, policy_freq=2, target_update_rate=250, min_log_std=-20.0,
+                max_log_std=2.0, tmp=-1.0, seed=0, device=0) -> Config:
+    return Config(algo, state_dim, action_dim, hidden, batch, int(use_lap), discount, policy_lr,
+                  critic_lr, tau, target_policy_noise, noise_clip, policy_freq, target_update_rate,
+                  min_log_std, max_log_std, tmp, seed, device)

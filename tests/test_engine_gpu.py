@@ -1,0 +1,142 @@
+"""Parity of the HIP engine (through the C ABI) against reference goldens + the oracle.
+
+Tolerances (SURVEY.md §4 evidence: fp32 reference vs fp64 of the same math):
+forward outputs |d| <= 1e-5 + 1e-5 |ref|; per-step losses rel 1e-3 over <= 10 steps on identical
+batches; parameters after k Adam steps within 2*lr*k + 1e-5 (Adam's first steps are ~lr*sign(g),
+so near-zero gradients may flip sign between summation orders).
+"""
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+E = pytest.importorskip("rl._engine")
+from harness import engine_from_golden, parse, run_with_tapes  # noqa: E402
+from oracle import spec  # noqa: E402
+
+
+def test_lap_sampler_device():
+    g = load_golden("lap_sampler")
+    for n, seed in ((65536, 11), (1000000, 12), (1, 13), (4097, 14)):
+        rep = E.Replay(n, 3, 2, True)
+        rep.append(np.zeros((n, 3)), np.zeros((n, 2)), np.zeros(n), np.zeros((n, 3)), np.ones(n))
+        p = spec.init_priorities(n, seed)
+        rep.set_priority(p, float(p.max()))
+        ind = rep.sample_indices(g[f"n{n}_u"])
+        np.testing.assert_array_equal(ind, g[f"n{n}_ind"])
+        rep.close()
+
+
+def test_uniform_sampler_device():
+    g = load_golden("uniform_sampler")
+    for size in (1, 7, 25000):
+        rep = E.Replay(size, 3, 2, False)
+        rep.append(np.zeros((size, 3)), np.zeros((size, 2)), np.zeros(size), np.zeros((size, 3)),
+                   np.ones(size))
+        ind = rep.sample_indices(g[f"s{size}_u"])
+        np.testing.assert_array_equal(ind, g[f"s{size}_ind"])
+        rep.close()
+
+
+def test_priority_scatter_last_writer_wins():
+    g = load_golden("lap_sampler")
+    rep = E.Replay(64, 3, 2, True)
+    rep.append(np.zeros((64, 3)), np.zeros((64, 2)), np.zeros(64), np.zeros((64, 3)), np.ones(64))
+    rep.set_priority(g["scatter_base"], 1.0)
+    rep.update_priority(g["scatter_ind"], g["scatter_new"])
+    np.testing.assert_array_equal(rep.get_priority(64), g["scatter_out"])
+    assert rep.state()[2] == max(1.0, float(g["scatter_new"].max()))
+    rep.reset_max_priority()
+    assert rep.state()[2] == float(g["scatter_out"].max())
+
+
+def test_replay_gather_roundtrip():
+    rng = np.random.default_rng(0)
+    n, S, A = 100, 17, 6
+    rep = E.Replay(64, S, A, False)  # wraps around: rows 64..99 overwrite 0..35
+    s = rng.standard_normal((n, S)).astype(np.float32)
+    a = rng.standard_normal((n, A)).astype(np.float32)
+    r = rng.standard_normal(n).astype(np.float32)
+    s2 = rng.standard_normal((n, S)).astype(np.float32)
+    d = (rng.random(n) > 0.5).astype(np.float32)
+    rep.append(s, a, r, s2, d)
+    ptr, size, _ = rep.state()
+    assert (ptr, size) == (36, 64)
+    ind = np.array([0, 35, 36, 63])
+    gs, ga, gr, gs2, gd = rep.gather(ind)
+    src = np.array([64, 99, 36, 63])
+    np.testing.assert_array_equal(gs, s[src])
+    np.testing.assert_array_equal(ga, a[src])
+    np.testing.assert_array_equal(gr, r[src])
+    np.testing.assert_array_equal(gs2, s2[src])
+    np.testing.assert_array_equal(gd, d[src])
+
+
+def _fwd_check(name):
+    g = load_golden(name)
+    alg, env, H, B, *_ = parse(g)
+    S, A, hi = spec.TASKS[env]
+    eng, rep, tp = engine_from_golden(g)
+    s, a, *_ = rep.gather(np.arange(B))
+    if alg == "td7":
+        out = eng.act(s, A)
+        ref = g["fwd_pi"]
+    elif alg == "td3":
+        out = np.tanh(eng.act(s, A))
+        ref = g["fwd_pi"]
+    else:
+        out = eng.act(s, 2 * A)
+        ref = np.concatenate([g["fwd_mean"], g["fwd_log_std"]], 1)
+    n = ref.shape[0]
+    np.testing.assert_allclose(out[:n], ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny", "sac_tiny", "td7_humanoid", "sac_humanoid",
+                                  "td3_halfcheetah"])
+def test_forward_matches_reference(name):
+    _fwd_check(name)
+
+
+TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny"]
+FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid"]
+
+
+@pytest.mark.parametrize("name", TINY + FULL)
+def test_step_trajectory_matches_reference(name):
+    g = load_golden(name)
+    alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
+    eng, rep, tp = engine_from_golden(g)
+
+    def check(t):
+        np.testing.assert_array_equal(eng.last_indices(), g["ind"][t])
+        if use_lap:
+            np.testing.assert_allclose(rep.get_priority(Ncap), g[f"prio_{t}"], rtol=1e-4, atol=1e-5)
+        if f"vbounds_{t}" in g:
+            np.testing.assert_allclose(eng.value_bounds(), g[f"vbounds_{t}"].astype(np.float32),
+                                       rtol=1e-4, atol=1e-4)
+
+    infos = run_with_tapes(eng, tp, n_steps, check)
+    ref = g["info"]
+    k = ref.shape[1]
+    np.testing.assert_array_equal(np.isnan(infos[:, :k]), np.isnan(ref))
+    np.testing.assert_allclose(infos[:, :k], ref, rtol=2e-3, atol=1e-4, equal_nan=True)
+    # parameters after the trajectory
+    n_upd = n_steps
+    tol = 2 * 3e-4 * n_upd + 1e-4
+    for key in g:
+        if not key.startswith("out_") or key == "out_log_alpha":
+            continue
+        net, rest = key[4:].split(".", 1)
+        if rest.endswith(":digest"):
+            pname = rest[: -len(":digest")]
+            v = eng.get_param(net, pname)
+            base = key[: -len(":digest")]
+            np.testing.assert_allclose(v[g[base + ":pos"]], g[base + ":vals"], rtol=0, atol=tol)
+        elif ":" not in rest:
+            v = eng.get_param(net, rest, g[key].shape)
+            d = np.abs(v - g[key])
+            assert d.max() <= tol, (key, d.max())
+            assert (d <= 1e-5).mean() >= 0.99, (key, (d <= 1e-5).mean())
