@@ -1,0 +1,227 @@
+"""Benchmark: TD7 Humanoid-v4 (obs 376, act 17) batch 256 gradient-steps/sec on MI355X.
+
+One gradient step = one ``Agent.train_ops(replay.sample(B), replay)`` of the reference
+(rl/runner/run.py:87-96): LAP sampling over a full 1M-transition HBM replay, encoder /
+critic / (every 2nd step) actor updates with Adam, LAP priority update, hard target update
+every 250 steps.  Synthetic replay: s, s' ~ N(0,1), a ~ U(-1,1),
+r ~ N(0,1), notdone ~ Bernoulli(0.99), priorities 1.0; random-init weights of the
+reference architecture (nn.Linear default init family).
+
+Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`` runs one
+independent seed per GPU (replicas; no collective on the data path); a gloo
+group is used only for the start barrier and the max-over-ranks timing.
+
+Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd")]
+
+S, A, H, B, N_REPLAY = 376, 17, 256, 256, 1_000_000
+METRIC = "gradient-steps/sec (whole node), TD7 Humanoid-v4 batch=256 at 1/2/4/8 GPUs"
+PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 MFMA dense (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+# SURVEY.md §8(d) algorithmic work for TD7 Humanoid B=256: 6,217,088 MAC/sample (3.183 GFLOP/step).
+SURVEY_MACS_PER_SAMPLE = 6_217_088
+
+
+def td7_macs_per_sample(S, A, H, policy_freq=2):
+    """Algorithmic MACs per sample (SURVEY.md §8d convention): forward i*o, weight-grad i*o for
+    trained layers, input-grad only for needed columns, no grads into frozen nets, policy phase
+    weighted by 1/policy_freq."""
+    HH = H * H
+    enc_fwd = 2 * (S * H + 2 * HH) + (H + A) * H + 2 * HH          # zs(s'), zs(s), zsa(s)
+    enc_w = S * H + 2 * HH + (H + A) * H + 2 * HH
+    enc_i = 5 * HH                                                 # zsa3, zsa2, zsa1[zs], zs3, zs2
+    E = enc_fwd + enc_w + enc_i
+    critic_fwd = (S + A) * H + 3 * HH + HH + H                     # q01, q1 (3H in), q2, q3
+    actor_fwd = S * H + 2 * HH + HH + H * A                        # l0, l1 (2H in), l2, l3
+    zs = S * H + 2 * HH
+    zsa = (H + A) * H + 2 * HH
+    Q = (zs + actor_fwd + zsa + 2 * critic_fwd                     # target branch
+         + zs + zsa                                                # fixed encoder on s
+         + 2 * critic_fwd + 2 * critic_fwd                         # online fwd + weight grads
+         + 2 * (H + HH + HH))                                      # input grads q3, q2, q1[norm]
+    P = (actor_fwd + zsa + 2 * critic_fwd
+         + 2 * (H + HH + 2 * HH + A * H)                           # critics: q3, q2, q1[norm,zsa], q01[a]
+         + HH + HH + A * H                                         # fe.zsa3, zsa2, zsa1[a]
+         + H * A + HH + HH                                         # actor l3, l2, l1[l0]
+         + actor_fwd)                                              # actor weight grads
+    return E + Q + P / policy_freq
+
+
+def td7_param_counts(S, A, H):
+    enc = S * H + H + 2 * (HH := H * H) + 2 * H + (H + A) * H + H + 2 * HH + 2 * H
+    actor = S * H + H + 2 * HH + H + HH + H + A * H + A
+    critic = (S + A) * H + H + 3 * HH + H + HH + H + H + 1
+    return enc, actor, critic
+
+
+def td7_bytes_per_step(S, A, H, B, N, target_update_rate=250, policy_freq=2):
+    """Algorithmic HBM bytes per step: gather + index/priority + LAP scan +
+    Adam 28 B/updated param + hard-copy traffic amortised."""
+    enc, actor, critic = td7_param_counts(S, A, H)
+    gather = B * (2 * S + A + 2) * 4
+    adam = 28 * (enc + 2 * critic + actor / policy_freq)
+    hard = 8 * (2 * critic + 2 * enc) / target_update_rate
+    return gather + B * 8 + 4 * N + adam + hard
+
+
+def cpu_baseline(seconds=12.0):
+    """Oracle (torch-CPU restatement of td7.py train_ops + lap.py sample) on host cores."""
+    import torch
+
+    from oracle import agents, replay, spec
+
+    threads = torch.get_num_threads()
+    rng = np.random.default_rng(0)
+    nets = spec.agent_params("td7", S, A, H, 123)
+    orc = agents.TD7Oracle(nets, use_lap=True)
+    rep = replay.Replay(N_REPLAY, S, A, np.full(A, 0.4, np.float32), np.zeros(A, np.float32), True)
+    blk = 4096
+    base_s = rng.standard_normal((blk, S), dtype=np.float32)
+    base_s2 = rng.standard_normal((blk, S), dtype=np.float32)
+    for i in range(0, N_REPLAY, blk):
+        n = min(blk, N_REPLAY - i)
+        rep.state[i:i + n] = base_s[:n]
+        rep.next_state[i:i + n] = base_s2[:n]
+    rep.action[:] = rng.uniform(-1, 1, (N_REPLAY, A)).astype(np.float32)
+    rep.reward[:, 0] = rng.standard_normal(N_REPLAY).astype(np.float32)
+    rep.done[:, 0] = (rng.random(N_REPLAY) < 0.99).astype(np.float32)
+    rep.priority[:] = 1.0
+    rep.size, rep.ptr = N_REPLAY, 0
+
+    def one():
+        u = rng.random(B, dtype=np.float32)
+        batch = rep.gather(rep.sample_indices(u))
+        orc.step(batch, rep, rng.standard_normal((B, A), dtype=np.float32))
+
+    for _ in range(3):
+        one()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds or n < 10:
+        one()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "gradient-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} TD7 Humanoid B=256 steps (LAP over 1M priorities, policy every 2nd step) "
+                      f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: start barrier + timing reduction only
+        dist.init_process_group("gloo")
+
+    import torch
+
+    from rl import _engine as E
+    from rl.nn.layout import init_agent
+
+    # --- engine: one independent seed per GPU (seed 111, 222, ... as scripts/td7_exp.sh)
+    cfg = E.make_config(E.RLE_TD7, S, A, H, B, use_lap=True, seed=111 * (rank + 1), device=local)
+    eng = E.Engine(cfg)
+    for net, params in init_agent("td7", S, A, H, 123 + rank).items():
+        for name, v in params.items():
+            eng.set_param(net, name, v)
+    rep = E.Replay(N_REPLAY, S, A, True, device=local)
+    rep.fill_random(N_REPLAY, seed=rank)
+    eng.bind(rep)
+    lv_policy, lv_plain = eng.graph_stats()
+
+    eng.step_timed(args.warmup)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(local)
+    t0 = time.perf_counter()
+    gpu_ms = eng.step_timed(args.steps)
+    torch.cuda.synchronize(local)
+    t1 = time.perf_counter()
+    wall = t1 - t0
+    if dist:
+        t = torch.tensor([wall, gpu_ms / 1e3], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, gpu_s = float(t[0]), float(t[1])
+    else:
+        gpu_s = gpu_ms / 1e3
+
+    if rank != 0:
+        if dist:
+            dist.barrier()
+        return
+    n_gpus = world
+    value = n_gpus * args.steps / wall
+    macs = SURVEY_MACS_PER_SAMPLE  # the §8(d) contract figure (own derivation: td7_macs_per_sample)
+    flop_step = 2.0 * macs * B
+    bytes_step = td7_bytes_per_step(S, A, H, B, N_REPLAY)
+    # launches per step: average over the policy / non-policy graphs (+ hard update amortised)
+    launches = (lv_policy + lv_plain) / 2.0
+    per_launch_s = gpu_s / (args.steps * launches)
+    achieved = flop_step / launches / per_launch_s / 1e12
+    roofline = {
+        "bound": "mfma",
+        "achieved": round(achieved, 3),
+        "peak": PEAK_FP32_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_FP32_TFLOPS, 5),
+        "traffic": None,
+        "kernel": "rle_level (one launch per dependency level of the step graph)",
+        "flop_per_step": flop_step,
+        "launches_per_step": launches,
+        "avg_launch_us": round(per_launch_s * 1e6, 3),
+        "hbm_bytes_per_step_algorithmic": round(bytes_step),
+        "hbm_achieved_GBs": round(bytes_step * args.steps / gpu_s / 1e9, 2),
+    }
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "gradient-steps/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic",
+        "config": {"workload": "TD7 Humanoid-v4 gradient step, LAP over 1M HBM replay",
+                   "algo": "td7", "obs_dim": S, "act_dim": A, "hidden": H, "batch": B,
+                   "replay": N_REPLAY, "lap": True, "policy_freq": 2, "target_update_rate": 250,
+                   "parallelism": f"replicas x{n_gpus} (one seed per GPU, no collective)"},
+        "roofline": roofline,
+        "gpu_event_s": round(gpu_s, 6),
+    }
+    if n_gpus == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -38,7 +38,7 @@ typedef struct rle_config {
   int algo;                 /* RLE_TD7 / RLE_TD3 / RLE_SAC */
   int state_dim, action_dim;
   int hidden;               /* hidden width (TD7: hdim = zs_dim) */
-  int batch;                /* B (multiple of 4, <= 1024) */
+  int batch;                /* B (multiple of 16, <= 1024) */
   int use_lap;              /* TD7/TD3: LAP Huber + priority update */
   float discount;           /* td7.py:37 / td3.py:36 / sac.py:30 */
   float policy_lr, critic_lr;
@@ -108,6 +108,9 @@ int rle_set_value_bounds(rle_engine* e, const float* in4);
  * device incl. sampling and LAP priority update.  info_out: [n_steps][RLE_INFO_MAX] (per-agent
  * key order; NaN = None).  One host sync per call. */
 int rle_step(rle_engine* e, int n_steps, float* info_out);
+/* Benchmark form of rle_step: n_steps without info readback, bracketed by HIP events recorded
+ * on the engine's own stream; *gpu_ms = elapsed event time.  Syncs once at the end. */
+int rle_step_timed(rle_engine* e, int n_steps, float* gpu_ms);
 /* Parity mode: replace the Philox draws of the next n_steps with tapes.
  * u [n][B] (torch.rand in sample), eps [n][B][A] (randn_like target noise, or SAC next-state
  * rsample noise), eps_pi [n][B][A] (SAC policy rsample noise, may be NULL), ind [n][B]
@@ -123,6 +126,9 @@ int rle_last_indices(rle_engine* e, long long* ind_out);
 int rle_act(rle_engine* e, const float* obs, int n, float* out);
 /* Launches per gradient step of each captured graph kind (for roofline accounting). */
 int rle_graph_stats(rle_engine* e, int* levels_policy_step, int* levels_plain_step);
+/* Human-readable description of a captured graph (which: 0 policy step, 1 plain step,
+ * 2 hard update): one line per level with workgroups and ops.  Writes at most len bytes. */
+int rle_graph_describe(rle_engine* e, int which, char* buf, int len);
 /* Copy all weights/optimizer state/counters of src into dst (checkpoint agent,
  * ckpt_agent.load_state_dict(agent), run_w_checkpoint.py:140). Same config required. */
 int rle_copy_state(rle_engine* dst, rle_engine* src);

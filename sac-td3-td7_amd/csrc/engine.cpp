@@ -125,16 +125,43 @@ struct View {
   }
 };
 
+// Layout invariants the GEMM main loop relies on (kernels.hip, "GEMM"): reduction
+// segments 16-aligned, sorted and disjoint; every segment of a FWD/DX operand
+// and of a DW A operand spans the whole operand row range (x0 == 0); DW B
+// segments split the columns at 16-aligned bounds and share one reduction range.
+static void check_gemm(const GemmArgs& g) {
+  auto chk = [&](const Operand& o, bool xsplit, int xn) {
+    REQUIRE(o.nseg >= 1 && o.nseg <= kMaxSeg, "gemm: bad segment count");
+    for (int q = 0; q < o.nseg; ++q) {
+      const Seg& s = o.seg[q];
+      REQUIRE(s.p != nullptr && s.r0 % 16 == 0 && s.r1 > s.r0, "gemm: bad reduction segment");
+      if (!xsplit) {
+        REQUIRE(s.x0 == 0 && s.x1 >= xn, "gemm: segment must span the operand rows");
+        if (q) REQUIRE(s.r0 >= o.seg[q - 1].r1, "gemm: reduction segments unsorted/overlapping");
+      } else {
+        REQUIRE(s.x0 % 16 == 0 && s.x1 % 16 == 0 && s.r0 == o.seg[0].r0 && s.r1 == o.seg[0].r1,
+                "gemm: bad column split");
+      }
+    }
+  };
+  chk(g.A, false, g.M);
+  chk(g.B, g.mode == GEMM_DW, g.N);
+  REQUIRE(g.R <= 16 * 1024, "gemm: reduction too long");
+}
+
 struct Prog {
   struct Item {
-    Op op;
+    std::vector<Op> ops;  // one op, or a group writing disjoint parts of the same buffers
     std::vector<int> rd, wr;
     int level = 0;
   };
   std::vector<Item> items;
-  void add(const Op& op, std::vector<int> rd, std::vector<int> wr) {
+  void add(const Op& op, std::vector<int> rd, std::vector<int> wr) { add_group({op}, std::move(rd), std::move(wr)); }
+  void add_group(std::vector<Op> ops, std::vector<int> rd, std::vector<int> wr) {
+    for (const Op& op : ops)
+      if (op.kind == OP_GEMM) check_gemm(op.gemm);
     Item it;
-    it.op = op;
+    it.ops = std::move(ops);
     it.rd = std::move(rd);
     it.wr = std::move(wr);
     items.push_back(std::move(it));
@@ -160,7 +187,8 @@ struct Prog {
       maxl = std::max(maxl, l);
     }
     std::vector<std::vector<Op>> levels(maxl + 1);
-    for (auto& it : items) levels[it.level].push_back(it.op);
+    for (auto& it : items)
+      for (auto& op : it.ops) levels[it.level].push_back(op);
     for (auto& lv : levels) {
       int wg = 0;
       for (auto& op : lv) {
@@ -177,6 +205,7 @@ struct Graph {
   hipGraphExec_t x = nullptr;
   Op* d_ops = nullptr;
   std::vector<int> nops, nwg, off;
+  std::string desc;
   int levels() const { return (int)nops.size(); }
 };
 
@@ -251,7 +280,8 @@ struct Engine {
     L.bname = pre + ".bias";
     L.out = out;
     L.seg_w = segw;
-    for (int w : segw) L.seg_p.push_back(r4(w));
+    // every input segment padded to 16 so a 16-wide reduction chunk never straddles two
+    for (int w : segw) L.seg_p.push_back(r16(w));
     L.K = 0;
     for (int p : L.seg_p) L.K += p;
     L.res = next_id++;
@@ -373,11 +403,11 @@ struct Engine {
   }
 
   // ---------------------------------------------------------------- buffers
-  // Zero-initialised activation buffer; feature dims padded to 4 (16-B rows),
+  // Zero-initialised activation buffer; feature dims padded to 16 (64-B rows),
   // single-column vectors kept dense (ld 1).
   View buf(int rows, int cols) {
     View v;
-    v.ld = cols == 1 ? 1 : r4(cols);
+    v.ld = cols == 1 ? 1 : r16(cols);
     v.rows = rows;
     v.cols = v.ld;
     v.p = mem.make<float>((size_t)rows * v.ld + 4);
@@ -406,77 +436,108 @@ struct Engine {
   }
 
   // Y = act(X W^T + b) over concatenated input segments (each a list of row pieces).
+  // The GEMM kernel wants every A segment to span the op's whole row range, so
+  // row pieces split the op into one sub-op per row range (same level, disjoint
+  // output rows).
   View fwd(Prog& pg, const Layer& L, const std::vector<std::vector<View>>& ins, int M, int act, View* pre_out,
            bool normed, const View* noise = nullptr, int noise_row0 = 0) {
     REQUIRE(ins.size() == L.seg_p.size(), "fwd: input segment count mismatch for " + L.wname);
-    Op op{};
-    op.kind = OP_GEMM;
-    GemmArgs& g = op.gemm;
+    REQUIRE(M % kTileM == 0, "fwd: rows must be a multiple of 16");
     std::vector<int> rd{L.res}, wr;
-    int koff = 0, ns = 0;
+    std::vector<int> cuts{0, M};
     for (size_t s = 0; s < ins.size(); ++s) {
       int xo = 0;
       for (const View& v : ins[s]) {
         REQUIRE(v.cols == L.seg_p[s], "fwd: segment width mismatch for " + L.wname);
-        REQUIRE(ns < kMaxSeg, "fwd: too many operand segments");
-        g.A.seg[ns++] = seg_contig(v, xo, koff, koff + L.seg_p[s]);
         xo += v.rows;
+        if (xo < M) cuts.push_back(xo);
         rd.push_back(v.id);
         if (v.norm) rd.push_back(v.norm_id);
       }
       REQUIRE(xo >= M, "fwd: input rows < M");
-      koff += L.seg_p[s];
     }
-    g.A.nseg = ns;
-    Seg w{};
-    w.p = param(L);
-    w.ld = L.K;
-    w.x0 = 0;
-    w.x1 = L.out;
-    w.r0 = 0;
-    w.r1 = L.K;
-    g.B.seg[0] = w;
-    g.B.nseg = 1;
-    g.M = M;
-    g.N = L.out;
-    g.R = L.K;
-    g.tiles_m = cdiv(M, kTile);
-    g.tiles_n = cdiv(L.out, kTile);
-    g.epi = EPI_STORE;
-    g.act = act;
+    std::sort(cuts.begin(), cuts.end());
+    cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+    REQUIRE((int)ins.size() <= kMaxSeg, "fwd: too many operand segments");
+    const int tiles_n = cdiv(L.out, kTileN);
     View out = buf(M, L.out);
-    g.out = out.p;
-    g.ldo = out.ld;
-    g.bias = bias(L);
     wr.push_back(out.id);
     if (pre_out) {
       *pre_out = buf(M, L.out);
-      g.pre = pre_out->p;
-      g.ldpre = pre_out->ld;
       wr.push_back(pre_out->id);
     }
+    float* part = nullptr;
     if (normed) {
-      float* part = mem.make<float>((size_t)g.tiles_n * M);
-      g.norm_out = part;
-      g.norm_ld = M;
+      part = mem.make<float>((size_t)tiles_n * M);
       out.norm = part;
       out.norm_ld = M;
       out.norm_row0 = 0;
-      out.nparts = g.tiles_n;
+      out.nparts = tiles_n;
       out.width = L.out;
       out.norm_id = next_id++;
       wr.push_back(out.norm_id);
     }
-    if (noise) {
-      g.noise = noise->p;
-      g.ldnoise = noise->ld;
-      g.noise_row0 = noise_row0;
-      g.noise_sigma = cfg.target_policy_noise;
-      g.noise_clip = cfg.noise_clip;
-      rd.push_back(noise->id);
+    if (noise) rd.push_back(noise->id);
+    std::vector<Op> ops;
+    for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
+      const int ra = cuts[ci], rb = cuts[ci + 1], m = rb - ra;
+      REQUIRE(ra % kTileM == 0, "fwd: row pieces must be 16-aligned");
+      Op op{};
+      op.kind = OP_GEMM;
+      GemmArgs& g = op.gemm;
+      g.mode = GEMM_FWD;
+      int koff = 0;
+      for (size_t s = 0; s < ins.size(); ++s) {
+        int xo = 0;
+        for (const View& v : ins[s]) {
+          if (ra >= xo && ra < xo + v.rows) {
+            g.A.seg[s] = seg_contig(v.sub(ra - xo, m), 0, koff, koff + L.seg_p[s]);
+            break;
+          }
+          xo += v.rows;
+        }
+        koff += L.seg_p[s];
+      }
+      g.A.nseg = (int)ins.size();
+      Seg w{};
+      w.p = param(L);
+      w.ld = L.K;
+      w.x0 = 0;
+      w.x1 = L.out;
+      w.r0 = 0;
+      w.r1 = L.K;
+      g.B.seg[0] = w;
+      g.B.nseg = 1;
+      g.M = m;
+      g.N = L.out;
+      g.R = L.K;
+      g.tiles_m = cdiv(m, kTileM);
+      g.tiles_n = tiles_n;
+      g.epi = EPI_STORE;
+      g.act = act;
+      g.out = out.p + (size_t)ra * out.ld;
+      g.ldo = out.ld;
+      g.bias = bias(L);
+      if (pre_out) {
+        g.pre = pre_out->p + (size_t)ra * pre_out->ld;
+        g.ldpre = pre_out->ld;
+      }
+      if (normed) {
+        g.norm_out = part + ra;
+        g.norm_ld = M;
+      }
+      if (noise && rb > noise_row0) {
+        const int first = std::max(ra, noise_row0);  // first noised row (global)
+        g.noise = noise->p + (size_t)(first - noise_row0) * noise->ld;
+        g.ldnoise = noise->ld;
+        g.noise_row0 = first - ra;
+        g.noise_sigma = cfg.target_policy_noise;
+        g.noise_clip = cfg.noise_clip;
+      }
+      op.wg_count = g.tiles_m * g.tiles_n;
+      ops.push_back(op);
     }
-    op.wg_count = g.tiles_m * g.tiles_n;
-    pg.add(op, rd, wr);
+    pg.add_group(std::move(ops), rd, wr);
     return out;
   }
 
@@ -491,6 +552,7 @@ struct Engine {
     Op op{};
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
+    g.mode = GEMM_DX;
     std::vector<int> rd, wr;
     REQUIRE((int)terms.size() <= kMaxSeg, "dx: too many terms");
     int roff = 0;
@@ -513,7 +575,7 @@ struct Engine {
       b.r1 = roff + tm.L->out;
       b.strided = 1;
       g.B.seg[t] = b;
-      roff += r4(tm.L->out);
+      roff += r16(tm.L->out);
       rd.push_back(tm.dz.id);
       rd.push_back(tm.L->res);
     }
@@ -521,8 +583,8 @@ struct Engine {
     g.M = M;
     g.N = ncols;
     g.R = roff;
-    g.tiles_m = cdiv(M, kTile);
-    g.tiles_n = cdiv(ncols, kTile);
+    g.tiles_m = cdiv(M, kTileM);
+    g.tiles_n = cdiv(ncols, kTileN);
     g.epi = EPI_STORE;
     g.act = ACT_NONE;
     View out = buf(M, ncols);
@@ -547,6 +609,7 @@ struct Engine {
     Op op{};
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
+    g.mode = GEMM_DW;
     std::vector<int> rd{dz.id, L.res, R_CNT}, wr{L.res};
     Seg a{};
     a.p = dz.p;
@@ -586,8 +649,8 @@ struct Engine {
     g.M = L.out;
     g.N = L.K;
     g.R = Brows;
-    g.tiles_m = cdiv(L.out, kTile);
-    g.tiles_n = cdiv(L.K, kTile) + 1;
+    g.tiles_m = cdiv(L.out, kTileM);
+    g.tiles_n = cdiv(L.K, kTileN) + 1;
     g.epi = EPI_ADAM;
     AdamArgs& ad = g.adam;
     ad.w = param(L);
@@ -600,7 +663,7 @@ struct Engine {
     ad.beta2 = 0.999f;
     ad.eps = 1e-8f;
     ad.ldw = L.K;
-    ad.bias_col = r16(L.K);
+    ad.bias_col = cdiv(L.K, kTileN) * kTileN;
     ad.gsq = gsq;
     ad.gsq_b = gsq_b;
     op.wg_count = g.tiles_m * g.tiles_n;
@@ -799,6 +862,7 @@ struct Engine {
       Op op{};
       op.kind = OP_GEMM;
       GemmArgs& g = op.gemm;
+      g.mode = GEMM_FWD;
       g.A.seg[0] = seg_contig(ea2, 0, 0, L.K);
       g.A.nseg = 1;
       Seg w{};
@@ -811,8 +875,8 @@ struct Engine {
       g.M = B;
       g.N = L.out;
       g.R = L.K;
-      g.tiles_m = cdiv(B, kTile);
-      g.tiles_n = cdiv(L.out, kTile);
+      g.tiles_m = cdiv(B, kTileM);
+      g.tiles_n = cdiv(L.out, kTileN);
       g.epi = EPI_MSE;
       g.bias = bias(L);
       ed3 = buf(B, L.out);
@@ -1220,14 +1284,14 @@ struct Engine {
       }
       if (!sac) {
         // per-tile grad-square partials for norm/policy (rl/nn/utils.py:13-19)
-        for (auto& L : pi.layers) ngsq += cdiv(L.out, kTile) * cdiv(L.K, kTile) + cdiv(L.out, kTile);
+        for (auto& L : pi.layers) ngsq += cdiv(L.out, kTileM) * cdiv(L.K, kTileN) + cdiv(L.out, kTileM);
         gsq = mem.make<float>(ngsq);
       }
       std::vector<int> tens;
       float* gp = gsq;
       auto gsq_for = [&](const Layer& L, int t_w, int t_b) -> std::pair<float*, float*> {
         if (!gsq) return {nullptr, nullptr};
-        int nw = cdiv(L.out, kTile) * cdiv(L.K, kTile), nb = cdiv(L.out, kTile);
+        int nw = cdiv(L.out, kTileM) * cdiv(L.K, kTileN), nb = cdiv(L.out, kTileM);
         float* w = gp;
         float* b = gp + nw;
         gp += nw + nb;
@@ -1246,9 +1310,10 @@ struct Engine {
       dw(pg, pi.layers[1], d1, {h0s}, B, CNT_ADAM_PI, cfg.policy_lr, g1.first, g1.second);
       dw(pg, pi.layers[0], d0, {s}, B, CNT_ADAM_PI, cfg.policy_lr, g0.first, g0.second);
       if (gsq) {
-        gsq_tensor_d = mem.make<int>(tens.size());
-        HIPCHK(hipMemcpy(gsq_tensor_d, tens.data(), tens.size() * 4, hipMemcpyHostToDevice));
-        gsq_id = next_id++;
+        // tensor t owns tiles [gsq_offs[t], gsq_offs[t+1]) (params() order: w0, b0, w1, b1, w2, b2)
+        gsq_offs.assign(1, 0);
+        for (size_t i = 0; i < tens.size(); ++i)
+          if (i + 1 == tens.size() || tens[i + 1] != tens[i]) gsq_offs.push_back((int)i + 1);
       }
     }
     // Polyak (td3.py:194-204 on policy steps incl. aliased policy Q2; sac.py:243-249 every step)
@@ -1272,8 +1337,8 @@ struct Engine {
         info_sum(a, 1, ploss_part, hw, 4, -1.f / (float)B);
         a.kind[2] = INFO_GNORM;
         a.gsq = gsq;
-        a.ngsq = ngsq;
-        a.gsq_tensor = gsq_tensor_d;
+        a.ngsq_t = (int)gsq_offs.size() - 1;
+        for (size_t q = 0; q < gsq_offs.size(); ++q) a.gsq_off[q] = gsq_offs[q];
         for (auto& L : pi.layers) rd.push_back(L.res);
       } else {
         a.kind[1] = INFO_NAN;
@@ -1309,8 +1374,7 @@ struct Engine {
     if (policy) cn.push_back(CNT_ADAM_PI);
     add_step_end(pg, op, rd, cn);
   }
-  int* gsq_tensor_d = nullptr;
-  int gsq_id = -1;
+  std::vector<int> gsq_offs;
 
   // ---------------------------------------------------------------- graphs
   Graph capture(Prog& pg) {
@@ -1324,6 +1388,20 @@ struct Engine {
       for (auto& op : lv) wg += op.wg_count;
       G.nwg.push_back(wg);
       total += lv.size();
+    }
+    static const char* kname[] = {"?", "gemm", "normbwd", "sreduce", "sgather", "head", "prio",
+                                  "sacfwd", "sacbwd", "end", "polyak", "copy", "maxred", "ctrl"};
+    for (size_t l = 0; l < levels.size(); ++l) {
+      G.desc += "L" + std::to_string(l) + " wg=" + std::to_string(G.nwg[l]) + ":";
+      for (auto& op : levels[l]) {
+        G.desc += std::string(" ") + kname[op.kind];
+        if (op.kind == OP_GEMM) {
+          const char* ep = op.gemm.epi == EPI_ADAM ? "adam" : (op.gemm.epi == EPI_MSE ? "mse" : "st");
+          G.desc += "[" + std::to_string(op.gemm.M) + "x" + std::to_string(op.gemm.N) + "x" +
+                    std::to_string(op.gemm.R) + " " + ep + "]";
+        }
+      }
+      G.desc += "\n";
     }
     std::vector<Op> flat_ops;
     flat_ops.reserve(total);
@@ -1395,12 +1473,18 @@ struct Engine {
   }
 
   // ---------------------------------------------------------------- run
-  void step(int n, float* info_out) {
+  void step(int n, float* info_out, float* gpu_ms = nullptr) {
     REQUIRE(replay, "no replay bound");
     REQUIRE(replay->size > 0, "replay is empty");
     if (!built) build();
     const int pf = std::max(1, cfg.policy_freq);
     int done = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (gpu_ms) {
+      HIPCHK(hipEventCreate(&ev0));
+      HIPCHK(hipEventCreate(&ev1));
+      HIPCHK(hipEventRecord(ev0, stream));
+    }
     while (done < n) {
       const int chunk = std::min(n - done, info_cap);
       int zero = 0;
@@ -1426,8 +1510,15 @@ struct Engine {
         HIPCHK(hipMemcpyAsync(info_out + (size_t)done * kInfoMax, info, (size_t)chunk * kInfoMax * sizeof(float),
                               hipMemcpyDeviceToHost, stream));
       }
-      HIPCHK(hipStreamSynchronize(stream));
+      if (!gpu_ms) HIPCHK(hipStreamSynchronize(stream));
       done += chunk;
+    }
+    if (gpu_ms) {
+      HIPCHK(hipEventRecord(ev1, stream));
+      HIPCHK(hipEventSynchronize(ev1));
+      HIPCHK(hipEventElapsedTime(gpu_ms, ev0, ev1));
+      (void)hipEventDestroy(ev0);
+      (void)hipEventDestroy(ev1);
     }
   }
   int ctrl_tape_mode_host = 0;
@@ -1476,9 +1567,9 @@ int rle_replay_create(int device, long long capacity, int state_dim, int action_
     r.device = device;
     r.cap = capacity;
     r.S = state_dim;
-    r.Sp = rle::r4(state_dim);
+    r.Sp = rle::r16(state_dim);
     r.A = action_dim;
-    r.Ap = rle::r4(action_dim);
+    r.Ap = rle::r16(action_dim);
     r.lap = lap ? 1 : 0;
     try {
       HIPCHK(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
@@ -1751,7 +1842,8 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
   return guard([&] {
     REQUIRE(cfg && out, "create: null");
     REQUIRE(cfg->algo >= 0 && cfg->algo <= 2, "create: bad algo");
-    REQUIRE(cfg->batch > 0 && cfg->batch % 4 == 0 && cfg->batch <= 1024, "create: batch must be a multiple of 4, <= 1024");
+    REQUIRE(cfg->batch > 0 && cfg->batch % 16 == 0 && cfg->batch <= 1024,
+            "create: batch must be a multiple of 16, <= 1024");
     REQUIRE(cfg->state_dim > 0 && cfg->action_dim > 0 && cfg->hidden > 0 && cfg->hidden % 4 == 0,
             "create: bad dims (hidden must be a multiple of 4)");
     HIPCHK(hipSetDevice(cfg->device));
@@ -1761,11 +1853,11 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
     e.cfg = *cfg;
     e.algo = cfg->algo;
     e.S = cfg->state_dim;
-    e.Sp = rle::r4(e.S);
+    e.Sp = rle::r16(e.S);
     e.A = cfg->action_dim;
-    e.Ap = rle::r4(e.A);
+    e.Ap = rle::r16(e.A);
     e.H = cfg->hidden;
-    e.Hp = rle::r4(e.H);
+    e.Hp = rle::r16(e.H);
     e.B = cfg->batch;
     HIPCHK(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
     if (e.algo == RLE_TD7) {
@@ -1907,6 +1999,16 @@ int rle_step(rle_engine* h, int n_steps, float* info_out) {
   });
 }
 
+int rle_step_timed(rle_engine* h, int n_steps, float* gpu_ms) {
+  return guard([&] {
+    REQUIRE(n_steps >= 0 && gpu_ms, "step_timed: bad args");
+    Engine& e = *h->e;
+    HIPCHK(hipSetDevice(e.cfg.device));
+    if (e.replay) HIPCHK(hipStreamSynchronize(e.replay->stream));
+    e.step(n_steps, nullptr, gpu_ms);
+  });
+}
+
 int rle_set_tapes(rle_engine* h, int n, const float* u, const float* eps, const float* eps_pi, const long long* ind) {
   return guard([&] {
     Engine& e = *h->e;
@@ -1991,6 +2093,16 @@ int rle_graph_stats(rle_engine* h, int* lp, int* lplain) {
     if (!e.built) e.build();
     if (lp) *lp = e.g_policy.levels();
     if (lplain) *lplain = e.g_plain.levels();
+  });
+}
+
+int rle_graph_describe(rle_engine* h, int which, char* buf, int len) {
+  return guard([&] {
+    Engine& e = *h->e;
+    if (!e.built) e.build();
+    const rle::Graph& G = which == 0 ? e.g_policy : (which == 1 ? e.g_plain : e.g_hard);
+    REQUIRE(buf && len > 0, "describe: bad buffer");
+    std::snprintf(buf, (size_t)len, "%s", G.desc.c_str());
   });
 }
 

@@ -6,6 +6,13 @@
 // workgroup is 256 threads (4 waves of 64).  The whole step is captured into
 // a hipGraph, so one gradient step = one graph launch, no host sync.
 //
+// Memory-access discipline (what makes a level fast on CDNA4): op descriptors
+// are read through the constant address space (scalar loads into SGPRs, no
+// per-field latency chains) and every tensor access goes through the global
+// address space (global_load/store, counted on vmcnt only) -- plain C++
+// pointers loaded from a descriptor would compile to flat loads that force
+// `s_waitcnt vmcnt(0) lgkmcnt(0)` after every access.
+//
 // Op kinds (reference rows they implement):
 //   GEMM          Linear forward / input-grad / weight-grad+Adam for every layer
 //                 of rl/nn/{sale,mlp}.py (a6-a11, a24), v_mfma_f32_16x16x4_f32
@@ -23,11 +30,33 @@
 
 #include "ops.h"
 
+#define CAS __attribute__((address_space(4)))
+#define GAS __attribute__((address_space(1)))
+
 namespace rle {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+template <class T>
+__device__ __forceinline__ const GAS T* G(const T* p) {
+  return (const GAS T*)p;
+}
+template <class T>
+__device__ __forceinline__ GAS T* GW(T* p) {
+  return (GAS T*)p;
+}
+
 // ---------------------------------------------------------------- utilities
+
+__device__ __forceinline__ float4 ld4g(const GAS float* p) {
+  const f32x4 v = *(const GAS f32x4*)p;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st4g(GAS float* p, const float4& v) {
+  f32x4 w;
+  w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+  *(GAS f32x4*)p = w;
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -41,14 +70,23 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// Deterministic per-workgroup sum (tree inside waves, fixed wave order).
+__device__ __forceinline__ float wg_sum(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return r;
+}
+
 // Ordered-int key of a float: monotone under signed int comparison.
 __device__ __forceinline__ int fkey(float f) {
   int i = __float_as_int(f);
   return i >= 0 ? i : i ^ 0x7FFFFFFF;
 }
-__device__ __forceinline__ float unkey(int k) {
-  return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF);
-}
+__device__ __forceinline__ float unkey(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
 
 // Philox4x32-10 counter-based RNG.
 __device__ __forceinline__ uint4 philox(uint2 key, uint4 c) {
@@ -71,76 +109,11 @@ __device__ __forceinline__ float normal_from(unsigned a, unsigned b) {
 
 // AvgL1Norm denominator from column-tile partial |x| sums (fixed order).
 __device__ __forceinline__ float norm_m(const float* part, int ld, int row, int nparts, int width) {
+  const GAS float* p = G(part);
   float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(size_t)p * ld + row];
-  float m = s / (float)width;
+  for (int q = 0; q < nparts; ++q) s += p[(size_t)q * ld + row];
+  const float m = s / (float)width;
   return m < 1e-8f ? 1e-8f : m;
-}
-
-// ---------------------------------------------------------------- GEMM
-
-struct OpTables {
-  float inv_lane[kMaxSeg];      // contiguous+normed segs: 1/m for this lane's x
-  int tab_off[kMaxSeg];         // strided+normed segs: LDS table offset (or -1)
-};
-
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-
-__device__ __forceinline__ float4 load_operand(const Operand& op, int x, int r, const OpTables& tb,
-                                               const float* tabs) {
-  for (int s = 0; s < op.nseg; ++s) {
-    const Seg& sg = op.seg[s];
-    if (x >= sg.x0 && x < sg.x1 && r >= sg.r0 && r < sg.r1) {
-      float4 v;
-      if (!sg.strided) {
-        v = ld4(sg.p + (size_t)(x - sg.x0) * sg.ld + (r - sg.r0));
-        if (sg.norm) {
-          float iv = tb.inv_lane[s];
-          v.x *= iv; v.y *= iv; v.z *= iv; v.w *= iv;
-        }
-      } else {
-        const float* q = sg.p + (size_t)(r - sg.r0) * sg.ld + (x - sg.x0);
-        const int nr = sg.r1 - r;  // rows past r1 (reduction padding) read as zero
-        v.x = q[0];
-        v.y = nr > 1 ? q[sg.ld] : 0.f;
-        v.z = nr > 2 ? q[2 * sg.ld] : 0.f;
-        v.w = nr > 3 ? q[3 * sg.ld] : 0.f;
-        if (sg.norm) {
-          const float* t = tabs + tb.tab_off[s] + (r - sg.r0);
-          v.x *= t[0];
-          if (nr > 1) v.y *= t[1];
-          if (nr > 2) v.z *= t[2];
-          if (nr > 3) v.w *= t[3];
-        }
-      }
-      return v;
-    }
-  }
-  return make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-// Builds per-lane inverse norms and LDS tables for normed segments.
-__device__ void prep_tables(const Operand& op, int x, OpTables& tb, float* tabs, int& tab_used) {
-  for (int s = 0; s < kMaxSeg; ++s) {
-    tb.inv_lane[s] = 1.f;
-    tb.tab_off[s] = -1;
-  }
-  for (int s = 0; s < op.nseg; ++s) {
-    const Seg& sg = op.seg[s];
-    if (!sg.norm) continue;
-    if (!sg.strided) {
-      if (x >= sg.x0 && x < sg.x1)
-        tb.inv_lane[s] = 1.f / norm_m(sg.norm, sg.norm_ld, x - sg.x0 + sg.norm_row0, sg.norm_nparts,
-                                      sg.norm_width);
-    } else {
-      int n = sg.r1 - sg.r0;
-      tb.tab_off[s] = tab_used;
-      for (int i = threadIdx.x; i < n; i += kThreads)
-        tabs[tab_used + i] =
-            1.f / norm_m(sg.norm, sg.norm_ld, i + sg.norm_row0, sg.norm_nparts, sg.norm_width);
-      tab_used += (n + 3) & ~3;
-    }
-  }
 }
 
 __device__ __forceinline__ float act_fwd(int act, float v) {
@@ -163,120 +136,375 @@ __device__ __forceinline__ float act_bwd(int act, float saved) {
   }
 }
 
-__device__ void op_gemm(const GemmArgs& g, int t, float* smem) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int it = t / g.tiles_n, jt = t - it * g.tiles_n;
-  const int i0 = it * kTile, j0 = jt * kTile;
-  const bool bias_tile = (g.epi == EPI_ADAM) && (j0 >= g.adam.bias_col);
-  float* red = smem;             // [4][256]
-  float* tabs = smem + 4 * 256;  // normalisation tables
-  const int xa = i0 + (lane & 15), xb = j0 + (lane & 15), rl = 4 * (lane >> 4);
+// LDS table of 1/m for n consecutive rows of a normed tensor (out of line: keeps
+// the GEMM main loops' register allocation independent of this rare prologue).
+__device__ __forceinline__ void build_norm_tab(const float* part, int ld, int row0, int nparts,
+                                                         int width, int n, float* dst) {
+#pragma unroll 1
+  for (int i = threadIdx.x; i < n; i += kThreads) dst[i] = 1.f / norm_m(part, ld, i + row0, nparts, width);
+#pragma unroll 1
+  for (int i = n + threadIdx.x; i < ((n + 15) & ~15); i += kThreads) dst[i] = 0.f;
+}
 
-  OpTables ta, tbb;
-  int used = 0;
-  prep_tables(g.A, xa, ta, tabs, used);
-  if (!bias_tile) prep_tables(g.B, xb, tbb, tabs, used);
-  if (used) __syncthreads();
+// ---------------------------------------------------------------- GEMM
+//
+// One workgroup = one 16 x 64 output tile; wave w owns columns [16w, 16w+16)
+// and the FULL reduction.  Each lane owns one output row (operand A) and one
+// output column (operand B) of the v_mfma_f32_16x16x4_f32 fragment and
+// streams 4 consecutive reduction indices per 16-wide chunk: a contiguous
+// operand is one 16-byte buffer load per lane per chunk, a strided one four
+// 4-byte loads.  Operand segments are 16-aligned in BOTH the reduction and
+// the operand-row dimension (host invariant, checked in engine.cpp), so the
+// segment of a chunk is wave-uniform: it is selected with scalar compares
+// and addressed through a buffer resource built from SGPRs.  Lanes and
+// reduction rows outside the segment get an out-of-range voffset, which the
+// buffer unit returns as 0 -- the main loop has no branches around its loads,
+// so the 4-chunk register ring (loads for chunk c+4 issue right after chunk
+// c's MFMAs) survives s_waitcnt placement.  AvgL1Norm scales (deferred
+// normalisation) are applied when a chunk is consumed, never when it is
+// loaded.  Epilogue operands (bias, derivative source, Adam m/v/param) are
+// fetched before the main loop; the epilogue runs from registers (lane: rows
+// 4*(l>>4)+q, column l&15).
 
-  const int nch = (g.R + 15) >> 4;
-  const int c0 = (nch * wave) >> 2, c1 = (nch * (wave + 1)) >> 2;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const float bone = (xb == g.adam.bias_col) ? 1.f : 0.f;
-  for (int c = c0; c < c1; ++c) {
-    const int r = c * 16 + rl;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-    if (xa < g.M && r < g.R) a = load_operand(g.A, xa, r, ta, tabs);
-    if (bias_tile) {
-      if (r < g.R) b = make_float4(bone, bone, bone, bone);
-    } else if (xb < g.N && r < g.R) {
-      b = load_operand(g.B, xb, r, tbb, tabs);
-    }
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
-  }
-  // C layout (16x16x4): lane l holds rows 4*(l>>4)+q, col l&15.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+static_assert(kMaxSeg == 4, "LaneOp holds 4 segments");
+constexpr int kOOB = 0x7ffffff0;  // voffset beyond any num_records: the load returns 0
+
+struct LaneOp {
+  f32x4 inv;  // contiguous + normed: 1/m of the lane's row, per segment (vector, not array:
+              // a per-chunk select must stay in registers)
+  i32x4 tab;  // strided + normed: LDS offset of the segment's 1/m table, -1 = none
+  int xw;     // first operand row/column of this wave (wave-uniform)
+  bool norm;  // any normed segment
+};
+
+__device__ __forceinline__ void lane_op(const CAS Operand& op, bool STRIDED, int x, int xw, LaneOp& L,
+                                        float* tabs, int& used) {
+  L.inv = f32x4{1.f, 1.f, 1.f, 1.f};
+  L.tab = i32x4{-1, -1, -1, -1};
+  L.xw = xw;
+  L.norm = false;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) red[wave * 256 + (4 * (lane >> 4) + q) * 16 + (lane & 15)] = acc[q];
-  __syncthreads();
-  float v = red[tid] + red[256 + tid] + red[512 + tid] + red[768 + tid];
-  const int row = tid >> 4, col = tid & 15;
-  const int i = i0 + row, j = j0 + col;
+  for (int s = 0; s < kMaxSeg; ++s) {
+    if (s < op.nseg) {
+      const CAS Seg& sg = op.seg[s];
+      if (sg.norm) {
+        L.norm = true;
+        if (!STRIDED) {
+          if (x >= sg.x0 && x < sg.x1)
+            L.inv[s] = 1.f / norm_m(sg.norm, sg.norm_ld, x - sg.x0 + sg.norm_row0, sg.norm_nparts, sg.norm_width);
+        } else {
+          const int n = sg.r1 - sg.r0;
+          L.tab[s] = used;
+          build_norm_tab(sg.norm, sg.norm_ld, sg.norm_row0, sg.norm_nparts, sg.norm_width, n, tabs + used);
+          used += (n + 15) & ~15;
+        }
+      }
+    }
+  }
+}
+
+// v[q] for a wave-uniform q as a select chain (a variable extract is lowered to scratch).
+template <class V>
+__device__ __forceinline__ auto pick(const V& v, int q) -> decltype(v[0] + 0) {
+  return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
+}
+
+__device__ __forceinline__ float4 as_f4(u32x4 v) {
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+// Load cursor of one operand: walks the reduction chunk by chunk, segment after
+// segment (segments are 16-aligned and back to back in the reduction, host
+// invariant), so a chunk costs one voffset add and a counter decrement; the
+// segment switch (scalar descriptor loads) happens once per segment.
+template <bool STRIDED>
+struct Cursor {
+  __amdgpu_buffer_rsrc_t rs;  // current segment (wave-uniform)
+  int voff;                   // this lane's byte offset of the next chunk
+  int step;                   // bytes per chunk
+  int left;                   // chunks left in the segment
+  int s;                      // segment index (nseg: past the end)
+  int ldb;                    // strided: bytes per reduction row
+  int rrem;                   // strided: segment rows left from this lane's first row
+  int toff;                   // strided + normed: LDS 1/m table offset of the next chunk (-1: none)
+  float inv;                  // contiguous + normed: lane row's 1/m in the segment
+
+  __device__ __forceinline__ void open(const CAS Operand& op, const LaneOp& L, int x, int rl, int q, int x0) {
+    s = q;
+    if (q >= op.nseg) {  // past the last segment: everything reads as 0
+      rs = __builtin_amdgcn_make_buffer_rsrc((void*)nullptr, 0, 0, 0x00020000);
+      left = 1 << 30;
+      voff = 0;
+      step = 0;
+      rrem = 0;
+      toff = -1;
+      inv = 1.f;
+      return;
+    }
+    const CAS Seg& sg = op.seg[q];
+    rs = __builtin_amdgcn_make_buffer_rsrc((void*)sg.p, 0, 0x7fff0000, 0x00020000);
+    const int n = sg.r1 - sg.r0;
+    left = (n + 15) >> 4;
+    if (!STRIDED) {
+      voff = ((x - x0) * sg.ld + rl) * 4;
+      step = 64;
+      inv = pick(L.inv, q);
+      toff = -1;
+    } else {
+      ldb = sg.ld * 4;
+      voff = (x - x0) * 4 + rl * ldb;
+      step = 16 * ldb;
+      rrem = n - rl;
+      toff = pick(L.tab, q);
+      inv = 1.f;
+    }
+  }
+  // Loads this lane's 4 values of the next chunk; returns the chunk's norm
+  // scale handle (contiguous: 1/m, strided: table offset) through inv_out/toff_out.
+  __device__ __forceinline__ float4 next(const CAS Operand& op, const LaneOp& L, int x, int rl, int x0, bool ok,
+                                         float& inv_out, int& toff_out) {
+    if (left == 0) open(op, L, x, rl, s + 1, x0);
+    float4 v;
+    if (!STRIDED) {
+      v = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rs, ok ? voff : kOOB, 0, 0));
+    } else {
+      v.x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && rrem > 0 ? voff : kOOB, 0, 0));
+      v.y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && rrem > 1 ? voff + ldb : kOOB, 0, 0));
+      v.z = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && rrem > 2 ? voff + 2 * ldb : kOOB, 0, 0));
+      v.w = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && rrem > 3 ? voff + 3 * ldb : kOOB, 0, 0));
+      rrem -= 16;
+    }
+    inv_out = inv;
+    toff_out = toff;
+    if (STRIDED && toff >= 0) toff += 16;
+    voff += step;
+    --left;
+    return v;
+  }
+};
+
+// Deferred AvgL1Norm of a consumed chunk.
+template <bool STRIDED>
+__device__ __forceinline__ float4 chunk_scale(float4 v, float inv, int toff, int rl, const float* tabs) {
+  if (!STRIDED) {
+    v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+  } else if (toff >= 0) {
+    const float4 w = *(const float4*)(tabs + toff + rl);
+    v.x *= w.x; v.y *= w.y; v.z *= w.z; v.w *= w.w;
+  }
+  return v;
+}
+
+__device__ __forceinline__ f32x4 mfma4(const float4& a, const float4& b, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+  return acc;
+}
+
+// Main loop, one instantiation per operand layout (FWD <0,0>, DX <0,1>, DW <1,1>,
+// DW bias column <1,-,1> with B = ones).  xa_w / xb_w: the wave's first A row / B
+// column (wave-uniform).
+template <bool SA, bool SB, bool BIAS>
+__device__ __forceinline__ f32x4 gemm_mainloop(const CAS GemmArgs& g, int xa, int xb, int xa_w, int xb_w,
+                                               bool active, float* tabs) {
+  const int lane = threadIdx.x & 63;
+  LaneOp la, lb;
+  int used = 0;
+  lane_op(g.A, SA, xa, xa_w, la, tabs, used);
+  if (!BIAS) lane_op(g.B, SB, xb, xb_w, lb, tabs, used);
+  if (used) __syncthreads();
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  if (!active) return acc0;
+  const bool a_ok = xa < g.M;
+  const bool b_ok = BIAS ? (xb == g.adam.bias_col) : (xb < g.N);
+  const int rl = 4 * (lane >> 4);
+  const int nch = (g.R + 15) >> 4;
+  const bool an = la.norm, bn = !BIAS && lb.norm;
+  // B of a DW op: the segments split the columns; the wave's 16 columns lie in one of them.
+  int qb = 0, xb0 = 0;
+  if (SA && SB && !BIAS) {
+#pragma unroll
+    for (int q = 0; q < kMaxSeg; ++q)
+      if (q < g.B.nseg && xb_w >= g.B.seg[q].x0 && xb_w < g.B.seg[q].x1) qb = q;
+    xb0 = g.B.seg[qb].x0;
+  }
+  Cursor<SA> ca;
+  Cursor<SB> cb;
+  ca.open(g.A, la, xa, rl, 0, 0);
+  if (!BIAS) cb.open(g.B, lb, xb, rl, qb, xb0);
+  const int nb_end = (SA && SB) ? qb + 1 : g.B.nseg;  // DW: one B segment only
+  const float4 ones = b_ok ? make_float4(1.f, 1.f, 1.f, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+  auto ldA = [&](float& i, int& t) { return ca.next(g.A, la, xa, rl, 0, a_ok, i, t); };
+  auto ldB = [&](float& i, int& t) {
+    if constexpr (BIAS) return ones;  // db = sum_r dZ(r, n); A is zero past R
+    else {
+      if (cb.left == 0 && cb.s + 1 >= nb_end) cb.s = kMaxSeg;  // DW: never walk into another column block
+      return cb.next(g.B, lb, xb, rl, xb0, b_ok, i, t);
+    }
+  };
+  auto use = [&](float4 a, float4 b, float ia, int ta, float ib, int tb, f32x4 acc) {
+    if (an) a = chunk_scale<SA>(a, ia, ta, rl, tabs);
+    if (bn) b = chunk_scale<SB>(b, ib, tb, rl, tabs);
+    return mfma4(a, b, acc);
+  };
+  float ia0, ia1, ia2, ia3, ib0, ib1, ib2, ib3;
+  int ta0, ta1, ta2, ta3, tb0, tb1, tb2, tb3;
+  float4 a0 = ldA(ia0, ta0), b0 = ldB(ib0, tb0), a1 = ldA(ia1, ta1), b1 = ldB(ib1, tb1);
+  float4 a2 = ldA(ia2, ta2), b2 = ldB(ib2, tb2), a3 = ldA(ia3, ta3), b3 = ldB(ib3, tb3);
+#pragma unroll 1
+  for (int c = 0; c < nch; c += 4) {
+    acc0 = use(a0, b0, ia0, ta0, ib0, tb0, acc0);
+    a0 = ldA(ia0, ta0); b0 = ldB(ib0, tb0);
+    acc1 = use(a1, b1, ia1, ta1, ib1, tb1, acc1);
+    a1 = ldA(ia1, ta1); b1 = ldB(ib1, tb1);
+    acc0 = use(a2, b2, ia2, ta2, ib2, tb2, acc0);
+    a2 = ldA(ia2, ta2); b2 = ldB(ib2, tb2);
+    acc1 = use(a3, b3, ia3, ta3, ib3, tb3, acc1);
+    a3 = ldA(ia3, ta3); b3 = ldB(ib3, tb3);
+  }
+  return acc0 + acc1;
+}
+
+__device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* smem) {
+  // wave index via readfirstlane: the compiler then treats every wave-derived
+  // condition as uniform (scalar branches; divergent-region structurisation of the
+  // four inlined main loops otherwise keeps all of them live: ~250 VGPRs)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int it = t / g.tiles_n, jt = t - it * g.tiles_n;
+  const int i0 = it * kTileM, j0 = jt * kTileN + wave * 16;
+  const bool bias_tile = (g.epi == EPI_ADAM) && (jt * kTileN >= g.adam.bias_col);
+  float* red = smem;            // [64] reduction scratch
+  float* tabs = smem + 64;      // normalisation tables
+  const int xa = i0 + (lane & 15), xb = j0 + (lane & 15);
+  const int j = xb;                       // output column of this lane
+  const int ib = i0 + 4 * (lane >> 4);    // first of this lane's 4 output rows
+  const bool jok = bias_tile ? (j == g.adam.bias_col) : (j < g.N);
+  const bool active = bias_tile ? (wave == 0) : (j0 < g.N);  // wave-uniform
+
+  // ---- epilogue operands fetched ahead of the main loop
+  float pre_b = 0.f, ds[4] = {1.f, 1.f, 1.f, 1.f}, pp[4] = {0.f, 0.f, 0.f, 0.f}, mm[4] = {0.f, 0.f, 0.f, 0.f},
+        vv[4] = {0.f, 0.f, 0.f, 0.f};
+  GAS float* ptr[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (g.epi != EPI_ADAM) {
+    if (g.bias && jok) pre_b = G(g.bias)[j];
+    if (g.dsrc && jok) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (ib + q < g.M) ds[q] = G(g.dsrc)[(size_t)(ib + q) * g.lddact + j];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = ib + q;
+      if (jok && i < g.M) ptr[q] = bias_tile ? GW(g.adam.b) + i : GW(g.adam.w) + (size_t)i * g.adam.ldw + j;
+      if (ptr[q]) {
+        pp[q] = *ptr[q];
+        mm[q] = ptr[q][g.adam.mo];
+        vv[q] = ptr[q][g.adam.vo];
+      }
+    }
+  }
+
+  const int xa_w = i0, xb_w = j0;  // wave-uniform operand origins
+  // The distinct empty asm statements head each arm so the compiler cannot hoist
+  // the arms' common descriptor loads above the branch (that keeps all four
+  // main loops' scalar state live at once and spills it into ~150 extra VGPRs).
+  f32x4 acc;
+  if (g.mode == GEMM_FWD) {
+    asm volatile("; gemm fwd" ::);
+    acc = gemm_mainloop<false, false, false>(g, xa, xb, xa_w, xb_w, active, tabs);
+  } else if (g.mode == GEMM_DX) {
+    asm volatile("; gemm dx" ::);
+    acc = gemm_mainloop<false, true, false>(g, xa, xb, xa_w, xb_w, active, tabs);
+  } else if (!bias_tile) {
+    asm volatile("; gemm dw" ::);
+    acc = gemm_mainloop<true, true, false>(g, xa, xb, xa_w, xb_w, active, tabs);
+  } else {
+    asm volatile("; gemm db" ::);
+    acc = gemm_mainloop<true, true, true>(g, xa, xb, xa_w, xb_w, active, tabs);
+  }
 
   if (g.epi == EPI_STORE) {
-    float y = 0.f;
-    const bool ok = (i < g.M) && (j < g.N);
-    if (ok) {
-      if (g.bias) v += g.bias[j];
-      if (g.pre) g.pre[(size_t)i * g.ldpre + j] = v;
-      y = act_fwd(g.act, v);
-      if (g.noise && i >= g.noise_row0) {
-        float e = g.noise[(size_t)(i - g.noise_row0) * g.ldnoise + j] * g.noise_sigma;
-        e = fminf(fmaxf(e, -g.noise_clip), g.noise_clip);
-        y = fminf(fmaxf(y + e, -1.f), 1.f);
-      }
-      if (g.dsrc) y *= act_bwd(g.dact, g.dsrc[(size_t)i * g.lddact + j]);
-      g.out[(size_t)i * g.ldo + j] = y;
-    }
-    if (g.norm_out) {
-      float s = ok ? fabsf(y) : 0.f;
+    float rowabs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-      if (col == 0 && i < g.M) g.norm_out[(size_t)jt * g.norm_ld + i] = s;
+    for (int q = 0; q < 4; ++q) {
+      const int i = ib + q;
+      if (i < g.M && jok) {
+        const float v = acc[q] + pre_b;
+        if (g.pre) GW(g.pre)[(size_t)i * g.ldpre + j] = v;
+        float y = act_fwd(g.act, v);
+        if (g.noise && i >= g.noise_row0) {  // target policy smoothing (td7.py:188-194)
+          float e = G(g.noise)[(size_t)(i - g.noise_row0) * g.ldnoise + j] * g.noise_sigma;
+          e = fminf(fmaxf(e, -g.noise_clip), g.noise_clip);
+          y = fminf(fmaxf(y + e, -1.f), 1.f);
+        }
+        if (g.dsrc) y *= act_bwd(g.dact, ds[q]);
+        GW(g.out)[(size_t)i * g.ldo + j] = y;
+        rowabs[q] = fabsf(y);
+      }
     }
-  } else if (g.epi == EPI_MSE) {
+    if (g.norm_out) {  // |y| summed over the tile's 64 columns, per row
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) rowabs[q] += __shfl_xor(rowabs[q], o, 64);
+      }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[wave * 16 + 4 * (lane >> 4) + q] = rowabs[q];
+      }
+      __syncthreads();
+      if (tid < 16 && i0 + tid < g.M)
+        GW(g.norm_out)[(size_t)jt * g.norm_ld + i0 + tid] =
+            (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
+    }
+  } else if (g.epi == EPI_MSE) {  // td7.py:256 encoder loss, grad wrt zsa
     float d2 = 0.f;
-    if (i < g.M && j < g.N) {
-      if (g.bias) v += g.bias[j];
-      const Seg& sg = g.tgt;
-      float tv = sg.p[(size_t)(i - sg.x0) * sg.ld + j];
-      if (sg.norm)
-        tv *= 1.f / norm_m(sg.norm, sg.norm_ld, i - sg.x0 + sg.norm_row0, sg.norm_nparts, sg.norm_width);
-      float d = v - tv;
-      g.out[(size_t)i * g.ldo + j] = (2.f * d) * g.mse_scale;  // mse_scale = 1/n
-      d2 = d * d;
+    const CAS Seg& sg = g.tgt;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = ib + q;
+      if (i < g.M && jok) {
+        const float v = acc[q] + pre_b;
+        float tv = G(sg.p)[(size_t)(i - sg.x0) * sg.ld + j];
+        if (sg.norm) tv *= 1.f / norm_m(sg.norm, sg.norm_ld, i - sg.x0 + sg.norm_row0, sg.norm_nparts, sg.norm_width);
+        const float d = v - tv;
+        GW(g.out)[(size_t)i * g.ldo + j] = (2.f * d) * g.mse_scale;  // mse_scale = 1/n
+        d2 += d * d;
+      }
     }
-    d2 = wave_sum(d2);
-    __syncthreads();
-    if (lane == 0) red[wave] = d2;
-    __syncthreads();
-    if (tid == 0) g.loss_part[t] = red[0] + red[1] + red[2] + red[3];
+    d2 = wg_sum(d2, red);
+    if (tid == 0) GW(g.loss_part)[t] = d2;
   } else {  // EPI_ADAM (torch.optim.Adam single-tensor law, see oracle/agents.py)
-    const AdamArgs& ad = g.adam;
-    float* p = nullptr;
-    if (bias_tile) {
-      if (j == ad.bias_col && i < g.M) p = ad.b + i;
-    } else if (i < g.M && j < g.N) {
-      p = ad.w + (size_t)i * ad.ldw + j;
-    }
+    const CAS AdamArgs& ad = g.adam;
+    const double tt = (double)(*G(ad.t) + 1);
+    const double bc1 = 1.0 - pow((double)ad.beta1, tt);
+    const double bc2 = 1.0 - pow((double)ad.beta2, tt);
+    const float step_size = (float)((double)ad.lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
     float gg = 0.f;
-    if (p) {
-      const double tt = (double)(*ad.t + 1);
-      const double bc1 = 1.0 - pow((double)ad.beta1, tt);
-      const double bc2 = 1.0 - pow((double)ad.beta2, tt);
-      const float step_size = (float)((double)ad.lr / bc1);
-      const float bc2s = (float)sqrt(bc2);
-      float* m = p + ad.mo;
-      float* vv = p + ad.vo;
-      float mm = *m, v2 = *vv;
-      mm = mm + (1.f - ad.beta1) * (v - mm);
-      v2 = v2 * ad.beta2 + ((1.f - ad.beta2) * v) * v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!ptr[q]) continue;
+      const float gv = acc[q];
+      float m = mm[q], v2 = vv[q];
+      m = m + (1.f - ad.beta1) * (gv - m);
+      v2 = v2 * ad.beta2 + ((1.f - ad.beta2) * gv) * gv;
       const float denom = sqrtf(v2) / bc2s + ad.eps;
-      *m = mm;
-      *vv = v2;
-      *p = *p + (-step_size * mm) / denom;
-      gg = v * v;
+      ptr[q][ad.mo] = m;
+      ptr[q][ad.vo] = v2;
+      *ptr[q] = pp[q] + (-step_size * m) / denom;
+      gg += gv * gv;
     }
     if (ad.gsq) {
-      gg = wave_sum(gg);
-      __syncthreads();
-      if (lane == 0) red[wave] = gg;
-      __syncthreads();
+      gg = wg_sum(gg, red);
       if (tid == 0) {
-        float s = red[0] + red[1] + red[2] + red[3];
-        if (bias_tile) ad.gsq_b[it] = s;
-        else ad.gsq[it * (g.tiles_n - 1) + jt] = s;
+        if (bias_tile) GW(ad.gsq_b)[it] = gg;
+        else GW(ad.gsq)[it * (g.tiles_n - 1) + jt] = gg;
       }
     }
   }
@@ -284,70 +512,91 @@ __device__ void op_gemm(const GemmArgs& g, int t, float* smem) {
 
 // ---------------------------------------------------------------- AvgL1Norm backward
 
-__device__ void op_normbwd(const NormBwdArgs& a, int t) {
+__device__ __forceinline__ void op_normbwd(const CAS NormBwdArgs& a, int t) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = t * 4 + wave;
   if (row >= a.rows) return;
-  const float* x = a.x + (size_t)row * a.ldx;
-  const float* g = a.g + (size_t)row * a.ldg;
+  const GAS float* x = G(a.x) + (size_t)row * a.ldx;
+  const GAS float* g = G(a.g) + (size_t)row * a.ldg;
   // m recomputed from the same partials the forward consumers used
   float s = 0.f;
-  for (int p = 0; p < a.norm_nparts; ++p) s += a.norm[(size_t)p * a.norm_ld + row + a.norm_row0];
+  for (int q = 0; q < a.norm_nparts; ++q) s += G(a.norm)[(size_t)q * a.norm_ld + row + a.norm_row0];
   const float mean = s / (float)a.width;
   const bool clamped = mean < 1e-8f;
-  const float m = clamped ? 1e-8f : mean;
-  const float inv = 1.f / m;
+  const float inv = 1.f / (clamped ? 1e-8f : mean);
+  float xv[8], gv[8];
   float dot = 0.f;
-  for (int k = lane; k < a.width; k += 64) dot += g[k] * x[k];
+  const int per = (a.width + 63) / 64;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int k = lane + 64 * u;
+    xv[u] = (u < per && k < a.width) ? x[k] : 0.f;
+    gv[u] = (u < per && k < a.width) ? g[k] : 0.f;
+    dot += gv[u] * xv[u];
+  }
   dot = wave_sum(dot);
   // y = x / m: dy/dx path g/m ; dm path -(sum g x)/m^2 * sign(x)/n (unless clamped)
   const float gm = clamped ? 0.f : (-dot * inv * inv) / (float)a.width;
-  float* dx = a.dx + (size_t)row * a.lddx;
-  for (int k = lane; k < a.width; k += 64) {
-    const float xv = x[k];
-    const float sg = xv > 0.f ? 1.f : (xv < 0.f ? -1.f : 0.f);
-    dx[k] = g[k] * inv + sg * gm;
+  GAS float* dx = GW(a.dx) + (size_t)row * a.lddx;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int k = lane + 64 * u;
+    if (u < per && k < a.width) {
+      const float sg = xv[u] > 0.f ? 1.f : (xv[u] < 0.f ? -1.f : 0.f);
+      dx[k] = gv[u] * inv + sg * gm;
+    }
   }
 }
 
 // ---------------------------------------------------------------- critic heads
 
-__device__ void op_head(const HeadArgs& h, int t, float* smem) {
+__device__ __forceinline__ void op_head(const CAS HeadArgs& h, int t, float* smem) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = t * 4 + wave;
   float acc0 = 0.f, acc1 = 0.f;  // per-row loss terms
   float ykey = 0.f;
-  bool valid = b < h.rows;
+  const bool valid = b < h.rows;
   if (valid) {
     float q[2];
+    float wv[2][8];
+    const int per = (h.H + 63) / 64;
+#pragma unroll
     for (int n = 0; n < 2; ++n) {
-      const float* hr = h.h[n] + (size_t)b * h.ldh;
+      const GAS float* hr = G(h.h[n]) + (size_t)b * h.ldh;
+      const GAS float* wr = G(h.w[n]);
       float s = 0.f;
-      for (int k = lane; k < h.H; k += 64) s += hr[k] * h.w[n][k];
-      q[n] = wave_sum(s) + h.b[n][0];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = lane + 64 * u;
+        const bool in = u < per && k < h.H;
+        wv[n][u] = in ? wr[k] : 0.f;
+        s += (in ? hr[k] : 0.f) * wv[n][u];
+      }
+      q[n] = wave_sum(s) + G(h.b[n])[0];
     }
     float dq[2] = {0.f, 0.f};
     bool want_dz = false;
     switch (h.mode) {
-      case HEAD_TD7_TARGET: {
+      case HEAD_TD7_TARGET: {  // td7.py:211-218
         float v = fminf(q[0], q[1]);
-        v = fminf(fmaxf(v, h.vt[1]), h.vt[0]);
-        float y = h.reward[b] + (h.gamma * v) * h.notdone[b];
-        if (lane == 0) h.y[b] = y;
+        v = fminf(fmaxf(v, G(h.vt)[1]), G(h.vt)[0]);
+        const float y = G(h.reward)[b] + (h.gamma * v) * G(h.notdone)[b];
+        if (lane == 0) GW(h.y)[b] = y;
         ykey = y;
         break;
       }
-      case HEAD_MLP_TARGET: {
+      case HEAD_MLP_TARGET: {  // td3.py:160-164, sac.py:188-193
         float v = fminf(q[0], q[1]);
-        if (h.sac) v = v - expf(h.log_alpha[0]) * h.logpi[b];
-        float y = h.reward[b] + (h.gamma * v) * h.notdone[b];
-        if (lane == 0) h.y[b] = y;
+        if (h.sac) v = v - expf(G(h.log_alpha)[0]) * G(h.logpi)[b];
+        const float y = G(h.reward)[b] + (h.gamma * v) * G(h.notdone)[b];
+        if (lane == 0) GW(h.y)[b] = y;
         break;
       }
       case HEAD_TD7_LOSS:
-      case HEAD_MLP_LOSS: {
-        const float y = h.y[b];
+      case HEAD_MLP_LOSS: {  // td7.py:231-244, td3.py:169-182
+        const float y = G(h.y)[b];
         float dmax = 0.f;
+#pragma unroll
         for (int n = 0; n < 2; ++n) {
           const float diff = q[n] - y;
           if (h.lap) {
@@ -363,25 +612,25 @@ __device__ void op_head(const HeadArgs& h, int t, float* smem) {
             dq[n] = -e * h.inv_b;
           }
         }
-        if (h.lap && lane == 0) h.prio[b] = (float)pow((double)fmaxf(dmax, 1.f), 0.4);
+        if (h.lap && lane == 0) GW(h.prio)[b] = (float)pow((double)fmaxf(dmax, 1.f), 0.4);
         want_dz = true;
         break;
       }
-      case HEAD_TD7_POLICY: {
+      case HEAD_TD7_POLICY: {  // td7.py:274-275
         acc0 = q[0] + q[1];
         dq[0] = dq[1] = -0.5f * h.inv_b;
         want_dz = true;
         break;
       }
-      case HEAD_MLP_POLICY: {
+      case HEAD_MLP_POLICY: {  // td3.py:191, sac.py:227-229
         const float mn = fminf(q[0], q[1]);
         // torch.minimum backward: ties split the gradient
-        const float g = -h.inv_b;
-        dq[0] = q[0] < q[1] ? g : (q[0] == q[1] ? 0.5f * g : 0.f);
-        dq[1] = q[1] < q[0] ? g : (q[0] == q[1] ? 0.5f * g : 0.f);
+        const float gq = -h.inv_b;
+        dq[0] = q[0] < q[1] ? gq : (q[0] == q[1] ? 0.5f * gq : 0.f);
+        dq[1] = q[1] < q[0] ? gq : (q[0] == q[1] ? 0.5f * gq : 0.f);
         if (h.sac) {
-          const float lp = h.logpi[b];
-          acc0 = -mn + lp * expf(h.log_alpha[0]);
+          const float lp = G(h.logpi)[b];
+          acc0 = -mn + lp * expf(G(h.log_alpha)[0]);
           acc1 = lp;
         } else {
           acc0 = mn;
@@ -391,11 +640,16 @@ __device__ void op_head(const HeadArgs& h, int t, float* smem) {
       }
     }
     if (want_dz) {
+#pragma unroll
       for (int n = 0; n < 2; ++n) {
-        if (lane == 0 && h.dq[n]) h.dq[n][b] = dq[n];
-        const float* ds = h.dsrc[n] + (size_t)b * h.ldd;
-        float* dz = h.dz[n] + (size_t)b * h.lddz;
-        for (int k = lane; k < h.H; k += 64) dz[k] = (dq[n] * h.w[n][k]) * act_bwd(h.dact, ds[k]);
+        if (lane == 0 && h.dq[n]) GW(h.dq[n])[b] = dq[n];
+        const GAS float* ds = G(h.dsrc[n]) + (size_t)b * h.ldd;
+        GAS float* dz = GW(h.dz[n]) + (size_t)b * h.lddz;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = lane + 64 * u;
+          if (u < per && k < h.H) dz[k] = (dq[n] * wv[n][u]) * act_bwd(h.dact, ds[k]);
+        }
       }
     }
   }
@@ -411,10 +665,13 @@ __device__ void op_head(const HeadArgs& h, int t, float* smem) {
   __syncthreads();
   if (threadIdx.x == 0) {
     if (h.loss_part) {
-      h.loss_part[t * 4 + 0] = red[0] + red[2] + red[4] + red[6];
-      h.loss_part[t * 4 + 1] = red[1] + red[3] + red[5] + red[7];
+      GAS float* lp = GW(h.loss_part);
+      lp[t * 4 + 0] = (red[0] + red[2]) + (red[4] + red[6]);
+      lp[t * 4 + 1] = (red[1] + red[3]) + (red[5] + red[7]);
+      lp[t * 4 + 2] = 0.f;
+      lp[t * 4 + 3] = 0.f;
     }
-    if (h.mode == HEAD_TD7_TARGET) {
+    if (h.mode == HEAD_TD7_TARGET) {  // value_max / value_min tracking (td7.py:217-218)
       int mx = ired[0], mn = ired[1];
       for (int w = 1; w < 4; ++w) {
         mx = max(mx, ired[2 * w]);
@@ -430,79 +687,107 @@ __device__ void op_head(const HeadArgs& h, int t, float* smem) {
 
 constexpr int kBlk = 4096;  // priorities per block-sum
 
-__device__ void op_sample_reduce(const SampleArgs& s, int t, float* smem) {
-  const long long size = *s.size;
+// Exact fp64 block sums of the priorities (lap.py:47; Q8: any-order fp64 is exact).
+__device__ __forceinline__ void op_sample_reduce(const CAS SampleArgs& s, int t, float* smem) {
+  const long long size = *G(s.size);
   const long long base = (long long)t * kBlk;
   double acc = 0.0;
-  for (int k = threadIdx.x; k < kBlk; k += kThreads) {
-    long long i = base + k;
-    if (i < size) acc += (double)s.priority[i];
+#pragma unroll
+  for (int u = 0; u < kBlk / (4 * kThreads); ++u) {
+    const long long k = base + (long long)(u * kThreads + threadIdx.x) * 4;
+    if (k + 3 < size) {
+      const float4 v = ld4g(G(s.priority) + k);
+      acc += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (k + e < size) acc += (double)G(s.priority)[k + e];
+    }
   }
   acc = wave_sum_d(acc);
   double* dred = reinterpret_cast<double*>(smem);
   if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) s.bsum[t] = dred[0] + dred[1] + dred[2] + dred[3];
+  if (threadIdx.x == 0) GW(s.bsum)[t] = (dred[0] + dred[1]) + (dred[2] + dred[3]);
 }
 
-__device__ void op_sample_gather(const SampleArgs& s, int b, float* smem) {
+// Exclusive scan of 256 per-thread doubles held in LDS, by one wave, fixed order.
+__device__ __forceinline__ void scan256(double* tsum) {
   const int tid = threadIdx.x;
-  const long long size = *s.size;
-  const int tape = *s.tape_mode;
-  const long long pos = *s.tape_pos;
+  if (tid < 64) {
+    const double v0 = tsum[4 * tid], v1 = tsum[4 * tid + 1], v2 = tsum[4 * tid + 2], v3 = tsum[4 * tid + 3];
+    const double s4 = ((v0 + v1) + v2) + v3;
+    double inc = s4;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double nv = __shfl_up(inc, o, 64);
+      if (tid >= o) inc += nv;
+    }
+    const double ex = inc - s4;
+    tsum[4 * tid] = ex;
+    tsum[4 * tid + 1] = ex + v0;
+    tsum[4 * tid + 2] = (ex + v0) + v1;
+    tsum[4 * tid + 3] = ((ex + v0) + v1) + v2;
+  }
+}
+
+// One workgroup per query: uniform / LAP index search (searchsorted left over the
+// fp32-rounded exact prefix), noise for this row, then the coalesced row gather.
+__device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b, float* smem) {
+  const int tid = threadIdx.x;
+  const long long size = *G(s.size);
+  const int tape = *G(s.tape_mode);
+  const long long pos = *G(s.tape_pos);
   const uint2 key = make_uint2((unsigned)s.seed, (unsigned)(s.seed >> 32));
-  const unsigned long long step = (unsigned long long)*s.ctrl_rng;
+  const unsigned long long step = (unsigned long long)*G(s.ctrl_rng);
   // noise tensors for this row
   for (int j = tid; j < s.A; j += kThreads) {
     float e, e2 = 0.f;
     if (tape) {
-      e = s.tape_eps[((size_t)pos * s.B + b) * s.A + j];
-      if (s.eps2) e2 = s.tape_eps2[((size_t)pos * s.B + b) * s.A + j];
+      e = G(s.tape_eps)[((size_t)pos * s.B + b) * s.A + j];
+      if (s.eps2) e2 = G(s.tape_eps2)[((size_t)pos * s.B + b) * s.A + j];
     } else {
-      uint4 r = philox(key, make_uint4((unsigned)(b * s.A + j), 1u, (unsigned)step, (unsigned)(step >> 32)));
+      const uint4 r = philox(key, make_uint4((unsigned)(b * s.A + j), 1u, (unsigned)step, (unsigned)(step >> 32)));
       e = normal_from(r.x, r.y);
       e2 = normal_from(r.z, r.w);
     }
-    s.eps[(size_t)b * s.ldeps + j] = e;
-    if (s.eps2) s.eps2[(size_t)b * s.ldeps + j] = e2;
+    GW(s.eps)[(size_t)b * s.ldeps + j] = e;
+    if (s.eps2) GW(s.eps2)[(size_t)b * s.ldeps + j] = e2;
   }
-  __shared__ long long found_s;
+  long long* found = reinterpret_cast<long long*>(smem);  // [1]
+  double* tsum = reinterpret_cast<double*>(smem) + 2;     // [256]
+  double* pref = tsum + kThreads;                         // [nb <= 2048]
   long long ind;
   if (tape == 2) {
-    ind = s.tape_ind[(size_t)pos * s.B + b];
+    ind = G(s.tape_ind)[(size_t)pos * s.B + b];
   } else {
     float u;
-    if (tape) u = s.tape_u[(size_t)pos * s.B + b];
+    if (tape) u = G(s.tape_u)[(size_t)pos * s.B + b];
     else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
-    if (tid == 0) s.u_out[b] = u;
+    if (tid == 0) GW(s.u_out)[b] = u;
     if (!s.lap) {
       // searchsorted(cumsum(ones(size)), u*size): first j in 1..size with j >= v
       const float v = u * (float)size;
-      long long k = (long long)ceilf(v) - 1;
+      const long long k = (long long)ceilf(v) - 1;
       ind = k < 0 ? 0 : (k > size - 1 ? size - 1 : k);
     } else {
       // exact fp64 prefix over block sums, rounded to fp32 per element (Q8)
-      double* pref = reinterpret_cast<double*>(smem);          // [nb]
-      double* wsum = pref + 2048;                              // [4]
       const int nb = (int)((size + kBlk - 1) / kBlk);
       const int per = (nb + kThreads - 1) / kThreads;
       double loc = 0.0;
       for (int q = 0; q < per; ++q) {
-        int k = tid * per + q;
-        if (k < nb) { loc += s.bsum[k]; pref[k] = loc; }
+        const int k = tid * per + q;
+        if (k < nb) {
+          loc += G(s.bsum)[k];
+          pref[k] = loc;
+        }
       }
-      // exclusive scan of thread totals
-      double* tsum = wsum + 8;                                  // [256]
       tsum[tid] = loc;
       __syncthreads();
-      if (tid == 0) {
-        double run = 0.0;
-        for (int q = 0; q < kThreads; ++q) { double x = tsum[q]; tsum[q] = run; run += x; }
-      }
+      scan256(tsum);
       __syncthreads();
       const double off = tsum[tid];
       for (int q = 0; q < per; ++q) {
-        int k = tid * per + q;
+        const int k = tid * per + q;
         if (k < nb) pref[k] += off;
       }
       __syncthreads();
@@ -511,75 +796,75 @@ __device__ void op_sample_gather(const SampleArgs& s, int b, float* smem) {
       // first block whose rounded inclusive prefix >= v (monotone)
       int lo = 0, hi = nb - 1;
       while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if ((float)pref[mid] >= v) hi = mid; else lo = mid + 1;
+        const int mid = (lo + hi) >> 1;
+        if ((float)pref[mid] >= v) hi = mid;
+        else lo = mid + 1;
       }
-      const int blk = lo;
-      const double base = blk ? pref[blk - 1] : 0.0;
-      const long long e0 = (long long)blk * kBlk;
+      const double base = lo ? pref[lo - 1] : 0.0;
+      const long long e0 = (long long)lo * kBlk + (long long)tid * 16;
       // each thread owns 16 consecutive priorities of the block
-      double tl = 0.0;
       float pv[16];
+      double tl = 0.0;
+#pragma unroll
       for (int q = 0; q < 16; ++q) {
-        long long i = e0 + tid * 16 + q;
-        pv[q] = (i < size) ? s.priority[i] : 0.f;
+        pv[q] = (e0 + q < size) ? G(s.priority)[e0 + q] : 0.f;
         tl += (double)pv[q];
       }
       __syncthreads();
       tsum[tid] = tl;
-      if (tid == 0) found_s = 0x7FFFFFFFFFFFFFFFll;
+      if (tid == 0) *found = 0x7FFFFFFFFFFFFFFFll;
       __syncthreads();
-      if (tid == 0) {
-        double run = 0.0;
-        for (int q = 0; q < kThreads; ++q) { double x = tsum[q]; tsum[q] = run; run += x; }
-      }
+      scan256(tsum);
       __syncthreads();
       double run = base + tsum[tid];
       long long mine = 0x7FFFFFFFFFFFFFFFll;
+#pragma unroll
       for (int q = 0; q < 16; ++q) {
-        long long i = e0 + tid * 16 + q;
         run += (double)pv[q];
-        if (i < size && (float)run >= v) { mine = i; break; }
+        if (mine == 0x7FFFFFFFFFFFFFFFll && e0 + q < size && (float)run >= v) mine = e0 + q;
       }
-      if (mine != 0x7FFFFFFFFFFFFFFFll) atomicMin((unsigned long long*)&found_s, (unsigned long long)mine);
+      if (mine != 0x7FFFFFFFFFFFFFFFll) atomicMin((unsigned long long*)found, (unsigned long long)mine);
       __syncthreads();
-      ind = found_s;
+      ind = *found;
       if (ind >= size) ind = size - 1;
     }
   }
   // gather the transition (coalesced float4 copies)
-  const float4* st = reinterpret_cast<const float4*>(s.state + (size_t)ind * s.Sp);
-  const float4* nst = reinterpret_cast<const float4*>(s.next_state + (size_t)ind * s.Sp);
-  float4* d0 = reinterpret_cast<float4*>(s.ss + (size_t)b * s.ldss);
-  float4* d1 = reinterpret_cast<float4*>(s.ss + (size_t)(s.B + b) * s.ldss);
-  for (int k = tid; k < s.Sp / 4; k += kThreads) {
-    d0[k] = st[k];
-    d1[k] = nst[k];
+  const GAS float* st = G(s.state) + (size_t)ind * s.Sp;
+  const GAS float* nst = G(s.next_state) + (size_t)ind * s.Sp;
+  GAS float* d0 = GW(s.ss) + (size_t)b * s.ldss;
+  GAS float* d1 = GW(s.ss) + (size_t)(s.B + b) * s.ldss;
+  for (int k = tid * 4; k < s.Sp; k += kThreads * 4) {
+    st4g(d0 + k, ld4g(st + k));
+    st4g(d1 + k, ld4g(nst + k));
   }
-  const float4* ac = reinterpret_cast<const float4*>(s.action + (size_t)ind * s.Ap);
-  float4* da = reinterpret_cast<float4*>(s.a + (size_t)b * s.lda);
-  for (int k = tid; k < s.Ap / 4; k += kThreads) da[k] = ac[k];
+  const GAS float* ac = G(s.action) + (size_t)ind * s.Ap;
+  GAS float* da = GW(s.a) + (size_t)b * s.lda;
+  for (int k = tid * 4; k < s.Ap; k += kThreads * 4) st4g(da + k, ld4g(ac + k));
   if (tid == 0) {
-    s.r[b] = s.reward[ind];
-    s.nd[b] = s.notdone[ind];
-    s.ind[b] = ind;
+    GW(s.r)[b] = G(s.reward)[ind];
+    GW(s.nd)[b] = G(s.notdone)[ind];
+    GW(s.ind)[b] = ind;
   }
 }
 
 // LAPReplayMemory.update_priority (lap.py:66-69): last duplicate wins (Q9).
-__device__ void op_priority(const PriorityArgs& a, float* smem) {
+__device__ __forceinline__ void op_priority(const CAS PriorityArgs& a, float* smem) {
   long long* sind = reinterpret_cast<long long*>(smem);
   float* red = smem + 2 * 1024;
-  for (int b = threadIdx.x; b < a.B; b += kThreads) sind[b] = a.ind[b];
+  for (int b = threadIdx.x; b < a.B; b += kThreads) sind[b] = G(a.ind)[b];
   __syncthreads();
   float mx = -INFINITY;
   for (int b = threadIdx.x; b < a.B; b += kThreads) {
     const long long me = sind[b];
     bool last = true;
     for (int c = b + 1; c < a.B; ++c)
-      if (sind[c] == me) { last = false; break; }
-    const float pv = a.p[b];
-    if (last) a.priority[me] = pv;
+      if (sind[c] == me) {
+        last = false;
+        break;
+      }
+    const float pv = G(a.p)[b];
+    if (last) GW(a.priority)[me] = pv;
     mx = fmaxf(mx, pv);
   }
 #pragma unroll
@@ -587,19 +872,19 @@ __device__ void op_priority(const PriorityArgs& a, float* smem) {
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    *a.max_priority = fmaxf(m, *a.max_priority);
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    GW(a.max_priority)[0] = fmaxf(m, G(a.max_priority)[0]);
   }
 }
 
 // ---------------------------------------------------------------- SAC Gaussian-tanh
 
-__device__ void op_sac_actor(const SacActorArgs& s, int t) {
+__device__ __forceinline__ void op_sac_actor(const CAS SacActorArgs& s, int t) {
   const int b = t * kThreads + threadIdx.x;
   if (b >= s.rows) return;
-  const float* o = s.out + (size_t)b * s.ldo;
-  const float* e = (b < s.eps_row_split) ? s.eps2 + (size_t)b * s.ldeps
-                                         : s.eps + (size_t)(b - s.eps_row_split) * s.ldeps;
+  const GAS float* o = G(s.out) + (size_t)b * s.ldo;
+  const GAS float* e = (b < s.eps_row_split) ? G(s.eps2) + (size_t)b * s.ldeps
+                                             : G(s.eps) + (size_t)(b - s.eps_row_split) * s.ldeps;
   const float c = (float)0.9189385332046727;  // log(sqrt(2*pi))
   float lp = 0.f, corr = 0.f;
   for (int j = 0; j < s.A; ++j) {
@@ -612,17 +897,17 @@ __device__ void op_sac_actor(const SacActorArgs& s, int t) {
     const float d = u - mu;
     lp += -(d * d) / (2.f * var) - logf(sd) - c;
     corr += logf((1.f - a * a) + 1e-6f);
-    s.act[(size_t)b * s.ldact + j] = a;
+    GW(s.act)[(size_t)b * s.ldact + j] = a;
   }
-  s.logpi[b] = lp - corr;
+  GW(s.logpi)[b] = lp - corr;
 }
 
-__device__ void op_sac_actor_bwd(const SacActorArgs& s, int t) {
+__device__ __forceinline__ void op_sac_actor_bwd(const CAS SacActorArgs& s, int t) {
   const int b = t * kThreads + threadIdx.x;
   if (b >= s.rows) return;
-  const float* o = s.out + (size_t)b * s.ldo;
-  const float* e = s.eps2 + (size_t)b * s.ldeps;
-  const float w = expf(s.log_alpha[0]) * s.inv_b;   // d obj / d logpi_b
+  const GAS float* o = G(s.out) + (size_t)b * s.ldo;
+  const GAS float* e = G(s.eps2) + (size_t)b * s.ldeps;
+  const float w = expf(G(s.log_alpha)[0]) * s.inv_b;  // d obj / d logpi_b
   for (int j = 0; j < s.A; ++j) {
     const float mu = o[s.mean_off + j];
     const float lsr = o[s.ls_off + j];
@@ -633,113 +918,119 @@ __device__ void op_sac_actor_bwd(const SacActorArgs& s, int t) {
     const float var = sd * sd;
     const float d = u - mu;
     // logpi = sum(-d^2/(2 var) - log sd - c) - sum log(1 - a^2 + 1e-6)
-    float ga = s.da[(size_t)b * s.ldda + j] + (w / ((1.f - a * a) + 1e-6f)) * (2.f * a);
+    const float ga = G(s.da)[(size_t)b * s.ldda + j] + (w / ((1.f - a * a) + 1e-6f)) * (2.f * a);
     float gu = ga * (1.f - a * a);
-    gu += -(w / (2.f * var)) * (2.f * d);           // d(-d^2/(2var))/du
-    float gmu = (w / (2.f * var)) * (2.f * d);      // via d = u - mu
-    float gvar = (w * (d * d)) / ((2.f * var) * (2.f * var)) * 2.f;
+    gu += -(w / (2.f * var)) * (2.f * d);       // d(-d^2/(2var))/du
+    float gmu = (w / (2.f * var)) * (2.f * d);  // via d = u - mu
+    const float gvar = (w * (d * d)) / ((2.f * var) * (2.f * var)) * 2.f;
     float gsd = gvar * (2.f * sd) - w / sd;
     gmu += gu;
     gsd += gu * e[j];
     float gls = gsd * sd;
     if (!(lsr >= s.min_log_std && lsr <= s.max_log_std)) gls = 0.f;
-    s.dout[(size_t)b * s.lddout + s.mean_off + j] = gmu;
-    s.dout[(size_t)b * s.lddout + s.ls_off + j] = gls;
+    GW(s.dout)[(size_t)b * s.lddout + s.mean_off + j] = gmu;
+    GW(s.dout)[(size_t)b * s.lddout + s.ls_off + j] = gls;
   }
 }
 
 // ---------------------------------------------------------------- step end
 
-__device__ void op_step_end(const StepEndArgs& a) {
-  if (threadIdx.x != 0) return;
-  float vals[kInfoMax];
+// Deterministic workgroup sum of p[i*stride], i < n (fixed strided + tree order).
+__device__ float block_sum(const float* p, int n, int stride, float* red) {
+  const GAS float* q = G(p);
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += kThreads) s += q[(size_t)i * stride];
+  return wg_sum(s, red);
+}
+
+__device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* smem) {
+  float* red = smem;
+  float* vals = smem + 8;
   const float nanv = __int_as_float(0x7FC00000);
-  float la = a.log_alpha ? *a.log_alpha : 0.f;
+  const float slp = a.logpi_part ? block_sum(a.logpi_part + 1, a.nlogpi, 4, red) : 0.f;
+  for (int k = 0; k < a.ninfo; ++k) {
+    float v = 0.f;
+    if (a.kind[k] == INFO_SUM || a.kind[k] == INFO_SAC_POL) {
+      v = block_sum(a.part[k], a.npart[k], a.stride[k], red);
+    } else if (a.kind[k] == INFO_GNORM) {
+      // per-tensor sum of squares -> sqrt -> sum (rl/nn/utils.py:13-19)
+      for (int q = 0; q < a.ngsq_t; ++q) {
+        const float ss = block_sum(a.gsq + a.gsq_off[q], a.gsq_off[q + 1] - a.gsq_off[q], 1, red);
+        v += sqrtf(ss);
+      }
+    }
+    if (threadIdx.x == 0) vals[k] = v;
+  }
+  if (threadIdx.x != 0) return;
+  const float la = a.log_alpha ? G(a.log_alpha)[0] : 0.f;
   const float alpha = expf(la);
-  float slp = 0.f;
-  if (a.logpi_part)
-    for (int i = 0; i < a.nlogpi; ++i) slp += a.logpi_part[i * 4 + 1];
   // mean_b(-lp_b - target_entropy); d/dla mean(exp(la) * c) = exp(la) * mean(c)
   const float gmean = (-slp) * a.inv_b - a.target_entropy;
   const float tmp_obj = alpha * gmean;
   for (int k = 0; k < a.ninfo; ++k) {
-    float v = 0.f;
+    float v = vals[k];
     switch (a.kind[k]) {
-      case INFO_SUM:
-        for (int i = 0; i < a.npart[k]; ++i) v += a.part[k][i * a.stride[k]];
-        v *= a.scale[k];
-        break;
+      case INFO_SUM: v *= a.scale[k]; break;
       case INFO_NAN: v = nanv; break;
-      case INFO_GNORM: {
-        // per-tensor sum of squares -> sqrt -> sum (rl/nn/utils.py:13-19)
-        float tot = 0.f, cur = 0.f;
-        int tcur = a.gsq_tensor[0];
-        for (int i = 0; i < a.ngsq; ++i) {
-          if (a.gsq_tensor[i] != tcur) { tot += sqrtf(cur); cur = 0.f; tcur = a.gsq_tensor[i]; }
-          cur += a.gsq[i];
-        }
-        v = tot + sqrtf(cur);
-        break;
-      }
+      case INFO_GNORM: break;
       case INFO_SAC_TMP: v = alpha; break;
-      case INFO_SAC_NTMP: v = tmp_obj; break;  // d/dla mean(exp(la)*c) = exp(la)*mean(c)
-      case INFO_SAC_POL: {
-        float s = 0.f;
-        for (int i = 0; i < a.npart[k]; ++i) s += a.part[k][i * a.stride[k]];
-        v = s * a.scale[k] + tmp_obj;
-        break;
-      }
+      case INFO_SAC_NTMP: v = tmp_obj; break;
+      case INFO_SAC_POL: v = v * a.scale[k] + tmp_obj; break;
       case INFO_SAC_TMPL: v = tmp_obj; break;
       case INFO_SAC_ENT: v = -slp * a.inv_b; break;
     }
     vals[k] = v;
   }
-  if (a.log_alpha && a.la_lr > 0.f) {
+  if (a.log_alpha && a.la_lr > 0.f) {  // optim_tmp.step (sac.py:283)
     const float g = tmp_obj;
-    const double tt = (double)(*a.la_t + 1);
+    const double tt = (double)(G(a.la_t)[0] + 1);
     const double bc1 = 1.0 - pow(0.9, tt), bc2 = 1.0 - pow(0.999, tt);
-    float m = *a.la_m, v2 = *a.la_v;
+    float m = G(a.la_m)[0], v2 = G(a.la_v)[0];
     m = m + (1.f - 0.9f) * (g - m);
     v2 = v2 * 0.999f + ((1.f - 0.999f) * g) * g;
     const float denom = sqrtf(v2) / (float)sqrt(bc2) + 1e-8f;
-    *a.la_m = m;
-    *a.la_v = v2;
-    *a.log_alpha = la + (-(float)(a.la_lr / bc1) * m) / denom;
-    *a.la_t += 1;
+    GW(a.la_m)[0] = m;
+    GW(a.la_v)[0] = v2;
+    GW(a.log_alpha)[0] = la + (-(float)(a.la_lr / bc1) * m) / denom;
+    GW(a.la_t)[0] += 1;
   }
-  int slot = *a.info_slot;
-  if (slot >= a.info_cap) slot = a.info_cap - 1;
-  for (int k = 0; k < a.ninfo; ++k) a.info[(size_t)slot * kInfoMax + k] = vals[k];
-  *a.info_slot = slot + 1;
+  if (a.info_slot) {
+    int slot = G(a.info_slot)[0];
+    if (slot >= a.info_cap) slot = a.info_cap - 1;
+    for (int k = 0; k < a.ninfo; ++k) GW(a.info)[(size_t)slot * kInfoMax + k] = vals[k];
+    GW(a.info_slot)[0] = slot + 1;
+  }
   for (int c = 0; c < 16; ++c)
-    if (a.cmask & (1 << c)) a.counters[c] += 1;
+    if (a.cmask & (1 << c)) GW(a.counters)[c] += 1;
 }
 
 // ---------------------------------------------------------------- flat ops
 
-__device__ void op_polyak(const FlatArgs& f, int t) {
+__device__ __forceinline__ void op_polyak(const CAS FlatArgs& f, int t) {
   const long long i0 = ((long long)t * kThreads + threadIdx.x) * 4;
+  GAS float* d = GW(f.dst);
+  const GAS float* src = G(f.src);
   for (long long i = i0; i < i0 + 4 && i < f.n; ++i) {
-    const float s = f.self_alias ? f.dst[i] : f.src[i];
+    const float s = f.self_alias ? d[i] : src[i];
     // tau*src + dst*(1-tau), each product rounded separately (Q2, no FMA)
-    f.dst[i] = __fadd_rn(__fmul_rn(f.tau, s), __fmul_rn(f.dst[i], f.omt));
+    d[i] = __fadd_rn(__fmul_rn(f.tau, s), __fmul_rn(d[i], f.omt));
   }
 }
 
-__device__ void op_copy(const FlatArgs& f, int t) {
+__device__ __forceinline__ void op_copy(const CAS FlatArgs& f, int t) {
   const long long i0 = ((long long)t * kThreads + threadIdx.x) * 4;
-  for (long long i = i0; i < i0 + 4 && i < f.n; ++i) f.dst[i] = f.src[i];
+  for (long long i = i0; i < i0 + 4 && i < f.n; ++i) GW(f.dst)[i] = G(f.src)[i];
 }
 
-__device__ void op_maxred(const FlatArgs& f, int t, float* smem) {
+__device__ __forceinline__ void op_maxred(const CAS FlatArgs& f, int t, float* smem) {
   float mx = -INFINITY;
   if (f.stage == 0) {
-    const long long size = *f.size;
+    const long long size = *G(f.size);
     const long long per = (size + f.nwg - 1) / f.nwg;
     const long long b0 = (long long)t * per, b1 = min(size, b0 + per);
-    for (long long i = b0 + threadIdx.x; i < b1; i += kThreads) mx = fmaxf(mx, f.src[i]);
+    for (long long i = b0 + threadIdx.x; i < b1; i += kThreads) mx = fmaxf(mx, G(f.src)[i]);
   } else {
-    for (int i = threadIdx.x; i < f.nwg; i += kThreads) mx = fmaxf(mx, f.partial[i]);
+    for (int i = threadIdx.x; i < f.nwg; i += kThreads) mx = fmaxf(mx, G(f.partial)[i]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -747,25 +1038,27 @@ __device__ void op_maxred(const FlatArgs& f, int t, float* smem) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const float m = fmaxf(fmaxf(smem[0], smem[1]), fmaxf(smem[2], smem[3]));
-    if (f.stage == 0) f.partial[t] = m; else *f.out = m;
+    if (f.stage == 0) GW(f.partial)[t] = m;
+    else GW(f.out)[0] = m;
   }
 }
 
-__device__ void op_ctrl(const CtrlArgs& c) {
+__device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
   if (threadIdx.x == 0) {
-    c.vt[0] = unkey(*c.vmax_key);
-    c.vt[1] = unkey(*c.vmin_key);
+    GW(c.vt)[0] = unkey(G(c.vmax_key)[0]);
+    GW(c.vt)[1] = unkey(G(c.vmin_key)[0]);
   }
 }
 
 // ---------------------------------------------------------------- dispatch
 
-__global__ __launch_bounds__(kThreads) void rle_level(const Op* __restrict__ ops, int nops) {
-  __shared__ __attribute__((aligned(16))) float smem[8192];  // 32 KB
+__global__ __launch_bounds__(kThreads) void rle_level(const Op* ops_g, int nops) {
+  __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
+  const CAS Op* ops = (const CAS Op*)ops_g;
   const int wg = blockIdx.x;
   int k = 0;
   while (k + 1 < nops && ops[k + 1].wg_begin <= wg) ++k;
-  const Op& op = ops[k];
+  const CAS Op& op = ops[k];
   const int t = wg - op.wg_begin;
   switch (op.kind) {
     case OP_GEMM: op_gemm(op.gemm, t, smem); break;
@@ -776,7 +1069,7 @@ __global__ __launch_bounds__(kThreads) void rle_level(const Op* __restrict__ ops
     case OP_PRIORITY: op_priority(op.prio, smem); break;
     case OP_SAC_ACTOR: op_sac_actor(op.sac, t); break;
     case OP_SAC_ACTOR_BWD: op_sac_actor_bwd(op.sac, t); break;
-    case OP_STEP_END: op_step_end(op.end); break;
+    case OP_STEP_END: op_step_end(op.end, smem); break;
     case OP_POLYAK: op_polyak(op.flat, t); break;
     case OP_COPY: op_copy(op.flat, t); break;
     case OP_MAXRED: op_maxred(op.flat, t, smem); break;
@@ -788,11 +1081,10 @@ __global__ __launch_bounds__(kThreads) void rle_level(const Op* __restrict__ ops
 // ---------------------------------------------------------------- standalone kernels
 
 // Scatter `count` staged transitions into the ring at ptr (wrapping).
-__global__ void rle_append_kernel(float* state, float* next_state, float* action, float* reward,
-                                  float* notdone, float* priority, const float* st_s, const float* st_ns,
-                                  const float* st_a, const float* st_r, const float* st_d, long long ptr,
-                                  long long cap, int count, int Sp, int Ap, const float* max_priority,
-                                  int lap) {
+__global__ void rle_append_kernel(float* state, float* next_state, float* action, float* reward, float* notdone,
+                                  float* priority, const float* st_s, const float* st_ns, const float* st_a,
+                                  const float* st_r, const float* st_d, long long ptr, long long cap, int count,
+                                  int Sp, int Ap, const float* max_priority, int lap) {
   const int i = blockIdx.x;
   if (i >= count) return;
   const long long row = (ptr + i) % cap;
@@ -810,46 +1102,40 @@ __global__ void rle_append_kernel(float* state, float* next_state, float* action
 
 // Synthetic replay for the benchmark: s, s' ~ N(0,1),
 // a ~ U(-1,1), r ~ N(0,1), notdone ~ Bernoulli(0.99), priority = 1.
-__global__ void rle_fill_kernel(float* state, float* next_state, float* action, float* reward,
-                                float* notdone, float* priority, long long n, int S, int Sp, int A, int Ap,
-                                unsigned long long seed) {
+__global__ void rle_fill_kernel(float* state, float* next_state, float* action, float* reward, float* notdone,
+                                float* priority, long long n, int S, int Sp, int A, int Ap, unsigned long long seed) {
   const long long row = blockIdx.x;
   if (row >= n) return;
   const uint2 key = make_uint2((unsigned)seed, (unsigned)(seed >> 32));
   for (int k = threadIdx.x; k < Sp; k += blockDim.x) {
-    uint4 r = philox(key, make_uint4((unsigned)row, (unsigned)k, 7u, (unsigned)(row >> 32)));
+    const uint4 r = philox(key, make_uint4((unsigned)row, (unsigned)k, 7u, (unsigned)(row >> 32)));
     state[row * Sp + k] = k < S ? normal_from(r.x, r.y) : 0.f;
     next_state[row * Sp + k] = k < S ? normal_from(r.z, r.w) : 0.f;
   }
   for (int k = threadIdx.x; k < Ap; k += blockDim.x) {
-    uint4 r = philox(key, make_uint4((unsigned)row, (unsigned)k, 8u, (unsigned)(row >> 32)));
+    const uint4 r = philox(key, make_uint4((unsigned)row, (unsigned)k, 8u, (unsigned)(row >> 32)));
     action[row * Ap + k] = k < A ? 2.f * u01(r.x) - 1.f : 0.f;
   }
   if (threadIdx.x == 0) {
-    uint4 r = philox(key, make_uint4((unsigned)row, 0u, 9u, (unsigned)(row >> 32)));
+    const uint4 r = philox(key, make_uint4((unsigned)row, 0u, 9u, (unsigned)(row >> 32)));
     reward[row] = normal_from(r.x, r.y);
     notdone[row] = u01(r.z) < 0.99f ? 1.f : 0.f;
     priority[row] = 1.f;
   }
 }
 
-}  // namespace rle
-
 // ---------------------------------------------------------------- host launchers
 
-extern "C++" {
-namespace rle {
 hipError_t launch_level(const Op* d_ops, int nops, int nwg, hipStream_t st) {
   hipLaunchKernelGGL(rle_level, dim3(nwg), dim3(kThreads), 0, st, d_ops, nops);
   return hipGetLastError();
 }
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
-                         const float* st_r, const float* st_d, long long ptr, long long cap, int count,
-                         int Sp, int Ap, const float* max_priority, int lap, hipStream_t st) {
-  hipLaunchKernelGGL(rle_append_kernel, dim3(count), dim3(256), 0, st, state, next_state, action, reward,
-                     notdone, priority, st_s, st_ns, st_a, st_r, st_d, ptr, cap, count, Sp, Ap, max_priority,
-                     lap);
+                         const float* st_r, const float* st_d, long long ptr, long long cap, int count, int Sp,
+                         int Ap, const float* max_priority, int lap, hipStream_t st) {
+  hipLaunchKernelGGL(rle_append_kernel, dim3(count), dim3(256), 0, st, state, next_state, action, reward, notdone,
+                     priority, st_s, st_ns, st_a, st_r, st_d, ptr, cap, count, Sp, Ap, max_priority, lap);
   return hipGetLastError();
 }
 hipError_t launch_fill(float* state, float* next_state, float* action, float* reward, float* notdone,
@@ -859,5 +1145,5 @@ hipError_t launch_fill(float* state, float* next_state, float* action, float* re
                      notdone, priority, n, S, Sp, A, Ap, seed);
   return hipGetLastError();
 }
+
 }  // namespace rle
-}

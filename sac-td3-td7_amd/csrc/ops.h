@@ -8,7 +8,8 @@
 namespace rle {
 
 constexpr int kThreads = 256;   // 4 waves per workgroup, every op kind
-constexpr int kTile = 16;       // GEMM output tile edge (v_mfma_f32_16x16x4_f32)
+constexpr int kTileM = 16;      // GEMM output tile rows (v_mfma_f32_16x16x4_f32)
+constexpr int kTileN = 64;      // GEMM output tile cols (4 waves x 16)
 constexpr int kMaxSeg = 4;
 constexpr int kInfoMax = 8;     // floats per step in the info ring
 
@@ -65,12 +66,19 @@ struct AdamArgs {
   long long mo, vo;      // element offsets of m / v arrays relative to params
   const long long* t;    // completed optimizer steps (device counter)
   float lr, beta1, beta2, eps;
-  int ldw, bias_col;     // bias_col = first padded column index of the bias tile (>= R... = padded K)
+  int ldw, bias_col;     // bias_col = first column of the bias tile = K rounded up to kTileN
   float* gsq;            // optional: per-tile sum of squared grads (weights), [tiles]
   float* gsq_b;          // optional: per-tile sum of squared grads (bias), [tiles_m]
 };
 
+enum GemmMode : int {
+  GEMM_FWD = 0,   // A contiguous (activations), B contiguous (W rows):  Y = X W^T
+  GEMM_DX = 1,    // A contiguous (dZ), B strided (W columns):            dX = dZ W
+  GEMM_DW = 2,    // A strided (dZ^T), B strided (X):                     dW = dZ^T X
+};
+
 struct GemmArgs {
+  int mode;              // GemmMode (operand layouts; every segment of an operand shares it)
   int M, N, R;           // output rows, output cols (x-extent of B), reduction length
   int tiles_m, tiles_n;  // tiles_n includes the extra bias tile column for EPI_ADAM
   int epi;
@@ -184,7 +192,7 @@ struct StepEndArgs {
   // SAC temperature
   float* log_alpha; float* la_m; float* la_v; long long* la_t; float la_lr; float target_entropy;
   const float* logpi_part; int nlogpi; float inv_b;
-  const float* gsq; int ngsq; const int* gsq_tensor;  // TD3 grad norm: per-tile sq sums -> per-tensor sqrt sum
+  const float* gsq; int gsq_off[9]; int ngsq_t;      // TD3 grad norm: tensor t = tiles [off[t], off[t+1])
 };
 
 enum InfoKind : int {

@@ -69,10 +69,12 @@ SIGNATURES = {
     "rle_get_value_bounds": (_int, [_vp, _f32p]),
     "rle_set_value_bounds": (_int, [_vp, _f32p]),
     "rle_step": (_int, [_vp, _int, _f32p]),
+    "rle_step_timed": (_int, [_vp, _int, _f32p]),
     "rle_set_tapes": (_int, [_vp, _int, _f32p, _f32p, _f32p, _i64p]),
     "rle_last_indices": (_int, [_vp, _i64p]),
     "rle_act": (_int, [_vp, _f32p, _int, _f32p]),
     "rle_graph_stats": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "rle_graph_describe": (_int, [_vp, _int, ctypes.c_char_p, _int]),
     "rle_copy_state": (_int, [_vp, _vp]),
     "rle_synchronize": (_int, [_vp]),
 }
@@ -256,6 +258,12 @@ class Engine:
         _check(lib().rle_step(self.h, n, _fp(info)))
         return info[:n] if want_info else None
 
+    def step_timed(self, n):
+        """n steps, no info readback; returns GPU ms from HIP events on the engine stream."""
+        ms = ctypes.c_float()
+        _check(lib().rle_step_timed(self.h, n, ctypes.byref(ms)))
+        return ms.value
+
     def set_tapes(self, u=None, eps=None, eps_pi=None, ind=None):
         if u is None and ind is None:
             _check(lib().rle_set_tapes(self.h, 0, None, None, None, None))
@@ -284,6 +292,11 @@ class Engine:
         a, b = _int(), _int()
         _check(lib().rle_graph_stats(self.h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+    def describe(self, which=0):
+        buf = ctypes.create_string_buffer(1 << 16)
+        _check(lib().rle_graph_describe(self.h, which, buf, len(buf)))
+        return buf.value.decode()
 
     def copy_state_from(self, other: "Engine"):
         _check(lib().rle_copy_state(self.h, other.h))

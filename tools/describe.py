@@ -1,0 +1,21 @@
+"""Print the level structure of the TD7 Humanoid step graphs (GPU box)."""
+import os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd")]
+from rl import _engine as E
+from rl.nn.layout import init_agent
+S, A, H, B = 376, 17, 256, 256
+algo = sys.argv[1] if len(sys.argv) > 1 else "td7"
+code = {"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[algo]
+if algo == "td3":
+    S, A = 17, 6
+eng = E.Engine(E.make_config(code, S, A, H, B, use_lap=(algo == "td7")))
+for net, params in init_agent(algo, S, A, H, 1).items():
+    for k, v in params.items():
+        eng.set_param(net, k, v)
+rep = E.Replay(1000000, S, A, algo == "td7")
+rep.fill_random(1000000, 1)
+eng.bind(rep)
+for w in (0, 1):
+    print(f"=== graph {w}")
+    print(eng.describe(w))

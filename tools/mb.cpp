@@ -1,0 +1,128 @@
+// Microbenchmark of the level-dispatch kernel on synthetic ops (GPU box only).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I sac-td3-td7_amd/csrc \
+//        tools/mb.cpp sac-td3-td7_amd/lib/kernels.o -o /tmp/mb
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "ops.h"
+
+namespace rle {
+hipError_t launch_level(const Op* d_ops, int nops, int nwg, hipStream_t st);
+}
+using namespace rle;
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e = (x);                                                         \
+    if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } \
+  } while (0)
+
+static float* dalloc(size_t n) {
+  float* p;
+  CK(hipMalloc(&p, n * 4));
+  std::vector<float> h(n);
+  for (size_t i = 0; i < n; ++i) h[i] = (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f;
+  CK(hipMemcpy(p, h.data(), n * 4, hipMemcpyHostToDevice));
+  return p;
+}
+
+static Op fwd_op(float* X, float* W, float* b, float* Y, int M, int N, int K) {
+  Op op{};
+  op.kind = OP_GEMM;
+  GemmArgs& g = op.gemm;
+  g.mode = GEMM_FWD;
+  g.M = M; g.N = N; g.R = K;
+  g.A.nseg = 1;
+  g.A.seg[0].p = X; g.A.seg[0].ld = K; g.A.seg[0].x0 = 0; g.A.seg[0].x1 = M; g.A.seg[0].r0 = 0; g.A.seg[0].r1 = K;
+  g.B.nseg = 1;
+  g.B.seg[0].p = W; g.B.seg[0].ld = K; g.B.seg[0].x0 = 0; g.B.seg[0].x1 = N; g.B.seg[0].r0 = 0; g.B.seg[0].r1 = K;
+  g.tiles_m = (M + kTileM - 1) / kTileM; g.tiles_n = (N + kTileN - 1) / kTileN;
+  g.epi = EPI_STORE; g.act = ACT_RELU; g.out = Y; g.ldo = N; g.bias = b;
+  op.wg_count = g.tiles_m * g.tiles_n;
+  return op;
+}
+
+static double time_level(std::vector<Op> ops, int reps, hipStream_t st) {
+  int wg = 0;
+  for (auto& o : ops) { o.wg_begin = wg; wg += o.wg_count; }
+  Op* d;
+  CK(hipMalloc(&d, ops.size() * sizeof(Op)));
+  CK(hipMemcpy(d, ops.data(), ops.size() * sizeof(Op), hipMemcpyHostToDevice));
+  // capture reps launches in a graph, like the engine
+  hipGraph_t g; hipGraphExec_t x;
+  CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  for (int i = 0; i < reps; ++i) CK(launch_level(d, (int)ops.size(), wg, st));
+  CK(hipStreamEndCapture(st, &g));
+  CK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+  CK(hipGraphLaunch(x, st));
+  CK(hipStreamSynchronize(st));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  CK(hipEventRecord(a, st));
+  CK(hipGraphLaunch(x, st));
+  CK(hipEventRecord(b, st));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  hipGraphExecDestroy(x); hipGraphDestroy(g); hipFree(d);
+  return ms * 1000.0 / reps;
+}
+
+int main() {
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const int K = 256, N = 256;
+  float* X = dalloc(2048 * 400);
+  float* W = dalloc(16 * 256 * 400);
+  float* bb = dalloc(4096);
+  float* Y = dalloc(16 * 2048 * 256);
+  long long* cnt; CK(hipMalloc(&cnt, 128)); CK(hipMemset(cnt, 0, 128));
+  const int reps = 200;
+  {
+    Op e{}; e.kind = 0; e.wg_count = 1;
+    printf("empty 1 WG          : %8.2f us\n", time_level({e}, reps, st));
+    e.wg_count = 256;
+    printf("empty 256 WG        : %8.2f us\n", time_level({e}, reps, st));
+    e.wg_count = 2048;
+    printf("empty 2048 WG       : %8.2f us\n", time_level({e}, reps, st));
+  }
+  {
+    Op e{}; e.kind = OP_STEP_END; e.wg_count = 1; e.end.counters = cnt; e.end.cmask = 1;
+    printf("step_end counters   : %8.2f us\n", time_level({e}, reps, st));
+  }
+  {  // correctness of one fwd tile set vs CPU
+    const int M = 256, Kc = 384;
+    Op o = fwd_op(X, W, bb, Y, M, N, Kc);
+    time_level({o}, 1, st);
+    std::vector<float> hx((size_t)M * Kc), hw((size_t)N * Kc), hb(N), hy((size_t)M * N);
+    CK(hipMemcpy(hx.data(), X, hx.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hw.data(), W, hw.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hb.data(), bb, hb.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hy.data(), Y, hy.size() * 4, hipMemcpyDeviceToHost));
+    double md = 0;
+    for (int i = 0; i < M; ++i)
+      for (int n = 0; n < N; ++n) {
+        double s = hb[n];
+        for (int k = 0; k < Kc; ++k) s += (double)hx[(size_t)i * Kc + k] * hw[(size_t)n * Kc + k];
+        s = s > 0 ? s : 0;
+        md = std::max(md, std::abs(s - hy[(size_t)i * N + n]));
+      }
+    printf("fwd correctness max|d| = %.3g\n", md);
+  }
+  for (int M : {256, 512}) {
+    Op o = fwd_op(X, W, bb, Y, M, N, K);
+    printf("fwd %dx%dx%d (%d WG): %8.2f us\n", M, N, K, o.wg_count, time_level({o}, reps, st));
+  }
+  {
+    Op o = fwd_op(X, W, bb, Y, 256, N, 384);
+    printf("fwd 256x256x384     : %8.2f us\n", time_level({o}, reps, st));
+    std::vector<Op> v;
+    for (int i = 0; i < 8; ++i) v.push_back(fwd_op(X, W + (size_t)i * 256 * 400, bb, Y + (size_t)i * 2048 * 256, 256, N, 384));
+    printf("8x fwd 256x256x384 (2048 WG): %8.2f us\n", time_level(v, reps, st));
+  }
+  return 0;
+}
