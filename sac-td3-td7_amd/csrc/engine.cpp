@@ -23,7 +23,7 @@
 #include "rle.h"
 
 namespace rle {
-hipError_t launch_level(const Op* d_ops, int nops, int nwg, hipStream_t st);
+hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st);
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count,
@@ -1411,7 +1411,7 @@ struct Engine {
     HIPCHK(hipMemcpy(G.d_ops, flat_ops.data(), total * sizeof(Op), hipMemcpyHostToDevice));
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     for (size_t l = 0; l < levels.size(); ++l) {
-      hipError_t e = launch_level(G.d_ops + G.off[l], G.nops[l], G.nwg[l], stream);
+      hipError_t e = launch_level(G.d_ops + G.off[l], levels[l].data(), G.nops[l], G.nwg[l], stream);
       if (e != hipSuccess) {
         hipGraph_t tmp;
         (void)hipStreamEndCapture(stream, &tmp);
@@ -1702,7 +1702,7 @@ static void run_eager(Replay& r, rle::DevMem& tmp, std::vector<std::vector<rle::
     }
     rle::Op* d = tmp.make<rle::Op>(lv.size());
     HIPCHK(hipMemcpy(d, lv.data(), lv.size() * sizeof(rle::Op), hipMemcpyHostToDevice));
-    HIPCHK(rle::launch_level(d, (int)lv.size(), wg, r.stream));
+    HIPCHK(rle::launch_level(d, lv.data(), (int)lv.size(), wg, r.stream));
   }
   HIPCHK(hipStreamSynchronize(r.stream));
 }

@@ -169,6 +169,7 @@ __device__ __forceinline__ void build_norm_tab(const float* part, int ld, int ro
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 static_assert(kMaxSeg == 4, "LaneOp holds 4 segments");
+constexpr int kRing = 4;          // GEMM main-loop chunks in flight per wave
 constexpr int kOOB = 0x7ffffff0;  // voffset beyond any num_records: the load returns 0
 
 struct LaneOp {
@@ -351,20 +352,25 @@ __device__ __forceinline__ f32x4 gemm_mainloop(const CAS GemmArgs& g, int xa, in
     if (bn) b = chunk_scale<SB>(b, ib, tb, rl, tabs);
     return mfma4(a, b, acc);
   };
-  float ia0, ia1, ia2, ia3, ib0, ib1, ib2, ib3;
-  int ta0, ta1, ta2, ta3, tb0, tb1, tb2, tb3;
-  float4 a0 = ldA(ia0, ta0), b0 = ldB(ib0, tb0), a1 = ldA(ia1, ta1), b1 = ldB(ib1, tb1);
-  float4 a2 = ldA(ia2, ta2), b2 = ldB(ib2, tb2), a3 = ldA(ia3, ta3), b3 = ldB(ib3, tb3);
+  // kRing chunks in flight: with L2 cold at every kernel start (operands come from
+  // MALL / HBM, ~1000+ cycles), 8 chunks keep the wave near the MFMA rate.
+  float4 ra[kRing], rb[kRing];
+  float ia[kRing], ib[kRing];
+  int ta[kRing], tb[kRing];
+#pragma unroll
+  for (int k = 0; k < kRing; ++k) {
+    ra[k] = ldA(ia[k], ta[k]);
+    rb[k] = ldB(ib[k], tb[k]);
+  }
 #pragma unroll 1
-  for (int c = 0; c < nch; c += 4) {
-    acc0 = use(a0, b0, ia0, ta0, ib0, tb0, acc0);
-    a0 = ldA(ia0, ta0); b0 = ldB(ib0, tb0);
-    acc1 = use(a1, b1, ia1, ta1, ib1, tb1, acc1);
-    a1 = ldA(ia1, ta1); b1 = ldB(ib1, tb1);
-    acc0 = use(a2, b2, ia2, ta2, ib2, tb2, acc0);
-    a2 = ldA(ia2, ta2); b2 = ldB(ib2, tb2);
-    acc1 = use(a3, b3, ia3, ta3, ib3, tb3, acc1);
-    a3 = ldA(ia3, ta3); b3 = ldB(ib3, tb3);
+  for (int c = 0; c < nch; c += kRing) {
+#pragma unroll
+    for (int k = 0; k < kRing; ++k) {
+      if (k & 1) acc1 = use(ra[k], rb[k], ia[k], ta[k], ib[k], tb[k], acc1);
+      else acc0 = use(ra[k], rb[k], ia[k], ta[k], ib[k], tb[k], acc0);
+      ra[k] = ldA(ia[k], ta[k]);
+      rb[k] = ldB(ib[k], tb[k]);
+    }
   }
   return acc0 + acc1;
 }
@@ -1052,15 +1058,24 @@ __device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
 
 // ---------------------------------------------------------------- dispatch
 
-__global__ __launch_bounds__(kThreads) void rle_level(const Op* ops_g, int nops) {
+__global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
   __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
-  const CAS Op* ops = (const CAS Op*)ops_g;
+  const CAS Op* ops = (const CAS Op*)la.ops;
   const int wg = blockIdx.x;
-  int k = 0;
-  while (k + 1 < nops && ops[k + 1].wg_begin <= wg) ++k;
+  // op of this workgroup: from the kernel-argument table (SGPRs, no dependent
+  // descriptor loads), or by scanning descriptors for an oversized level
+  int k = 0, kind;
+  if (la.nops <= kLevelOps) {
+#pragma unroll
+    for (int q = 1; q < kLevelOps; ++q) k = (q < la.nops && la.wg_begin[q] <= wg) ? q : k;
+    kind = la.kind[k];
+  } else {
+    while (k + 1 < la.nops && ops[k + 1].wg_begin <= wg) ++k;
+    kind = ops[k].kind;
+  }
   const CAS Op& op = ops[k];
-  const int t = wg - op.wg_begin;
-  switch (op.kind) {
+  const int t = wg - (la.nops <= kLevelOps ? la.wg_begin[k] : op.wg_begin);
+  switch (kind) {
     case OP_GEMM: op_gemm(op.gemm, t, smem); break;
     case OP_NORMBWD: op_normbwd(op.nb, t); break;
     case OP_SAMPLE_REDUCE: op_sample_reduce(op.sample, t, smem); break;
@@ -1126,8 +1141,15 @@ __global__ void rle_fill_kernel(float* state, float* next_state, float* action, 
 
 // ---------------------------------------------------------------- host launchers
 
-hipError_t launch_level(const Op* d_ops, int nops, int nwg, hipStream_t st) {
-  hipLaunchKernelGGL(rle_level, dim3(nwg), dim3(kThreads), 0, st, d_ops, nops);
+hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st) {
+  LevelArgs la{};
+  la.ops = d_ops;
+  la.nops = nops;
+  for (int q = 0; q < nops && q < kLevelOps; ++q) {
+    la.wg_begin[q] = h_ops[q].wg_begin;
+    la.kind[q] = (unsigned char)h_ops[q].kind;
+  }
+  hipLaunchKernelGGL(rle_level, dim3(nwg), dim3(kThreads), 0, st, la);
   return hipGetLastError();
 }
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,

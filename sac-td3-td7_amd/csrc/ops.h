@@ -235,6 +235,16 @@ struct Op {
   };
 };
 
+// Kernel argument of one level launch: the workgroup -> op table travels in the
+// kernarg segment (one scalar load burst) instead of being searched in memory.
+constexpr int kLevelOps = 24;
+struct LevelArgs {
+  const Op* ops;
+  int nops;
+  int wg_begin[kLevelOps];
+  unsigned char kind[kLevelOps];
+};
+
 // Device control block.
 struct Ctrl {
   long long counters[16];   // [0..3] adam steps per optimizer, [4] rng step, [5] tape pos

@@ -11,7 +11,7 @@
 #include "ops.h"
 
 namespace rle {
-hipError_t launch_level(const Op* d_ops, int nops, int nwg, hipStream_t st);
+hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st);
 }
 using namespace rle;
 
@@ -55,7 +55,7 @@ static double time_level(std::vector<Op> ops, int reps, hipStream_t st) {
   // capture reps launches in a graph, like the engine
   hipGraph_t g; hipGraphExec_t x;
   CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-  for (int i = 0; i < reps; ++i) CK(launch_level(d, (int)ops.size(), wg, st));
+  for (int i = 0; i < reps; ++i) CK(launch_level(d, ops.data(), (int)ops.size(), wg, st));
   CK(hipStreamEndCapture(st, &g));
   CK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
   CK(hipGraphLaunch(x, st));
@@ -68,7 +68,7 @@ static double time_level(std::vector<Op> ops, int reps, hipStream_t st) {
   CK(hipEventSynchronize(b));
   float ms;
   CK(hipEventElapsedTime(&ms, a, b));
-  hipGraphExecDestroy(x); hipGraphDestroy(g); hipFree(d);
+  CK(hipGraphExecDestroy(x)); CK(hipGraphDestroy(g)); CK(hipFree(d));
   return ms * 1000.0 / reps;
 }
 
@@ -76,8 +76,8 @@ int main() {
   hipStream_t st;
   CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   const int K = 256, N = 256;
-  float* X = dalloc(2048 * 400);
-  float* W = dalloc(16 * 256 * 400);
+  float* X = dalloc(2048 * 1100);
+  float* W = dalloc(16 * 256 * 1100);
   float* bb = dalloc(4096);
   float* Y = dalloc(16 * 2048 * 256);
   long long* cnt; CK(hipMalloc(&cnt, 128)); CK(hipMemset(cnt, 0, 128));
@@ -112,6 +112,14 @@ int main() {
         md = std::max(md, std::abs(s - hy[(size_t)i * N + n]));
       }
     printf("fwd correctness max|d| = %.3g\n", md);
+  }
+  for (int Kk : {16, 64, 128, 256, 512, 1024}) {
+    Op o = fwd_op(X, W, bb, Y, 256, N, Kk);
+    printf("fwd 256x256xK=%4d (64 WG): %8.2f us\n", Kk, time_level({o}, reps, st));
+  }
+  for (int Kk : {16, 256, 1024}) {
+    Op o = fwd_op(X, W, bb, Y, 16, 64, Kk);
+    printf("fwd 16x64xK=%4d (1 WG)   : %8.2f us\n", Kk, time_level({o}, reps, st));
   }
   for (int M : {256, 512}) {
     Op o = fwd_op(X, W, bb, Y, M, N, K);
