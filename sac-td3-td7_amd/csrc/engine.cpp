@@ -110,18 +110,37 @@ struct Replay {
 
 // ------------------------------------------------------------------ programs
 
+// A tensor of the step program: fragment images (ops.h "tensor images") for
+// anything a GEMM touches, or a plain vector for 1-column tensors outside GEMMs.
 struct View {
-  float* p = nullptr;
-  int ld = 0, rows = 0, cols = 0;
+  Mat m{};                      // images (m.n / m.t may be null)
+  float* p = nullptr;           // plain vector data (1-column tensors), else null
+  int rows = 0, cols = 0;       // rows (16-multiple for images), padded columns
   int id = -1;
   const float* norm = nullptr;  // AvgL1Norm partials (producer |x| column-tile sums)
   int norm_ld = 0, norm_row0 = 0, nparts = 0, width = 0, norm_id = -1;
   View sub(int r0, int n) const {
     View v = *this;
-    v.p = p + (size_t)r0 * ld;
+    if (m.n || m.t) {
+      if (r0 % 16) throw Error{RLE_EINVAL, "sub-view of an image must start at a 16-row boundary"};
+      if (m.n) v.m.n = m.n + (size_t)(r0 / 16) * m.cbn * 256;
+      if (m.t) v.m.t = m.t + (size_t)(r0 / 16) * 256;
+    }
+    if (p) v.p = p + r0;
     v.rows = n;
     v.norm_row0 += r0;
     return v;
+  }
+  NormRef nref() const {
+    NormRef r{};
+    if (norm) {
+      r.part = norm;
+      r.ld = norm_ld;
+      r.row0 = norm_row0;
+      r.nparts = nparts;
+      r.width = width;
+    }
+    return r;
   }
 };
 
@@ -137,7 +156,7 @@ static void check_gemm(const GemmArgs& g) {
       REQUIRE(s.p != nullptr && s.r0 % 16 == 0 && s.r1 > s.r0, "gemm: bad reduction segment");
       if (!xsplit) {
         REQUIRE(s.x0 == 0 && s.x1 >= xn, "gemm: segment must span the operand rows");
-        if (q) REQUIRE(s.r0 >= o.seg[q - 1].r1, "gemm: reduction segments unsorted/overlapping");
+        if (q) REQUIRE(s.r0 == r16(o.seg[q - 1].r1), "gemm: reduction segments must be back to back");
       } else {
         REQUIRE(s.x0 % 16 == 0 && s.x1 % 16 == 0 && s.r0 == o.seg[0].r0 && s.r1 == o.seg[0].r1,
                 "gemm: bad column split");
@@ -213,7 +232,8 @@ struct Layer {
   std::string wname, bname;
   int out = 0, K = 0;
   std::vector<int> seg_w, seg_p;  // logical / padded widths of input segments
-  size_t w_off = 0, b_off = 0;
+  int rb = 0, cb = 0;             // 16-blocks of out rows / K columns
+  size_t wn_off = 0, wt_off = 0, b_off = 0;  // N image, T image, bias [16 rb]
   int res = -1;
 };
 
@@ -322,16 +342,20 @@ struct Engine {
     return n;
   }
 
+  // Per layer: weight N image | weight T image | bias (padded to 16 rows); the
+  // Adam m / v arenas mirror the layout at +nP / +2nP (m, v live at the T offsets).
   void layout_params() {
     size_t off = 0;
     for (auto& n : nets) {
       n.off = off;
       for (auto& L : n.layers) {
-        L.w_off = off;
-        off += (size_t)L.out * L.K;
-        off = (off + 3) & ~(size_t)3;
-        L.b_off = off;
-        off += (size_t)r4(L.out);
+        L.rb = cdiv(L.out, 16);
+        L.cb = L.K / 16;
+        const size_t img = (size_t)L.rb * L.cb * 256;
+        L.wn_off = off;
+        L.wt_off = off + img;
+        L.b_off = off + 2 * img;
+        off += 2 * img + (size_t)L.rb * 16;
       }
       n.size = off - n.off;
     }
@@ -339,8 +363,22 @@ struct Engine {
     P = mem.make<float>(3 * nP);  // params | m | v
   }
 
-  float* param(const Layer& L) { return P + L.w_off; }
+  Mat wmat(const Layer& L, int which = 0) {
+    Mat m{};
+    m.n = P + (size_t)which * nP + L.wn_off;
+    m.t = P + (size_t)which * nP + L.wt_off;
+    m.cbn = L.cb;
+    m.rbs = L.rb;
+    return m;
+  }
   float* bias(const Layer& L) { return P + L.b_off; }
+
+  static size_t h_nidx(int cbn, int r, int c) {
+    return ((size_t)(r >> 4) * cbn + (c >> 4)) * 256 + ((c >> 2) & 3) * 64 + (r & 15) * 4 + (c & 3);
+  }
+  static size_t h_tidx(int rbs, int r, int c) {
+    return ((size_t)(c >> 4) * rbs + (r >> 4)) * 256 + ((r >> 2) & 3) * 64 + (c & 15) * 4 + (r & 3);
+  }
 
   // locate (net, torch param name) -> (layer, is_bias)
   std::pair<Layer*, bool> find_param(const std::string& netn, const std::string& name) {
@@ -382,56 +420,86 @@ struct Engine {
       else HIPCHK(hipMemcpy(host, d, sizeof(float) * L.out, hipMemcpyDeviceToHost));
       return;
     }
-    std::vector<float> pad((size_t)L.out * L.K, 0.f);
-    float* d = P + base + L.w_off;
+    // weights: both images written from the logical [out][sum seg_w] array (params);
+    // read back from the T image (Adam m / v live only there)
+    const size_t img = (size_t)L.rb * L.cb * 256;
+    std::vector<float> tim(img, 0.f), nim(img, 0.f);
+    float* dt = P + base + L.wt_off;
+    float* dn = P + base + L.wn_off;
     int klog = 0;
     for (int w : L.seg_w) klog += w;
-    if (!to_dev) HIPCHK(hipMemcpy(pad.data(), d, pad.size() * 4, hipMemcpyDeviceToHost));
+    if (!to_dev) HIPCHK(hipMemcpy(tim.data(), dt, img * 4, hipMemcpyDeviceToHost));
     for (int o = 0; o < L.out; ++o) {
       int lc = 0, pc = 0;
       for (size_t s = 0; s < L.seg_w.size(); ++s) {
         for (int c = 0; c < L.seg_w[s]; ++c) {
-          float& dv = pad[(size_t)o * L.K + pc + c];
           float& hv = host[(size_t)o * klog + lc + c];
-          if (to_dev) dv = hv; else hv = dv;
+          const size_t ti = h_tidx(L.rb, o, pc + c);
+          if (to_dev) {
+            tim[ti] = hv;
+            nim[h_nidx(L.cb, o, pc + c)] = hv;
+          } else {
+            hv = tim[ti];
+          }
         }
         lc += L.seg_w[s];
         pc += L.seg_p[s];
       }
     }
-    if (to_dev) HIPCHK(hipMemcpy(d, pad.data(), pad.size() * 4, hipMemcpyHostToDevice));
+    if (to_dev) {
+      HIPCHK(hipMemcpy(dt, tim.data(), img * 4, hipMemcpyHostToDevice));
+      if (which == 0) HIPCHK(hipMemcpy(dn, nim.data(), img * 4, hipMemcpyHostToDevice));
+    }
   }
 
   // ---------------------------------------------------------------- buffers
-  // Zero-initialised activation buffer; feature dims padded to 16 (64-B rows),
-  // single-column vectors kept dense (ld 1).
-  View buf(int rows, int cols) {
+  // Zero-initialised tensor images (rows and columns padded to 16; padding stays
+  // zero, which the GEMM reduction relies on), or a dense vector.
+  View buf(int rows, int cols, bool want_n = true, bool want_t = true) {
     View v;
-    v.ld = cols == 1 ? 1 : r16(cols);
+    v.rows = r16(rows);
+    v.cols = r16(cols);
+    const size_t img = (size_t)v.rows * v.cols;
+    v.m.cbn = v.cols / 16;
+    v.m.rbs = v.rows / 16;
+    if (want_n) v.m.n = mem.make<float>(img);
+    if (want_t) v.m.t = mem.make<float>(img);
     v.rows = rows;
-    v.cols = v.ld;
-    v.p = mem.make<float>((size_t)rows * v.ld + 4);
+    v.id = next_id++;
+    return v;
+  }
+  View vec(int rows) {
+    View v;
+    v.rows = rows;
+    v.cols = 1;
+    v.p = mem.make<float>((size_t)rows + 4);
     v.id = next_id++;
     return v;
   }
 
   // ---------------------------------------------------------------- op builders
-  static Seg seg_contig(const View& v, int x0, int r0, int r1) {
+  // Operand segments: N image (x = tensor rows, reduction along columns) or
+  // T image (x = tensor columns, reduction along rows).
+  static Seg seg_n(const View& v, int r0, int r1) {
     Seg s{};
-    s.p = v.p;
-    s.ld = v.ld;
-    s.x0 = x0;
-    s.x1 = x0 + v.rows;
+    s.p = v.m.n;
+    s.xs = v.m.cbn;
+    s.x0 = 0;
+    s.x1 = v.rows;
     s.r0 = r0;
     s.r1 = r1;
-    s.strided = 0;
-    if (v.norm) {
-      s.norm = v.norm;
-      s.norm_ld = v.norm_ld;
-      s.norm_row0 = v.norm_row0;
-      s.norm_nparts = v.nparts;
-      s.norm_width = v.width;
-    }
+    s.norm = v.nref();
+    return s;
+  }
+  static Seg seg_t(const View& v, int x0, int r0, int r1) {
+    Seg s{};
+    s.p = v.m.t;
+    s.xs = v.m.rbs;
+    s.x0 = x0;
+    s.x1 = x0 + v.cols;
+    s.r0 = r0;
+    s.r1 = r1;
+    s.norm = v.nref();
     return s;
   }
 
@@ -448,7 +516,7 @@ struct Engine {
     for (size_t s = 0; s < ins.size(); ++s) {
       int xo = 0;
       for (const View& v : ins[s]) {
-        REQUIRE(v.cols == L.seg_p[s], "fwd: segment width mismatch for " + L.wname);
+        REQUIRE(v.cols == L.seg_p[s] && v.m.n, "fwd: segment width / image mismatch for " + L.wname);
         xo += v.rows;
         if (xo < M) cuts.push_back(xo);
         rd.push_back(v.id);
@@ -463,7 +531,7 @@ struct Engine {
     View out = buf(M, L.out);
     wr.push_back(out.id);
     if (pre_out) {
-      *pre_out = buf(M, L.out);
+      *pre_out = buf(M, L.out, false, true);
       wr.push_back(pre_out->id);
     }
     float* part = nullptr;
@@ -491,7 +559,7 @@ struct Engine {
         int xo = 0;
         for (const View& v : ins[s]) {
           if (ra >= xo && ra < xo + v.rows) {
-            g.A.seg[s] = seg_contig(v.sub(ra - xo, m), 0, koff, koff + L.seg_p[s]);
+            g.A.seg[s] = seg_n(v.sub(ra - xo, m), koff, koff + L.seg_p[s]);
             break;
           }
           xo += v.rows;
@@ -500,8 +568,8 @@ struct Engine {
       }
       g.A.nseg = (int)ins.size();
       Seg w{};
-      w.p = param(L);
-      w.ld = L.K;
+      w.p = P + L.wn_off;
+      w.xs = L.cb;
       w.x0 = 0;
       w.x1 = L.out;
       w.r0 = 0;
@@ -515,21 +583,16 @@ struct Engine {
       g.tiles_n = tiles_n;
       g.epi = EPI_STORE;
       g.act = act;
-      g.out = out.p + (size_t)ra * out.ld;
-      g.ldo = out.ld;
+      g.out = out.sub(ra, m).m;
       g.bias = bias(L);
-      if (pre_out) {
-        g.pre = pre_out->p + (size_t)ra * pre_out->ld;
-        g.ldpre = pre_out->ld;
-      }
+      if (pre_out) g.pre = pre_out->sub(ra, m).m;
       if (normed) {
         g.norm_out = part + ra;
         g.norm_ld = M;
       }
       if (noise && rb > noise_row0) {
         const int first = std::max(ra, noise_row0);  // first noised row (global)
-        g.noise = noise->p + (size_t)(first - noise_row0) * noise->ld;
-        g.ldnoise = noise->ld;
+        g.noise = noise->sub(first - noise_row0, rb - first).m;
         g.noise_row0 = first - ra;
         g.noise_sigma = cfg.target_policy_noise;
         g.noise_clip = cfg.noise_clip;
@@ -558,22 +621,15 @@ struct Engine {
     int roff = 0;
     for (size_t t = 0; t < terms.size(); ++t) {
       const DxTerm& tm = terms[t];
-      Seg a{};
-      a.p = tm.dz.p;
-      a.ld = tm.dz.ld;
-      a.x0 = 0;
-      a.x1 = M;
-      a.r0 = roff;
-      a.r1 = roff + tm.L->out;
-      g.A.seg[t] = a;
-      Seg b{};
-      b.p = param(*tm.L) + tm.col0;
-      b.ld = tm.L->K;
+      REQUIRE(tm.dz.m.n && tm.col0 % 16 == 0, "dx: operand layout");
+      g.A.seg[t] = seg_n(tm.dz, roff, roff + tm.L->out);
+      Seg b{};  // W[:, col0 : col0 + ncols] through the T image
+      b.p = P + tm.L->wt_off + (size_t)(tm.col0 / 16) * tm.L->rb * 256;
+      b.xs = tm.L->rb;
       b.x0 = 0;
       b.x1 = ncols;
       b.r0 = roff;
       b.r1 = roff + tm.L->out;
-      b.strided = 1;
       g.B.seg[t] = b;
       roff += r16(tm.L->out);
       rd.push_back(tm.dz.id);
@@ -588,12 +644,11 @@ struct Engine {
     g.epi = EPI_STORE;
     g.act = ACT_NONE;
     View out = buf(M, ncols);
-    g.out = out.p;
-    g.ldo = out.ld;
+    g.out = out.m;
     if (saved) {
+      REQUIRE(saved->m.t, "dx: derivative source needs a T image");
       g.dact = dact;
-      g.dsrc = saved->p;
-      g.lddact = saved->ld;
+      g.dsrc = saved->m;
       rd.push_back(saved->id);
     }
     wr.push_back(out.id);
@@ -606,42 +661,20 @@ struct Engine {
   void dw(Prog& pg, const Layer& L, const View& dz, const std::vector<View>& X, int Brows, int cnt, float lr,
           float* gsq = nullptr, float* gsq_b = nullptr) {
     REQUIRE(X.size() == L.seg_p.size(), "dw: input count mismatch for " + L.wname);
+    REQUIRE(dz.m.t, "dw: dZ needs a T image");
     Op op{};
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
     g.mode = GEMM_DW;
     std::vector<int> rd{dz.id, L.res, R_CNT}, wr{L.res};
-    Seg a{};
-    a.p = dz.p;
-    a.ld = dz.ld;
-    a.x0 = 0;
-    a.x1 = L.out;
-    a.r0 = 0;
-    a.r1 = Brows;
-    a.strided = 1;
-    g.A.seg[0] = a;
+    g.A.seg[0] = seg_t(dz, 0, 0, Brows);
     g.A.nseg = 1;
     int koff = 0;
     for (size_t s = 0; s < X.size(); ++s) {
       const View& v = X[s];
-      REQUIRE(v.cols == L.seg_p[s] && v.rows >= Brows, "dw: input view mismatch for " + L.wname);
-      Seg b{};
-      b.p = v.p;
-      b.ld = v.ld;
-      b.x0 = koff;
-      b.x1 = koff + L.seg_p[s];
-      b.r0 = 0;
-      b.r1 = Brows;
-      b.strided = 1;
-      if (v.norm) {
-        b.norm = v.norm;
-        b.norm_ld = v.norm_ld;
-        b.norm_row0 = v.norm_row0;
-        b.norm_nparts = v.nparts;
-        b.norm_width = v.width;
-        rd.push_back(v.norm_id);
-      }
-      g.B.seg[s] = b;
+      REQUIRE(v.cols == L.seg_p[s] && v.rows >= Brows && v.m.t, "dw: input view mismatch for " + L.wname);
+      g.B.seg[s] = seg_t(v, koff, 0, Brows);
+      if (v.norm) rd.push_back(v.norm_id);
       rd.push_back(v.id);
       koff += L.seg_p[s];
     }
@@ -653,7 +686,7 @@ struct Engine {
     g.tiles_n = cdiv(L.K, kTileN) + 1;
     g.epi = EPI_ADAM;
     AdamArgs& ad = g.adam;
-    ad.w = param(L);
+    ad.w = wmat(L);
     ad.b = bias(L);
     ad.mo = (long long)nP;
     ad.vo = 2LL * (long long)nP;
@@ -662,7 +695,6 @@ struct Engine {
     ad.beta1 = 0.9f;
     ad.beta2 = 0.999f;
     ad.eps = 1e-8f;
-    ad.ldw = L.K;
     ad.bias_col = cdiv(L.K, kTileN) * kTileN;
     ad.gsq = gsq;
     ad.gsq_b = gsq_b;
@@ -672,26 +704,20 @@ struct Engine {
 
   View normbwd(Prog& pg, const View& gv, const View& x) {
     REQUIRE(x.norm, "normbwd: x is not a normed view");
+    REQUIRE(gv.m.t && x.m.t && gv.rows % 16 == 0, "normbwd: operand layout");
     Op op{};
     op.kind = OP_NORMBWD;
     NormBwdArgs& a = op.nb;
     View out = buf(gv.rows, x.width);
-    a.g = gv.p;
-    a.ldg = gv.ld;
-    a.x = x.p;
-    a.ldx = x.ld;
-    a.dx = out.p;
-    a.lddx = out.ld;
+    a.g = gv.m;
+    a.x = x.m;
+    a.dx = out.m;
     a.rows = gv.rows;
     a.width = x.width;
-    a.norm = x.norm;
-    a.norm_ld = x.norm_ld;
-    a.norm_row0 = x.norm_row0;
-    a.norm_nparts = x.nparts;
-    op.wg_count = cdiv(gv.rows, 4);
+    a.norm = x.nref();
+    op.wg_count = cdiv(gv.rows, 16);
     pg.add(op, {gv.id, x.id, x.norm_id}, {out.id});
-    View o = out;
-    return o;
+    return out;
   }
 
   // polyak / copy over a whole net range
@@ -755,17 +781,14 @@ struct Engine {
     s.B = B;
     s.bsum = rp.bsum;
     s.nblk = rp.nblk;
-    s.ss = ss.p;
-    s.ldss = ss.ld;
-    s.a = act_in.p;
-    s.lda = act_in.ld;
+    s.ss = ss.m;
+    s.a = act_in.m;
     s.r = rw.p;
     s.nd = nd.p;
     s.ind = ind;
     s.u_out = u_buf;
-    s.eps = eps.p;
-    s.ldeps = eps.ld;
-    s.eps2 = sac ? eps2.p : nullptr;
+    s.eps = eps.m;
+    if (sac) s.eps2 = eps2.m;
     s.ctrl_rng = &ctrl->counters[4];
     s.seed = cfg.seed;
     s.tape_mode = &ctrl->tape_mode;
@@ -785,16 +808,17 @@ struct Engine {
     h.H = H;
     h.gamma = cfg.discount;
     h.inv_b = 1.f / (float)B;
-    op.wg_count = cdiv(rows, 4);
+    op.wg_count = cdiv(rows, 16);
     return op;
   }
 
   void set_head_twin(HeadArgs& h, const View& h1, const View& h2, const Layer& l1, const Layer& l2) {
-    h.h[0] = h1.p;
-    h.h[1] = h2.p;
-    h.ldh = h1.ld;
-    h.w[0] = param(l1);
-    h.w[1] = param(l2);
+    REQUIRE(h1.m.t && h2.m.t && l1.out == 1 && l2.out == 1, "head: operand layout");
+    h.h[0] = h1.m;
+    h.h[1] = h2.m;
+    h.w[0] = P + l1.wt_off;
+    h.w[1] = P + l2.wt_off;
+    h.w_rbs = l1.rb;
     h.b[0] = bias(l1);
     h.b[1] = bias(l2);
   }
@@ -863,11 +887,11 @@ struct Engine {
       op.kind = OP_GEMM;
       GemmArgs& g = op.gemm;
       g.mode = GEMM_FWD;
-      g.A.seg[0] = seg_contig(ea2, 0, 0, L.K);
+      g.A.seg[0] = seg_n(ea2, 0, L.K);
       g.A.nseg = 1;
       Seg w{};
-      w.p = param(L);
-      w.ld = L.K;
+      w.p = P + L.wn_off;
+      w.xs = L.cb;
       w.x1 = L.out;
       w.r1 = L.K;
       g.B.seg[0] = w;
@@ -880,9 +904,9 @@ struct Engine {
       g.epi = EPI_MSE;
       g.bias = bias(L);
       ed3 = buf(B, L.out);
-      g.out = ed3.p;
-      g.ldo = ed3.ld;
-      g.tgt = seg_contig(ezs2, 0, 0, L.out);
+      g.out = ed3.m;
+      g.tgt = ezs2.m;
+      g.tgt_norm = ezs2.nref();
       enc_tiles = g.tiles_m * g.tiles_n;
       enc_loss = mem.make<float>(enc_tiles);
       g.loss_part = enc_loss;
@@ -932,7 +956,7 @@ struct Engine {
       View t1 = fwd(pg, tq[n]->layers[1], {{t01}, {tzsa}, {tzs}}, B, ACT_ELU, nullptr, false);
       th[n] = fwd(pg, tq[n]->layers[2], {{t1}}, B, ACT_ELU, nullptr, false);
     }
-    View y = buf(B, 1);
+    View y = vec(B);
     {
       Op op = head_op(HEAD_TD7_TARGET, B);
       HeadArgs& h = op.head;
@@ -953,25 +977,23 @@ struct Engine {
       c1[n] = fwd(pg, q[n]->layers[1], {{c01[n]}, {fzsa}, {fzs}}, B, ACT_ELU, &c1z[n], false);
       c2[n] = fwd(pg, q[n]->layers[2], {{c1[n]}}, B, ACT_ELU, &c2z[n], false);
     }
-    View dz2[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1), buf(B, 1)};
-    View prio = buf(B, 1);
-    const int hw = cdiv(B, 4);
+    View dz2[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
+    View prio = vec(B);
+    const int hw = cdiv(B, 16);
     qloss_part = mem.make<float>((size_t)hw * 4);
     {
       Op op = head_op(HEAD_TD7_LOSS, B);
       HeadArgs& h = op.head;
       set_head_twin(h, c2[0], c2[1], q[0]->layers[3], q[1]->layers[3]);
-      h.dsrc[0] = c2z[0].p;
-      h.dsrc[1] = c2z[1].p;
-      h.ldd = c2z[0].ld;
+      h.dsrc[0] = c2z[0].m;
+      h.dsrc[1] = c2z[1].m;
       h.dact = ACT_ELU;
       h.lap = lap;
       h.y = y.p;
-      h.dz[0] = dz2[0].p;
-      h.dz[1] = dz2[1].p;
-      h.lddz = dz2[0].ld;
-      h.dq[0] = dq[0].p;
-      h.dq[1] = dq[1].p;
+      h.dz[0] = dz2[0].m;
+      h.dz[1] = dz2[1].m;
+      h.dq[0] = dq[0].m;
+      h.dq[1] = dq[1].m;
       h.loss_part = qloss_part;
       h.prio = prio.p;
       pg.add(op, {c2[0].id, c2[1].id, c2z[0].id, c2z[1].id, q[0]->layers[3].res, q[1]->layers[3].res, y.id},
@@ -1016,13 +1038,11 @@ struct Engine {
         Op op = head_op(HEAD_TD7_POLICY, B);
         HeadArgs& h = op.head;
         set_head_twin(h, p2[0], p2[1], q[0]->layers[3], q[1]->layers[3]);
-        h.dsrc[0] = p2z[0].p;
-        h.dsrc[1] = p2z[1].p;
-        h.ldd = p2z[0].ld;
+        h.dsrc[0] = p2z[0].m;
+        h.dsrc[1] = p2z[1].m;
         h.dact = ACT_ELU;
-        h.dz[0] = dzp2[0].p;
-        h.dz[1] = dzp2[1].p;
-        h.lddz = dzp2[0].ld;
+        h.dz[0] = dzp2[0].m;
+        h.dz[1] = dzp2[1].m;
         h.loss_part = ploss_part;
         pg.add(op, {p2[0].id, p2[1].id, p2z[0].id, p2z[1].id, q[0]->layers[3].res, q[1]->layers[3].res},
                {dzp2[0].id, dzp2[1].id, ploss_id = next_id++});
@@ -1132,20 +1152,17 @@ struct Engine {
     } else {
       raw = fwd(pg, pi.layers[2], {{h1}}, B2, ACT_NONE, nullptr, false);
       actv = buf(B2, A);
-      logpi = buf(B2, 1);
+      logpi = vec(B2);
       Op op{};
       op.kind = OP_SAC_ACTOR;
       SacActorArgs& a = op.sac;
-      a.out = raw.p;
-      a.ldo = raw.ld;
+      a.out = raw.m;
       a.A = A;
       a.rows = B2;
-      a.eps = eps.p;
-      a.eps2 = eps2.p;
-      a.ldeps = eps.ld;
+      a.eps = eps.m;
+      a.eps2 = eps2.m;
       a.eps_row_split = B;
-      a.act = actv.p;
-      a.ldact = actv.ld;
+      a.act = actv.m;
       a.logpi = logpi.p;
       a.min_log_std = cfg.min_log_std;
       a.max_log_std = cfg.max_log_std;
@@ -1158,7 +1175,7 @@ struct Engine {
     // target critics + y
     View th0[2], th1[2];
     for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n]);
-    View y = buf(B, 1);
+    View y = vec(B);
     {
       Op op = head_op(HEAD_MLP_TARGET, B);
       HeadArgs& h = op.head;
@@ -1179,25 +1196,23 @@ struct Engine {
     // online critics
     View c0[2], c1[2];
     for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c0[n], c1[n]);
-    View dz1[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1), buf(B, 1)};
-    View prio = buf(B, 1);
-    const int hw = cdiv(B, 4);
+    View dz1[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
+    View prio = vec(B);
+    const int hw = cdiv(B, 16);
     qloss_part = mem.make<float>((size_t)hw * 4);
     {
       Op op = head_op(HEAD_MLP_LOSS, B);
       HeadArgs& h = op.head;
       set_head_twin(h, c1[0], c1[1], q[0]->layers[2], q[1]->layers[2]);
-      h.dsrc[0] = c1[0].p;
-      h.dsrc[1] = c1[1].p;
-      h.ldd = c1[0].ld;
+      h.dsrc[0] = c1[0].m;
+      h.dsrc[1] = c1[1].m;
       h.dact = ACT_RELU;
       h.lap = lap;
       h.y = y.p;
-      h.dz[0] = dz1[0].p;
-      h.dz[1] = dz1[1].p;
-      h.lddz = dz1[0].ld;
-      h.dq[0] = dq[0].p;
-      h.dq[1] = dq[1].p;
+      h.dz[0] = dz1[0].m;
+      h.dz[1] = dz1[1].m;
+      h.dq[0] = dq[0].m;
+      h.dq[1] = dq[1].m;
       h.loss_part = qloss_part;
       h.prio = prio.p;
       pg.add(op, {c1[0].id, c1[1].id, q[0]->layers[2].res, q[1]->layers[2].res, y.id},
@@ -1233,13 +1248,11 @@ struct Engine {
         Op op = head_op(HEAD_MLP_POLICY, B);
         HeadArgs& h = op.head;
         set_head_twin(h, p1[0], p1[1], q[0]->layers[2], q[1]->layers[2]);
-        h.dsrc[0] = p1[0].p;
-        h.dsrc[1] = p1[1].p;
-        h.ldd = p1[0].ld;
+        h.dsrc[0] = p1[0].m;
+        h.dsrc[1] = p1[1].m;
         h.dact = ACT_RELU;
-        h.dz[0] = dzp1[0].p;
-        h.dz[1] = dzp1[1].p;
-        h.lddz = dzp1[0].ld;
+        h.dz[0] = dzp1[0].m;
+        h.dz[1] = dzp1[1].m;
         h.loss_part = ploss_part;
         std::vector<int> rd{p1[0].id, p1[1].id, q[0]->layers[2].res, q[1]->layers[2].res};
         if (sac) {
@@ -1263,20 +1276,16 @@ struct Engine {
         Op op{};
         op.kind = OP_SAC_ACTOR_BWD;
         SacActorArgs& a = op.sac;
-        a.out = raw.p;
-        a.ldo = raw.ld;
+        a.out = raw.m;
         a.A = A;
         a.rows = B;
-        a.eps2 = eps2.p;
-        a.ldeps = eps2.ld;
+        a.eps2 = eps2.m;
         a.min_log_std = cfg.min_log_std;
         a.max_log_std = cfg.max_log_std;
         a.mean_off = 0;
         a.ls_off = A;
-        a.da = da.p;
-        a.ldda = da.ld;
-        a.dout = dout.p;
-        a.lddout = dout.ld;
+        a.da = da.m;
+        a.dout = dout.m;
         a.log_alpha = P + (nP - 4);
         a.inv_b = 1.f / (float)B;
         op.wg_count = cdiv(B, kThreads);
@@ -1426,10 +1435,10 @@ struct Engine {
   void alloc_step_buffers() {
     ss = buf(2 * B, S);
     act_in = buf(B, A);
-    rw = buf(B, 1);
-    nd = buf(B, 1);
-    eps = buf(B, A);
-    eps2 = buf(B, A);
+    rw = vec(B);
+    nd = vec(B);
+    eps = buf(B, A, false, true);
+    eps2 = buf(B, A, false, true);
     ind = mem.make<long long>(B);
     u_buf = mem.make<float>(B);
     ind_id = next_id++;
@@ -1729,17 +1738,21 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     s.B = n;
     s.bsum = r.bsum;
     s.nblk = r.nblk;
-    s.ss = tmp.make<float>((size_t)2 * n * r.Sp);
-    s.ldss = r.Sp;
-    s.a = tmp.make<float>((size_t)n * r.Ap);
-    s.lda = r.Ap;
+    auto timg = [&](int rows, int cols) {  // scratch T image (outputs are not read back)
+      rle::Mat m{};
+      m.rbs = rle::r16(rows) / 16;
+      m.cbn = cols / 16;
+      m.t = tmp.make<float>((size_t)rle::r16(rows) * cols);
+      return m;
+    };
+    s.ss = timg(2 * n, r.Sp);
+    s.a = timg(n, r.Ap);
     s.r = tmp.make<float>(n);
     s.nd = tmp.make<float>(n);
     long long* dind = tmp.make<long long>(n);
     s.ind = dind;
     s.u_out = tmp.make<float>(n);
-    s.eps = tmp.make<float>((size_t)n * r.Ap);
-    s.ldeps = r.Ap;
+    s.eps = timg(n, r.Ap);
     long long* cnt = tmp.make<long long>(2);
     int* mode = tmp.make<int>(1);
     const int one = 1;
@@ -2051,23 +2064,24 @@ int rle_act(rle_engine* h, const float* obs, int n, float* out) {
     auto it = e.act_graphs.find(n);
     if (it == e.act_graphs.end()) {
       rle::Prog pg;
-      rle::View in = e.buf(n, e.S);
+      const int M = rle::r16(n);  // image rows; rows n..M-1 are padding
+      rle::View in = e.buf(M, e.S, true, false);
       rle::View o;
       if (e.algo == RLE_TD7) {  // td7.py:158-162
         rle::Net& fe = e.net("fixed_encoder");
         rle::Net& pi = e.net("policy");
-        rle::View h1 = e.fwd(pg, fe.layers[0], {{in}}, n, rle::ACT_ELU, nullptr, false);
-        rle::View h2 = e.fwd(pg, fe.layers[1], {{h1}}, n, rle::ACT_ELU, nullptr, false);
-        rle::View zs = e.fwd(pg, fe.layers[2], {{h2}}, n, rle::ACT_NONE, nullptr, true);
-        rle::View p0 = e.fwd(pg, pi.layers[0], {{in}}, n, rle::ACT_NONE, nullptr, true);
-        rle::View p1 = e.fwd(pg, pi.layers[1], {{p0}, {zs}}, n, rle::ACT_RELU, nullptr, false);
-        rle::View p2 = e.fwd(pg, pi.layers[2], {{p1}}, n, rle::ACT_RELU, nullptr, false);
-        o = e.fwd(pg, pi.layers[3], {{p2}}, n, rle::ACT_TANH, nullptr, false);
+        rle::View h1 = e.fwd(pg, fe.layers[0], {{in}}, M, rle::ACT_ELU, nullptr, false);
+        rle::View h2 = e.fwd(pg, fe.layers[1], {{h1}}, M, rle::ACT_ELU, nullptr, false);
+        rle::View zs = e.fwd(pg, fe.layers[2], {{h2}}, M, rle::ACT_NONE, nullptr, true);
+        rle::View p0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_NONE, nullptr, true);
+        rle::View p1 = e.fwd(pg, pi.layers[1], {{p0}, {zs}}, M, rle::ACT_RELU, nullptr, false);
+        rle::View p2 = e.fwd(pg, pi.layers[2], {{p1}}, M, rle::ACT_RELU, nullptr, false);
+        o = e.fwd(pg, pi.layers[3], {{p2}}, M, rle::ACT_TANH, nullptr, false);
       } else {
         rle::Net& pi = e.net("policy");
-        rle::View h0 = e.fwd(pg, pi.layers[0], {{in}}, n, rle::ACT_RELU, nullptr, false);
-        rle::View h1 = e.fwd(pg, pi.layers[1], {{h0}}, n, rle::ACT_RELU, nullptr, false);
-        o = e.fwd(pg, pi.layers[2], {{h1}}, n, rle::ACT_NONE, nullptr, false);
+        rle::View h0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_RELU, nullptr, false);
+        rle::View h1 = e.fwd(pg, pi.layers[1], {{h0}}, M, rle::ACT_RELU, nullptr, false);
+        o = e.fwd(pg, pi.layers[2], {{h1}}, M, rle::ACT_NONE, nullptr, false);
       }
       rle::Graph G = e.capture(pg);
       it = e.act_graphs.emplace(n, std::make_pair(G, o)).first;
@@ -2076,14 +2090,17 @@ int rle_act(rle_engine* h, const float* obs, int n, float* out) {
     rle::View in = e.act_inputs[n];
     rle::View o = it->second.second;
     const int W = e.algo == RLE_SAC ? 2 * e.A : e.A;
-    std::vector<float> pad((size_t)n * in.ld, 0.f);
-    for (int i = 0; i < n; ++i) std::memcpy(&pad[(size_t)i * in.ld], obs + (size_t)i * e.S, e.S * 4);
-    HIPCHK(hipMemcpyAsync(in.p, pad.data(), pad.size() * 4, hipMemcpyHostToDevice, e.stream));
+    const int M = rle::r16(n);
+    std::vector<float> img((size_t)M * in.cols, 0.f);
+    for (int i = 0; i < n; ++i)
+      for (int c = 0; c < e.S; ++c) img[Engine::h_nidx(in.m.cbn, i, c)] = obs[(size_t)i * e.S + c];
+    HIPCHK(hipMemcpyAsync(in.m.n, img.data(), img.size() * 4, hipMemcpyHostToDevice, e.stream));
     HIPCHK(hipGraphLaunch(it->second.first.x, e.stream));
-    std::vector<float> res((size_t)n * o.ld);
-    HIPCHK(hipMemcpyAsync(res.data(), o.p, res.size() * 4, hipMemcpyDeviceToHost, e.stream));
+    std::vector<float> res((size_t)M * o.cols);
+    HIPCHK(hipMemcpyAsync(res.data(), o.m.t, res.size() * 4, hipMemcpyDeviceToHost, e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
-    for (int i = 0; i < n; ++i) std::memcpy(out + (size_t)i * W, &res[(size_t)i * o.ld], W * 4);
+    for (int i = 0; i < n; ++i)
+      for (int c = 0; c < W; ++c) out[(size_t)i * W + c] = res[Engine::h_tidx(o.m.rbs, i, c)];
   });
 }
 

@@ -136,75 +136,73 @@ __device__ __forceinline__ float act_bwd(int act, float saved) {
   }
 }
 
-// LDS table of 1/m for n consecutive rows of a normed tensor (out of line: keeps
-// the GEMM main loops' register allocation independent of this rare prologue).
-__device__ __forceinline__ void build_norm_tab(const float* part, int ld, int row0, int nparts,
-                                                         int width, int n, float* dst) {
+__device__ __forceinline__ float norm_inv(const CAS NormRef& nr, int row) {
+  return 1.f / norm_m(nr.part, nr.ld, row + nr.row0, nr.nparts, nr.width);
+}
+
+// LDS table of 1/m for n consecutive rows of a normed tensor (16-padded with 0).
+__device__ __forceinline__ void build_norm_tab(const CAS NormRef& nr, int n, float* dst) {
 #pragma unroll 1
-  for (int i = threadIdx.x; i < n; i += kThreads) dst[i] = 1.f / norm_m(part, ld, i + row0, nparts, width);
+  for (int i = threadIdx.x; i < n; i += kThreads) dst[i] = norm_inv(nr, i);
 #pragma unroll 1
   for (int i = n + threadIdx.x; i < ((n + 15) & ~15); i += kThreads) dst[i] = 0.f;
+}
+
+// ---------------------------------------------------------------- tensor images (ops.h "tensor images")
+__device__ __forceinline__ size_t nidx(int cbn, int r, int c) {
+  return ((size_t)(r >> 4) * cbn + (c >> 4)) * 256 + ((c >> 2) & 3) * 64 + (r & 15) * 4 + (c & 3);
+}
+__device__ __forceinline__ size_t tidx(int rbs, int r, int c) {
+  return ((size_t)(c >> 4) * rbs + (r >> 4)) * 256 + ((r >> 2) & 3) * 64 + (c & 15) * 4 + (r & 3);
+}
+// Element read (T image preferred, else N) / write (every kept image).
+__device__ __forceinline__ float mat_ld(const CAS Mat& m, int r, int c) {
+  return m.t ? G(m.t)[tidx(m.rbs, r, c)] : G(m.n)[nidx(m.cbn, r, c)];
+}
+__device__ __forceinline__ void mat_st(const CAS Mat& m, int r, int c, float v) {
+  if (m.t) GW(m.t)[tidx(m.rbs, r, c)] = v;
+  if (m.n) GW(m.n)[nidx(m.cbn, r, c)] = v;
+}
+// Four consecutive rows r..r+3 (r % 4 == 0) of column c: one float4 of the T image.
+__device__ __forceinline__ float4 mat_ld4(const CAS Mat& m, int r, int c) {
+  return ld4g(G(m.t) + tidx(m.rbs, r, c));
+}
+__device__ __forceinline__ void mat_st4(const CAS Mat& m, int r, int c, float4 v) {
+  if (m.t) st4g(GW(m.t) + tidx(m.rbs, r, c), v);
+  if (m.n) {
+    GAS float* q = GW(m.n) + nidx(m.cbn, r, c);  // rows r..r+3 are 4 floats apart in the N image
+    q[0] = v.x;
+    q[4] = v.y;
+    q[8] = v.z;
+    q[12] = v.w;
+  }
 }
 
 // ---------------------------------------------------------------- GEMM
 //
 // One workgroup = one 16 x 64 output tile; wave w owns columns [16w, 16w+16)
-// and the FULL reduction.  Each lane owns one output row (operand A) and one
-// output column (operand B) of the v_mfma_f32_16x16x4_f32 fragment and
-// streams 4 consecutive reduction indices per 16-wide chunk: a contiguous
-// operand is one 16-byte buffer load per lane per chunk, a strided one four
-// 4-byte loads.  Operand segments are 16-aligned in BOTH the reduction and
-// the operand-row dimension (host invariant, checked in engine.cpp), so the
-// segment of a chunk is wave-uniform: it is selected with scalar compares
-// and addressed through a buffer resource built from SGPRs.  Lanes and
-// reduction rows outside the segment get an out-of-range voffset, which the
-// buffer unit returns as 0 -- the main loop has no branches around its loads,
-// so the 4-chunk register ring (loads for chunk c+4 issue right after chunk
-// c's MFMAs) survives s_waitcnt placement.  AvgL1Norm scales (deferred
-// normalisation) are applied when a chunk is consumed, never when it is
-// loaded.  Epilogue operands (bias, derivative source, Adam m/v/param) are
-// fetched before the main loop; the epilogue runs from registers (lane: rows
-// 4*(l>>4)+q, column l&15).
+// and the FULL reduction.  Both operands are fragment images (ops.h), so each
+// 16-wide reduction chunk is one lane-linear 16-byte buffer load per lane per
+// operand -- the wave reads whole 1 KB blocks (8 full cache lines) instead of
+// 16 row pieces.  A load cursor per operand walks the reduction block by block
+// and segment by segment; 4 chunks are kept in flight in a register ring.
+// AvgL1Norm scales (deferred normalisation) are applied when a chunk is
+// consumed.  Epilogue operands (bias, derivative source, Adam w/m/v) are
+// fetched before the main loop; the accumulator fragment (rows 4*(l>>4)+q,
+// column l&15) is exactly one float4 of a T image, so T-image traffic in the
+// epilogue is one 16-byte access per lane.
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 static_assert(kMaxSeg == 4, "LaneOp holds 4 segments");
-constexpr int kRing = 4;          // GEMM main-loop chunks in flight per wave
-constexpr int kOOB = 0x7ffffff0;  // voffset beyond any num_records: the load returns 0
+constexpr int kRing = 4;  // GEMM main-loop chunks in flight per wave
 
 struct LaneOp {
-  f32x4 inv;  // contiguous + normed: 1/m of the lane's row, per segment (vector, not array:
-              // a per-chunk select must stay in registers)
-  i32x4 tab;  // strided + normed: LDS offset of the segment's 1/m table, -1 = none
-  int xw;     // first operand row/column of this wave (wave-uniform)
+  f32x4 inv;  // N-image operand + normed: 1/m of the lane's row, per segment (vector, not
+              // array: a per-chunk select must stay in registers)
+  i32x4 tab;  // T-image operand + normed: LDS offset of the segment's 1/m table, -1 = none
   bool norm;  // any normed segment
 };
-
-__device__ __forceinline__ void lane_op(const CAS Operand& op, bool STRIDED, int x, int xw, LaneOp& L,
-                                        float* tabs, int& used) {
-  L.inv = f32x4{1.f, 1.f, 1.f, 1.f};
-  L.tab = i32x4{-1, -1, -1, -1};
-  L.xw = xw;
-  L.norm = false;
-#pragma unroll
-  for (int s = 0; s < kMaxSeg; ++s) {
-    if (s < op.nseg) {
-      const CAS Seg& sg = op.seg[s];
-      if (sg.norm) {
-        L.norm = true;
-        if (!STRIDED) {
-          if (x >= sg.x0 && x < sg.x1)
-            L.inv[s] = 1.f / norm_m(sg.norm, sg.norm_ld, x - sg.x0 + sg.norm_row0, sg.norm_nparts, sg.norm_width);
-        } else {
-          const int n = sg.r1 - sg.r0;
-          L.tab[s] = used;
-          build_norm_tab(sg.norm, sg.norm_ld, sg.norm_row0, sg.norm_nparts, sg.norm_width, n, tabs + used);
-          used += (n + 15) & ~15;
-        }
-      }
-    }
-  }
-}
 
 // v[q] for a wave-uniform q as a select chain (a variable extract is lowered to scratch).
 template <class V>
@@ -212,84 +210,76 @@ __device__ __forceinline__ auto pick(const V& v, int q) -> decltype(v[0] + 0) {
   return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
 }
 
+__device__ __forceinline__ void lane_op(const CAS Operand& op, bool T, int x, LaneOp& L, float* tabs, int& used) {
+  L.inv = f32x4{1.f, 1.f, 1.f, 1.f};
+  L.tab = i32x4{-1, -1, -1, -1};
+  L.norm = false;
+#pragma unroll
+  for (int s = 0; s < kMaxSeg; ++s) {
+    if (s < op.nseg) {
+      const CAS Seg& sg = op.seg[s];
+      if (sg.norm.part) {
+        L.norm = true;
+        if (!T) {
+          if (x >= sg.x0 && x < sg.x1) L.inv[s] = norm_inv(sg.norm, x - sg.x0);
+        } else {
+          const int n = sg.r1 - sg.r0;
+          L.tab[s] = used;
+          build_norm_tab(sg.norm, n, tabs + used);
+          used += (n + 15) & ~15;
+        }
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ float4 as_f4(u32x4 v) {
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
 
-// Load cursor of one operand: walks the reduction chunk by chunk, segment after
-// segment (segments are 16-aligned and back to back in the reduction, host
-// invariant), so a chunk costs one voffset add and a counter decrement; the
-// segment switch (scalar descriptor loads) happens once per segment.
-template <bool STRIDED>
+// Load cursor of one operand: lane-linear 1 KB block per chunk, segment after segment.
 struct Cursor {
   __amdgpu_buffer_rsrc_t rs;  // current segment (wave-uniform)
   int voff;                   // this lane's byte offset of the next chunk
-  int step;                   // bytes per chunk
   int left;                   // chunks left in the segment
-  int s;                      // segment index (nseg: past the end)
-  int ldb;                    // strided: bytes per reduction row
-  int rrem;                   // strided: segment rows left from this lane's first row
-  int toff;                   // strided + normed: LDS 1/m table offset of the next chunk (-1: none)
-  float inv;                  // contiguous + normed: lane row's 1/m in the segment
+  int s;                      // segment index (>= nseg: past the end, reads 0)
+  int toff;                   // T image + normed: LDS 1/m table offset of the next chunk (-1: none)
+  float inv;                  // N image + normed: lane row's 1/m in the segment
 
-  __device__ __forceinline__ void open(const CAS Operand& op, const LaneOp& L, int x, int rl, int q, int x0) {
+  __device__ __forceinline__ void open(const CAS Operand& op, const LaneOp& L, int xw, int q) {
     s = q;
-    if (q >= op.nseg) {  // past the last segment: everything reads as 0
+    if (q >= op.nseg) {
       rs = __builtin_amdgcn_make_buffer_rsrc((void*)nullptr, 0, 0, 0x00020000);
       left = 1 << 30;
       voff = 0;
-      step = 0;
-      rrem = 0;
       toff = -1;
       inv = 1.f;
       return;
     }
     const CAS Seg& sg = op.seg[q];
     rs = __builtin_amdgcn_make_buffer_rsrc((void*)sg.p, 0, 0x7fff0000, 0x00020000);
-    const int n = sg.r1 - sg.r0;
-    left = (n + 15) >> 4;
-    if (!STRIDED) {
-      voff = ((x - x0) * sg.ld + rl) * 4;
-      step = 64;
-      inv = pick(L.inv, q);
-      toff = -1;
-    } else {
-      ldb = sg.ld * 4;
-      voff = (x - x0) * 4 + rl * ldb;
-      step = 16 * ldb;
-      rrem = n - rl;
-      toff = pick(L.tab, q);
-      inv = 1.f;
-    }
+    left = (sg.r1 - sg.r0 + 15) >> 4;
+    voff = ((xw - sg.x0) >> 4) * sg.xs * 1024 + (threadIdx.x & 63) * 16;
+    inv = pick(L.inv, q);
+    toff = pick(L.tab, q);
   }
-  // Loads this lane's 4 values of the next chunk; returns the chunk's norm
-  // scale handle (contiguous: 1/m, strided: table offset) through inv_out/toff_out.
-  __device__ __forceinline__ float4 next(const CAS Operand& op, const LaneOp& L, int x, int rl, int x0, bool ok,
-                                         float& inv_out, int& toff_out) {
-    if (left == 0) open(op, L, x, rl, s + 1, x0);
-    float4 v;
-    if (!STRIDED) {
-      v = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rs, ok ? voff : kOOB, 0, 0));
-    } else {
-      v.x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && rrem > 0 ? voff : kOOB, 0, 0));
-      v.y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && rrem > 1 ? voff + ldb : kOOB, 0, 0));
-      v.z = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && rrem > 2 ? voff + 2 * ldb : kOOB, 0, 0));
-      v.w = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && rrem > 3 ? voff + 3 * ldb : kOOB, 0, 0));
-      rrem -= 16;
-    }
+  __device__ __forceinline__ float4 next(const CAS Operand& op, const LaneOp& L, int xw, float& inv_out,
+                                         int& toff_out) {
+    if (left == 0) open(op, L, xw, s + 1);
+    const float4 v = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
     inv_out = inv;
     toff_out = toff;
-    if (STRIDED && toff >= 0) toff += 16;
-    voff += step;
+    if (toff >= 0) toff += 16;
+    voff += 1024;
     --left;
     return v;
   }
 };
 
 // Deferred AvgL1Norm of a consumed chunk.
-template <bool STRIDED>
+template <bool T>
 __device__ __forceinline__ float4 chunk_scale(float4 v, float inv, int toff, int rl, const float* tabs) {
-  if (!STRIDED) {
+  if (!T) {
     v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
   } else if (toff >= 0) {
     const float4 w = *(const float4*)(tabs + toff + rl);
@@ -306,54 +296,49 @@ __device__ __forceinline__ f32x4 mfma4(const float4& a, const float4& b, f32x4 a
   return acc;
 }
 
-// Main loop, one instantiation per operand layout (FWD <0,0>, DX <0,1>, DW <1,1>,
-// DW bias column <1,-,1> with B = ones).  xa_w / xb_w: the wave's first A row / B
-// column (wave-uniform).
-template <bool SA, bool SB, bool BIAS>
+// Main loop, one instantiation per operand image pair (FWD <N,N>, DX <N,T>,
+// DW <T,T>, DW bias column <T,-> with B = ones).  xa_w / xb_w: the wave's first
+// A row / B column (wave-uniform).
+template <bool TA, bool TB, bool BIAS>
 __device__ __forceinline__ f32x4 gemm_mainloop(const CAS GemmArgs& g, int xa, int xb, int xa_w, int xb_w,
                                                bool active, float* tabs) {
   const int lane = threadIdx.x & 63;
   LaneOp la, lb;
   int used = 0;
-  lane_op(g.A, SA, xa, xa_w, la, tabs, used);
-  if (!BIAS) lane_op(g.B, SB, xb, xb_w, lb, tabs, used);
+  lane_op(g.A, TA, xa, la, tabs, used);
+  if (!BIAS) lane_op(g.B, TB, xb, lb, tabs, used);
   if (used) __syncthreads();
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
   if (!active) return acc0;
-  const bool a_ok = xa < g.M;
-  const bool b_ok = BIAS ? (xb == g.adam.bias_col) : (xb < g.N);
+  const bool b_ok = BIAS ? (xb == g.adam.bias_col) : true;
   const int rl = 4 * (lane >> 4);
   const int nch = (g.R + 15) >> 4;
   const bool an = la.norm, bn = !BIAS && lb.norm;
-  // B of a DW op: the segments split the columns; the wave's 16 columns lie in one of them.
-  int qb = 0, xb0 = 0;
-  if (SA && SB && !BIAS) {
+  // DW B: the segments split the columns; the wave's 16 columns lie in one of them
+  int qb = 0;
+  if (TA && TB && !BIAS) {
 #pragma unroll
-    for (int q = 0; q < kMaxSeg; ++q)
-      if (q < g.B.nseg && xb_w >= g.B.seg[q].x0 && xb_w < g.B.seg[q].x1) qb = q;
-    xb0 = g.B.seg[qb].x0;
+    for (int q = 1; q < kMaxSeg; ++q)
+      if (q < g.B.nseg && xb_w >= g.B.seg[q].x0) qb = q;
   }
-  Cursor<SA> ca;
-  Cursor<SB> cb;
-  ca.open(g.A, la, xa, rl, 0, 0);
-  if (!BIAS) cb.open(g.B, lb, xb, rl, qb, xb0);
-  const int nb_end = (SA && SB) ? qb + 1 : g.B.nseg;  // DW: one B segment only
+  Cursor ca, cb;
+  ca.open(g.A, la, xa_w, 0);
+  if (!BIAS) cb.open(g.B, lb, xb_w, qb);
+  const int nb_end = (TA && TB) ? qb + 1 : g.B.nseg;  // DW: one B segment only
   const float4 ones = b_ok ? make_float4(1.f, 1.f, 1.f, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
-  auto ldA = [&](float& i, int& t) { return ca.next(g.A, la, xa, rl, 0, a_ok, i, t); };
+  auto ldA = [&](float& i, int& t) { return ca.next(g.A, la, xa_w, i, t); };
   auto ldB = [&](float& i, int& t) {
     if constexpr (BIAS) return ones;  // db = sum_r dZ(r, n); A is zero past R
     else {
       if (cb.left == 0 && cb.s + 1 >= nb_end) cb.s = kMaxSeg;  // DW: never walk into another column block
-      return cb.next(g.B, lb, xb, rl, xb0, b_ok, i, t);
+      return cb.next(g.B, lb, xb_w, i, t);
     }
   };
   auto use = [&](float4 a, float4 b, float ia, int ta, float ib, int tb, f32x4 acc) {
-    if (an) a = chunk_scale<SA>(a, ia, ta, rl, tabs);
-    if (bn) b = chunk_scale<SB>(b, ib, tb, rl, tabs);
+    if (an) a = chunk_scale<TA>(a, ia, ta, rl, tabs);
+    if (bn) b = chunk_scale<TB>(b, ib, tb, rl, tabs);
     return mfma4(a, b, acc);
   };
-  // kRing chunks in flight: with L2 cold at every kernel start (operands come from
-  // MALL / HBM, ~1000+ cycles), 8 chunks keep the wave near the MFMA rate.
   float4 ra[kRing], rb[kRing];
   float ia[kRing], ib[kRing];
   int ta[kRing], tb[kRing];
@@ -377,8 +362,7 @@ __device__ __forceinline__ f32x4 gemm_mainloop(const CAS GemmArgs& g, int xa, in
 
 __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* smem) {
   // wave index via readfirstlane: the compiler then treats every wave-derived
-  // condition as uniform (scalar branches; divergent-region structurisation of the
-  // four inlined main loops otherwise keeps all of them live: ~250 VGPRs)
+  // condition as uniform (scalar branches)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int it = t / g.tiles_n, jt = t - it * g.tiles_n;
   const int i0 = it * kTileM, j0 = jt * kTileN + wave * 16;
@@ -392,33 +376,31 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
   const bool active = bias_tile ? (wave == 0) : (j0 < g.N);  // wave-uniform
 
   // ---- epilogue operands fetched ahead of the main loop
-  float pre_b = 0.f, ds[4] = {1.f, 1.f, 1.f, 1.f}, pp[4] = {0.f, 0.f, 0.f, 0.f}, mm[4] = {0.f, 0.f, 0.f, 0.f},
-        vv[4] = {0.f, 0.f, 0.f, 0.f};
-  GAS float* ptr[4] = {nullptr, nullptr, nullptr, nullptr};
+  float pre_b = 0.f;
+  float4 ds = make_float4(1.f, 1.f, 1.f, 1.f), pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
+  size_t wt = 0;  // T-image element offset of (ib, j) in the weight (EPI_ADAM)
   if (g.epi != EPI_ADAM) {
     if (g.bias && jok) pre_b = G(g.bias)[j];
-    if (g.dsrc && jok) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (ib + q < g.M) ds[q] = G(g.dsrc)[(size_t)(ib + q) * g.lddact + j];
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = ib + q;
-      if (jok && i < g.M) ptr[q] = bias_tile ? GW(g.adam.b) + i : GW(g.adam.w) + (size_t)i * g.adam.ldw + j;
-      if (ptr[q]) {
-        pp[q] = *ptr[q];
-        mm[q] = ptr[q][g.adam.mo];
-        vv[q] = ptr[q][g.adam.vo];
+    if (g.dsrc.t && jok) ds = mat_ld4(g.dsrc, ib, j);
+  } else if (active) {
+    const CAS AdamArgs& ad = g.adam;
+    if (bias_tile) {
+      if (jok) {
+        pp = ld4g(G(ad.b) + ib);
+        mm = ld4g(G(ad.b) + ib + ad.mo);
+        vv = ld4g(G(ad.b) + ib + ad.vo);
       }
+    } else {
+      wt = tidx(ad.w.rbs, ib, j);
+      pp = ld4g(G(ad.w.t) + wt);
+      mm = ld4g(G(ad.w.t) + wt + ad.mo);
+      vv = ld4g(G(ad.w.t) + wt + ad.vo);
     }
   }
 
   const int xa_w = i0, xb_w = j0;  // wave-uniform operand origins
   // The distinct empty asm statements head each arm so the compiler cannot hoist
-  // the arms' common descriptor loads above the branch (that keeps all four
-  // main loops' scalar state live at once and spills it into ~150 extra VGPRs).
+  // the arms' common descriptor loads above the branch.
   f32x4 acc;
   if (g.mode == GEMM_FWD) {
     asm volatile("; gemm fwd" ::);
@@ -436,22 +418,25 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
 
   if (g.epi == EPI_STORE) {
     float rowabs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (jok) {
+      float v[4] = {acc[0] + pre_b, acc[1] + pre_b, acc[2] + pre_b, acc[3] + pre_b};
+      if (g.pre.t) mat_st4(g.pre, ib, j, make_float4(v[0], v[1], v[2], v[3]));
+      float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool noised = g.noise.t && ib >= g.noise_row0;  // target policy smoothing (td7.py:188-194)
+      if (noised) e = mat_ld4(g.noise, ib - g.noise_row0, j);
+      const float ev[4] = {e.x, e.y, e.z, e.w}, dv[4] = {ds.x, ds.y, ds.z, ds.w};
+      float y[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = ib + q;
-      if (i < g.M && jok) {
-        const float v = acc[q] + pre_b;
-        if (g.pre) GW(g.pre)[(size_t)i * g.ldpre + j] = v;
-        float y = act_fwd(g.act, v);
-        if (g.noise && i >= g.noise_row0) {  // target policy smoothing (td7.py:188-194)
-          float e = G(g.noise)[(size_t)(i - g.noise_row0) * g.ldnoise + j] * g.noise_sigma;
-          e = fminf(fmaxf(e, -g.noise_clip), g.noise_clip);
-          y = fminf(fmaxf(y + e, -1.f), 1.f);
+      for (int q = 0; q < 4; ++q) {
+        y[q] = act_fwd(g.act, v[q]);
+        if (noised) {
+          const float nz = fminf(fmaxf(ev[q] * g.noise_sigma, -g.noise_clip), g.noise_clip);
+          y[q] = fminf(fmaxf(y[q] + nz, -1.f), 1.f);
         }
-        if (g.dsrc) y *= act_bwd(g.dact, ds[q]);
-        GW(g.out)[(size_t)i * g.ldo + j] = y;
-        rowabs[q] = fabsf(y);
+        if (g.dsrc.t) y[q] *= act_bwd(g.dact, dv[q]);
+        rowabs[q] = fabsf(y[q]);
       }
+      mat_st4(g.out, ib, j, make_float4(y[0], y[1], y[2], y[3]));
     }
     if (g.norm_out) {  // |y| summed over the tile's 64 columns, per row
 #pragma unroll
@@ -470,18 +455,18 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
     }
   } else if (g.epi == EPI_MSE) {  // td7.py:256 encoder loss, grad wrt zsa
     float d2 = 0.f;
-    const CAS Seg& sg = g.tgt;
+    if (jok) {
+      const float4 tv = mat_ld4(g.tgt, ib, j);
+      const float tq[4] = {tv.x, tv.y, tv.z, tv.w};
+      float gr[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = ib + q;
-      if (i < g.M && jok) {
-        const float v = acc[q] + pre_b;
-        float tv = G(sg.p)[(size_t)(i - sg.x0) * sg.ld + j];
-        if (sg.norm) tv *= 1.f / norm_m(sg.norm, sg.norm_ld, i - sg.x0 + sg.norm_row0, sg.norm_nparts, sg.norm_width);
-        const float d = v - tv;
-        GW(g.out)[(size_t)i * g.ldo + j] = (2.f * d) * g.mse_scale;  // mse_scale = 1/n
+      for (int q = 0; q < 4; ++q) {
+        const float tn = tq[q] * norm_inv(g.tgt_norm, ib + q);
+        const float d = (acc[q] + pre_b) - tn;
+        gr[q] = (2.f * d) * g.mse_scale;  // mse_scale = 1/n
         d2 += d * d;
       }
+      mat_st4(g.out, ib, j, make_float4(gr[0], gr[1], gr[2], gr[3]));
     }
     d2 = wg_sum(d2, red);
     if (tid == 0) GW(g.loss_part)[t] = d2;
@@ -493,18 +478,37 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
     const float step_size = (float)((double)ad.lr / bc1);
     const float bc2s = (float)sqrt(bc2);
     float gg = 0.f;
+    if (active && jok) {
+      const float p4[4] = {pp.x, pp.y, pp.z, pp.w}, m4[4] = {mm.x, mm.y, mm.z, mm.w}, v4[4] = {vv.x, vv.y, vv.z, vv.w};
+      float po[4], mo[4], vo[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (!ptr[q]) continue;
-      const float gv = acc[q];
-      float m = mm[q], v2 = vv[q];
-      m = m + (1.f - ad.beta1) * (gv - m);
-      v2 = v2 * ad.beta2 + ((1.f - ad.beta2) * gv) * gv;
-      const float denom = sqrtf(v2) / bc2s + ad.eps;
-      ptr[q][ad.mo] = m;
-      ptr[q][ad.vo] = v2;
-      *ptr[q] = pp[q] + (-step_size * m) / denom;
-      gg += gv * gv;
+      for (int q = 0; q < 4; ++q) {
+        const float gv = acc[q];
+        float m = m4[q], v2 = v4[q];
+        m = m + (1.f - ad.beta1) * (gv - m);
+        v2 = v2 * ad.beta2 + ((1.f - ad.beta2) * gv) * gv;
+        const float denom = sqrtf(v2) / bc2s + ad.eps;
+        const bool ok = ib + q < g.M;  // weight rows past out stay untouched (zero)
+        po[q] = ok ? p4[q] + (-step_size * m) / denom : p4[q];
+        mo[q] = ok ? m : m4[q];
+        vo[q] = ok ? v2 : v4[q];
+        gg += ok ? gv * gv : 0.f;
+      }
+      const float4 P = make_float4(po[0], po[1], po[2], po[3]);
+      if (bias_tile) {
+        st4g(GW(ad.b) + ib, P);
+        st4g(GW(ad.b) + ib + ad.mo, make_float4(mo[0], mo[1], mo[2], mo[3]));
+        st4g(GW(ad.b) + ib + ad.vo, make_float4(vo[0], vo[1], vo[2], vo[3]));
+      } else {
+        st4g(GW(ad.w.t) + wt, P);
+        st4g(GW(ad.w.t) + wt + ad.mo, make_float4(mo[0], mo[1], mo[2], mo[3]));
+        st4g(GW(ad.w.t) + wt + ad.vo, make_float4(vo[0], vo[1], vo[2], vo[3]));
+        GAS float* qn = GW(ad.w.n) + nidx(ad.w.cbn, ib, j);
+        qn[0] = po[0];
+        qn[4] = po[1];
+        qn[8] = po[2];
+        qn[12] = po[3];
+      }
     }
     if (ad.gsq) {
       gg = wg_sum(gg, red);
@@ -518,143 +522,170 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
 
 // ---------------------------------------------------------------- AvgL1Norm backward
 
+// 16 rows per workgroup, 4 per wave: lane k reads a float4 (4 rows) of column k
+// from the T images; the per-row dot products are wave reductions.
 __device__ __forceinline__ void op_normbwd(const CAS NormBwdArgs& a, int t) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row = t * 4 + wave;
-  if (row >= a.rows) return;
-  const GAS float* x = G(a.x) + (size_t)row * a.ldx;
-  const GAS float* g = G(a.g) + (size_t)row * a.ldg;
-  // m recomputed from the same partials the forward consumers used
-  float s = 0.f;
-  for (int q = 0; q < a.norm_nparts; ++q) s += G(a.norm)[(size_t)q * a.norm_ld + row + a.norm_row0];
-  const float mean = s / (float)a.width;
-  const bool clamped = mean < 1e-8f;
-  const float inv = 1.f / (clamped ? 1e-8f : mean);
-  float xv[8], gv[8];
-  float dot = 0.f;
+  const int r0 = t * 16 + wave * 4;
+  if (r0 >= a.rows) return;
+  float inv[4], gmv[4];
+  bool clamped[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float s = 0.f;  // m recomputed from the same partials the forward consumers used
+    for (int p = 0; p < a.norm.nparts; ++p) s += G(a.norm.part)[(size_t)p * a.norm.ld + r0 + q + a.norm.row0];
+    const float mean = s / (float)a.width;
+    clamped[q] = mean < 1e-8f;
+    inv[q] = 1.f / (clamped[q] ? 1e-8f : mean);
+  }
+  float4 xv[8], gv[8];
+  float dot[4] = {0.f, 0.f, 0.f, 0.f};
   const int per = (a.width + 63) / 64;
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int k = lane + 64 * u;
-    xv[u] = (u < per && k < a.width) ? x[k] : 0.f;
-    gv[u] = (u < per && k < a.width) ? g[k] : 0.f;
-    dot += gv[u] * xv[u];
+    const bool in = u < per && k < a.width;
+    xv[u] = in ? mat_ld4(a.x, r0, k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[u] = in ? mat_ld4(a.g, r0, k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    dot[0] += gv[u].x * xv[u].x;
+    dot[1] += gv[u].y * xv[u].y;
+    dot[2] += gv[u].z * xv[u].z;
+    dot[3] += gv[u].w * xv[u].w;
   }
-  dot = wave_sum(dot);
-  // y = x / m: dy/dx path g/m ; dm path -(sum g x)/m^2 * sign(x)/n (unless clamped)
-  const float gm = clamped ? 0.f : (-dot * inv * inv) / (float)a.width;
-  GAS float* dx = GW(a.dx) + (size_t)row * a.lddx;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    dot[q] = wave_sum(dot[q]);
+    // y = x / m: dy/dx path g/m ; dm path -(sum g x)/m^2 * sign(x)/n (unless clamped)
+    gmv[q] = clamped[q] ? 0.f : (-dot[q] * inv[q] * inv[q]) / (float)a.width;
+  }
+  auto sgn = [](float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); };
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int k = lane + 64 * u;
     if (u < per && k < a.width) {
-      const float sg = xv[u] > 0.f ? 1.f : (xv[u] < 0.f ? -1.f : 0.f);
-      dx[k] = gv[u] * inv + sg * gm;
+      const float4 o = make_float4(gv[u].x * inv[0] + sgn(xv[u].x) * gmv[0], gv[u].y * inv[1] + sgn(xv[u].y) * gmv[1],
+                                   gv[u].z * inv[2] + sgn(xv[u].z) * gmv[2], gv[u].w * inv[3] + sgn(xv[u].w) * gmv[3]);
+      mat_st4(a.dx, r0, k, o);
     }
   }
 }
 
 // ---------------------------------------------------------------- critic heads
 
+// Last critic layer (H -> 1) as a dot product fused with the TD target / loss /
+// priority / policy objective and the gradient into the last hidden layer.
+// 16 rows per workgroup, 4 per wave (lane k: float4 of 4 rows from T images).
 __device__ __forceinline__ void op_head(const CAS HeadArgs& h, int t, float* smem) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b = t * 4 + wave;
-  float acc0 = 0.f, acc1 = 0.f;  // per-row loss terms
-  float ykey = 0.f;
-  const bool valid = b < h.rows;
-  if (valid) {
-    float q[2];
+  const int r0 = t * 16 + wave * 4;
+  float acc0 = 0.f, acc1 = 0.f;  // per-wave loss terms (sum over its rows)
+  int kmax = (int)0x80000000, kmin = 0x7FFFFFFF;
+  if (r0 < h.rows) {
+    float q[2][4];
     float wv[2][8];
     const int per = (h.H + 63) / 64;
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-      const GAS float* hr = G(h.h[n]) + (size_t)b * h.ldh;
-      const GAS float* wr = G(h.w[n]);
-      float s = 0.f;
+      float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int k = lane + 64 * u;
         const bool in = u < per && k < h.H;
-        wv[n][u] = in ? wr[k] : 0.f;
-        s += (in ? hr[k] : 0.f) * wv[n][u];
+        wv[n][u] = in ? G(h.w[n])[tidx(h.w_rbs, 0, k)] : 0.f;
+        const float4 hv = in ? mat_ld4(h.h[n], r0, k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        s[0] += hv.x * wv[n][u];
+        s[1] += hv.y * wv[n][u];
+        s[2] += hv.z * wv[n][u];
+        s[3] += hv.w * wv[n][u];
       }
-      q[n] = wave_sum(s) + G(h.b[n])[0];
-    }
-    float dq[2] = {0.f, 0.f};
-    bool want_dz = false;
-    switch (h.mode) {
-      case HEAD_TD7_TARGET: {  // td7.py:211-218
-        float v = fminf(q[0], q[1]);
-        v = fminf(fmaxf(v, G(h.vt)[1]), G(h.vt)[0]);
-        const float y = G(h.reward)[b] + (h.gamma * v) * G(h.notdone)[b];
-        if (lane == 0) GW(h.y)[b] = y;
-        ykey = y;
-        break;
-      }
-      case HEAD_MLP_TARGET: {  // td3.py:160-164, sac.py:188-193
-        float v = fminf(q[0], q[1]);
-        if (h.sac) v = v - expf(G(h.log_alpha)[0]) * G(h.logpi)[b];
-        const float y = G(h.reward)[b] + (h.gamma * v) * G(h.notdone)[b];
-        if (lane == 0) GW(h.y)[b] = y;
-        break;
-      }
-      case HEAD_TD7_LOSS:
-      case HEAD_MLP_LOSS: {  // td7.py:231-244, td3.py:169-182
-        const float y = G(h.y)[b];
-        float dmax = 0.f;
+      const float bb = G(h.b[n])[0];
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          const float diff = q[n] - y;
-          if (h.lap) {
-            const float d = fabsf(diff);
-            const float hub = d < 1.f ? 0.5f * (d * d) : d;
-            if (n == 0) acc0 += hub; else acc1 += hub;
-            const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-            dq[n] = (d < 1.f ? d : 1.f) * sg * h.inv_b;
-            dmax = fmaxf(dmax, d);
-          } else {
-            const float e = y - q[n];
-            if (n == 0) acc0 += e * e; else acc1 += e * e;
-            dq[n] = -e * h.inv_b;
+      for (int r = 0; r < 4; ++r) q[n][r] = wave_sum(s[r]) + bb;
+    }
+    float dq[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    bool want_dz = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = r0 + r;
+      switch (h.mode) {
+        case HEAD_TD7_TARGET: {  // td7.py:211-218
+          float v = fminf(q[0][r], q[1][r]);
+          v = fminf(fmaxf(v, G(h.vt)[1]), G(h.vt)[0]);
+          const float y = G(h.reward)[b] + (h.gamma * v) * G(h.notdone)[b];
+          if (lane == 0) GW(h.y)[b] = y;
+          kmax = max(kmax, fkey(y));
+          kmin = min(kmin, fkey(y));
+          break;
+        }
+        case HEAD_MLP_TARGET: {  // td3.py:160-164, sac.py:188-193
+          float v = fminf(q[0][r], q[1][r]);
+          if (h.sac) v = v - expf(G(h.log_alpha)[0]) * G(h.logpi)[b];
+          const float y = G(h.reward)[b] + (h.gamma * v) * G(h.notdone)[b];
+          if (lane == 0) GW(h.y)[b] = y;
+          break;
+        }
+        case HEAD_TD7_LOSS:
+        case HEAD_MLP_LOSS: {  // td7.py:231-244, td3.py:169-182
+          const float y = G(h.y)[b];
+          float dmax = 0.f;
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const float diff = q[n][r] - y;
+            if (h.lap) {
+              const float d = fabsf(diff);
+              const float hub = d < 1.f ? 0.5f * (d * d) : d;
+              if (n == 0) acc0 += hub; else acc1 += hub;
+              const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+              dq[n][r] = (d < 1.f ? d : 1.f) * sg * h.inv_b;
+              dmax = fmaxf(dmax, d);
+            } else {
+              const float e = y - q[n][r];
+              if (n == 0) acc0 += e * e; else acc1 += e * e;
+              dq[n][r] = -e * h.inv_b;
+            }
           }
+          if (h.lap && lane == 0) GW(h.prio)[b] = (float)pow((double)fmaxf(dmax, 1.f), 0.4);
+          want_dz = true;
+          break;
         }
-        if (h.lap && lane == 0) GW(h.prio)[b] = (float)pow((double)fmaxf(dmax, 1.f), 0.4);
-        want_dz = true;
-        break;
-      }
-      case HEAD_TD7_POLICY: {  // td7.py:274-275
-        acc0 = q[0] + q[1];
-        dq[0] = dq[1] = -0.5f * h.inv_b;
-        want_dz = true;
-        break;
-      }
-      case HEAD_MLP_POLICY: {  // td3.py:191, sac.py:227-229
-        const float mn = fminf(q[0], q[1]);
-        // torch.minimum backward: ties split the gradient
-        const float gq = -h.inv_b;
-        dq[0] = q[0] < q[1] ? gq : (q[0] == q[1] ? 0.5f * gq : 0.f);
-        dq[1] = q[1] < q[0] ? gq : (q[0] == q[1] ? 0.5f * gq : 0.f);
-        if (h.sac) {
-          const float lp = G(h.logpi)[b];
-          acc0 = -mn + lp * expf(G(h.log_alpha)[0]);
-          acc1 = lp;
-        } else {
-          acc0 = mn;
+        case HEAD_TD7_POLICY: {  // td7.py:274-275
+          acc0 += q[0][r] + q[1][r];
+          dq[0][r] = dq[1][r] = -0.5f * h.inv_b;
+          want_dz = true;
+          break;
         }
-        want_dz = true;
-        break;
+        case HEAD_MLP_POLICY: {  // td3.py:191, sac.py:227-229
+          const float mn = fminf(q[0][r], q[1][r]);
+          // torch.minimum backward: ties split the gradient
+          const float gq = -h.inv_b;
+          dq[0][r] = q[0][r] < q[1][r] ? gq : (q[0][r] == q[1][r] ? 0.5f * gq : 0.f);
+          dq[1][r] = q[1][r] < q[0][r] ? gq : (q[0][r] == q[1][r] ? 0.5f * gq : 0.f);
+          if (h.sac) {
+            const float lp = G(h.logpi)[b];
+            acc0 += -mn + lp * expf(G(h.log_alpha)[0]);
+            acc1 += lp;
+          } else {
+            acc0 += mn;
+          }
+          want_dz = true;
+          break;
+        }
       }
     }
     if (want_dz) {
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        if (lane == 0 && h.dq[n]) GW(h.dq[n])[b] = dq[n];
-        const GAS float* ds = G(h.dsrc[n]) + (size_t)b * h.ldd;
-        GAS float* dz = GW(h.dz[n]) + (size_t)b * h.lddz;
+        if (lane == 0 && h.dq[n].t) mat_st4(h.dq[n], r0, 0, make_float4(dq[n][0], dq[n][1], dq[n][2], dq[n][3]));
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int k = lane + 64 * u;
-          if (u < per && k < h.H) dz[k] = (dq[n] * wv[n][u]) * act_bwd(h.dact, ds[k]);
+          if (u < per && k < h.H) {
+            const float4 d = mat_ld4(h.dsrc[n], r0, k);
+            const float w = wv[n][u];
+            mat_st4(h.dz[n], r0, k,
+                    make_float4((dq[n][0] * w) * act_bwd(h.dact, d.x), (dq[n][1] * w) * act_bwd(h.dact, d.y),
+                                (dq[n][2] * w) * act_bwd(h.dact, d.z), (dq[n][3] * w) * act_bwd(h.dact, d.w)));
+          }
         }
       }
     }
@@ -663,10 +694,10 @@ __device__ __forceinline__ void op_head(const CAS HeadArgs& h, int t, float* sme
   float* red = smem;
   int* ired = reinterpret_cast<int*>(smem + 16);
   if (lane == 0) {
-    red[wave * 2 + 0] = valid ? acc0 : 0.f;
-    red[wave * 2 + 1] = valid ? acc1 : 0.f;
-    ired[wave * 2 + 0] = valid ? fkey(ykey) : (int)0x80000000;
-    ired[wave * 2 + 1] = valid ? fkey(ykey) : (int)0x7FFFFFFF;
+    red[wave * 2 + 0] = acc0;
+    red[wave * 2 + 1] = acc1;
+    ired[wave * 2 + 0] = kmax;
+    ired[wave * 2 + 1] = kmin;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -745,19 +776,19 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
   const long long pos = *G(s.tape_pos);
   const uint2 key = make_uint2((unsigned)s.seed, (unsigned)(s.seed >> 32));
   const unsigned long long step = (unsigned long long)*G(s.ctrl_rng);
-  // noise tensors for this row
+  // noise tensors for this row (T images)
   for (int j = tid; j < s.A; j += kThreads) {
     float e, e2 = 0.f;
     if (tape) {
       e = G(s.tape_eps)[((size_t)pos * s.B + b) * s.A + j];
-      if (s.eps2) e2 = G(s.tape_eps2)[((size_t)pos * s.B + b) * s.A + j];
+      if (s.eps2.t) e2 = G(s.tape_eps2)[((size_t)pos * s.B + b) * s.A + j];
     } else {
       const uint4 r = philox(key, make_uint4((unsigned)(b * s.A + j), 1u, (unsigned)step, (unsigned)(step >> 32)));
       e = normal_from(r.x, r.y);
       e2 = normal_from(r.z, r.w);
     }
-    GW(s.eps)[(size_t)b * s.ldeps + j] = e;
-    if (s.eps2) GW(s.eps2)[(size_t)b * s.ldeps + j] = e2;
+    mat_st(s.eps, b, j, e);
+    if (s.eps2.t) mat_st(s.eps2, b, j, e2);
   }
   long long* found = reinterpret_cast<long long*>(smem);  // [1]
   double* tsum = reinterpret_cast<double*>(smem) + 2;     // [256]
@@ -835,18 +866,15 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
       if (ind >= size) ind = size - 1;
     }
   }
-  // gather the transition (coalesced float4 copies)
+  // gather the transition into the batch images (rows b and B + b of ss)
   const GAS float* st = G(s.state) + (size_t)ind * s.Sp;
   const GAS float* nst = G(s.next_state) + (size_t)ind * s.Sp;
-  GAS float* d0 = GW(s.ss) + (size_t)b * s.ldss;
-  GAS float* d1 = GW(s.ss) + (size_t)(s.B + b) * s.ldss;
-  for (int k = tid * 4; k < s.Sp; k += kThreads * 4) {
-    st4g(d0 + k, ld4g(st + k));
-    st4g(d1 + k, ld4g(nst + k));
+  for (int k = tid; k < s.Sp; k += kThreads) {
+    mat_st(s.ss, b, k, st[k]);
+    mat_st(s.ss, s.B + b, k, nst[k]);
   }
   const GAS float* ac = G(s.action) + (size_t)ind * s.Ap;
-  GAS float* da = GW(s.a) + (size_t)b * s.lda;
-  for (int k = tid * 4; k < s.Ap; k += kThreads * 4) st4g(da + k, ld4g(ac + k));
+  for (int k = tid; k < s.Ap; k += kThreads) mat_st(s.a, b, k, ac[k]);
   if (tid == 0) {
     GW(s.r)[b] = G(s.reward)[ind];
     GW(s.nd)[b] = G(s.notdone)[ind];
@@ -888,22 +916,22 @@ __device__ __forceinline__ void op_priority(const CAS PriorityArgs& a, float* sm
 __device__ __forceinline__ void op_sac_actor(const CAS SacActorArgs& s, int t) {
   const int b = t * kThreads + threadIdx.x;
   if (b >= s.rows) return;
-  const GAS float* o = G(s.out) + (size_t)b * s.ldo;
-  const GAS float* e = (b < s.eps_row_split) ? G(s.eps2) + (size_t)b * s.ldeps
-                                             : G(s.eps) + (size_t)(b - s.eps_row_split) * s.ldeps;
+  const bool pol = b < s.eps_row_split;  // rows < split use eps2 (policy), else eps (target)
+  const int eb = pol ? b : b - s.eps_row_split;
   const float c = (float)0.9189385332046727;  // log(sqrt(2*pi))
   float lp = 0.f, corr = 0.f;
   for (int j = 0; j < s.A; ++j) {
-    const float mu = o[s.mean_off + j];
-    const float ls = fminf(fmaxf(o[s.ls_off + j], s.min_log_std), s.max_log_std);
+    const float mu = mat_ld(s.out, b, s.mean_off + j);
+    const float ls = fminf(fmaxf(mat_ld(s.out, b, s.ls_off + j), s.min_log_std), s.max_log_std);
     const float sd = expf(ls);
-    const float u = mu + e[j] * sd;
+    const float ej = pol ? mat_ld(s.eps2, eb, j) : mat_ld(s.eps, eb, j);
+    const float u = mu + ej * sd;
     const float a = tanhf(u);
     const float var = sd * sd;
     const float d = u - mu;
     lp += -(d * d) / (2.f * var) - logf(sd) - c;
     corr += logf((1.f - a * a) + 1e-6f);
-    GW(s.act)[(size_t)b * s.ldact + j] = a;
+    mat_st(s.act, b, j, a);
   }
   GW(s.logpi)[b] = lp - corr;
 }
@@ -911,31 +939,30 @@ __device__ __forceinline__ void op_sac_actor(const CAS SacActorArgs& s, int t) {
 __device__ __forceinline__ void op_sac_actor_bwd(const CAS SacActorArgs& s, int t) {
   const int b = t * kThreads + threadIdx.x;
   if (b >= s.rows) return;
-  const GAS float* o = G(s.out) + (size_t)b * s.ldo;
-  const GAS float* e = G(s.eps2) + (size_t)b * s.ldeps;
   const float w = expf(G(s.log_alpha)[0]) * s.inv_b;  // d obj / d logpi_b
   for (int j = 0; j < s.A; ++j) {
-    const float mu = o[s.mean_off + j];
-    const float lsr = o[s.ls_off + j];
+    const float mu = mat_ld(s.out, b, s.mean_off + j);
+    const float lsr = mat_ld(s.out, b, s.ls_off + j);
     const float ls = fminf(fmaxf(lsr, s.min_log_std), s.max_log_std);
     const float sd = expf(ls);
-    const float u = mu + e[j] * sd;
+    const float ej = mat_ld(s.eps2, b, j);
+    const float u = mu + ej * sd;
     const float a = tanhf(u);
     const float var = sd * sd;
     const float d = u - mu;
     // logpi = sum(-d^2/(2 var) - log sd - c) - sum log(1 - a^2 + 1e-6)
-    const float ga = G(s.da)[(size_t)b * s.ldda + j] + (w / ((1.f - a * a) + 1e-6f)) * (2.f * a);
+    const float ga = mat_ld(s.da, b, j) + (w / ((1.f - a * a) + 1e-6f)) * (2.f * a);
     float gu = ga * (1.f - a * a);
     gu += -(w / (2.f * var)) * (2.f * d);       // d(-d^2/(2var))/du
     float gmu = (w / (2.f * var)) * (2.f * d);  // via d = u - mu
     const float gvar = (w * (d * d)) / ((2.f * var) * (2.f * var)) * 2.f;
     float gsd = gvar * (2.f * sd) - w / sd;
     gmu += gu;
-    gsd += gu * e[j];
+    gsd += gu * ej;
     float gls = gsd * sd;
     if (!(lsr >= s.min_log_std && lsr <= s.max_log_std)) gls = 0.f;
-    GW(s.dout)[(size_t)b * s.lddout + s.mean_off + j] = gmu;
-    GW(s.dout)[(size_t)b * s.lddout + s.ls_off + j] = gls;
+    mat_st(s.dout, b, s.mean_off + j, gmu);
+    mat_st(s.dout, b, s.ls_off + j, gls);
   }
 }
 

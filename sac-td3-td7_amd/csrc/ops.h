@@ -29,21 +29,45 @@ enum OpKind : int {
   OP_CTRL = 13,
 };
 
+// ---------------------------------------------------------------- tensor images
+//
+// Every 2D tensor that feeds a GEMM lives in 16x16 "fragment blocks" of 1 KB
+// (rows and columns padded to 16), in one or both of two images:
+//   N image (row fragments):    block (rb, cb) at n + (rb * cbn + cb) * 256,
+//                               element (r, c) inside at ((c%16)/4)*64 + (r%16)*4 + c%4
+//   T image (column fragments): block (rb, cb) at t + (cb * rbs + rb) * 256,
+//                               element (r, c) inside at ((r%16)/4)*64 + (c%16)*4 + r%4
+// Lane l of a wave reads float l*4..l*4+3 of a block: in the N image that is row
+// l%16, columns 4(l/16)..+3 -- exactly the v_mfma_f32_16x16x4_f32 A/B fragment
+// when the reduction runs along columns; the T image gives the fragment when
+// it runs along rows.  So every GEMM operand load is one lane-linear 16-byte
+// load per lane per 16-wide reduction chunk (a whole 1 KB block per wave).
+struct Mat {
+  float* n;   // N image (nullptr: not kept)
+  float* t;   // T image (nullptr: not kept)
+  int cbn;    // column blocks per row-block in the N image
+  int rbs;    // row blocks per column-block in the T image (the allocation's, for sub-views)
+};
+
+// Deferred AvgL1Norm of a producer output (rl/nn/sale.py:11-13): the consumer
+// value is x / m(row), m = max(sum_p part[p*ld + row0 + row] / width, 1e-8).
+struct NormRef {
+  const float* part;
+  int ld, row0, nparts, width;
+};
+
 // One rectangle of a GEMM operand in (x, r) space: x = output row (operand A)
-// or output column (operand B); r = reduction index.
-//   strided == 0 : elem(x, r) = p[(x - x0) * ld + (r - r0)]   (float4 along r)
-//   strided == 1 : elem(x, r) = p[(r - r0) * ld + (x - x0)]
-// If norm != nullptr the stored values are pre-AvgL1Norm outputs x and the
-// operand value is x / m(row) with m = max(sum_p norm[p*norm_ld + row] / width, 1e-8)
-// (rl/nn/sale.py:11-13), row = (strided ? r - r0 : x - x0) + norm_row0.
+// or output column (operand B); r = reduction index.  The operand is an image
+// (N or T, whichever makes r the fragment's reduction direction) starting at p:
+//   block of (x, r) = p + ((x - x0) / 16 * xs + (r - r0) / 16) * 256
+// Reduction segments are 16-aligned and back to back (r0 of one == padded r1 of
+// the previous); x-split segments (GEMM_DW B only) are 16-aligned in x.
 struct Seg {
   const float* p;
-  const float* norm;
-  int ld;
+  int xs;          // blocks per x-block step
   int x0, x1, r0, r1;
-  int strided;
-  int norm_ld, norm_row0, norm_nparts, norm_width;
   int pad_;
+  NormRef norm;    // norm.part == nullptr: plain operand
 };
 
 struct Operand {
@@ -61,12 +85,12 @@ enum Epi : int {
 };
 
 struct AdamArgs {
-  float* w;              // weight base [N][ldw]
-  float* b;              // bias [N] (bias tile column j0 == bias_col)
-  long long mo, vo;      // element offsets of m / v arrays relative to params
+  Mat w;                 // weight images [N out rows][K cols] (both kept: FWD reads N, DX reads T)
+  float* b;              // bias [16 * row blocks] (bias tile column j0 == bias_col)
+  long long mo, vo;      // element offsets of m / v arrays relative to params (m, v kept at T-image offsets)
   const long long* t;    // completed optimizer steps (device counter)
   float lr, beta1, beta2, eps;
-  int ldw, bias_col;     // bias_col = first column of the bias tile = K rounded up to kTileN
+  int bias_col;          // first column of the bias tile = K rounded up to kTileN
   float* gsq;            // optional: per-tile sum of squared grads (weights), [tiles]
   float* gsq_b;          // optional: per-tile sum of squared grads (bias), [tiles_m]
 };
@@ -84,27 +108,26 @@ struct GemmArgs {
   int epi;
   int act;               // forward activation (EPI_STORE)
   Operand A, B;
-  float* out; int ldo;
+  Mat out;                         // output images (EPI_STORE, EPI_MSE)
   const float* bias;
-  float* pre; int ldpre;           // pre-activation store (optional)
+  Mat pre;                         // pre-activation store, T image (optional)
   float* norm_out; int norm_ld;    // |y| partials: norm_out[jt * norm_ld + i] (optional)
-  int dact; int lddact;            // derivative mask: out *= act'(dsrc[i][j])
-  const float* dsrc;
-  const float* noise; int ldnoise; int noise_row0; float noise_sigma, noise_clip;  // tanh-noise
-  Seg tgt;                         // EPI_MSE target (normed view)
+  int dact;                        // derivative mask: out *= act'(dsrc(i, j))
+  Mat dsrc;                        // T image
+  Mat noise; int noise_row0; float noise_sigma, noise_clip;  // tanh-noise (T image)
+  Mat tgt; NormRef tgt_norm;       // EPI_MSE target (T image of a normed view)
   float* loss_part;                // EPI_MSE per-tile partial sums
-  float mse_scale;                 // 2/n
+  float mse_scale;                 // 1/n
   int pad_;
   AdamArgs adam;
 };
 
-// AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise)
+// AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise);
+// 16 rows per workgroup (4 per wave), T images in, N + T images out.
 struct NormBwdArgs {
-  const float* g; int ldg;
-  const float* x; int ldx;
-  float* dx; int lddx;
+  Mat g, x, dx;
   int rows, width;
-  const float* norm; int norm_ld, norm_row0, norm_nparts;  // partials for m (x rows)
+  NormRef norm;  // partials for m (x rows)
 };
 
 enum HeadMode : int {
@@ -116,17 +139,18 @@ enum HeadMode : int {
   HEAD_MLP_POLICY = 5,   // TD3: -mean(min);  SAC: mean(-min + alpha*logpi)
 };
 
-struct HeadArgs {
+struct HeadArgs {                   // 16 rows per workgroup (4 per wave)
   int mode, rows, H, lap;
-  const float* h[2]; int ldh;        // last hidden (post-activation) of each twin
-  const float* dsrc[2]; int ldd;     // derivative source (Z for ELU, H for ReLU)
+  Mat h[2];                          // last hidden (post-activation) of each twin, T image
+  Mat dsrc[2];                       // derivative source (Z for ELU, H for ReLU), T image
   int dact;
-  const float* w[2];                 // last-layer weight row [H]
+  const float* w[2];                 // last-layer weight row: T image of a [1][H] matrix
+  int w_rbs;                         // its row-block stride (1)
   const float* b[2];                 // last-layer bias [1]
   const float* reward; const float* notdone;
   float* y;                          // target (written by *_TARGET, read by *_LOSS)
-  float* dz[2]; int lddz;            // grad wrt last hidden pre-activation
-  float* dq[2];                      // grad wrt q (for dW of last layer)
+  Mat dz[2];                         // grad wrt last hidden pre-activation (N + T)
+  Mat dq[2];                         // grad wrt q, T image of [rows][1] (dW of last layer)
   float* loss_part;                  // per-workgroup partial sums [wg][4]
   float* prio;                       // LAP priority out [rows]
   float gamma;
@@ -148,13 +172,13 @@ struct SampleArgs {
   int lap, B;
   double* bsum; int nblk;            // LAP block sums (fp64), 4096 priorities per block
   // outputs
-  float* ss; int ldss;               // [2B][Sp] rows 0..B-1 state, B..2B-1 next_state
-  float* a; int lda;                 // [B][Ap]
+  Mat ss;                            // [2B][Sp] rows 0..B-1 state, B..2B-1 next_state (N + T)
+  Mat a;                             // [B][Ap] (N + T)
   float* r; float* nd;               // [B]
   long long* ind;                    // [B]
   float* u_out;                      // [B] uniform used (debug)
-  float* eps; int ldeps;             // [B][Ap] target smoothing / SAC next noise
-  float* eps2;                       // [B][Ap] SAC policy noise (optional)
+  Mat eps;                           // [B][Ap] target smoothing / SAC next noise (T)
+  Mat eps2;                          // [B][Ap] SAC policy noise (optional, T)
   // randomness
   const long long* ctrl_rng;         // step counter for Philox
   unsigned long long seed;
@@ -169,16 +193,16 @@ struct PriorityArgs {
 };
 
 struct SacActorArgs {
-  const float* out; int ldo;         // raw head output [rows][2A(p)]: mean | log_std
+  Mat out;                           // raw head output [rows][2A(p)]: mean | log_std (T)
   int A, rows;                       // rows = 2B
-  const float* eps; int ldeps; int eps_row_split; const float* eps2;  // rows < split use eps2 (policy), else eps (target)
-  float* act; int ldact;             // tanh action
+  Mat eps; int eps_row_split; Mat eps2;  // rows < split use eps2 (policy), else eps (target) (T)
+  Mat act;                           // tanh action (N + T)
   float* logpi;                      // [rows]
   float min_log_std, max_log_std;
   int mean_off, ls_off;              // column offsets of mean / log_std blocks
   // backward
-  const float* da; int ldda;         // grad wrt action from critics [B][Ap]
-  float* dout; int lddout;           // grad wrt raw output [B][2A(p)]
+  Mat da;                            // grad wrt action from critics [B][Ap] (T)
+  Mat dout;                          // grad wrt raw output [B][2A(p)] (N + T)
   const float* log_alpha; float inv_b;
 };
 

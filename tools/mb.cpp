@@ -30,6 +30,7 @@ static float* dalloc(size_t n) {
   return p;
 }
 
+// Y = relu(X W^T + b); X: N image [M][K], W: N image [N][K], Y: T image [M][N].
 static Op fwd_op(float* X, float* W, float* b, float* Y, int M, int N, int K) {
   Op op{};
   op.kind = OP_GEMM;
@@ -37,13 +38,21 @@ static Op fwd_op(float* X, float* W, float* b, float* Y, int M, int N, int K) {
   g.mode = GEMM_FWD;
   g.M = M; g.N = N; g.R = K;
   g.A.nseg = 1;
-  g.A.seg[0].p = X; g.A.seg[0].ld = K; g.A.seg[0].x0 = 0; g.A.seg[0].x1 = M; g.A.seg[0].r0 = 0; g.A.seg[0].r1 = K;
+  g.A.seg[0].p = X; g.A.seg[0].xs = K / 16; g.A.seg[0].x0 = 0; g.A.seg[0].x1 = M; g.A.seg[0].r0 = 0; g.A.seg[0].r1 = K;
   g.B.nseg = 1;
-  g.B.seg[0].p = W; g.B.seg[0].ld = K; g.B.seg[0].x0 = 0; g.B.seg[0].x1 = N; g.B.seg[0].r0 = 0; g.B.seg[0].r1 = K;
+  g.B.seg[0].p = W; g.B.seg[0].xs = K / 16; g.B.seg[0].x0 = 0; g.B.seg[0].x1 = N; g.B.seg[0].r0 = 0; g.B.seg[0].r1 = K;
   g.tiles_m = (M + kTileM - 1) / kTileM; g.tiles_n = (N + kTileN - 1) / kTileN;
-  g.epi = EPI_STORE; g.act = ACT_RELU; g.out = Y; g.ldo = N; g.bias = b;
+  g.epi = EPI_STORE; g.act = ACT_RELU; g.bias = b;
+  g.out.t = Y; g.out.rbs = M / 16; g.out.cbn = N / 16;
   op.wg_count = g.tiles_m * g.tiles_n;
   return op;
+}
+
+static size_t nidx(int cbn, int r, int c) {
+  return ((size_t)(r >> 4) * cbn + (c >> 4)) * 256 + ((c >> 2) & 3) * 64 + (r & 15) * 4 + (c & 3);
+}
+static size_t tidx(int rbs, int r, int c) {
+  return ((size_t)(c >> 4) * rbs + (r >> 4)) * 256 + ((r >> 2) & 3) * 64 + (c & 15) * 4 + (r & 3);
 }
 
 static double time_level(std::vector<Op> ops, int reps, hipStream_t st) {
@@ -107,9 +116,9 @@ int main() {
     for (int i = 0; i < M; ++i)
       for (int n = 0; n < N; ++n) {
         double s = hb[n];
-        for (int k = 0; k < Kc; ++k) s += (double)hx[(size_t)i * Kc + k] * hw[(size_t)n * Kc + k];
+        for (int k = 0; k < Kc; ++k) s += (double)hx[nidx(Kc / 16, i, k)] * hw[nidx(Kc / 16, n, k)];
         s = s > 0 ? s : 0;
-        md = std::max(md, std::abs(s - hy[(size_t)i * N + n]));
+        md = std::max(md, std::abs(s - hy[tidx(M / 16, i, n)]));
       }
     printf("fwd correctness max|d| = %.3g\n", md);
   }
