@@ -129,6 +129,12 @@ int rle_graph_stats(rle_engine* e, int* levels_policy_step, int* levels_plain_st
 /* Human-readable description of a captured graph (which: 0 policy step, 1 plain step,
  * 2 hard update): one line per level with workgroups and ops.  Writes at most len bytes. */
 int rle_graph_describe(rle_engine* e, int which, char* buf, int len);
+/* Diagnostics: phase timestamps of the last replay of a captured graph (graphs are
+ * traced only when RLE_TRACE=1 is set in the environment before the first step).
+ * out[4*w .. 4*w+3] = s_memrealtime (100 MHz) at entry, main-loop start, main-loop
+ * end (GEMM ops) and exit of workgroup w, levels concatenated in order; *n_out = number
+ * of workgroups written (0 when tracing is off). */
+int rle_graph_trace(rle_engine* e, int which, unsigned long long* out, long long cap, long long* n_out);
 /* Copy all weights/optimizer state/counters of src into dst (checkpoint agent,
  * ckpt_agent.load_state_dict(agent), run_w_checkpoint.py:140). Same config required. */
 int rle_copy_state(rle_engine* dst, rle_engine* src);

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -23,7 +24,9 @@
 #include "rle.h"
 
 namespace rle {
-hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st);
+hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
+                        unsigned long long* trace = nullptr);
+int level_capacity();
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count,
@@ -144,6 +147,15 @@ struct View {
   }
 };
 
+// GEMM tile width: the narrowest tile (more workgroups, reduction split across the
+// 4 waves) while the output has at most 640 16x16 blocks per width step.
+static int pick_tn(int M, int N) {
+  const int blocks = cdiv(M, 16) * cdiv(N, 16);
+  if (blocks <= 640) return 16;
+  if (blocks <= 1280) return 32;
+  return 64;
+}
+
 // Layout invariants the GEMM main loop relies on (kernels.hip, "GEMM"): reduction
 // segments 16-aligned, sorted and disjoint; every segment of a FWD/DX operand
 // and of a DW A operand spans the whole operand row range (x0 == 0); DW B
@@ -168,6 +180,25 @@ static void check_gemm(const GemmArgs& g) {
   REQUIRE(g.R <= 16 * 1024, "gemm: reduction too long");
 }
 
+// Device-side dispatch fields of a GEMM op: compiled variant, split count, tile-row
+// reciprocal (kernels.hip gemm_v).
+static void gemm_finalize(GemmArgs& g) {
+  int norm = 0;
+  for (int q = 0; q < g.A.nseg; ++q) norm |= g.A.seg[q].norm.part != nullptr;
+  for (int q = 0; q < g.B.nseg; ++q) norm |= g.B.seg[q].norm.part != nullptr;
+  const int act = g.mode == GEMM_FWD ? g.act : (g.mode == GEMM_DX ? g.dact : ACT_NONE);
+  REQUIRE(g.mode != GEMM_DX || !norm, "gemm: no DX variant with normed operands");
+  REQUIRE(g.mode != GEMM_DW || g.epi == EPI_ADAM, "gemm: DW is always fused with Adam");
+  REQUIRE(g.epi != EPI_MSE || act == ACT_NONE, "gemm: MSE epilogue takes no activation");
+  REQUIRE((g.dact == ACT_NONE) == (g.dsrc.t == nullptr) || g.mode != GEMM_DX, "gemm: DX derivative source");
+  g.vid = gemm_vid(g.mode, g.epi, act, norm);
+  REQUIRE(g.tn == 16 || g.tn == 32 || g.tn == 64, "gemm: tile width");
+  g.ks_log = g.tn == 16 ? 2 : (g.tn == 32 ? 1 : 0);
+  REQUIRE(g.R % 16 == 0, "gemm: reduction length must be a multiple of 16");
+  REQUIRE((long long)g.tiles_m * g.tiles_n < 65536, "gemm: too many tiles");
+  g.inv_tiles_n = 1.f / (float)g.tiles_n;
+}
+
 struct Prog {
   struct Item {
     std::vector<Op> ops;  // one op, or a group writing disjoint parts of the same buffers
@@ -177,8 +208,11 @@ struct Prog {
   std::vector<Item> items;
   void add(const Op& op, std::vector<int> rd, std::vector<int> wr) { add_group({op}, std::move(rd), std::move(wr)); }
   void add_group(std::vector<Op> ops, std::vector<int> rd, std::vector<int> wr) {
-    for (const Op& op : ops)
-      if (op.kind == OP_GEMM) check_gemm(op.gemm);
+    for (Op& op : ops)
+      if (op.kind == OP_GEMM) {
+        gemm_finalize(op.gemm);
+        check_gemm(op.gemm);
+      }
     Item it;
     it.ops = std::move(ops);
     it.rd = std::move(rd);
@@ -223,6 +257,8 @@ struct Graph {
   hipGraph_t g = nullptr;
   hipGraphExec_t x = nullptr;
   Op* d_ops = nullptr;
+  unsigned long long* trace = nullptr;  // [total wg][4] when RLE_TRACE=1
+  long long trace_n = 0;
   std::vector<int> nops, nwg, off;
   std::string desc;
   int levels() const { return (int)nops.size(); }
@@ -527,7 +563,9 @@ struct Engine {
     std::sort(cuts.begin(), cuts.end());
     cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
     REQUIRE((int)ins.size() <= kMaxSeg, "fwd: too many operand segments");
-    const int tiles_n = cdiv(L.out, kTileN);
+    const auto tq = choose_tn(M, L.out);
+    const int tn = tq.first;
+    const int tiles_n = cdiv(L.out, tn);
     View out = buf(M, L.out);
     wr.push_back(out.id);
     if (pre_out) {
@@ -579,6 +617,7 @@ struct Engine {
       g.M = m;
       g.N = L.out;
       g.R = L.K;
+      g.tn = tn;
       g.tiles_m = cdiv(m, kTileM);
       g.tiles_n = tiles_n;
       g.epi = EPI_STORE;
@@ -598,6 +637,7 @@ struct Engine {
         g.noise_clip = cfg.noise_clip;
       }
       op.wg_count = g.tiles_m * g.tiles_n;
+      op.seq = tq.second;
       ops.push_back(op);
     }
     pg.add_group(std::move(ops), rd, wr);
@@ -639,8 +679,11 @@ struct Engine {
     g.M = M;
     g.N = ncols;
     g.R = roff;
+    const auto tq = choose_tn(M, ncols);
+    g.tn = tq.first;
+    op.seq = tq.second;
     g.tiles_m = cdiv(M, kTileM);
-    g.tiles_n = cdiv(ncols, kTileN);
+    g.tiles_n = cdiv(ncols, g.tn);
     g.epi = EPI_STORE;
     g.act = ACT_NONE;
     View out = buf(M, ncols);
@@ -656,6 +699,21 @@ struct Engine {
     pg.add(op, rd, wr);
     return out;
   }
+
+  // Tile width of the next GEMM op: from the plan of a previous build pass
+  // (capture() widens tiles of levels that exceed one resident wave of
+  // workgroups), else the per-op default.  Returns the op's creation index too.
+  std::vector<int> tn_plan;
+  int tn_seq = 0;
+  std::pair<int, int> choose_tn(int M, int N) {
+    const int seq = tn_seq++;
+    const int t = seq < (int)tn_plan.size() ? tn_plan[seq] : pick_tn(M, N);
+    return {t, seq};
+  }
+  // per-tile grad-square partial slots of a dW op (weights at the narrowest tile width,
+  // so any plan fits; unused slots stay zero; bias)
+  static int dw_gsq_w(const Layer& L) { return cdiv(L.out, kTileM) * cdiv(L.K, 16); }
+  static int dw_gsq_b(const Layer& L) { return cdiv(L.out, kTileM); }
 
   // dW = dZ^T [X], db = sum dZ, fused Adam (torch.optim.Adam law).
   void dw(Prog& pg, const Layer& L, const View& dz, const std::vector<View>& X, int Brows, int cnt, float lr,
@@ -682,8 +740,11 @@ struct Engine {
     g.M = L.out;
     g.N = L.K;
     g.R = Brows;
+    const auto tq = choose_tn(L.out, L.K);
+    g.tn = tq.first;
+    op.seq = tq.second;
     g.tiles_m = cdiv(L.out, kTileM);
-    g.tiles_n = cdiv(L.K, kTileN) + 1;
+    g.tiles_n = cdiv(L.K, g.tn) + 1;
     g.epi = EPI_ADAM;
     AdamArgs& ad = g.adam;
     ad.w = wmat(L);
@@ -695,7 +756,7 @@ struct Engine {
     ad.beta1 = 0.9f;
     ad.beta2 = 0.999f;
     ad.eps = 1e-8f;
-    ad.bias_col = cdiv(L.K, kTileN) * kTileN;
+    ad.bias_col = cdiv(L.K, g.tn) * g.tn;
     ad.gsq = gsq;
     ad.gsq_b = gsq_b;
     op.wg_count = g.tiles_m * g.tiles_n;
@@ -899,8 +960,11 @@ struct Engine {
       g.M = B;
       g.N = L.out;
       g.R = L.K;
+      const auto tq = choose_tn(B, L.out);
+      g.tn = tq.first;
+      op.seq = tq.second;
       g.tiles_m = cdiv(B, kTileM);
-      g.tiles_n = cdiv(L.out, kTileN);
+      g.tiles_n = cdiv(L.out, g.tn);
       g.epi = EPI_MSE;
       g.bias = bias(L);
       ed3 = buf(B, L.out);
@@ -1293,14 +1357,14 @@ struct Engine {
       }
       if (!sac) {
         // per-tile grad-square partials for norm/policy (rl/nn/utils.py:13-19)
-        for (auto& L : pi.layers) ngsq += cdiv(L.out, kTileM) * cdiv(L.K, kTileN) + cdiv(L.out, kTileM);
+        for (auto& L : pi.layers) ngsq += dw_gsq_w(L) + dw_gsq_b(L);
         gsq = mem.make<float>(ngsq);
       }
       std::vector<int> tens;
       float* gp = gsq;
       auto gsq_for = [&](const Layer& L, int t_w, int t_b) -> std::pair<float*, float*> {
         if (!gsq) return {nullptr, nullptr};
-        int nw = cdiv(L.out, kTileM) * cdiv(L.K, kTileN), nb = cdiv(L.out, kTileM);
+        int nw = dw_gsq_w(L), nb = dw_gsq_b(L);
         float* w = gp;
         float* b = gp + nw;
         gp += nw + nb;
@@ -1418,9 +1482,17 @@ struct Engine {
       for (auto& op : lv) flat_ops.push_back(op);
     G.d_ops = mem.make<Op>(total);
     HIPCHK(hipMemcpy(G.d_ops, flat_ops.data(), total * sizeof(Op), hipMemcpyHostToDevice));
+    const char* tr_env = std::getenv("RLE_TRACE");
+    if (tr_env && tr_env[0] == '1') {
+      for (int w : G.nwg) G.trace_n += w;
+      G.trace = mem.make<unsigned long long>((size_t)G.trace_n * 4);
+    }
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    long long tr_off = 0;
     for (size_t l = 0; l < levels.size(); ++l) {
-      hipError_t e = launch_level(G.d_ops + G.off[l], levels[l].data(), G.nops[l], G.nwg[l], stream);
+      hipError_t e = launch_level(G.d_ops + G.off[l], levels[l].data(), G.nops[l], G.nwg[l], stream,
+                                  G.trace ? G.trace + tr_off * 4 : nullptr);
+      tr_off += G.nwg[l];
       if (e != hipSuccess) {
         hipGraph_t tmp;
         (void)hipStreamEndCapture(stream, &tmp);
@@ -1456,25 +1528,68 @@ struct Engine {
     t_ind = mem.make<long long>((size_t)tape_cap * B);
   }
 
+  // Builds a step program twice: the first pass fixes the level schedule, then
+  // GEMM tiles of any level with more workgroups than fit on the device at once
+  // are widened (16 -> 32 -> 64 columns, fewer workgroups, longer reductions per
+  // wave) and the program is rebuilt with that tile plan.
+  template <class F>
+  Prog plan_build(F&& f) {
+    tn_plan.clear();
+    tn_seq = 0;
+    Prog p0;
+    f(p0);
+    std::vector<int> plan(tn_seq, 16);
+    auto levels = p0.schedule();
+    for (auto& lv : levels)
+      for (auto& op : lv)
+        if (op.kind == OP_GEMM) plan[op.seq] = op.gemm.tn;
+    const int cap = std::max(256, level_capacity());
+    auto wg_of = [&](const Op& op) {
+      if (op.kind != OP_GEMM) return op.wg_count;
+      const GemmArgs& g = op.gemm;
+      return g.tiles_m * (cdiv(g.N, plan[op.seq]) + (g.epi == EPI_ADAM ? 1 : 0));
+    };
+    for (auto& lv : levels) {
+      while (true) {
+        long long total = 0;
+        for (auto& op : lv) total += wg_of(op);
+        if (total <= cap) break;
+        int best = -1, best_wg = 0;
+        for (auto& op : lv)
+          if (op.kind == OP_GEMM && plan[op.seq] < 64 && wg_of(op) > best_wg) {
+            best = op.seq;
+            best_wg = wg_of(op);
+          }
+        if (best < 0) break;
+        plan[best] *= 2;
+      }
+    }
+    tn_plan = plan;
+    tn_seq = 0;
+    Prog p;
+    f(p);
+    tn_plan.clear();
+    return p;
+  }
+
   void build() {
     REQUIRE(replay, "no replay bound");
     ensure_tapes(1024);
-    Prog p1, p2;
     if (algo == RLE_TD7) {
-      build_td7(p1, true);
+      Prog p1 = plan_build([&](Prog& p) { build_td7(p, true); });
       g_policy = capture(p1);
-      build_td7(p2, false);
+      Prog p2 = plan_build([&](Prog& p) { build_td7(p, false); });
       g_plain = capture(p2);
       Prog ph;
       build_td7_hard(ph);
       g_hard = capture(ph);
     } else if (algo == RLE_TD3) {
-      build_mlp(p1, true);
+      Prog p1 = plan_build([&](Prog& p) { build_mlp(p, true); });
       g_policy = capture(p1);
-      build_mlp(p2, false);
+      Prog p2 = plan_build([&](Prog& p) { build_mlp(p, false); });
       g_plain = capture(p2);
     } else {
-      build_mlp(p1, true);
+      Prog p1 = plan_build([&](Prog& p) { build_mlp(p, true); });
       g_policy = capture(p1);
       g_plain = g_policy;
     }
@@ -1569,6 +1684,7 @@ const char* rle_last_error(void) { return rle::g_err.c_str(); }
 int rle_replay_create(int device, long long capacity, int state_dim, int action_dim, int lap, rle_replay** out) {
   return guard([&] {
     REQUIRE(out && capacity > 0 && state_dim > 0 && action_dim > 0, "rle_replay_create: bad args");
+    REQUIRE(state_dim <= 1024 && action_dim <= 128, "rle_replay_create: state_dim <= 1024, action_dim <= 128");
     REQUIRE(capacity <= 2048LL * 4096, "rle_replay_create: capacity > 8M transitions");
     HIPCHK(hipSetDevice(device));
     auto* h = new rle_replay();
@@ -1857,6 +1973,8 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
     REQUIRE(cfg->algo >= 0 && cfg->algo <= 2, "create: bad algo");
     REQUIRE(cfg->batch > 0 && cfg->batch % 16 == 0 && cfg->batch <= 1024,
             "create: batch must be a multiple of 16, <= 1024");
+    REQUIRE(cfg->state_dim <= 1024 && cfg->action_dim <= 128 && cfg->hidden <= 512,
+            "create: state_dim <= 1024, action_dim <= 128, hidden <= 512");
     REQUIRE(cfg->state_dim > 0 && cfg->action_dim > 0 && cfg->hidden > 0 && cfg->hidden % 4 == 0,
             "create: bad dims (hidden must be a multiple of 4)");
     HIPCHK(hipSetDevice(cfg->device));
@@ -2120,6 +2238,21 @@ int rle_graph_describe(rle_engine* h, int which, char* buf, int len) {
     const rle::Graph& G = which == 0 ? e.g_policy : (which == 1 ? e.g_plain : e.g_hard);
     REQUIRE(buf && len > 0, "describe: bad buffer");
     std::snprintf(buf, (size_t)len, "%s", G.desc.c_str());
+  });
+}
+
+int rle_graph_trace(rle_engine* h, int which, unsigned long long* out, long long cap, long long* n_out) {
+  return guard([&] {
+    Engine& e = *h->e;
+    REQUIRE(n_out, "trace: null n_out");
+    if (!e.built) e.build();
+    const rle::Graph& G = which == 0 ? e.g_policy : (which == 1 ? e.g_plain : e.g_hard);
+    *n_out = G.trace ? G.trace_n : 0;
+    if (!G.trace || !out) return;
+    REQUIRE(cap >= G.trace_n * 4, "trace: buffer too small");
+    HIPCHK(hipStreamSynchronize(e.stream));
+    HIPCHK(hipMemcpy(out, G.trace, (size_t)G.trace_n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    *n_out = G.trace_n;
   });
 }
 

@@ -107,12 +107,25 @@ __device__ __forceinline__ float normal_from(unsigned a, unsigned b) {
   return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
 }
 
-// AvgL1Norm denominator from column-tile partial |x| sums (fixed order).
-__device__ __forceinline__ float norm_m(const float* part, int ld, int row, int nparts, int width) {
-  const GAS float* p = G(part);
+// AvgL1Norm mean |x| of a row from column-tile partial |x| sums (sequential order);
+// the partials are loaded 16 at a time (clamped, independent) so a row costs one
+// memory round trip per 16 partials.
+__device__ __forceinline__ float norm_mean(const float* part, int ld, int row, int nparts, int width) {
+  const GAS float* p = G(part) + row;
   float s = 0.f;
-  for (int q = 0; q < nparts; ++q) s += p[(size_t)q * ld + row];
-  const float m = s / (float)width;
+  for (int q0 = 0; q0 < nparts; q0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = p[(size_t)min(q0 + q, nparts - 1) * ld];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (q0 + q < nparts) s += v[q];
+  }
+  return s / (float)width;
+}
+// Denominator m = clamp(mean, min=1e-8) (rl/nn/sale.py:11-13).
+__device__ __forceinline__ float norm_m(const float* part, int ld, int row, int nparts, int width) {
+  const float m = norm_mean(part, ld, row, nparts, width);
   return m < 1e-8f ? 1e-8f : m;
 }
 
@@ -178,116 +191,53 @@ __device__ __forceinline__ void mat_st4(const CAS Mat& m, int r, int c, float4 v
   }
 }
 
+// Phase timestamps of one workgroup (wave 0, lane 0): [0] entry, [1] main loop
+// start, [2] main loop end (GEMM only), [3] exit.
+__device__ __forceinline__ void trace_mark(unsigned long long* tr, int slot) {
+  if (tr && threadIdx.x == 0) tr[slot] = __builtin_amdgcn_s_memrealtime();
+}
+#ifdef RLE_TRACE_FINE
+constexpr int kTraceSlots = 8;
+__device__ unsigned long long* g_fine;
+#define FINE_MARK(slot)                                                                       \
+  do {                                                                                        \
+    if (g_fine && threadIdx.x == 0)                                                           \
+      g_fine[(size_t)blockIdx.x * kTraceSlots + (slot)] = __builtin_amdgcn_s_memrealtime();   \
+  } while (0)
+#else
+#define FINE_MARK(slot) \
+  do {                  \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------- GEMM
 //
-// One workgroup = one 16 x 64 output tile; wave w owns columns [16w, 16w+16)
-// and the FULL reduction.  Both operands are fragment images (ops.h), so each
+// One workgroup = one 16 x tn output tile (tn in {16, 32, 64}); its 4 waves are
+// tn/16 column groups x 64/tn reduction splits, split partials summed through
+// LDS in a fixed order.  Both operands are fragment images (ops.h), so each
 // 16-wide reduction chunk is one lane-linear 16-byte buffer load per lane per
-// operand -- the wave reads whole 1 KB blocks (8 full cache lines) instead of
-// 16 row pieces.  A load cursor per operand walks the reduction block by block
-// and segment by segment; 4 chunks are kept in flight in a register ring.
-// AvgL1Norm scales (deferred normalisation) are applied when a chunk is
-// consumed.  Epilogue operands (bias, derivative source, Adam w/m/v) are
-// fetched before the main loop; the accumulator fragment (rows 4*(l>>4)+q,
-// column l&15) is exactly one float4 of a T image, so T-image traffic in the
-// epilogue is one 16-byte access per lane.
+// operand (whole 1 KB blocks per wave), 4 chunks in flight.
+//
+// Code size is the first-order cost here: the instruction cache is invalidated
+// at every dispatch and a wave fetches code at ~0.4 us per KB (tools/mbic.hip),
+// while a level's arithmetic is ~1 us.  So every op runs a compile-time
+// specialised variant (mode, epilogue, activation, norm: GemmArgs::vid) whose
+// straight-line path contains only what that op does: no per-element
+// activation switch, no segment bookkeeping inside the chunk loop (segments
+// are walked by an outer loop), and no normalisation code in the plain case.
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-static_assert(kMaxSeg == 4, "LaneOp holds 4 segments");
-constexpr int kRing = 4;  // GEMM main-loop chunks in flight per wave
-
-struct LaneOp {
-  f32x4 inv;  // N-image operand + normed: 1/m of the lane's row, per segment (vector, not
-              // array: a per-chunk select must stay in registers)
-  i32x4 tab;  // T-image operand + normed: LDS offset of the segment's 1/m table, -1 = none
-  bool norm;  // any normed segment
-};
-
-// v[q] for a wave-uniform q as a select chain (a variable extract is lowered to scratch).
-template <class V>
-__device__ __forceinline__ auto pick(const V& v, int q) -> decltype(v[0] + 0) {
-  return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
-}
-
-__device__ __forceinline__ void lane_op(const CAS Operand& op, bool T, int x, LaneOp& L, float* tabs, int& used) {
-  L.inv = f32x4{1.f, 1.f, 1.f, 1.f};
-  L.tab = i32x4{-1, -1, -1, -1};
-  L.norm = false;
-#pragma unroll
-  for (int s = 0; s < kMaxSeg; ++s) {
-    if (s < op.nseg) {
-      const CAS Seg& sg = op.seg[s];
-      if (sg.norm.part) {
-        L.norm = true;
-        if (!T) {
-          if (x >= sg.x0 && x < sg.x1) L.inv[s] = norm_inv(sg.norm, x - sg.x0);
-        } else {
-          const int n = sg.r1 - sg.r0;
-          L.tab[s] = used;
-          build_norm_tab(sg.norm, n, tabs + used);
-          used += (n + 15) & ~15;
-        }
-      }
-    }
-  }
-}
+constexpr int kOOB = 0x7ffffff0;  // voffset beyond num_records: the load returns 0
 
 __device__ __forceinline__ float4 as_f4(u32x4 v) {
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
-
-// Load cursor of one operand: lane-linear 1 KB block per chunk, segment after segment.
-struct Cursor {
-  __amdgpu_buffer_rsrc_t rs;  // current segment (wave-uniform)
-  int voff;                   // this lane's byte offset of the next chunk
-  int left;                   // chunks left in the segment
-  int s;                      // segment index (>= nseg: past the end, reads 0)
-  int toff;                   // T image + normed: LDS 1/m table offset of the next chunk (-1: none)
-  float inv;                  // N image + normed: lane row's 1/m in the segment
-
-  __device__ __forceinline__ void open(const CAS Operand& op, const LaneOp& L, int xw, int q) {
-    s = q;
-    if (q >= op.nseg) {
-      rs = __builtin_amdgcn_make_buffer_rsrc((void*)nullptr, 0, 0, 0x00020000);
-      left = 1 << 30;
-      voff = 0;
-      toff = -1;
-      inv = 1.f;
-      return;
-    }
-    const CAS Seg& sg = op.seg[q];
-    rs = __builtin_amdgcn_make_buffer_rsrc((void*)sg.p, 0, 0x7fff0000, 0x00020000);
-    left = (sg.r1 - sg.r0 + 15) >> 4;
-    voff = ((xw - sg.x0) >> 4) * sg.xs * 1024 + (threadIdx.x & 63) * 16;
-    inv = pick(L.inv, q);
-    toff = pick(L.tab, q);
-  }
-  __device__ __forceinline__ float4 next(const CAS Operand& op, const LaneOp& L, int xw, float& inv_out,
-                                         int& toff_out) {
-    if (left == 0) open(op, L, xw, s + 1);
-    const float4 v = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
-    inv_out = inv;
-    toff_out = toff;
-    if (toff >= 0) toff += 16;
-    voff += 1024;
-    --left;
-    return v;
-  }
-};
-
-// Deferred AvgL1Norm of a consumed chunk.
-template <bool T>
-__device__ __forceinline__ float4 chunk_scale(float4 v, float inv, int toff, int rl, const float* tabs) {
-  if (!T) {
-    v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
-  } else if (toff >= 0) {
-    const float4 w = *(const float4*)(tabs + toff + rl);
-    v.x *= w.x; v.y *= w.y; v.z *= w.z; v.w *= w.w;
-  }
-  return v;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0x7fff0000, 0x00020000);
 }
-
+__device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int off) {
+  return as_f4(__builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
 __device__ __forceinline__ f32x4 mfma4(const float4& a, const float4& b, f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
@@ -295,165 +245,223 @@ __device__ __forceinline__ f32x4 mfma4(const float4& a, const float4& b, f32x4 a
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
   return acc;
 }
-
-// Main loop, one instantiation per operand image pair (FWD <N,N>, DX <N,T>,
-// DW <T,T>, DW bias column <T,-> with B = ones).  xa_w / xb_w: the wave's first
-// A row / B column (wave-uniform).
-template <bool TA, bool TB, bool BIAS>
-__device__ __forceinline__ f32x4 gemm_mainloop(const CAS GemmArgs& g, int xa, int xb, int xa_w, int xb_w,
-                                               bool active, float* tabs) {
-  const int lane = threadIdx.x & 63;
-  LaneOp la, lb;
-  int used = 0;
-  lane_op(g.A, TA, xa, la, tabs, used);
-  if (!BIAS) lane_op(g.B, TB, xb, lb, tabs, used);
-  if (used) __syncthreads();
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-  if (!active) return acc0;
-  const bool b_ok = BIAS ? (xb == g.adam.bias_col) : true;
-  const int rl = 4 * (lane >> 4);
-  const int nch = (g.R + 15) >> 4;
-  const bool an = la.norm, bn = !BIAS && lb.norm;
-  // DW B: the segments split the columns; the wave's 16 columns lie in one of them
-  int qb = 0;
-  if (TA && TB && !BIAS) {
-#pragma unroll
-    for (int q = 1; q < kMaxSeg; ++q)
-      if (q < g.B.nseg && xb_w >= g.B.seg[q].x0) qb = q;
-  }
-  Cursor ca, cb;
-  ca.open(g.A, la, xa_w, 0);
-  if (!BIAS) cb.open(g.B, lb, xb_w, qb);
-  const int nb_end = (TA && TB) ? qb + 1 : g.B.nseg;  // DW: one B segment only
-  const float4 ones = b_ok ? make_float4(1.f, 1.f, 1.f, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
-  auto ldA = [&](float& i, int& t) { return ca.next(g.A, la, xa_w, i, t); };
-  auto ldB = [&](float& i, int& t) {
-    if constexpr (BIAS) return ones;  // db = sum_r dZ(r, n); A is zero past R
-    else {
-      if (cb.left == 0 && cb.s + 1 >= nb_end) cb.s = kMaxSeg;  // DW: never walk into another column block
-      return cb.next(g.B, lb, xb_w, i, t);
-    }
-  };
-  auto use = [&](float4 a, float4 b, float ia, int ta, float ib, int tb, f32x4 acc) {
-    if (an) a = chunk_scale<TA>(a, ia, ta, rl, tabs);
-    if (bn) b = chunk_scale<TB>(b, ib, tb, rl, tabs);
-    return mfma4(a, b, acc);
-  };
-  float4 ra[kRing], rb[kRing];
-  float ia[kRing], ib[kRing];
-  int ta[kRing], tb[kRing];
-#pragma unroll
-  for (int k = 0; k < kRing; ++k) {
-    ra[k] = ldA(ia[k], ta[k]);
-    rb[k] = ldB(ib[k], tb[k]);
-  }
-#pragma unroll 1
-  for (int c = 0; c < nch; c += kRing) {
-#pragma unroll
-    for (int k = 0; k < kRing; ++k) {
-      if (k & 1) acc1 = use(ra[k], rb[k], ia[k], ta[k], ib[k], tb[k], acc1);
-      else acc0 = use(ra[k], rb[k], ia[k], ta[k], ib[k], tb[k], acc0);
-      ra[k] = ldA(ia[k], ta[k]);
-      rb[k] = ldB(ib[k], tb[k]);
-    }
-  }
-  return acc0 + acc1;
+__device__ __forceinline__ float4 scale4(float4 v, float s) { return make_float4(v.x * s, v.y * s, v.z * s, v.w * s); }
+__device__ __forceinline__ float4 mul4(float4 v, float4 s) {
+  return make_float4(v.x * s.x, v.y * s.y, v.z * s.z, v.w * s.w);
 }
 
-__device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* smem) {
-  // wave index via readfirstlane: the compiler then treats every wave-derived
-  // condition as uniform (scalar branches)
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int it = t / g.tiles_n, jt = t - it * g.tiles_n;
-  const int i0 = it * kTileM, j0 = jt * kTileN + wave * 16;
-  const bool bias_tile = (g.epi == EPI_ADAM) && (jt * kTileN >= g.adam.bias_col);
-  float* red = smem;            // [64] reduction scratch
-  float* tabs = smem + 64;      // normalisation tables
-  const int xa = i0 + (lane & 15), xb = j0 + (lane & 15);
-  const int j = xb;                       // output column of this lane
-  const int ib = i0 + 4 * (lane >> 4);    // first of this lane's 4 output rows
-  const bool jok = bias_tile ? (j == g.adam.bias_col) : (j < g.N);
-  const bool active = bias_tile ? (wave == 0) : (j0 < g.N);  // wave-uniform
+template <int ACT>
+__device__ __forceinline__ float act_f(float v) {
+  if constexpr (ACT == ACT_RELU) return v > 0.f ? v : 0.f;
+  else if constexpr (ACT == ACT_ELU) return v > 0.f ? v : expm1f(v);
+  else if constexpr (ACT == ACT_TANH) return tanhf(v);
+  else return v;
+}
+template <int ACT>
+__device__ __forceinline__ float act_b(float saved) {  // see act_bwd
+  if constexpr (ACT == ACT_RELU) return saved > 0.f ? 1.f : 0.f;
+  else if constexpr (ACT == ACT_ELU) return saved > 0.f ? 1.f : expf(saved);
+  else if constexpr (ACT == ACT_TANH) return 1.f - saved * saved;
+  else return 1.f;
+}
+
+// Reduction over chunks [k0, k1) of one operand pair: A from (ra, va), B from
+// (rb, vb) (byte offsets of chunk k0, +1 KB per chunk); 4 chunks in flight.
+// SA / SB: per-chunk scaling (deferred AvgL1Norm) by a lane constant (N image)
+// or an LDS table of 4 rows (T image, tab = float offset of chunk k0's rows).
+template <int SA, int SB>
+__device__ __forceinline__ f32x4 chunk_loop(__amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rb, int vb,
+                                            int n, f32x4 acc, float inva, const float* taba, const float* tabb,
+                                            bool bias_ones) {
+  const int rl = ((threadIdx.x & 63) >> 4) << 2;
+  float4 a[4], b[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    a[r] = bload(ra, r < n ? va + r * 1024 : kOOB);
+    b[r] = bias_ones ? make_float4(1.f, 1.f, 1.f, 1.f) : bload(rb, r < n ? vb + r * 1024 : kOOB);
+  }
+  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int c = 0; c < n; c += 4) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float4 x = a[r], y = b[r];
+      if constexpr (SA == 1) x = scale4(x, inva);
+      // (table rows past n are not built: clamp; their chunks load as zeros anyway)
+      if constexpr (SA == 2) x = mul4(x, *(const float4*)(taba + min(c + r, n - 1) * 16 + rl));
+      if constexpr (SB == 2) y = mul4(y, *(const float4*)(tabb + min(c + r, n - 1) * 16 + rl));
+      if (r & 1) acc1 = mfma4(x, y, acc1);
+      else acc = mfma4(x, y, acc);
+      const int nx = c + r + 4;
+      a[r] = bload(ra, nx < n ? va + nx * 1024 : kOOB);
+      if (!bias_ones) b[r] = bload(rb, nx < n ? vb + nx * 1024 : kOOB);
+    }
+  }
+  return acc + acc1;
+}
+
+template <int MODE, int EPI, int ACT, bool NORM>
+__device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ksl = g.ks_log;
+  const int cg = wave >> ksl, kp = wave & ((1 << ksl) - 1);
+  const int it = (int)(((float)t + 0.5f) * g.inv_tiles_n);
+  const int jt = t - it * g.tiles_n;
+  const int i0 = it << 4, j0 = jt * g.tn + (cg << 4);
+  const bool bias_tile = EPI == EPI_ADAM && jt * g.tn >= g.adam.bias_col;
+  const bool lead = kp == 0;
+  const bool active = bias_tile ? cg == 0 : j0 < g.N;  // wave-uniform
+  const int j = j0 + (lane & 15), ib = i0 + ((lane >> 4) << 2);
+  const bool jok = active && lead && (bias_tile ? j == g.adam.bias_col : j < g.N);
+  float* red = smem;               // [64] reduction scratch
+  float* part = smem + 64;         // [4 waves][64][4] split-K partials
+  float* tabs = smem + 64 + 1024;  // AvgL1Norm 1/m tables (T-image operands)
+  const int nch = g.R >> 4;
+  const int per = (nch + (1 << ksl) - 1) >> ksl;
+  const int c0 = kp * per, c1 = min(nch, c0 + per);
 
   // ---- epilogue operands fetched ahead of the main loop
   float pre_b = 0.f;
   float4 ds = make_float4(1.f, 1.f, 1.f, 1.f), pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
-  size_t wt = 0;  // T-image element offset of (ib, j) in the weight (EPI_ADAM)
-  if (g.epi != EPI_ADAM) {
-    if (g.bias && jok) pre_b = G(g.bias)[j];
-    if (g.dsrc.t && jok) ds = mat_ld4(g.dsrc, ib, j);
-  } else if (active) {
-    const CAS AdamArgs& ad = g.adam;
-    if (bias_tile) {
-      if (jok) {
+  size_t wt = 0;
+  if constexpr (EPI != EPI_ADAM) {
+    if (jok && g.bias) pre_b = G(g.bias)[j];
+    if constexpr (MODE == GEMM_DX && ACT != ACT_NONE) {
+      if (jok) ds = mat_ld4(g.dsrc, ib, j);
+    }
+  } else {
+    if (jok) {
+      const CAS AdamArgs& ad = g.adam;
+      if (bias_tile) {
         pp = ld4g(G(ad.b) + ib);
         mm = ld4g(G(ad.b) + ib + ad.mo);
         vv = ld4g(G(ad.b) + ib + ad.vo);
+      } else {
+        wt = tidx(ad.w.rbs, ib, j);
+        pp = ld4g(G(ad.w.t) + wt);
+        mm = ld4g(G(ad.w.t) + wt + ad.mo);
+        vv = ld4g(G(ad.w.t) + wt + ad.vo);
       }
-    } else {
-      wt = tidx(ad.w.rbs, ib, j);
-      pp = ld4g(G(ad.w.t) + wt);
-      mm = ld4g(G(ad.w.t) + wt + ad.mo);
-      vv = ld4g(G(ad.w.t) + wt + ad.vo);
     }
   }
+  trace_mark(tr, 1);
 
-  const int xa_w = i0, xb_w = j0;  // wave-uniform operand origins
-  // The distinct empty asm statements head each arm so the compiler cannot hoist
-  // the arms' common descriptor loads above the branch.
-  f32x4 acc;
-  if (g.mode == GEMM_FWD) {
-    asm volatile("; gemm fwd" ::);
-    acc = gemm_mainloop<false, false, false>(g, xa, xb, xa_w, xb_w, active, tabs);
-  } else if (g.mode == GEMM_DX) {
-    asm volatile("; gemm dx" ::);
-    acc = gemm_mainloop<false, true, false>(g, xa, xb, xa_w, xb_w, active, tabs);
-  } else if (!bias_tile) {
-    asm volatile("; gemm dw" ::);
-    acc = gemm_mainloop<true, true, false>(g, xa, xb, xa_w, xb_w, active, tabs);
+  // ---- reduction
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int lb = lane * 16;
+  if constexpr (MODE != GEMM_DW) {
+    // A: N image, segments along the reduction; B: W (FWD: N image, one segment over
+    // the whole reduction; DX: T image, one segment per A segment)
+    const CAS Seg& w0 = g.B.seg[0];
+    for (int q = 0; q < g.A.nseg; ++q) {
+      const CAS Seg& sa = g.A.seg[q];
+      const int s0 = sa.r0 >> 4;
+      const int k0 = max(c0, s0), k1 = min(c1, (sa.r1 + 15) >> 4);
+      if (!active || k0 >= k1) continue;
+      float inva = 1.f;
+      if constexpr (NORM) {
+        if (sa.norm.part) inva = norm_inv(sa.norm, i0 + (lane & 15));
+      }
+      const int va = ((i0 >> 4) * sa.xs + (k0 - s0)) * 1024 + lb;
+      if constexpr (MODE == GEMM_FWD) {
+        const int vb = ((j0 >> 4) * w0.xs + k0) * 1024 + lb;
+        acc = chunk_loop<NORM ? 1 : 0, 0>(rsrc(sa.p), va, rsrc(w0.p), vb, k1 - k0, acc, inva, nullptr, nullptr,
+                                          false);
+      } else {
+        const CAS Seg& sb = g.B.seg[q];
+        const int vb = ((j0 >> 4) * sb.xs + (k0 - s0)) * 1024 + lb;
+        acc = chunk_loop<0, 0>(rsrc(sa.p), va, rsrc(sb.p), vb, k1 - k0, acc, 1.f, nullptr, nullptr, false);
+      }
+    }
   } else {
-    asm volatile("; gemm db" ::);
-    acc = gemm_mainloop<true, true, true>(g, xa, xb, xa_w, xb_w, active, tabs);
-  }
-
-  if (g.epi == EPI_STORE) {
-    float rowabs[4] = {0.f, 0.f, 0.f, 0.f};
-    if (jok) {
-      float v[4] = {acc[0] + pre_b, acc[1] + pre_b, acc[2] + pre_b, acc[3] + pre_b};
-      if (g.pre.t) mat_st4(g.pre, ib, j, make_float4(v[0], v[1], v[2], v[3]));
-      float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
-      const bool noised = g.noise.t && ib >= g.noise_row0;  // target policy smoothing (td7.py:188-194)
-      if (noised) e = mat_ld4(g.noise, ib - g.noise_row0, j);
-      const float ev[4] = {e.x, e.y, e.z, e.w}, dv[4] = {ds.x, ds.y, ds.z, ds.w};
-      float y[4];
+    // DW: A = dZ (T image, x = output row), B = X (T image, x = output column; the
+    // wave's 16 columns lie in one column segment); both reduce over batch rows
+    const CAS Seg& sa = g.A.seg[0];
+    int qb = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        y[q] = act_fwd(g.act, v[q]);
-        if (noised) {
-          const float nz = fminf(fmaxf(ev[q] * g.noise_sigma, -g.noise_clip), g.noise_clip);
-          y[q] = fminf(fmaxf(y[q] + nz, -1.f), 1.f);
-        }
-        if (g.dsrc.t) y[q] *= act_bwd(g.dact, dv[q]);
-        rowabs[q] = fabsf(y[q]);
-      }
-      mat_st4(g.out, ib, j, make_float4(y[0], y[1], y[2], y[3]));
-    }
-    if (g.norm_out) {  // |y| summed over the tile's 64 columns, per row
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) rowabs[q] += __shfl_xor(rowabs[q], o, 64);
-      }
-      if ((lane & 15) == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) red[wave * 16 + 4 * (lane >> 4) + q] = rowabs[q];
+    for (int q = 1; q < kMaxSeg; ++q)
+      if (q < g.B.nseg && j0 >= g.B.seg[q].x0) qb = q;
+    const CAS Seg& sb = g.B.seg[qb];
+    const float* tb = nullptr;
+    if constexpr (NORM) {
+      // 1/m of every reduction row of every normed B segment, segment by segment
+      int off = 0, mine = -1;
+      for (int q = 0; q < g.B.nseg; ++q) {
+        const CAS Seg& s = g.B.seg[q];
+        if (!s.norm.part) continue;
+        build_norm_tab(s.norm, s.r1 - s.r0, tabs + off);
+        if (q == qb) mine = off;
+        off += (s.r1 - s.r0 + 15) & ~15;
       }
       __syncthreads();
-      if (tid < 16 && i0 + tid < g.M)
-        GW(g.norm_out)[(size_t)jt * g.norm_ld + i0 + tid] =
-            (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
+      if (mine >= 0) tb = tabs + mine + c0 * 16;
     }
-  } else if (g.epi == EPI_MSE) {  // td7.py:256 encoder loss, grad wrt zsa
+    if (active && c0 < c1) {
+      const int va = ((i0 >> 4) * sa.xs + c0) * 1024 + lb;
+      const int vb = (((j0 - sb.x0) >> 4) * sb.xs + c0) * 1024 + lb;
+      if (NORM && tb && !bias_tile)  // the bias column's B is ones: never scaled
+        acc = chunk_loop<0, 2>(rsrc(sa.p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, tb, bias_tile);
+      else
+        acc = chunk_loop<0, 0>(rsrc(sa.p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, nullptr, bias_tile);
+    }
+  }
+  trace_mark(tr, 2);
+  if (ksl) {  // split-K: partials of splits 1.. through LDS, summed by split 0 in fixed order
+    if (!lead) *(f32x4*)(part + (wave * 64 + lane) * 4) = acc;
+    __syncthreads();
+    if (lead) {
+      for (int q = 1; q < (1 << ksl); ++q) acc += *(const f32x4*)(part + ((wave + q) * 64 + lane) * 4);
+    }
+  }
+
+  // ---- epilogue
+  if constexpr (EPI == EPI_STORE) {
+    float rowabs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (jok) {
+      float y[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y[q] = acc[q] + pre_b;
+      if constexpr (MODE == GEMM_FWD) {
+        if (g.pre.t) mat_st4(g.pre, ib, j, make_float4(y[0], y[1], y[2], y[3]));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] = act_f<ACT>(y[q]);
+        if constexpr (ACT == ACT_TANH) {
+          if (g.noise.t && ib >= g.noise_row0) {  // target policy smoothing (td7.py:188-194)
+            const float4 e = mat_ld4(g.noise, ib - g.noise_row0, j);
+            const float ev[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float nz = fminf(fmaxf(ev[q] * g.noise_sigma, -g.noise_clip), g.noise_clip);
+              y[q] = fminf(fmaxf(y[q] + nz, -1.f), 1.f);
+            }
+          }
+        }
+      } else {  // DX: derivative mask
+        const float dv[4] = {ds.x, ds.y, ds.z, ds.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] *= act_b<ACT>(dv[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rowabs[q] = fabsf(y[q]);
+      mat_st4(g.out, ib, j, make_float4(y[0], y[1], y[2], y[3]));
+    }
+    if constexpr (MODE == GEMM_FWD) {
+      if (g.norm_out) {  // |y| summed over the tile's tn columns, per row
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) rowabs[q] += __shfl_xor(rowabs[q], o, 64);
+        }
+        if ((lane & 15) == 0) *(float4*)(red + wave * 16 + ((lane >> 4) << 2)) =
+            make_float4(rowabs[0], rowabs[1], rowabs[2], rowabs[3]);
+        __syncthreads();
+        if (tid < 16)
+          GW(g.norm_out)[(size_t)jt * g.norm_ld + i0 + tid] =
+              (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
+      }
+    }
+  } else if constexpr (EPI == EPI_MSE) {  // td7.py:256 encoder loss, grad wrt zsa
     float d2 = 0.f;
     if (jok) {
       const float4 tv = mat_ld4(g.tgt, ib, j);
@@ -461,8 +469,7 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
       float gr[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float tn = tq[q] * norm_inv(g.tgt_norm, ib + q);
-        const float d = (acc[q] + pre_b) - tn;
+        const float d = (acc[q] + pre_b) - tq[q] * norm_inv(g.tgt_norm, ib + q);
         gr[q] = (2.f * d) * g.mse_scale;  // mse_scale = 1/n
         d2 += d * d;
       }
@@ -472,21 +479,18 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
     if (tid == 0) GW(g.loss_part)[t] = d2;
   } else {  // EPI_ADAM (torch.optim.Adam single-tensor law, see oracle/agents.py)
     const CAS AdamArgs& ad = g.adam;
-    const double tt = (double)(*G(ad.t) + 1);
-    const double bc1 = 1.0 - pow((double)ad.beta1, tt);
-    const double bc2 = 1.0 - pow((double)ad.beta2, tt);
-    const float step_size = (float)((double)ad.lr / bc1);
-    const float bc2s = (float)sqrt(bc2);
     float gg = 0.f;
-    if (active && jok) {
+    if (jok) {
+      const double tt = (double)(*G(ad.t) + 1);
+      const float step_size = (float)((double)ad.lr / (1.0 - pow((double)ad.beta1, tt)));
+      const float bc2s = (float)sqrt(1.0 - pow((double)ad.beta2, tt));
       const float p4[4] = {pp.x, pp.y, pp.z, pp.w}, m4[4] = {mm.x, mm.y, mm.z, mm.w}, v4[4] = {vv.x, vv.y, vv.z, vv.w};
       float po[4], mo[4], vo[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float gv = acc[q];
-        float m = m4[q], v2 = v4[q];
-        m = m + (1.f - ad.beta1) * (gv - m);
-        v2 = v2 * ad.beta2 + ((1.f - ad.beta2) * gv) * gv;
+        const float m = m4[q] + (1.f - ad.beta1) * (gv - m4[q]);
+        const float v2 = v4[q] * ad.beta2 + ((1.f - ad.beta2) * gv) * gv;
         const float denom = sqrtf(v2) / bc2s + ad.eps;
         const bool ok = ib + q < g.M;  // weight rows past out stay untouched (zero)
         po[q] = ok ? p4[q] + (-step_size * m) / denom : p4[q];
@@ -494,15 +498,11 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
         vo[q] = ok ? v2 : v4[q];
         gg += ok ? gv * gv : 0.f;
       }
-      const float4 P = make_float4(po[0], po[1], po[2], po[3]);
-      if (bias_tile) {
-        st4g(GW(ad.b) + ib, P);
-        st4g(GW(ad.b) + ib + ad.mo, make_float4(mo[0], mo[1], mo[2], mo[3]));
-        st4g(GW(ad.b) + ib + ad.vo, make_float4(vo[0], vo[1], vo[2], vo[3]));
-      } else {
-        st4g(GW(ad.w.t) + wt, P);
-        st4g(GW(ad.w.t) + wt + ad.mo, make_float4(mo[0], mo[1], mo[2], mo[3]));
-        st4g(GW(ad.w.t) + wt + ad.vo, make_float4(vo[0], vo[1], vo[2], vo[3]));
+      GAS float* pw = bias_tile ? GW(ad.b) + ib : GW(ad.w.t) + wt;
+      st4g(pw, make_float4(po[0], po[1], po[2], po[3]));
+      st4g(pw + ad.mo, make_float4(mo[0], mo[1], mo[2], mo[3]));
+      st4g(pw + ad.vo, make_float4(vo[0], vo[1], vo[2], vo[3]));
+      if (!bias_tile) {
         GAS float* qn = GW(ad.w.n) + nidx(ad.w.cbn, ib, j);
         qn[0] = po[0];
         qn[4] = po[1];
@@ -520,6 +520,34 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
   }
 }
 
+__device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
+#define RLE_V(mode, epi, act, norm)                      \
+  case gemm_vid(mode, epi, act, norm):                   \
+    asm volatile("; gemm variant " #mode #epi #act #norm ::); \
+    gemm_v<mode, epi, act, norm>(g, t, smem, tr);        \
+    break;
+  switch (g.vid) {
+    RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, false)
+    RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, true)
+    RLE_V(GEMM_FWD, EPI_STORE, ACT_RELU, false)
+    RLE_V(GEMM_FWD, EPI_STORE, ACT_RELU, true)
+    RLE_V(GEMM_FWD, EPI_STORE, ACT_ELU, false)
+    RLE_V(GEMM_FWD, EPI_STORE, ACT_ELU, true)
+    RLE_V(GEMM_FWD, EPI_STORE, ACT_TANH, false)
+    RLE_V(GEMM_FWD, EPI_STORE, ACT_TANH, true)
+    RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, false)
+    RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, true)
+    RLE_V(GEMM_DX, EPI_STORE, ACT_NONE, false)
+    RLE_V(GEMM_DX, EPI_STORE, ACT_RELU, false)
+    RLE_V(GEMM_DX, EPI_STORE, ACT_ELU, false)
+    RLE_V(GEMM_DX, EPI_STORE, ACT_TANH, false)
+    RLE_V(GEMM_DW, EPI_ADAM, ACT_NONE, false)
+    RLE_V(GEMM_DW, EPI_ADAM, ACT_NONE, true)
+    default: break;
+  }
+#undef RLE_V
+}
+
 // ---------------------------------------------------------------- AvgL1Norm backward
 
 // 16 rows per workgroup, 4 per wave: lane k reads a float4 (4 rows) of column k
@@ -531,10 +559,8 @@ __device__ __forceinline__ void op_normbwd(const CAS NormBwdArgs& a, int t) {
   float inv[4], gmv[4];
   bool clamped[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float s = 0.f;  // m recomputed from the same partials the forward consumers used
-    for (int p = 0; p < a.norm.nparts; ++p) s += G(a.norm.part)[(size_t)p * a.norm.ld + r0 + q + a.norm.row0];
-    const float mean = s / (float)a.width;
+  for (int q = 0; q < 4; ++q) {  // m recomputed exactly as the forward consumers did (norm_m)
+    const float mean = norm_mean(a.norm.part, a.norm.ld, r0 + q + a.norm.row0, a.norm.nparts, a.width);
     clamped[q] = mean < 1e-8f;
     inv[q] = 1.f / (clamped[q] ? 1e-8f : mean);
   }
@@ -575,116 +601,166 @@ __device__ __forceinline__ void op_normbwd(const CAS NormBwdArgs& a, int t) {
 // Last critic layer (H -> 1) as a dot product fused with the TD target / loss /
 // priority / policy objective and the gradient into the last hidden layer.
 // 16 rows per workgroup, 4 per wave (lane k: float4 of 4 rows from T images).
-__device__ __forceinline__ void op_head(const CAS HeadArgs& h, int t, float* smem) {
+// Every phase issues all of its loads before the first use (clamped indices,
+// zeroed when out of range): no load sits behind a branch, so each phase costs
+// one memory round trip.
+constexpr int kHeadU = 4;  // columns per lane per pass (256 per pass)
+__device__ __forceinline__ void op_head(const CAS HeadArgs& h, int t, float* smem, unsigned long long* tr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r0 = t * 16 + wave * 4;
   float acc0 = 0.f, acc1 = 0.f;  // per-wave loss terms (sum over its rows)
   int kmax = (int)0x80000000, kmin = 0x7FFFFFFF;
   if (r0 < h.rows) {
-    float q[2][4];
-    float wv[2][8];
-    const int per = (h.H + 63) / 64;
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = lane + 64 * u;
-        const bool in = u < per && k < h.H;
-        wv[n][u] = in ? G(h.w[n])[tidx(h.w_rbs, 0, k)] : 0.f;
-        const float4 hv = in ? mat_ld4(h.h[n], r0, k) : make_float4(0.f, 0.f, 0.f, 0.f);
-        s[0] += hv.x * wv[n][u];
-        s[1] += hv.y * wv[n][u];
-        s[2] += hv.z * wv[n][u];
-        s[3] += hv.w * wv[n][u];
-      }
-      const float bb = G(h.b[n])[0];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) q[n][r] = wave_sum(s[r]) + bb;
-    }
-    float dq[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    bool want_dz = false;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = r0 + r;
-      switch (h.mode) {
-        case HEAD_TD7_TARGET: {  // td7.py:211-218
-          float v = fminf(q[0][r], q[1][r]);
-          v = fminf(fmaxf(v, G(h.vt)[1]), G(h.vt)[0]);
-          const float y = G(h.reward)[b] + (h.gamma * v) * G(h.notdone)[b];
-          if (lane == 0) GW(h.y)[b] = y;
-          kmax = max(kmax, fkey(y));
-          kmin = min(kmin, fkey(y));
-          break;
-        }
-        case HEAD_MLP_TARGET: {  // td3.py:160-164, sac.py:188-193
-          float v = fminf(q[0][r], q[1][r]);
-          if (h.sac) v = v - expf(G(h.log_alpha)[0]) * G(h.logpi)[b];
-          const float y = G(h.reward)[b] + (h.gamma * v) * G(h.notdone)[b];
-          if (lane == 0) GW(h.y)[b] = y;
-          break;
-        }
-        case HEAD_TD7_LOSS:
-        case HEAD_MLP_LOSS: {  // td7.py:231-244, td3.py:169-182
-          const float y = G(h.y)[b];
-          float dmax = 0.f;
-#pragma unroll
-          for (int n = 0; n < 2; ++n) {
-            const float diff = q[n][r] - y;
-            if (h.lap) {
-              const float d = fabsf(diff);
-              const float hub = d < 1.f ? 0.5f * (d * d) : d;
-              if (n == 0) acc0 += hub; else acc1 += hub;
-              const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-              dq[n][r] = (d < 1.f ? d : 1.f) * sg * h.inv_b;
-              dmax = fmaxf(dmax, d);
-            } else {
-              const float e = y - q[n][r];
-              if (n == 0) acc0 += e * e; else acc1 += e * e;
-              dq[n][r] = -e * h.inv_b;
-            }
-          }
-          if (h.lap && lane == 0) GW(h.prio)[b] = (float)pow((double)fmaxf(dmax, 1.f), 0.4);
-          want_dz = true;
-          break;
-        }
-        case HEAD_TD7_POLICY: {  // td7.py:274-275
-          acc0 += q[0][r] + q[1][r];
-          dq[0][r] = dq[1][r] = -0.5f * h.inv_b;
-          want_dz = true;
-          break;
-        }
-        case HEAD_MLP_POLICY: {  // td3.py:191, sac.py:227-229
-          const float mn = fminf(q[0][r], q[1][r]);
-          // torch.minimum backward: ties split the gradient
-          const float gq = -h.inv_b;
-          dq[0][r] = q[0][r] < q[1][r] ? gq : (q[0][r] == q[1][r] ? 0.5f * gq : 0.f);
-          dq[1][r] = q[1][r] < q[0][r] ? gq : (q[0][r] == q[1][r] ? 0.5f * gq : 0.f);
-          if (h.sac) {
-            const float lp = G(h.logpi)[b];
-            acc0 += -mn + lp * expf(G(h.log_alpha)[0]);
-            acc1 += lp;
-          } else {
-            acc0 += mn;
-          }
-          want_dz = true;
-          break;
-        }
-      }
-    }
-    if (want_dz) {
+    // ---- phase 1: q = h . w + b for both twins (each pass: all loads first)
+    float s[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int kb = 0; kb < h.H; kb += 64 * kHeadU) {
+      float wv[2][kHeadU];
+      float4 hv[2][kHeadU];
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        if (lane == 0 && h.dq[n].t) mat_st4(h.dq[n], r0, 0, make_float4(dq[n][0], dq[n][1], dq[n][2], dq[n][3]));
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int k = lane + 64 * u;
-          if (u < per && k < h.H) {
-            const float4 d = mat_ld4(h.dsrc[n], r0, k);
-            const float w = wv[n][u];
-            mat_st4(h.dz[n], r0, k,
-                    make_float4((dq[n][0] * w) * act_bwd(h.dact, d.x), (dq[n][1] * w) * act_bwd(h.dact, d.y),
-                                (dq[n][2] * w) * act_bwd(h.dact, d.z), (dq[n][3] * w) * act_bwd(h.dact, d.w)));
+        for (int u = 0; u < kHeadU; ++u) {
+          const int k = kb + lane + 64 * u;
+          const int kc = k < h.H ? k : 0;
+          wv[n][u] = G(h.w[n])[tidx(h.w_rbs, 0, kc)];
+          hv[n][u] = mat_ld4(h.h[n], r0, kc);
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+#pragma unroll
+        for (int u = 0; u < kHeadU; ++u) {
+          const float w = (kb + lane + 64 * u < h.H) ? wv[n][u] : 0.f;
+          s[n][0] += hv[n][u].x * w;
+          s[n][1] += hv[n][u].y * w;
+          s[n][2] += hv[n][u].z * w;
+          s[n][3] += hv[n][u].w * w;
+        }
+      }
+    }
+    const float bb[2] = {G(h.b[0])[0], G(h.b[1])[0]};
+    // row scalars (rows r0..r0+3 are valid: rows % 16 == 0)
+    float rw[4], ndn[4], yv[4], lpv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      rw[r] = h.reward ? G(h.reward)[r0 + r] : 0.f;
+      ndn[r] = h.notdone ? G(h.notdone)[r0 + r] : 0.f;
+      yv[r] = (h.mode == HEAD_TD7_LOSS || h.mode == HEAD_MLP_LOSS) ? G(h.y)[r0 + r] : 0.f;
+      lpv[r] = h.sac ? G(h.logpi)[r0 + r] : 0.f;
+    }
+    const float alpha = h.sac ? expf(G(h.log_alpha)[0]) : 0.f;
+    float q[2][4];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) q[n][r] = wave_sum(s[n][r]) + bb[n];
+    }
+    trace_mark(tr, 1);
+    // ---- phase 2: per-row objective (wave-uniform mode)
+    float dq[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    bool want_dz = false;
+    if (h.mode == HEAD_TD7_TARGET) {  // td7.py:211-218
+      const float vtmax = G(h.vt)[0], vtmin = G(h.vt)[1];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = fminf(q[0][r], q[1][r]);
+        v = fminf(fmaxf(v, vtmin), vtmax);
+        const float y = rw[r] + (h.gamma * v) * ndn[r];
+        if (lane == 0) GW(h.y)[r0 + r] = y;
+        kmax = max(kmax, fkey(y));
+        kmin = min(kmin, fkey(y));
+      }
+    } else if (h.mode == HEAD_MLP_TARGET) {  // td3.py:160-164, sac.py:188-193
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = fminf(q[0][r], q[1][r]);
+        if (h.sac) v = v - alpha * lpv[r];
+        const float y = rw[r] + (h.gamma * v) * ndn[r];
+        if (lane == 0) GW(h.y)[r0 + r] = y;
+      }
+    } else if (h.mode == HEAD_TD7_LOSS || h.mode == HEAD_MLP_LOSS) {  // td7.py:231-244, td3.py:169-182
+      float pr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float dmax = 0.f;
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const float diff = q[n][r] - yv[r];
+          if (h.lap) {
+            const float d = fabsf(diff);
+            const float hub = d < 1.f ? 0.5f * (d * d) : d;
+            if (n == 0) acc0 += hub; else acc1 += hub;
+            const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+            dq[n][r] = (d < 1.f ? d : 1.f) * sg * h.inv_b;
+            dmax = fmaxf(dmax, d);
+          } else {
+            const float e = yv[r] - q[n][r];
+            if (n == 0) acc0 += e * e; else acc1 += e * e;
+            dq[n][r] = -e * h.inv_b;
+          }
+        }
+        pr[r] = dmax;
+      }
+      if (h.lap && lane < 4) {  // one row per lane: priority = max(|td|, 1)^alpha (lap.py:68)
+        const float dm = lane == 0 ? pr[0] : lane == 1 ? pr[1] : lane == 2 ? pr[2] : pr[3];
+        GW(h.prio)[r0 + lane] = (float)pow((double)fmaxf(dm, 1.f), 0.4);
+      }
+      want_dz = true;
+    } else if (h.mode == HEAD_TD7_POLICY) {  // td7.py:274-275
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc0 += q[0][r] + q[1][r];
+        dq[0][r] = dq[1][r] = -0.5f * h.inv_b;
+      }
+      want_dz = true;
+    } else {  // HEAD_MLP_POLICY: td3.py:191, sac.py:227-229
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float mn = fminf(q[0][r], q[1][r]);
+        // torch.minimum backward: ties split the gradient
+        const float gq = -h.inv_b;
+        dq[0][r] = q[0][r] < q[1][r] ? gq : (q[0][r] == q[1][r] ? 0.5f * gq : 0.f);
+        dq[1][r] = q[1][r] < q[0][r] ? gq : (q[0][r] == q[1][r] ? 0.5f * gq : 0.f);
+        if (h.sac) {
+          acc0 += -mn + lpv[r] * alpha;
+          acc1 += lpv[r];
+        } else {
+          acc0 += mn;
+        }
+      }
+      want_dz = true;
+    }
+    trace_mark(tr, 2);
+    // ---- phase 3: dq and dz = dq * w * act'(dsrc) (each pass: all loads first)
+    if (want_dz) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        if (lane == 0 && h.dq[n].t) mat_st4(h.dq[n], r0, 0, make_float4(dq[n][0], dq[n][1], dq[n][2], dq[n][3]));
+      for (int kb = 0; kb < h.H; kb += 64 * kHeadU) {
+        float wv[2][kHeadU];
+        float4 dv[2][kHeadU];
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+#pragma unroll
+          for (int u = 0; u < kHeadU; ++u) {
+            const int k = kb + lane + 64 * u;
+            const int kc = k < h.H ? k : 0;
+            wv[n][u] = G(h.w[n])[tidx(h.w_rbs, 0, kc)];
+            dv[n][u] = mat_ld4(h.dsrc[n], r0, kc);
+          }
+        }
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+#pragma unroll
+          for (int u = 0; u < kHeadU; ++u) {
+            const int k = kb + lane + 64 * u;
+            if (k < h.H) {
+              const float4 d = dv[n][u];
+              const float w = wv[n][u];
+              mat_st4(h.dz[n], r0, k,
+                      make_float4((dq[n][0] * w) * act_bwd(h.dact, d.x), (dq[n][1] * w) * act_bwd(h.dact, d.y),
+                                  (dq[n][2] * w) * act_bwd(h.dact, d.z), (dq[n][3] * w) * act_bwd(h.dact, d.w)));
+            }
           }
         }
       }
@@ -843,8 +919,13 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
       float pv[16];
       double tl = 0.0;
 #pragma unroll
+      for (int q = 0; q < 16; ++q) {  // unconditional (clamped) loads: one round trip for all 16
+        const long long e = e0 + q < size ? e0 + q : size - 1;
+        pv[q] = G(s.priority)[e];
+      }
+#pragma unroll
       for (int q = 0; q < 16; ++q) {
-        pv[q] = (e0 + q < size) ? G(s.priority)[e0 + q] : 0.f;
+        if (e0 + q >= size) pv[q] = 0.f;
         tl += (double)pv[q];
       }
       __syncthreads();
@@ -869,12 +950,26 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
   // gather the transition into the batch images (rows b and B + b of ss)
   const GAS float* st = G(s.state) + (size_t)ind * s.Sp;
   const GAS float* nst = G(s.next_state) + (size_t)ind * s.Sp;
-  for (int k = tid; k < s.Sp; k += kThreads) {
-    mat_st(s.ss, b, k, st[k]);
-    mat_st(s.ss, s.B + b, k, nst[k]);
+  constexpr int kGatherU = 4;  // Sp <= 1024
+  float sv[kGatherU], nv[kGatherU];
+#pragma unroll
+  for (int u = 0; u < kGatherU; ++u) {  // all loads first (clamped), then the image stores
+    const int k = tid + u * kThreads;
+    const int kc = k < s.Sp ? k : 0;
+    sv[u] = st[kc];
+    nv[u] = nst[kc];
   }
   const GAS float* ac = G(s.action) + (size_t)ind * s.Ap;
-  for (int k = tid; k < s.Ap; k += kThreads) mat_st(s.a, b, k, ac[k]);
+  const float av = ac[tid < s.Ap ? tid : 0];
+#pragma unroll
+  for (int u = 0; u < kGatherU; ++u) {
+    const int k = tid + u * kThreads;
+    if (k < s.Sp) {
+      mat_st(s.ss, b, k, sv[u]);
+      mat_st(s.ss, s.B + b, k, nv[u]);
+    }
+  }
+  if (tid < s.Ap) mat_st(s.a, b, tid, av);
   if (tid == 0) {
     GW(s.r)[b] = G(s.reward)[ind];
     GW(s.nd)[b] = G(s.notdone)[ind];
@@ -883,22 +978,43 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
 }
 
 // LAPReplayMemory.update_priority (lap.py:66-69): last duplicate wins (Q9).
+// Duplicates are resolved with an LDS hash table (open addressing, 2048 slots,
+// load factor <= 1/2): slot value = largest batch position holding that index.
 __device__ __forceinline__ void op_priority(const CAS PriorityArgs& a, float* smem) {
-  long long* sind = reinterpret_cast<long long*>(smem);
-  float* red = smem + 2 * 1024;
-  for (int b = threadIdx.x; b < a.B; b += kThreads) sind[b] = G(a.ind)[b];
+  constexpr int kSlots = 2048;
+  int* keys = reinterpret_cast<int*>(smem);
+  int* last = keys + kSlots;
+  float* red = smem + 2 * kSlots;
+  for (int i = threadIdx.x; i < kSlots; i += kThreads) {
+    keys[i] = -1;
+    last[i] = -1;
+  }
+  __syncthreads();
+  auto slot0 = [](int key) { return (int)(((unsigned)key * 2654435761u) >> 21); };  // 11 bits
+  int mine[4], myslot[4];
+  const int per = (a.B + kThreads - 1) / kThreads;  // B <= 1024
+  for (int u = 0; u < per; ++u) {
+    const int b = threadIdx.x + u * kThreads;
+    mine[u & 3] = -1;
+    if (b >= a.B) continue;
+    const int key = (int)G(a.ind)[b];
+    int h = slot0(key);
+    while (true) {
+      const int old = atomicCAS(&keys[h], -1, key);
+      if (old == -1 || old == key) break;
+      h = (h + 1) & (kSlots - 1);
+    }
+    atomicMax(&last[h], b);
+    mine[u & 3] = key;
+    myslot[u & 3] = h;
+  }
   __syncthreads();
   float mx = -INFINITY;
-  for (int b = threadIdx.x; b < a.B; b += kThreads) {
-    const long long me = sind[b];
-    bool last = true;
-    for (int c = b + 1; c < a.B; ++c)
-      if (sind[c] == me) {
-        last = false;
-        break;
-      }
+  for (int u = 0; u < per; ++u) {
+    const int b = threadIdx.x + u * kThreads;
+    if (b >= a.B) continue;
     const float pv = G(a.p)[b];
-    if (last) GW(a.priority)[me] = pv;
+    if (last[myslot[u & 3]] == b) GW(a.priority)[mine[u & 3]] = pv;
     mx = fmaxf(mx, pv);
   }
 #pragma unroll
@@ -968,33 +1084,69 @@ __device__ __forceinline__ void op_sac_actor_bwd(const CAS SacActorArgs& s, int 
 
 // ---------------------------------------------------------------- step end
 
-// Deterministic workgroup sum of p[i*stride], i < n (fixed strided + tree order).
-__device__ float block_sum(const float* p, int n, int stride, float* red) {
-  const GAS float* q = G(p);
-  float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += kThreads) s += q[(size_t)i * stride];
-  return wg_sum(s, red);
-}
-
+// All partial-sum reductions of the step end in one pass: every thread loads its
+// elements of every sum (independent loads, one memory round trip), parks its
+// per-sum partials in LDS, then wave w reduces sums w, w+4, ... (fixed order).
 __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* smem) {
-  float* red = smem;
-  float* vals = smem + 8;
+  constexpr int kSums = kInfoMax + 1 + 9;  // info sums, logpi, grad-norm tensors
+  float* th = smem;                        // [kSums][kThreads]
+  float* res = smem + kSums * kThreads;    // [kSums]
+  float* vals = res + kSums;               // [kInfoMax]
   const float nanv = __int_as_float(0x7FC00000);
-  const float slp = a.logpi_part ? block_sum(a.logpi_part + 1, a.nlogpi, 4, red) : 0.f;
-  for (int k = 0; k < a.ninfo; ++k) {
-    float v = 0.f;
-    if (a.kind[k] == INFO_SUM || a.kind[k] == INFO_SAC_POL) {
-      v = block_sum(a.part[k], a.npart[k], a.stride[k], red);
-    } else if (a.kind[k] == INFO_GNORM) {
-      // per-tensor sum of squares -> sqrt -> sum (rl/nn/utils.py:13-19)
-      for (int q = 0; q < a.ngsq_t; ++q) {
-        const float ss = block_sum(a.gsq + a.gsq_off[q], a.gsq_off[q + 1] - a.gsq_off[q], 1, red);
-        v += sqrtf(ss);
+  const int tid = threadIdx.x;
+  // sum list: j < ninfo -> info k (if summed); kInfoMax -> logpi; kInfoMax+1+q -> gsq tensor q
+  auto sum_src = [&](int j, const float*& p, int& n, int& stride) {
+    p = nullptr;
+    n = 0;
+    stride = 1;
+    if (j < kInfoMax) {
+      if (j < a.ninfo && (a.kind[j] == INFO_SUM || a.kind[j] == INFO_SAC_POL)) {
+        p = a.part[j];
+        n = a.npart[j];
+        stride = a.stride[j];
+      }
+    } else if (j == kInfoMax) {
+      if (a.logpi_part) {
+        p = a.logpi_part + 1;
+        n = a.nlogpi;
+        stride = 4;
+      }
+    } else {
+      const int q = j - kInfoMax - 1;
+      if (a.gsq && q < a.ngsq_t) {
+        p = a.gsq + a.gsq_off[q];
+        n = a.gsq_off[q + 1] - a.gsq_off[q];
       }
     }
-    if (threadIdx.x == 0) vals[k] = v;
+  };
+  for (int j = 0; j < kSums; ++j) {
+    const float* p;
+    int n, stride;
+    sum_src(j, p, n, stride);
+    float v = 0.f;
+    for (int i = tid; i < n; i += kThreads) v += G(p)[(size_t)i * stride];
+    th[j * kThreads + tid] = v;
   }
-  if (threadIdx.x != 0) return;
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int j = wave; j < kSums; j += 4) {
+    const float* r = th + j * kThreads;
+    float v = (r[lane] + r[lane + 64]) + (r[lane + 128] + r[lane + 192]);
+    v = wave_sum(v);
+    if (lane == 0) res[j] = v;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  const float slp = res[kInfoMax];
+  for (int k = 0; k < a.ninfo; ++k) {
+    float v = res[k];
+    if (a.kind[k] == INFO_GNORM) {
+      // per-tensor sum of squares -> sqrt -> sum (rl/nn/utils.py:13-19)
+      v = 0.f;
+      for (int q = 0; q < a.ngsq_t; ++q) v += sqrtf(res[kInfoMax + 1 + q]);
+    }
+    vals[k] = v;
+  }
   const float la = a.log_alpha ? G(a.log_alpha)[0] : 0.f;
   const float alpha = expf(la);
   // mean_b(-lp_b - target_entropy); d/dla mean(exp(la) * c) = exp(la) * mean(c)
@@ -1087,6 +1239,8 @@ __device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
 
 __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
   __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
+  unsigned long long* tr = la.trace ? la.trace + (size_t)blockIdx.x * 4 : nullptr;
+  trace_mark(tr, 0);
   const CAS Op* ops = (const CAS Op*)la.ops;
   const int wg = blockIdx.x;
   // op of this workgroup: from the kernel-argument table (SGPRs, no dependent
@@ -1103,11 +1257,16 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
   const CAS Op& op = ops[k];
   const int t = wg - (la.nops <= kLevelOps ? la.wg_begin[k] : op.wg_begin);
   switch (kind) {
-    case OP_GEMM: op_gemm(op.gemm, t, smem); break;
+    case OP_GEMM: op_gemm(op.gemm, t, smem, tr); break;
+#ifndef RLE_EXP_GEMM_ONLY
     case OP_NORMBWD: op_normbwd(op.nb, t); break;
     case OP_SAMPLE_REDUCE: op_sample_reduce(op.sample, t, smem); break;
     case OP_SAMPLE_GATHER: op_sample_gather(op.sample, t, smem); break;
-    case OP_HEAD: op_head(op.head, t, smem); break;
+    case OP_HEAD:
+      asm volatile("; op head begin" ::);
+      op_head(op.head, t, smem, tr);
+      asm volatile("; op head end" ::);
+      break;
     case OP_PRIORITY: op_priority(op.prio, smem); break;
     case OP_SAC_ACTOR: op_sac_actor(op.sac, t); break;
     case OP_SAC_ACTOR_BWD: op_sac_actor_bwd(op.sac, t); break;
@@ -1116,8 +1275,10 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
     case OP_COPY: op_copy(op.flat, t); break;
     case OP_MAXRED: op_maxred(op.flat, t, smem); break;
     case OP_CTRL: op_ctrl(op.ctrl); break;
+#endif
     default: break;
   }
+  trace_mark(tr, 3);
 }
 
 // ---------------------------------------------------------------- standalone kernels
@@ -1168,9 +1329,20 @@ __global__ void rle_fill_kernel(float* state, float* next_state, float* action, 
 
 // ---------------------------------------------------------------- host launchers
 
-hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st) {
+// Workgroups of rle_level resident at once on the current device.
+int level_capacity() {
+  int per_cu = 0, cus = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level, kThreads, 0) != hipSuccess) return 1024;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
+  return per_cu * cus;
+}
+
+hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
+                        unsigned long long* trace) {
   LevelArgs la{};
   la.ops = d_ops;
+  la.trace = trace;
   la.nops = nops;
   for (int q = 0; q < nops && q < kLevelOps; ++q) {
     la.wg_begin[q] = h_ops[q].wg_begin;

@@ -9,7 +9,7 @@ namespace rle {
 
 constexpr int kThreads = 256;   // 4 waves per workgroup, every op kind
 constexpr int kTileM = 16;      // GEMM output tile rows (v_mfma_f32_16x16x4_f32)
-constexpr int kTileN = 64;      // GEMM output tile cols (4 waves x 16)
+constexpr int kTileN = 64;      // widest GEMM output tile (GemmArgs::tn in {16, 32, 64})
 constexpr int kMaxSeg = 4;
 constexpr int kInfoMax = 8;     // floats per step in the info ring
 
@@ -90,10 +90,15 @@ struct AdamArgs {
   long long mo, vo;      // element offsets of m / v arrays relative to params (m, v kept at T-image offsets)
   const long long* t;    // completed optimizer steps (device counter)
   float lr, beta1, beta2, eps;
-  int bias_col;          // first column of the bias tile = K rounded up to kTileN
+  int bias_col;          // first column of the bias tile = K rounded up to the tile width tn
   float* gsq;            // optional: per-tile sum of squared grads (weights), [tiles]
   float* gsq_b;          // optional: per-tile sum of squared grads (bias), [tiles_m]
 };
+
+// Variant id of a GEMM op = mode * 32 + epi * 8 + act * 2 + norm (act: the forward
+// activation for GEMM_FWD, the derivative mask for GEMM_DX; norm: some operand
+// segment carries a deferred AvgL1Norm).
+constexpr int gemm_vid(int mode, int epi, int act, int norm) { return mode * 32 + epi * 8 + act * 2 + norm; }
 
 enum GemmMode : int {
   GEMM_FWD = 0,   // A contiguous (activations), B contiguous (W rows):  Y = X W^T
@@ -104,7 +109,12 @@ enum GemmMode : int {
 struct GemmArgs {
   int mode;              // GemmMode (operand layouts; every segment of an operand shares it)
   int M, N, R;           // output rows, output cols (x-extent of B), reduction length
-  int tiles_m, tiles_n;  // tiles_n includes the extra bias tile column for EPI_ADAM
+  int tn;                // tile width: 16 x tn output tile; the 4 waves are tn/16 column groups
+                         // x 64/tn reduction splits (partials summed through LDS, fixed order)
+  int tiles_m, tiles_n;  // tiles_n = cdiv(N, tn), + 1 bias tile column for EPI_ADAM
+  int vid;               // compiled variant (host: gemm_variant): mode, epilogue, activation, norm
+  int ks_log;            // log2(64 / tn): reduction splits per tile
+  float inv_tiles_n;     // 1 / tiles_n (tile row = floor((t + 0.5) * inv_tiles_n))
   int epi;
   int act;               // forward activation (EPI_STORE)
   Operand A, B;
@@ -245,7 +255,7 @@ struct Op {
   int kind;
   int wg_begin;     // first workgroup of this op within its level launch
   int wg_count;
-  int pad_;
+  int seq;          // host: GEMM creation index (tile-width plan), unused on the device
   union {
     GemmArgs gemm;
     NormBwdArgs nb;
@@ -264,6 +274,7 @@ struct Op {
 constexpr int kLevelOps = 24;
 struct LevelArgs {
   const Op* ops;
+  unsigned long long* trace;  // optional phase timestamps [wg][4] (s_memrealtime, 100 MHz)
   int nops;
   int wg_begin[kLevelOps];
   unsigned char kind[kLevelOps];

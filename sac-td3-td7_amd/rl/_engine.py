@@ -75,6 +75,7 @@ SIGNATURES = {
     "rle_act": (_int, [_vp, _f32p, _int, _f32p]),
     "rle_graph_stats": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "rle_graph_describe": (_int, [_vp, _int, ctypes.c_char_p, _int]),
+    "rle_graph_trace": (_int, [_vp, _int, ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)]),
     "rle_copy_state": (_int, [_vp, _vp]),
     "rle_synchronize": (_int, [_vp]),
 }
@@ -297,6 +298,16 @@ class Engine:
         buf = ctypes.create_string_buffer(1 << 16)
         _check(lib().rle_graph_describe(self.h, which, buf, len(buf)))
         return buf.value.decode()
+
+    def trace(self, which=0):
+        """Per-workgroup phase timestamps of the last replay of graph `which` (RLE_TRACE=1)."""
+        n = ctypes.c_longlong()
+        _check(lib().rle_graph_trace(self.h, which, None, 0, ctypes.byref(n)))
+        if n.value == 0:
+            return np.zeros((0, 4), np.uint64)
+        out = np.zeros((n.value, 4), np.uint64)
+        _check(lib().rle_graph_trace(self.h, which, out.ctypes.data, out.size, ctypes.byref(n)))
+        return out
 
     def copy_state_from(self, other: "Engine"):
         _check(lib().rle_copy_state(self.h, other.h))

@@ -11,7 +11,8 @@
 #include "ops.h"
 
 namespace rle {
-hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st);
+hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
+                        unsigned long long* trace = nullptr);
 }
 using namespace rle;
 
@@ -41,7 +42,11 @@ static Op fwd_op(float* X, float* W, float* b, float* Y, int M, int N, int K) {
   g.A.seg[0].p = X; g.A.seg[0].xs = K / 16; g.A.seg[0].x0 = 0; g.A.seg[0].x1 = M; g.A.seg[0].r0 = 0; g.A.seg[0].r1 = K;
   g.B.nseg = 1;
   g.B.seg[0].p = W; g.B.seg[0].xs = K / 16; g.B.seg[0].x0 = 0; g.B.seg[0].x1 = N; g.B.seg[0].r0 = 0; g.B.seg[0].r1 = K;
-  g.tiles_m = (M + kTileM - 1) / kTileM; g.tiles_n = (N + kTileN - 1) / kTileN;
+  g.tn = 16;
+  g.tiles_m = (M + kTileM - 1) / kTileM; g.tiles_n = (N + g.tn - 1) / g.tn;
+  g.vid = gemm_vid(GEMM_FWD, EPI_STORE, ACT_RELU, 0);
+  g.ks_log = 2;
+  g.inv_tiles_n = 1.f / (float)g.tiles_n;
   g.epi = EPI_STORE; g.act = ACT_RELU; g.bias = b;
   g.out.t = Y; g.out.rbs = M / 16; g.out.cbn = N / 16;
   op.wg_count = g.tiles_m * g.tiles_n;
@@ -55,6 +60,8 @@ static size_t tidx(int rbs, int r, int c) {
   return ((size_t)(c >> 4) * rbs + (r >> 4)) * 256 + ((r >> 2) & 3) * 64 + (c & 15) * 4 + (r & 3);
 }
 
+static unsigned long long* g_trace = nullptr;  // [wg][4] phase stamps of the last rep
+
 static double time_level(std::vector<Op> ops, int reps, hipStream_t st) {
   int wg = 0;
   for (auto& o : ops) { o.wg_begin = wg; wg += o.wg_count; }
@@ -64,7 +71,7 @@ static double time_level(std::vector<Op> ops, int reps, hipStream_t st) {
   // capture reps launches in a graph, like the engine
   hipGraph_t g; hipGraphExec_t x;
   CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-  for (int i = 0; i < reps; ++i) CK(launch_level(d, ops.data(), (int)ops.size(), wg, st));
+  for (int i = 0; i < reps; ++i) CK(launch_level(d, ops.data(), (int)ops.size(), wg, st, g_trace));
   CK(hipStreamEndCapture(st, &g));
   CK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
   CK(hipGraphLaunch(x, st));
@@ -80,6 +87,28 @@ static double time_level(std::vector<Op> ops, int reps, hipStream_t st) {
   CK(hipGraphExecDestroy(x)); CK(hipGraphDestroy(g)); CK(hipFree(d));
   return ms * 1000.0 / reps;
 }
+
+// entry-relative phase medians of the last traced level: prologue, loop, epilogue, total
+static void phases(const char* name, int nwg) {
+  std::vector<unsigned long long> t((size_t)nwg * 4);
+  CK(hipMemcpy(t.data(), g_trace, t.size() * 8, hipMemcpyDeviceToHost));
+  unsigned long long t0 = ~0ull, t3 = 0;
+  std::vector<double> pro, loop, epi;
+  for (int w = 0; w < nwg; ++w) {
+    t0 = std::min(t0, t[w * 4]);
+    t3 = std::max(t3, t[w * 4 + 3]);
+    pro.push_back((t[w * 4 + 1] - t[w * 4]) * 0.01);
+    loop.push_back((t[w * 4 + 2] - t[w * 4 + 1]) * 0.01);
+    epi.push_back((t[w * 4 + 3] - t[w * 4 + 2]) * 0.01);
+  }
+  auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+  printf("   %-28s span %6.2f us | pro %5.2f loop %5.2f epi %5.2f\n", name, (t3 - t0) * 0.01, med(pro), med(loop),
+         med(epi));
+}
+
+#ifdef RLE_TRACE_FINE
+namespace rle { extern __device__ unsigned long long* g_fine; }
+#endif
 
 int main() {
   hipStream_t st;
@@ -130,6 +159,46 @@ int main() {
     Op o = fwd_op(X, W, bb, Y, 16, 64, Kk);
     printf("fwd 16x64xK=%4d (1 WG)   : %8.2f us\n", Kk, time_level({o}, reps, st));
   }
+  CK(hipMalloc(&g_trace, 8 * 4 * 4096));
+  for (int Kk : {16, 256, 1024}) {
+    Op o = fwd_op(X, W, bb, Y, 256, N, Kk);
+    time_level({o}, 20, st);
+    char nm[64];
+    snprintf(nm, sizeof nm, "traced fwd 256x256xK=%d", Kk);
+    phases(nm, o.wg_count);
+  }
+  {
+    Op e{}; e.kind = 0; e.wg_count = 256;
+    time_level({e}, 20, st);
+    std::vector<unsigned long long> t(256 * 4);
+    CK(hipMemcpy(t.data(), g_trace, t.size() * 8, hipMemcpyDeviceToHost));
+    unsigned long long a = ~0ull, b = 0;
+    for (int w = 0; w < 256; ++w) { a = std::min(a, t[w * 4]); b = std::max(b, t[w * 4 + 3]); }
+    printf("   traced empty 256 WG span %6.2f us\n", (b - a) * 0.01);
+  }
+  CK(hipFree(g_trace));
+  g_trace = nullptr;
+#ifdef RLE_TRACE_FINE
+  {
+    unsigned long long* fine;
+    CK(hipMalloc(&fine, 8 * 8 * 4096));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(rle::g_fine), &fine, 8));
+    CK(hipMalloc(&g_trace, 8 * 4 * 4096));
+    for (int Kk : {16, 256}) {
+      Op o = fwd_op(X, W, bb, Y, 16, 64, Kk);
+      time_level({o}, 20, st);
+      unsigned long long t[4], f[8];
+      CK(hipMemcpy(t, g_trace, 32, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(f, fine, 64, hipMemcpyDeviceToHost));
+      printf("fine 1WG K=%d: entry->mark1 %.2f | ->lane_op %.2f ->seek %.2f ->issue %.2f ->loop end %.2f ->ret %.2f "
+             "->splitK %.2f ->exit %.2f us\n", Kk, (t[1] - t[0]) * 0.01, (f[0] - t[1]) * 0.01, (f[1] - f[0]) * 0.01,
+             (f[2] - f[1]) * 0.01, (f[3] - f[2]) * 0.01, (f[4] - f[3]) * 0.01, (f[5] - f[4]) * 0.01,
+             (t[3] - f[5]) * 0.01);
+    }
+    CK(hipFree(g_trace));
+    g_trace = nullptr;
+  }
+#endif
   for (int M : {256, 512}) {
     Op o = fwd_op(X, W, bb, Y, M, N, K);
     printf("fwd %dx%dx%d (%d WG): %8.2f us\n", M, N, K, o.wg_count, time_level({o}, reps, st));

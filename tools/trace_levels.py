@@ -1,0 +1,50 @@
+"""Per-level phase timing of the TD7 Humanoid step from in-kernel timestamps (GPU box).
+
+RLE_TRACE=1 python tools/trace_levels.py [steps]
+Phases per workgroup (s_memrealtime, 10 ns ticks): dispatch delay (entry - level's first
+entry), prologue (entry -> main loop), main loop, epilogue (-> exit); the level span is
+first entry -> last exit.
+"""
+import os
+import sys
+
+import numpy as np
+
+os.environ.setdefault("RLE_TRACE", "1")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd")]
+from rl import _engine as E  # noqa: E402
+from rl.nn.layout import init_agent  # noqa: E402
+
+S, A, H, B = 376, 17, 256, 256
+eng = E.Engine(E.make_config(E.RLE_TD7, S, A, H, B, use_lap=True))
+for net, params in init_agent("td7", S, A, H, 1).items():
+    for k, v in params.items():
+        eng.set_param(net, k, v)
+rep = E.Replay(1000000, S, A, True)
+rep.fill_random(1000000, 1)
+eng.bind(rep)
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+eng.step_timed(steps)
+for which in (0, 1):
+    tr = eng.trace(which).astype(np.int64)
+    desc = [l for l in eng.describe(which).splitlines() if l.startswith("L")]
+    print(f"=== graph {which}")
+    off = 0
+    prev_end = None
+    for line in desc:
+        nwg = int(line.split("wg=")[1].split(":")[0])
+        t = tr[off:off + nwg]
+        off += nwg
+        t0 = t[:, 0].min()
+        span = (t[:, 3].max() - t0) * 10 / 1000
+        gap = (t0 - prev_end) * 10 / 1000 if prev_end is not None else 0.0
+        prev_end = t[:, 3].max()
+        disp = (t[:, 0] - t0) * 10 / 1000
+        g = t[:, 1] > 0
+        pro = ((t[g, 1] - t[g, 0]) * 10 / 1000) if g.any() else np.zeros(1)
+        loop = ((t[g, 2] - t[g, 1]) * 10 / 1000) if g.any() else np.zeros(1)
+        epi = ((t[g, 3] - t[g, 2]) * 10 / 1000) if g.any() else np.zeros(1)
+        tot = (t[:, 3] - t[:, 0]) * 10 / 1000
+        print(f"gap {gap:5.2f} span {span:6.2f} | disp max {disp.max():5.2f} | wg med {np.median(tot):5.2f} max {tot.max():5.2f}"
+              f" | pro {np.median(pro):5.2f} loop {np.median(loop):5.2f} epi {np.median(epi):5.2f} | {line[:90]}")
