@@ -289,6 +289,7 @@ enum Res : int {
   R_PRIO,
   R_MAXP,
   R_REPLAY,
+  R_ADAMSC,  // Ctrl::adam_step / adam_bc2s (Adam bias corrections of this step)
   R_FIRST_DYNAMIC = 100,
 };
 
@@ -569,7 +570,7 @@ struct Engine {
     View out = buf(M, L.out);
     wr.push_back(out.id);
     if (pre_out) {
-      *pre_out = buf(M, L.out, false, true);
+      *pre_out = buf(M, L.out);  // T: DX epilogue masks; N: head rows
       wr.push_back(pre_out->id);
     }
     float* part = nullptr;
@@ -724,7 +725,7 @@ struct Engine {
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
     g.mode = GEMM_DW;
-    std::vector<int> rd{dz.id, L.res, R_CNT}, wr{L.res};
+    std::vector<int> rd{dz.id, L.res, R_ADAMSC}, wr{L.res};
     g.A.seg[0] = seg_t(dz, 0, 0, Brows);
     g.A.nseg = 1;
     int koff = 0;
@@ -751,10 +752,13 @@ struct Engine {
     ad.b = bias(L);
     ad.mo = (long long)nP;
     ad.vo = 2LL * (long long)nP;
-    ad.t = &ctrl->counters[cnt];
+    ad.step = &ctrl->adam_step[cnt];
+    ad.bc2s = &ctrl->adam_bc2s[cnt];
     ad.lr = lr;
     ad.beta1 = 0.9f;
     ad.beta2 = 0.999f;
+    ad.omb1 = (float)(1.0 - 0.9);
+    ad.omb2 = (float)(1.0 - 0.999);
     ad.eps = 1e-8f;
     ad.bias_col = cdiv(L.K, g.tn) * g.tn;
     ad.gsq = gsq;
@@ -765,7 +769,7 @@ struct Engine {
 
   View normbwd(Prog& pg, const View& gv, const View& x) {
     REQUIRE(x.norm, "normbwd: x is not a normed view");
-    REQUIRE(gv.m.t && x.m.t && gv.rows % 16 == 0, "normbwd: operand layout");
+    REQUIRE(gv.m.n && x.m.n && gv.rows % 16 == 0, "normbwd: operand layout");
     Op op{};
     op.kind = OP_NORMBWD;
     NormBwdArgs& a = op.nb;
@@ -776,7 +780,7 @@ struct Engine {
     a.rows = gv.rows;
     a.width = x.width;
     a.norm = x.nref();
-    op.wg_count = cdiv(gv.rows, 16);
+    op.wg_count = cdiv(gv.rows, 4);
     pg.add(op, {gv.id, x.id, x.norm_id}, {out.id});
     return out;
   }
@@ -838,6 +842,7 @@ struct Engine {
     s.A = A;
     s.Ap = Ap;
     s.size = rp.size_d;
+    s.cap = rp.cap;
     s.lap = rp.lap;
     s.B = B;
     s.bsum = rp.bsum;
@@ -869,17 +874,17 @@ struct Engine {
     h.H = H;
     h.gamma = cfg.discount;
     h.inv_b = 1.f / (float)B;
-    op.wg_count = cdiv(rows, 16);
+    op.wg_count = cdiv(rows, 4);
     return op;
   }
 
   void set_head_twin(HeadArgs& h, const View& h1, const View& h2, const Layer& l1, const Layer& l2) {
-    REQUIRE(h1.m.t && h2.m.t && l1.out == 1 && l2.out == 1, "head: operand layout");
+    REQUIRE(h1.m.n && h2.m.n && l1.out == 1 && l2.out == 1, "head: operand layout");
     h.h[0] = h1.m;
     h.h[1] = h2.m;
-    h.w[0] = P + l1.wt_off;
-    h.w[1] = P + l2.wt_off;
-    h.w_rbs = l1.rb;
+    h.w[0] = P + l1.wn_off;
+    h.w[1] = P + l2.wn_off;
+    h.w_cbn = l1.cb;
     h.b[0] = bias(l1);
     h.b[1] = bias(l2);
   }
@@ -927,6 +932,7 @@ struct Engine {
     Net* q[2] = {&net("q1"), &net("q2")};
     Net* tq[2] = {&net("target_q1"), &net("target_q2")};
     const bool lap = cfg.use_lap;
+    add_adam_scalars(pg);
     add_sampling(pg, false);
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
     // ---- encoder phase (td7.py:246-257): online encoder on [s; s'] (one GEMM per layer)
@@ -1043,7 +1049,7 @@ struct Engine {
     }
     View dz2[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
     View prio = vec(B);
-    const int hw = cdiv(B, 16);
+    const int hw = cdiv(B, 4);
     qloss_part = mem.make<float>((size_t)hw * 4);
     {
       Op op = head_op(HEAD_TD7_LOSS, B);
@@ -1164,6 +1170,7 @@ struct Engine {
     flat(pg, OP_COPY, net("fixed_encoder"), &net("encoder"), 0.f, false);
     Op c{};
     c.kind = OP_CTRL;
+    c.ctrl.mode = 0;
     c.ctrl.vmax_key = &ctrl->vmax_key;
     c.ctrl.vmin_key = &ctrl->vmin_key;
     c.ctrl.vt = ctrl->vt;
@@ -1205,6 +1212,7 @@ struct Engine {
     Net* q[2] = {&net("q1"), &net("q2")};
     Net* tq[2] = {&net("target_q1"), &net("target_q2")};
     const bool lap = cfg.use_lap && !sac;
+    add_adam_scalars(pg);
     add_sampling(pg, sac);
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
     // actor on [s; s'] (target policy aliases the policy, Q1; SAC policy unchanged until its step)
@@ -1262,7 +1270,7 @@ struct Engine {
     for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c0[n], c1[n]);
     View dz1[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
     View prio = vec(B);
-    const int hw = cdiv(B, 16);
+    const int hw = cdiv(B, 4);
     qloss_part = mem.make<float>((size_t)hw * 4);
     {
       Op op = head_op(HEAD_MLP_LOSS, B);
@@ -1596,6 +1604,44 @@ struct Engine {
     built = true;
   }
 
+  // Adam bias-correction scalars of this step from the completed-step counters; the
+  // op has no producers, so it runs in level 0 beside the LAP block sums.
+  void add_adam_scalars(Prog& pg) { pg.add(adam_scalars_op(), {R_CNT}, {R_ADAMSC}); }
+  Op adam_scalars_op() {
+    Op op{};
+    op.kind = OP_CTRL;
+    op.wg_count = 1;
+    CtrlArgs& c = op.ctrl;
+    c.mode = 1;
+    c.counters = ctrl->counters;
+    c.adam_step = ctrl->adam_step;
+    c.adam_bc2s = ctrl->adam_bc2s;
+    c.adam_lr[CNT_ADAM_Q] = cfg.critic_lr;
+    c.adam_lr[CNT_ADAM_PI] = cfg.policy_lr;
+    c.adam_lr[CNT_ADAM_ENC] = cfg.policy_lr;
+    return op;
+  }
+
+  // The same computed eagerly (creation / counters set), for readers outside a step.
+  void refresh_adam_scalars() {
+    Op op{};
+    op.kind = OP_CTRL;
+    op.wg_count = 1;
+    CtrlArgs& c = op.ctrl;
+    c.mode = 1;
+    c.counters = ctrl->counters;
+    c.adam_step = ctrl->adam_step;
+    c.adam_bc2s = ctrl->adam_bc2s;
+    c.adam_lr[CNT_ADAM_Q] = cfg.critic_lr;
+    c.adam_lr[CNT_ADAM_PI] = cfg.policy_lr;
+    c.adam_lr[CNT_ADAM_ENC] = cfg.policy_lr;
+    if (!ctrl_op) ctrl_op = mem.make<Op>(1);
+    HIPCHK(hipMemcpyAsync(ctrl_op, &op, sizeof(Op), hipMemcpyHostToDevice, stream));
+    HIPCHK(launch_level(ctrl_op, &op, 1, 1, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+  Op* ctrl_op = nullptr;
+
   // ---------------------------------------------------------------- run
   void step(int n, float* info_out, float* gpu_ms = nullptr) {
     REQUIRE(replay, "no replay bound");
@@ -1850,6 +1896,7 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     s.A = r.A;
     s.Ap = r.Ap;
     s.size = r.size_d;
+    s.cap = r.cap;
     s.lap = r.lap;
     s.B = n;
     s.bsum = r.bsum;
@@ -2013,6 +2060,7 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
     }
     e.info = e.mem.make<float>((size_t)e.info_cap * rle::kInfoMax);
     e.alloc_step_buffers();
+    e.refresh_adam_scalars();
     *out = h.release();
   });
 }
@@ -2090,6 +2138,7 @@ int rle_set_counters(rle_engine* h, const long long* in6) {
     c.la_t = in6[5];
     e.n_runs = in6[3];
     HIPCHK(hipMemcpy(e.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
+    e.refresh_adam_scalars();
   });
 }
 

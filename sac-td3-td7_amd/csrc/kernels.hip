@@ -45,6 +45,12 @@ template <class T>
 __device__ __forceinline__ GAS T* GW(T* p) {
   return (GAS T*)p;
 }
+// Uniform control value written by an earlier launch: scalar load (s_load, issued
+// with the other descriptor loads) instead of a vector load and its round trip.
+template <class T>
+__device__ __forceinline__ T sload(const T* p) {
+  return *(const CAS T*)p;
+}
 
 // ---------------------------------------------------------------- utilities
 
@@ -58,16 +64,44 @@ __device__ __forceinline__ void st4g(GAS float* p, const float4& v) {
   *(GAS f32x4*)p = w;
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Cross-lane reductions through DPP (register-to-register, a few cycles per step)
+// instead of ds_bpermute shuffles (an LDS round trip each).  Fixed order:
+// quad butterflies, row rotations, then row broadcasts into lane 63.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {  // lanes outside ROW_MASK read 0
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
+}
+// Sum over each row of 16 lanes, result in every lane of the row.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xb1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4e>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x124>(v);  // row_ror:4
+  v += dpp_f<0x128>(v);  // row_ror:8
   return v;
 }
-
+__device__ __forceinline__ float wave_sum(float v) {
+  v = row16_sum(v);
+  v += dpp_f<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
 __device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_d<0xb1>(v);
+  v += dpp_d<0x4e>(v);
+  v += dpp_d<0x124>(v);
+  v += dpp_d<0x128>(v);
+  v += dpp_d<0x142, 0xa>(v);
+  v += dpp_d<0x143, 0xc>(v);
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
 // Deterministic per-workgroup sum (tree inside waves, fixed wave order).
@@ -89,8 +123,8 @@ __device__ __forceinline__ int fkey(float f) {
 __device__ __forceinline__ float unkey(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
 
 // Philox4x32-10 counter-based RNG.
-__device__ __forceinline__ uint4 philox(uint2 key, uint4 c) {
-#pragma unroll
+__device__ __attribute__((noinline)) uint4 philox(uint2 key, uint4 c) {
+#pragma unroll 1
   for (int i = 0; i < 10; ++i) {
     unsigned hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
     unsigned hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
@@ -102,15 +136,18 @@ __device__ __forceinline__ uint4 philox(uint2 key, uint4 c) {
 }
 __device__ __forceinline__ float u01(unsigned x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 __device__ __forceinline__ float normal_from(unsigned a, unsigned b) {
-  float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
-  float u2 = (float)(b >> 8) * (1.0f / 16777216.0f);
-  return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+  // Box-Muller on the hardware transcendental units (no range reduction needed:
+  // v_cos_f32 takes revolutions): sqrt(-2 ln u1) * cos(2 pi u2), u1 in (0, 1]
+  const float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  const float u2 = (float)(b >> 8) * (1.0f / 16777216.0f);
+  const float l = __builtin_amdgcn_logf(u1) * -1.3862943611198906f;  // -2 ln u1 = -2 ln2 log2 u1
+  return __builtin_sqrtf(l) * __builtin_amdgcn_cosf(u2);
 }
 
 // AvgL1Norm mean |x| of a row from column-tile partial |x| sums (sequential order);
 // the partials are loaded 16 at a time (clamped, independent) so a row costs one
 // memory round trip per 16 partials.
-__device__ __forceinline__ float norm_mean(const float* part, int ld, int row, int nparts, int width) {
+__device__ __attribute__((noinline)) float norm_mean(const float* part, int ld, int row, int nparts, int width) {
   const GAS float* p = G(part) + row;
   float s = 0.f;
   for (int q0 = 0; q0 < nparts; q0 += 16) {
@@ -175,6 +212,19 @@ __device__ __forceinline__ float mat_ld(const CAS Mat& m, int r, int c) {
 __device__ __forceinline__ void mat_st(const CAS Mat& m, int r, int c, float v) {
   if (m.t) GW(m.t)[tidx(m.rbs, r, c)] = v;
   if (m.n) GW(m.n)[nidx(m.cbn, r, c)] = v;
+}
+// Columns c..c+3 (c % 4 == 0) of row r: one float4 of the N image.
+__device__ __forceinline__ float4 mat_ldr4(const CAS Mat& m, int r, int c) { return ld4g(G(m.n) + nidx(m.cbn, r, c)); }
+// Store columns c..c+3 of row r into every kept image (T: 4 floats 16 B apart).
+__device__ __forceinline__ void mat_str4(const CAS Mat& m, int r, int c, float4 v) {
+  if (m.n) st4g(GW(m.n) + nidx(m.cbn, r, c), v);
+  if (m.t) {
+    GAS float* q = GW(m.t) + tidx(m.rbs, r, c);
+    q[0] = v.x;
+    q[4] = v.y;
+    q[8] = v.z;
+    q[12] = v.w;
+  }
 }
 // Four consecutive rows r..r+3 (r % 4 == 0) of column c: one float4 of the T image.
 __device__ __forceinline__ float4 mat_ld4(const CAS Mat& m, int r, int c) {
@@ -449,10 +499,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     if constexpr (MODE == GEMM_FWD) {
       if (g.norm_out) {  // |y| summed over the tile's tn columns, per row
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-#pragma unroll
-          for (int o = 8; o > 0; o >>= 1) rowabs[q] += __shfl_xor(rowabs[q], o, 64);
-        }
+        for (int q = 0; q < 4; ++q) rowabs[q] = row16_sum(rowabs[q]);
         if ((lane & 15) == 0) *(float4*)(red + wave * 16 + ((lane >> 4) << 2)) =
             make_float4(rowabs[0], rowabs[1], rowabs[2], rowabs[3]);
         __syncthreads();
@@ -481,16 +528,14 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     const CAS AdamArgs& ad = g.adam;
     float gg = 0.f;
     if (jok) {
-      const double tt = (double)(*G(ad.t) + 1);
-      const float step_size = (float)((double)ad.lr / (1.0 - pow((double)ad.beta1, tt)));
-      const float bc2s = (float)sqrt(1.0 - pow((double)ad.beta2, tt));
+      const float step_size = sload(ad.step), bc2s = sload(ad.bc2s);  // this step's (level-0 CTRL op)
       const float p4[4] = {pp.x, pp.y, pp.z, pp.w}, m4[4] = {mm.x, mm.y, mm.z, mm.w}, v4[4] = {vv.x, vv.y, vv.z, vv.w};
       float po[4], mo[4], vo[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float gv = acc[q];
-        const float m = m4[q] + (1.f - ad.beta1) * (gv - m4[q]);
-        const float v2 = v4[q] * ad.beta2 + ((1.f - ad.beta2) * gv) * gv;
+        const float m = m4[q] + ad.omb1 * (gv - m4[q]);
+        const float v2 = v4[q] * ad.beta2 + (ad.omb2 * gv) * gv;
         const float denom = sqrtf(v2) / bc2s + ad.eps;
         const bool ok = ib + q < g.M;  // weight rows past out stay untouched (zero)
         po[q] = ok ? p4[q] + (-step_size * m) / denom : p4[q];
@@ -520,13 +565,13 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   }
 }
 
-__device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
+__device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, float* smem, unsigned long long* tr) {
 #define RLE_V(mode, epi, act, norm)                      \
   case gemm_vid(mode, epi, act, norm):                   \
     asm volatile("; gemm variant " #mode #epi #act #norm ::); \
     gemm_v<mode, epi, act, norm>(g, t, smem, tr);        \
     break;
-  switch (g.vid) {
+  switch (vid) {
     RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, false)
     RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, true)
     RLE_V(GEMM_FWD, EPI_STORE, ACT_RELU, false)
@@ -550,219 +595,150 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int t, float* sme
 
 // ---------------------------------------------------------------- AvgL1Norm backward
 
-// 16 rows per workgroup, 4 per wave: lane k reads a float4 (4 rows) of column k
-// from the T images; the per-row dot products are wave reductions.
+// One row per wave (4 per workgroup): lane l holds columns 4l..4l+3 (+256 per
+// pass) as float4s of the N images; the row dot product is one wave reduction.
 __device__ __forceinline__ void op_normbwd(const CAS NormBwdArgs& a, int t) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r0 = t * 16 + wave * 4;
-  if (r0 >= a.rows) return;
-  float inv[4], gmv[4];
-  bool clamped[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {  // m recomputed exactly as the forward consumers did (norm_m)
-    const float mean = norm_mean(a.norm.part, a.norm.ld, r0 + q + a.norm.row0, a.norm.nparts, a.width);
-    clamped[q] = mean < 1e-8f;
-    inv[q] = 1.f / (clamped[q] ? 1e-8f : mean);
-  }
-  float4 xv[8], gv[8];
-  float dot[4] = {0.f, 0.f, 0.f, 0.f};
-  const int per = (a.width + 63) / 64;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int k = lane + 64 * u;
-    const bool in = u < per && k < a.width;
-    xv[u] = in ? mat_ld4(a.x, r0, k) : make_float4(0.f, 0.f, 0.f, 0.f);
-    gv[u] = in ? mat_ld4(a.g, r0, k) : make_float4(0.f, 0.f, 0.f, 0.f);
-    dot[0] += gv[u].x * xv[u].x;
-    dot[1] += gv[u].y * xv[u].y;
-    dot[2] += gv[u].z * xv[u].z;
-    dot[3] += gv[u].w * xv[u].w;
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    dot[q] = wave_sum(dot[q]);
-    // y = x / m: dy/dx path g/m ; dm path -(sum g x)/m^2 * sign(x)/n (unless clamped)
-    gmv[q] = clamped[q] ? 0.f : (-dot[q] * inv[q] * inv[q]) / (float)a.width;
-  }
-  auto sgn = [](float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); };
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int k = lane + 64 * u;
-    if (u < per && k < a.width) {
-      const float4 o = make_float4(gv[u].x * inv[0] + sgn(xv[u].x) * gmv[0], gv[u].y * inv[1] + sgn(xv[u].y) * gmv[1],
-                                   gv[u].z * inv[2] + sgn(xv[u].z) * gmv[2], gv[u].w * inv[3] + sgn(xv[u].w) * gmv[3]);
-      mat_st4(a.dx, r0, k, o);
-    }
-  }
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int row = t * 4 + wave;
+  if (row >= a.rows) return;
+  const float mean = norm_mean(a.norm.part, a.norm.ld, row + a.norm.row0, a.norm.nparts, a.width);
+  const bool clamped = mean < 1e-8f;  // m recomputed exactly as the forward consumers did (norm_m)
+  const float inv = 1.f / (clamped ? 1e-8f : mean);
+  const int c0 = 4 * lane, c1 = c0 + 256;
+  const bool in0 = c0 < a.width, in1 = c1 < a.width;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 x0 = mat_ldr4(a.x, row, in0 ? c0 : 0), g0 = mat_ldr4(a.g, row, in0 ? c0 : 0);
+  const float4 x1 = in1 ? mat_ldr4(a.x, row, c1) : z, g1 = in1 ? mat_ldr4(a.g, row, c1) : z;
+  float dot = in0 ? (g0.x * x0.x + g0.y * x0.y) + (g0.z * x0.z + g0.w * x0.w) : 0.f;
+  if (in1) dot += (g1.x * x1.x + g1.y * x1.y) + (g1.z * x1.z + g1.w * x1.w);
+  dot = wave_sum(dot);
+  // y = x / m: dy/dx path g/m ; dm path -(sum g x)/m^2 * sign(x)/n (unless clamped)
+  const float gm = clamped ? 0.f : (-dot * inv * inv) / (float)a.width;
+  auto sgn = [](float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); };
+  auto f = [&](float4 gv, float4 xv) {
+    return make_float4(gv.x * inv + sgn(xv.x) * gm, gv.y * inv + sgn(xv.y) * gm, gv.z * inv + sgn(xv.z) * gm,
+                       gv.w * inv + sgn(xv.w) * gm);
+  };
+  if (in0) mat_str4(a.dx, row, c0, f(g0, x0));
+  if (in1) mat_str4(a.dx, row, c1, f(g1, x1));
 }
 
 // ---------------------------------------------------------------- critic heads
 
+// max(|td|, 1)^0.4 rounded from double (torch's float pow is correctly rounded).
+__device__ __attribute__((noinline)) float lap_priority(float d) { return (float)pow((double)fmaxf(d, 1.f), 0.4); }
+
 // Last critic layer (H -> 1) as a dot product fused with the TD target / loss /
-// priority / policy objective and the gradient into the last hidden layer.
-// 16 rows per workgroup, 4 per wave (lane k: float4 of 4 rows from T images).
-// Every phase issues all of its loads before the first use (clamped indices,
-// zeroed when out of range): no load sits behind a branch, so each phase costs
-// one memory round trip.
-constexpr int kHeadU = 4;  // columns per lane per pass (256 per pass)
-__device__ __forceinline__ void op_head(const CAS HeadArgs& h, int t, float* smem, unsigned long long* tr) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r0 = t * 16 + wave * 4;
-  float acc0 = 0.f, acc1 = 0.f;  // per-wave loss terms (sum over its rows)
+// priority / policy objective and the gradient into the last hidden layer.  One
+// row per wave (4 per workgroup): lane l holds columns 4l..4l+3 (+256 per pass)
+// as float4s of the N images, so every operand of the row -- both twins' hidden
+// layer, weights and derivative source -- is loaded in one round trip.
+template <int DACT>
+__device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* smem, unsigned long long* tr) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = t * 4 + wave;  // wave-uniform: per-row scalars come through s_load
+  float acc0 = 0.f, acc1 = 0.f;  // this row's loss terms
   int kmax = (int)0x80000000, kmin = 0x7FFFFFFF;
-  if (r0 < h.rows) {
-    // ---- phase 1: q = h . w + b for both twins (each pass: all loads first)
-    float s[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    for (int kb = 0; kb < h.H; kb += 64 * kHeadU) {
-      float wv[2][kHeadU];
-      float4 hv[2][kHeadU];
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-#pragma unroll
-        for (int u = 0; u < kHeadU; ++u) {
-          const int k = kb + lane + 64 * u;
-          const int kc = k < h.H ? k : 0;
-          wv[n][u] = G(h.w[n])[tidx(h.w_rbs, 0, kc)];
-          hv[n][u] = mat_ld4(h.h[n], r0, kc);
-        }
-      }
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-#pragma unroll
-        for (int u = 0; u < kHeadU; ++u) {
-          const float w = (kb + lane + 64 * u < h.H) ? wv[n][u] : 0.f;
-          s[n][0] += hv[n][u].x * w;
-          s[n][1] += hv[n][u].y * w;
-          s[n][2] += hv[n][u].z * w;
-          s[n][3] += hv[n][u].w * w;
-        }
-      }
-    }
-    const float bb[2] = {G(h.b[0])[0], G(h.b[1])[0]};
-    // row scalars (rows r0..r0+3 are valid: rows % 16 == 0)
-    float rw[4], ndn[4], yv[4], lpv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      rw[r] = h.reward ? G(h.reward)[r0 + r] : 0.f;
-      ndn[r] = h.notdone ? G(h.notdone)[r0 + r] : 0.f;
-      yv[r] = (h.mode == HEAD_TD7_LOSS || h.mode == HEAD_MLP_LOSS) ? G(h.y)[r0 + r] : 0.f;
-      lpv[r] = h.sac ? G(h.logpi)[r0 + r] : 0.f;
-    }
-    const float alpha = h.sac ? expf(G(h.log_alpha)[0]) : 0.f;
-    float q[2][4];
+  if (b < h.rows) {
+    const int c0 = 4 * lane, c1 = c0 + 256;
+    const bool in0 = c0 < h.H, in1 = c1 < h.H;
+    const int k0 = in0 ? c0 : 0, k1 = in1 ? c1 : 0;
+    const bool dz = h.mode != HEAD_TD7_TARGET && h.mode != HEAD_MLP_TARGET;
+    float4 hv[2][2], wv[2][2], dv[2][2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
+      hv[n][0] = mat_ldr4(h.h[n], b, k0);
+      hv[n][1] = mat_ldr4(h.h[n], b, k1);
+      wv[n][0] = ld4g(G(h.w[n]) + nidx(h.w_cbn, 0, k0));
+      wv[n][1] = ld4g(G(h.w[n]) + nidx(h.w_cbn, 0, k1));
+      if (dz) {
+        dv[n][0] = mat_ldr4(h.dsrc[n], b, k0);
+        dv[n][1] = mat_ldr4(h.dsrc[n], b, k1);
+      }
+    }
+    const float rw = h.reward ? sload(h.reward + b) : 0.f, ndn = h.notdone ? sload(h.notdone + b) : 0.f;
+    const float yv = (h.mode == HEAD_TD7_LOSS || h.mode == HEAD_MLP_LOSS) ? sload(h.y + b) : 0.f;
+    const float lp = h.sac ? sload(h.logpi + b) : 0.f;
+    const float alpha = h.sac ? expf(sload(h.log_alpha)) : 0.f;
+    const float bias0 = sload(h.b[0]), bias1 = sload(h.b[1]);
+    const float vtmax = h.vt ? sload(h.vt) : 0.f, vtmin = h.vt ? sload(h.vt + 1) : 0.f;
+    float q[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) q[n][r] = wave_sum(s[n][r]) + bb[n];
+    for (int n = 0; n < 2; ++n) {
+      float s = 0.f;
+      if (in0) s += (hv[n][0].x * wv[n][0].x + hv[n][0].y * wv[n][0].y) + (hv[n][0].z * wv[n][0].z + hv[n][0].w * wv[n][0].w);
+      if (in1) s += (hv[n][1].x * wv[n][1].x + hv[n][1].y * wv[n][1].y) + (hv[n][1].z * wv[n][1].z + hv[n][1].w * wv[n][1].w);
+      q[n] = wave_sum(s) + (n ? bias1 : bias0);
     }
     trace_mark(tr, 1);
-    // ---- phase 2: per-row objective (wave-uniform mode)
-    float dq[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    bool want_dz = false;
-    if (h.mode == HEAD_TD7_TARGET) {  // td7.py:211-218
-      const float vtmax = G(h.vt)[0], vtmin = G(h.vt)[1];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = fminf(q[0][r], q[1][r]);
+    float dq[2] = {0.f, 0.f};
+    switch (h.mode) {
+      case HEAD_TD7_TARGET: {  // td7.py:211-218
+        float v = fminf(q[0], q[1]);
         v = fminf(fmaxf(v, vtmin), vtmax);
-        const float y = rw[r] + (h.gamma * v) * ndn[r];
-        if (lane == 0) GW(h.y)[r0 + r] = y;
-        kmax = max(kmax, fkey(y));
-        kmin = min(kmin, fkey(y));
+        const float y = rw + (h.gamma * v) * ndn;
+        if (lane == 0) GW(h.y)[b] = y;
+        kmax = kmin = fkey(y);
+        break;
       }
-    } else if (h.mode == HEAD_MLP_TARGET) {  // td3.py:160-164, sac.py:188-193
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = fminf(q[0][r], q[1][r]);
-        if (h.sac) v = v - alpha * lpv[r];
-        const float y = rw[r] + (h.gamma * v) * ndn[r];
-        if (lane == 0) GW(h.y)[r0 + r] = y;
+      case HEAD_MLP_TARGET: {  // td3.py:160-164, sac.py:188-193
+        float v = fminf(q[0], q[1]);
+        if (h.sac) v = v - alpha * lp;
+        const float y = rw + (h.gamma * v) * ndn;
+        if (lane == 0) GW(h.y)[b] = y;
+        break;
       }
-    } else if (h.mode == HEAD_TD7_LOSS || h.mode == HEAD_MLP_LOSS) {  // td7.py:231-244, td3.py:169-182
-      float pr[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      case HEAD_TD7_LOSS:
+      case HEAD_MLP_LOSS: {  // td7.py:231-244, td3.py:169-182
         float dmax = 0.f;
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
-          const float diff = q[n][r] - yv[r];
+          const float diff = q[n] - yv;
           if (h.lap) {
             const float d = fabsf(diff);
             const float hub = d < 1.f ? 0.5f * (d * d) : d;
-            if (n == 0) acc0 += hub; else acc1 += hub;
+            if (n == 0) acc0 = hub; else acc1 = hub;
             const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-            dq[n][r] = (d < 1.f ? d : 1.f) * sg * h.inv_b;
+            dq[n] = (d < 1.f ? d : 1.f) * sg * h.inv_b;
             dmax = fmaxf(dmax, d);
           } else {
-            const float e = yv[r] - q[n][r];
-            if (n == 0) acc0 += e * e; else acc1 += e * e;
-            dq[n][r] = -e * h.inv_b;
+            const float e = yv - q[n];
+            if (n == 0) acc0 = e * e; else acc1 = e * e;
+            dq[n] = -e * h.inv_b;
           }
         }
-        pr[r] = dmax;
+        if (h.lap && lane == 0) GW(h.prio)[b] = lap_priority(dmax);
+        break;
       }
-      if (h.lap && lane < 4) {  // one row per lane: priority = max(|td|, 1)^alpha (lap.py:68)
-        const float dm = lane == 0 ? pr[0] : lane == 1 ? pr[1] : lane == 2 ? pr[2] : pr[3];
-        GW(h.prio)[r0 + lane] = (float)pow((double)fmaxf(dm, 1.f), 0.4);
-      }
-      want_dz = true;
-    } else if (h.mode == HEAD_TD7_POLICY) {  // td7.py:274-275
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        acc0 += q[0][r] + q[1][r];
-        dq[0][r] = dq[1][r] = -0.5f * h.inv_b;
-      }
-      want_dz = true;
-    } else {  // HEAD_MLP_POLICY: td3.py:191, sac.py:227-229
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float mn = fminf(q[0][r], q[1][r]);
+      case HEAD_TD7_POLICY:  // td7.py:274-275
+        acc0 = q[0] + q[1];
+        dq[0] = dq[1] = -0.5f * h.inv_b;
+        break;
+      default: {  // HEAD_MLP_POLICY: td3.py:191, sac.py:227-229
+        const float mn = fminf(q[0], q[1]);
         // torch.minimum backward: ties split the gradient
         const float gq = -h.inv_b;
-        dq[0][r] = q[0][r] < q[1][r] ? gq : (q[0][r] == q[1][r] ? 0.5f * gq : 0.f);
-        dq[1][r] = q[1][r] < q[0][r] ? gq : (q[0][r] == q[1][r] ? 0.5f * gq : 0.f);
+        dq[0] = q[0] < q[1] ? gq : (q[0] == q[1] ? 0.5f * gq : 0.f);
+        dq[1] = q[1] < q[0] ? gq : (q[0] == q[1] ? 0.5f * gq : 0.f);
         if (h.sac) {
-          acc0 += -mn + lpv[r] * alpha;
-          acc1 += lpv[r];
+          acc0 = -mn + lp * alpha;
+          acc1 = lp;
         } else {
-          acc0 += mn;
+          acc0 = mn;
         }
       }
-      want_dz = true;
     }
     trace_mark(tr, 2);
-    // ---- phase 3: dq and dz = dq * w * act'(dsrc) (each pass: all loads first)
-    if (want_dz) {
+    if (dz) {  // dz = dq * w * act'(dsrc); dq stored for the last layer's dW
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
-        if (lane == 0 && h.dq[n].t) mat_st4(h.dq[n], r0, 0, make_float4(dq[n][0], dq[n][1], dq[n][2], dq[n][3]));
-      for (int kb = 0; kb < h.H; kb += 64 * kHeadU) {
-        float wv[2][kHeadU];
-        float4 dv[2][kHeadU];
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-#pragma unroll
-          for (int u = 0; u < kHeadU; ++u) {
-            const int k = kb + lane + 64 * u;
-            const int kc = k < h.H ? k : 0;
-            wv[n][u] = G(h.w[n])[tidx(h.w_rbs, 0, kc)];
-            dv[n][u] = mat_ld4(h.dsrc[n], r0, kc);
-          }
-        }
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-#pragma unroll
-          for (int u = 0; u < kHeadU; ++u) {
-            const int k = kb + lane + 64 * u;
-            if (k < h.H) {
-              const float4 d = dv[n][u];
-              const float w = wv[n][u];
-              mat_st4(h.dz[n], r0, k,
-                      make_float4((dq[n][0] * w) * act_bwd(h.dact, d.x), (dq[n][1] * w) * act_bwd(h.dact, d.y),
-                                  (dq[n][2] * w) * act_bwd(h.dact, d.z), (dq[n][3] * w) * act_bwd(h.dact, d.w)));
-            }
-          }
-        }
+      for (int n = 0; n < 2; ++n) {
+        if (lane == 0 && h.dq[n].t) GW(h.dq[n].t)[tidx(h.dq[n].rbs, b, 0)] = dq[n];
+        auto g4 = [&](float4 w, float4 d) {
+          return make_float4((dq[n] * w.x) * act_b<DACT>(d.x), (dq[n] * w.y) * act_b<DACT>(d.y),
+                             (dq[n] * w.z) * act_b<DACT>(d.z), (dq[n] * w.w) * act_b<DACT>(d.w));
+        };
+        if (in0) mat_str4(h.dz[n], b, c0, g4(wv[n][0], dv[n][0]));
+        if (in1) mat_str4(h.dz[n], b, c1, g4(wv[n][1], dv[n][1]));
       }
     }
   }
@@ -796,13 +772,19 @@ __device__ __forceinline__ void op_head(const CAS HeadArgs& h, int t, float* sme
   }
 }
 
+__device__ __forceinline__ void op_head(const CAS HeadArgs& h, int t, float* smem, unsigned long long* tr) {
+  if (h.dact == ACT_ELU) op_head_t<ACT_ELU>(h, t, smem, tr);
+  else if (h.dact == ACT_RELU) op_head_t<ACT_RELU>(h, t, smem, tr);
+  else op_head_t<ACT_NONE>(h, t, smem, tr);
+}
+
 // ---------------------------------------------------------------- replay sampling
 
 constexpr int kBlk = 4096;  // priorities per block-sum
 
 // Exact fp64 block sums of the priorities (lap.py:47; Q8: any-order fp64 is exact).
 __device__ __forceinline__ void op_sample_reduce(const CAS SampleArgs& s, int t, float* smem) {
-  const long long size = *G(s.size);
+  const long long size = sload(s.size);
   const long long base = (long long)t * kBlk;
   double acc = 0.0;
 #pragma unroll
@@ -823,35 +805,38 @@ __device__ __forceinline__ void op_sample_reduce(const CAS SampleArgs& s, int t,
   if (threadIdx.x == 0) GW(s.bsum)[t] = (dred[0] + dred[1]) + (dred[2] + dred[3]);
 }
 
-// Exclusive scan of 256 per-thread doubles held in LDS, by one wave, fixed order.
-__device__ __forceinline__ void scan256(double* tsum) {
-  const int tid = threadIdx.x;
-  if (tid < 64) {
-    const double v0 = tsum[4 * tid], v1 = tsum[4 * tid + 1], v2 = tsum[4 * tid + 2], v3 = tsum[4 * tid + 3];
-    const double s4 = ((v0 + v1) + v2) + v3;
-    double inc = s4;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const double nv = __shfl_up(inc, o, 64);
-      if (tid >= o) inc += nv;
-    }
-    const double ex = inc - s4;
-    tsum[4 * tid] = ex;
-    tsum[4 * tid + 1] = ex + v0;
-    tsum[4 * tid + 2] = (ex + v0) + v1;
-    tsum[4 * tid + 3] = ((ex + v0) + v1) + v2;
-  }
+// Inclusive scan of a double over the 64 lanes (DPP: row shifts, then row broadcasts).
+__device__ __forceinline__ double wave_scan_incl_d(double v) {
+  v += dpp_d<0x111>(v);  // row_shr:1
+  v += dpp_d<0x112>(v);  // row_shr:2
+  v += dpp_d<0x114>(v);  // row_shr:4
+  v += dpp_d<0x118>(v);  // row_shr:8
+  v += dpp_d<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_d<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+// Exclusive scan of one double per thread over the workgroup (fixed order; the
+// priority sums are exact in fp64, so the order does not change a value, Q8).
+__device__ __forceinline__ double wg_scan_excl_d(double v, double* wtot, double& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const double inc = wave_scan_incl_d(v);
+  if (lane == 63) wtot[wave] = inc;
+  __syncthreads();
+  double before = 0.0;
+  for (int w = 0; w < wave; ++w) before += wtot[w];
+  total = ((wtot[0] + wtot[1]) + wtot[2]) + wtot[3];
+  return before + (inc - v);
 }
 
 // One workgroup per query: uniform / LAP index search (searchsorted left over the
 // fp32-rounded exact prefix), noise for this row, then the coalesced row gather.
-__device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b, float* smem) {
+__device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b, float* smem, unsigned long long* tr) {
   const int tid = threadIdx.x;
-  const long long size = *G(s.size);
-  const int tape = *G(s.tape_mode);
-  const long long pos = *G(s.tape_pos);
+  const long long size = sload(s.size);
+  const int tape = sload(s.tape_mode);
+  const long long pos = sload(s.tape_pos);
   const uint2 key = make_uint2((unsigned)s.seed, (unsigned)(s.seed >> 32));
-  const unsigned long long step = (unsigned long long)*G(s.ctrl_rng);
+  const unsigned long long step = (unsigned long long)sload(s.ctrl_rng);
   // noise tensors for this row (T images)
   for (int j = tid; j < s.A; j += kThreads) {
     float e, e2 = 0.f;
@@ -867,8 +852,6 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
     if (s.eps2.t) mat_st(s.eps2, b, j, e2);
   }
   long long* found = reinterpret_cast<long long*>(smem);  // [1]
-  double* tsum = reinterpret_cast<double*>(smem) + 2;     // [256]
-  double* pref = tsum + kThreads;                         // [nb <= 2048]
   long long ind;
   if (tape == 2) {
     ind = G(s.tape_ind)[(size_t)pos * s.B + b];
@@ -883,93 +866,92 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
       const long long k = (long long)ceilf(v) - 1;
       ind = k < 0 ? 0 : (k > size - 1 ? size - 1 : k);
     } else {
-      // exact fp64 prefix over block sums, rounded to fp32 per element (Q8)
+      // exact fp64 prefix over block sums, rounded to fp32 per element (Q8); thread
+      // tid owns blocks [tid*per, tid*per + per), per <= 8 (capacity <= 8M)
       const int nb = (int)((size + kBlk - 1) / kBlk);
       const int per = (nb + kThreads - 1) / kThreads;
+      double* wtot = reinterpret_cast<double*>(smem) + 2;  // [4]
+      int* fblk = reinterpret_cast<int*>(smem + 24);        // [1]
+      double* fbase = reinterpret_cast<double*>(smem) + 10;  // [1]
+      double bs[8];
       double loc = 0.0;
-      for (int q = 0; q < per; ++q) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
         const int k = tid * per + q;
-        if (k < nb) {
-          loc += G(s.bsum)[k];
-          pref[k] = loc;
+        bs[q] = G(s.bsum)[min(k, nb - 1)];
+        if (q >= per || k >= nb) bs[q] = 0.0;
+        loc += bs[q];
+      }
+      if (tid == 0) *fblk = 0x7FFFFFFF;
+      double total;
+      double run = wg_scan_excl_d(loc, wtot, total);
+      const float v = u * (float)total;
+      // first block whose rounded inclusive prefix >= v (the last block if none)
+      int mine = 0x7FFFFFFF;
+      double mbase = 0.0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = tid * per + q;
+        if (q < per && k < nb && mine == 0x7FFFFFFF) {
+          if ((float)(run + bs[q]) >= v || k == nb - 1) {
+            mine = k;
+            mbase = run;
+          }
+          run += bs[q];
         }
       }
-      tsum[tid] = loc;
+      if (mine != 0x7FFFFFFF) atomicMin(fblk, mine);
       __syncthreads();
-      scan256(tsum);
+      const int lo = *fblk;
+      trace_mark(tr, 1);
+      if (mine == lo) *fbase = mbase;
       __syncthreads();
-      const double off = tsum[tid];
-      for (int q = 0; q < per; ++q) {
-        const int k = tid * per + q;
-        if (k < nb) pref[k] += off;
-      }
-      __syncthreads();
-      const float total = (float)pref[nb - 1];
-      const float v = u * total;
-      // first block whose rounded inclusive prefix >= v (monotone)
-      int lo = 0, hi = nb - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((float)pref[mid] >= v) hi = mid;
-        else lo = mid + 1;
-      }
-      const double base = lo ? pref[lo - 1] : 0.0;
+      const double base = *fbase;
       const long long e0 = (long long)lo * kBlk + (long long)tid * 16;
-      // each thread owns 16 consecutive priorities of the block
+      // 16 priorities per thread: four 16-byte buffer loads (past the capacity read 0)
+      const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(s.priority + (size_t)lo * kBlk), 0, (int)(min((long long)kBlk, s.cap - (long long)lo * kBlk) * 4),
+          0x00020000);
       float pv[16];
-      double tl = 0.0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {  // unconditional (clamped) loads: one round trip for all 16
-        const long long e = e0 + q < size ? e0 + q : size - 1;
-        pv[q] = G(s.priority)[e];
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = bload(pr, (tid * 16 + 4 * q) * 4);
+        pv[4 * q] = x.x;
+        pv[4 * q + 1] = x.y;
+        pv[4 * q + 2] = x.z;
+        pv[4 * q + 3] = x.w;
       }
+      double tl = 0.0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         if (e0 + q >= size) pv[q] = 0.f;
         tl += (double)pv[q];
       }
-      __syncthreads();
-      tsum[tid] = tl;
       if (tid == 0) *found = 0x7FFFFFFFFFFFFFFFll;
-      __syncthreads();
-      scan256(tsum);
-      __syncthreads();
-      double run = base + tsum[tid];
-      long long mine = 0x7FFFFFFFFFFFFFFFll;
+      double btot;
+      run = base + wg_scan_excl_d(tl, wtot + 4, btot);
+      long long hit = 0x7FFFFFFFFFFFFFFFll;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         run += (double)pv[q];
-        if (mine == 0x7FFFFFFFFFFFFFFFll && e0 + q < size && (float)run >= v) mine = e0 + q;
+        if (hit == 0x7FFFFFFFFFFFFFFFll && e0 + q < size && (float)run >= v) hit = e0 + q;
       }
-      if (mine != 0x7FFFFFFFFFFFFFFFll) atomicMin((unsigned long long*)found, (unsigned long long)mine);
+      if (hit != 0x7FFFFFFFFFFFFFFFll) atomicMin((unsigned long long*)found, (unsigned long long)hit);
       __syncthreads();
       ind = *found;
       if (ind >= size) ind = size - 1;
     }
   }
-  // gather the transition into the batch images (rows b and B + b of ss)
-  const GAS float* st = G(s.state) + (size_t)ind * s.Sp;
-  const GAS float* nst = G(s.next_state) + (size_t)ind * s.Sp;
-  constexpr int kGatherU = 4;  // Sp <= 1024
-  float sv[kGatherU], nv[kGatherU];
-#pragma unroll
-  for (int u = 0; u < kGatherU; ++u) {  // all loads first (clamped), then the image stores
-    const int k = tid + u * kThreads;
-    const int kc = k < s.Sp ? k : 0;
-    sv[u] = st[kc];
-    nv[u] = nst[kc];
+  trace_mark(tr, 2);
+  // gather the transition into the batch images (rows b and B + b of ss): thread
+  // tid moves columns 4 tid .. 4 tid + 3 (rows are 16-float aligned)
+  const int c = 4 * tid;
+  if (c < s.Sp) {
+    const float4 v0 = ld4g(G(s.state) + (size_t)ind * s.Sp + c), v1 = ld4g(G(s.next_state) + (size_t)ind * s.Sp + c);
+    mat_str4(s.ss, b, c, v0);
+    mat_str4(s.ss, s.B + b, c, v1);
   }
-  const GAS float* ac = G(s.action) + (size_t)ind * s.Ap;
-  const float av = ac[tid < s.Ap ? tid : 0];
-#pragma unroll
-  for (int u = 0; u < kGatherU; ++u) {
-    const int k = tid + u * kThreads;
-    if (k < s.Sp) {
-      mat_st(s.ss, b, k, sv[u]);
-      mat_st(s.ss, s.B + b, k, nv[u]);
-    }
-  }
-  if (tid < s.Ap) mat_st(s.a, b, tid, av);
+  if (c < s.Ap) mat_str4(s.a, b, c, ld4g(G(s.action) + (size_t)ind * s.Ap + c));
   if (tid == 0) {
     GW(s.r)[b] = G(s.reward)[ind];
     GW(s.nd)[b] = G(s.notdone)[ind];
@@ -1084,6 +1066,18 @@ __device__ __forceinline__ void op_sac_actor_bwd(const CAS SacActorArgs& s, int 
 
 // ---------------------------------------------------------------- step end
 
+// torch.optim.Adam bias corrections of the step after t completed ones (double, as
+// the Python scalars of the reference): step = lr / (1 - 0.9^(t+1)), bc2s = sqrt(1 - 0.999^(t+1)).
+__device__ __attribute__((noinline)) float2 adam_bias(long long t, float lr) {
+  const double tt = (double)(t + 1);
+  return make_float2((float)((double)lr / (1.0 - pow(0.9, tt))), (float)sqrt(1.0 - pow(0.999, tt)));
+}
+__device__ __forceinline__ void adam_scalars(long long t, float lr, GAS float* step, GAS float* bc2s) {
+  const float2 r = adam_bias(t, lr);
+  *step = r.x;
+  *bc2s = r.y;
+}
+
 // All partial-sum reductions of the step end in one pass: every thread loads its
 // elements of every sum (independent loads, one memory round trip), parks its
 // per-sum partials in LDS, then wave w reduces sums w, w+4, ... (fixed order).
@@ -1094,6 +1088,14 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
   float* vals = res + kSums;               // [kInfoMax]
   const float nanv = __int_as_float(0x7FC00000);
   const int tid = threadIdx.x;
+  // tail operands loaded up front (independent of the sums: one round trip overall)
+  const bool w0 = tid < 64;
+  const long long cnt = (w0 && tid < 16) ? G(a.counters)[tid] : 0;
+  const int slot0 = (w0 && a.info_slot) ? G(a.info_slot)[0] : 0;
+  const bool sac_tmp = a.log_alpha && a.la_lr > 0.f;
+  const float la = a.log_alpha ? G(a.log_alpha)[0] : 0.f;
+  const float la_m = sac_tmp ? G(a.la_m)[0] : 0.f, la_v = sac_tmp ? G(a.la_v)[0] : 0.f;
+  const long long la_t = sac_tmp ? G(a.la_t)[0] : 0;
   // sum list: j < ninfo -> info k (if summed); kInfoMax -> logpi; kInfoMax+1+q -> gsq tensor q
   auto sum_src = [&](int j, const float*& p, int& n, int& stride) {
     p = nullptr;
@@ -1136,7 +1138,9 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
     if (lane == 0) res[j] = v;
   }
   __syncthreads();
-  if (tid != 0) return;
+  if (!w0) return;
+  // wave 0, every lane (uniform values from LDS); lane-parallel stores
+  if (tid < 16 && (a.cmask & (1 << tid))) GW(a.counters)[tid] = cnt + 1;
   const float slp = res[kInfoMax];
   for (int k = 0; k < a.ninfo; ++k) {
     float v = res[k];
@@ -1147,11 +1151,11 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
     }
     vals[k] = v;
   }
-  const float la = a.log_alpha ? G(a.log_alpha)[0] : 0.f;
   const float alpha = expf(la);
   // mean_b(-lp_b - target_entropy); d/dla mean(exp(la) * c) = exp(la) * mean(c)
   const float gmean = (-slp) * a.inv_b - a.target_entropy;
   const float tmp_obj = alpha * gmean;
+  float mine = 0.f;  // lane k < ninfo: info value k
   for (int k = 0; k < a.ninfo; ++k) {
     float v = vals[k];
     switch (a.kind[k]) {
@@ -1164,29 +1168,25 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
       case INFO_SAC_TMPL: v = tmp_obj; break;
       case INFO_SAC_ENT: v = -slp * a.inv_b; break;
     }
-    vals[k] = v;
+    if (tid == k) mine = v;
   }
-  if (a.log_alpha && a.la_lr > 0.f) {  // optim_tmp.step (sac.py:283)
+  if (sac_tmp && tid == 0) {  // optim_tmp.step (sac.py:283)
     const float g = tmp_obj;
-    const double tt = (double)(G(a.la_t)[0] + 1);
-    const double bc1 = 1.0 - pow(0.9, tt), bc2 = 1.0 - pow(0.999, tt);
-    float m = G(a.la_m)[0], v2 = G(a.la_v)[0];
-    m = m + (1.f - 0.9f) * (g - m);
-    v2 = v2 * 0.999f + ((1.f - 0.999f) * g) * g;
-    const float denom = sqrtf(v2) / (float)sqrt(bc2) + 1e-8f;
+    const float2 bc = adam_bias(la_t, a.la_lr);
+    float m = la_m, v2 = la_v;
+    m = m + (float)(1.0 - 0.9) * (g - m);
+    v2 = v2 * 0.999f + ((float)(1.0 - 0.999) * g) * g;
+    const float denom = sqrtf(v2) / bc.y + 1e-8f;
     GW(a.la_m)[0] = m;
     GW(a.la_v)[0] = v2;
-    GW(a.log_alpha)[0] = la + (-(float)(a.la_lr / bc1) * m) / denom;
-    GW(a.la_t)[0] += 1;
+    GW(a.log_alpha)[0] = la + (-bc.x * m) / denom;
+    GW(a.la_t)[0] = la_t + 1;
   }
   if (a.info_slot) {
-    int slot = G(a.info_slot)[0];
-    if (slot >= a.info_cap) slot = a.info_cap - 1;
-    for (int k = 0; k < a.ninfo; ++k) GW(a.info)[(size_t)slot * kInfoMax + k] = vals[k];
-    GW(a.info_slot)[0] = slot + 1;
+    const int slot = slot0 >= a.info_cap ? a.info_cap - 1 : slot0;
+    if (tid < a.ninfo) GW(a.info)[(size_t)slot * kInfoMax + tid] = mine;
+    if (tid == 0) GW(a.info_slot)[0] = slot + 1;
   }
-  for (int c = 0; c < 16; ++c)
-    if (a.cmask & (1 << c)) GW(a.counters)[c] += 1;
 }
 
 // ---------------------------------------------------------------- flat ops
@@ -1229,9 +1229,12 @@ __device__ __forceinline__ void op_maxred(const CAS FlatArgs& f, int t, float* s
 }
 
 __device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
-  if (threadIdx.x == 0) {
+  if (threadIdx.x != 0) return;
+  if (c.mode == 0) {
     GW(c.vt)[0] = unkey(G(c.vmax_key)[0]);
     GW(c.vt)[1] = unkey(G(c.vmin_key)[0]);
+  } else {
+    for (int k = 0; k < 3; ++k) adam_scalars(G(c.counters)[k], c.adam_lr[k], GW(c.adam_step) + k, GW(c.adam_bc2s) + k);
   }
 }
 
@@ -1245,37 +1248,41 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
   const int wg = blockIdx.x;
   // op of this workgroup: from the kernel-argument table (SGPRs, no dependent
   // descriptor loads), or by scanning descriptors for an oversized level
-  int k = 0, kind;
+  int k = 0, kind, vid;
   if (la.nops <= kLevelOps) {
 #pragma unroll
     for (int q = 1; q < kLevelOps; ++q) k = (q < la.nops && la.wg_begin[q] <= wg) ? q : k;
     kind = la.kind[k];
+    vid = la.vid[k];
   } else {
     while (k + 1 < la.nops && ops[k + 1].wg_begin <= wg) ++k;
     kind = ops[k].kind;
+    vid = ops[k].gemm.vid;
   }
   const CAS Op& op = ops[k];
   const int t = wg - (la.nops <= kLevelOps ? la.wg_begin[k] : op.wg_begin);
   switch (kind) {
-    case OP_GEMM: op_gemm(op.gemm, t, smem, tr); break;
+#define RLE_OP(K, call)                       \
+  case K:                                     \
+    asm volatile("; op case " #K ::);         \
+    call;                                     \
+    break;
+    RLE_OP(OP_GEMM, op_gemm(op.gemm, vid, t, smem, tr))
 #ifndef RLE_EXP_GEMM_ONLY
-    case OP_NORMBWD: op_normbwd(op.nb, t); break;
-    case OP_SAMPLE_REDUCE: op_sample_reduce(op.sample, t, smem); break;
-    case OP_SAMPLE_GATHER: op_sample_gather(op.sample, t, smem); break;
-    case OP_HEAD:
-      asm volatile("; op head begin" ::);
-      op_head(op.head, t, smem, tr);
-      asm volatile("; op head end" ::);
-      break;
-    case OP_PRIORITY: op_priority(op.prio, smem); break;
-    case OP_SAC_ACTOR: op_sac_actor(op.sac, t); break;
-    case OP_SAC_ACTOR_BWD: op_sac_actor_bwd(op.sac, t); break;
-    case OP_STEP_END: op_step_end(op.end, smem); break;
-    case OP_POLYAK: op_polyak(op.flat, t); break;
-    case OP_COPY: op_copy(op.flat, t); break;
-    case OP_MAXRED: op_maxred(op.flat, t, smem); break;
-    case OP_CTRL: op_ctrl(op.ctrl); break;
+    RLE_OP(OP_NORMBWD, op_normbwd(op.nb, t))
+    RLE_OP(OP_SAMPLE_REDUCE, op_sample_reduce(op.sample, t, smem))
+    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather(op.sample, t, smem, tr))
+    RLE_OP(OP_HEAD, op_head(op.head, t, smem, tr))
+    RLE_OP(OP_PRIORITY, op_priority(op.prio, smem))
+    RLE_OP(OP_SAC_ACTOR, op_sac_actor(op.sac, t))
+    RLE_OP(OP_SAC_ACTOR_BWD, op_sac_actor_bwd(op.sac, t))
+    RLE_OP(OP_STEP_END, op_step_end(op.end, smem))
+    RLE_OP(OP_POLYAK, op_polyak(op.flat, t))
+    RLE_OP(OP_COPY, op_copy(op.flat, t))
+    RLE_OP(OP_MAXRED, op_maxred(op.flat, t, smem))
+    RLE_OP(OP_CTRL, op_ctrl(op.ctrl))
 #endif
+#undef RLE_OP
     default: break;
   }
   trace_mark(tr, 3);
@@ -1347,6 +1354,7 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
   for (int q = 0; q < nops && q < kLevelOps; ++q) {
     la.wg_begin[q] = h_ops[q].wg_begin;
     la.kind[q] = (unsigned char)h_ops[q].kind;
+    la.vid[q] = (unsigned char)(h_ops[q].kind == OP_GEMM ? h_ops[q].gemm.vid : 0);
   }
   hipLaunchKernelGGL(rle_level, dim3(nwg), dim3(kThreads), 0, st, la);
   return hipGetLastError();

@@ -88,8 +88,10 @@ struct AdamArgs {
   Mat w;                 // weight images [N out rows][K cols] (both kept: FWD reads N, DX reads T)
   float* b;              // bias [16 * row blocks] (bias tile column j0 == bias_col)
   long long mo, vo;      // element offsets of m / v arrays relative to params (m, v kept at T-image offsets)
-  const long long* t;    // completed optimizer steps (device counter)
+  const float* step;     // lr / (1 - beta1^t) of this optimizer's next step (Ctrl::adam_step, STEP_END)
+  const float* bc2s;     // sqrt(1 - beta2^t) (Ctrl::adam_bc2s)
   float lr, beta1, beta2, eps;
+  float omb1, omb2;      // (float)(1 - beta1), (float)(1 - beta2) as torch casts the Python scalars
   int bias_col;          // first column of the bias tile = K rounded up to the tile width tn
   float* gsq;            // optional: per-tile sum of squared grads (weights), [tiles]
   float* gsq_b;          // optional: per-tile sum of squared grads (bias), [tiles_m]
@@ -133,7 +135,7 @@ struct GemmArgs {
 };
 
 // AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise);
-// 16 rows per workgroup (4 per wave), T images in, N + T images out.
+// 4 rows per workgroup (1 per wave), N images in, N + T images out.
 struct NormBwdArgs {
   Mat g, x, dx;
   int rows, width;
@@ -149,13 +151,13 @@ enum HeadMode : int {
   HEAD_MLP_POLICY = 5,   // TD3: -mean(min);  SAC: mean(-min + alpha*logpi)
 };
 
-struct HeadArgs {                   // 16 rows per workgroup (4 per wave)
+struct HeadArgs {                   // 4 rows per workgroup (1 per wave)
   int mode, rows, H, lap;
-  Mat h[2];                          // last hidden (post-activation) of each twin, T image
-  Mat dsrc[2];                       // derivative source (Z for ELU, H for ReLU), T image
+  Mat h[2];                          // last hidden (post-activation) of each twin, N image
+  Mat dsrc[2];                       // derivative source (Z for ELU, H for ReLU), N image
   int dact;
-  const float* w[2];                 // last-layer weight row: T image of a [1][H] matrix
-  int w_rbs;                         // its row-block stride (1)
+  const float* w[2];                 // last-layer weight row: N image of a [1][H] matrix
+  int w_cbn;                         // its column blocks
   const float* b[2];                 // last-layer bias [1]
   const float* reward; const float* notdone;
   float* y;                          // target (written by *_TARGET, read by *_LOSS)
@@ -179,6 +181,7 @@ struct SampleArgs {
   float* priority;
   int S, Sp, A, Ap;
   const long long* size;             // device replay size
+  long long cap;                     // replay capacity (priority array length)
   int lap, B;
   double* bsum; int nblk;            // LAP block sums (fp64), 4096 priorities per block
   // outputs
@@ -225,6 +228,7 @@ struct StepEndArgs {
   int kind[kInfoMax]; int ninfo;
   // SAC temperature
   float* log_alpha; float* la_m; float* la_v; long long* la_t; float la_lr; float target_entropy;
+  float* adam_step; float* adam_bc2s; float adam_lr[4];  // next-step Adam scalars of counters 0..2
   const float* logpi_part; int nlogpi; float inv_b;
   const float* gsq; int gsq_off[9]; int ngsq_t;      // TD3 grad norm: tensor t = tiles [off[t], off[t+1])
 };
@@ -247,8 +251,10 @@ struct FlatArgs {   // POLYAK / COPY / MAXRED
   int stage;
 };
 
-struct CtrlArgs {   // small control-plane writes (value bounds copy at hard update)
+struct CtrlArgs {   // small control-plane writes
+  int mode;          // 0: value bounds copy at the hard update; 1: Adam scalars from the counters
   const int* vmax_key; const int* vmin_key; float* vt;
+  const long long* counters; float* adam_step; float* adam_bc2s; float adam_lr[4];
 };
 
 struct Op {
@@ -278,6 +284,7 @@ struct LevelArgs {
   int nops;
   int wg_begin[kLevelOps];
   unsigned char kind[kLevelOps];
+  unsigned char vid[kLevelOps];  // GemmArgs::vid of GEMM ops (variant chosen before any descriptor load)
 };
 
 // Device control block.
@@ -291,6 +298,8 @@ struct Ctrl {
   float max_priority;
   float log_alpha, la_m, la_v;
   long long la_t;
+  float adam_step[4];       // per optimizer counter 0..2: lr / (1 - 0.9^(t+1)), t = counters[c]
+  float adam_bc2s[4];       // sqrt(1 - 0.999^(t+1))
 };
 
 enum Counter : int { CNT_ADAM_Q = 0, CNT_ADAM_PI = 1, CNT_ADAM_ENC = 2, CNT_RNG = 4, CNT_TAPE = 5 };
