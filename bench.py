@@ -120,6 +120,77 @@ def cpu_baseline(seconds=12.0):
                       f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads}"}
 
 
+def max_over_ranks(vals, dist=None):
+    """Element-wise max of per-rank timings (the slowest rank defines the job's time)."""
+    if dist is None:
+        return [float(v) for v in vals]
+    import torch
+
+    t = torch.tensor(vals, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t]
+
+
+def pmc_traffic():
+    """HBM bytes per rle_level launch from the committed PMC summary of the same command
+    (tools/pmc.sh + tools/pmc_summary.py --json): 2 x FETCH_SIZE (gfx950 reports half of
+    wide coalesced reads, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, both in KB.  None when
+    no summary is committed."""
+    path = os.path.join(REPO, "profiles", "r01_pmc.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pmc = json.load(f)
+    return round((2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0)
+
+
+def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain):
+    """The bench JSON line (everything but cpu_baseline) from the max-over-ranks timings."""
+    value = n_gpus * steps / wall
+    macs = SURVEY_MACS_PER_SAMPLE  # the §8(d) contract figure (own derivation: td7_macs_per_sample)
+    flop_step = 2.0 * macs * B
+    bytes_step = td7_bytes_per_step(S, A, H, B, N_REPLAY)
+    # launches per step: average over the policy / non-policy graphs (+ hard update amortised)
+    launches = (lv_policy + lv_plain) / 2.0
+    per_launch_s = gpu_s / (steps * launches)
+    achieved = flop_step / launches / per_launch_s / 1e12
+    roofline = {
+        "bound": "mfma",
+        "achieved": round(achieved, 3),
+        "peak": PEAK_FP32_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_FP32_TFLOPS, 5),
+        "traffic": pmc_traffic(),
+        "traffic_algorithmic": round(bytes_step / launches),
+        "kernel": "rle_level (one launch per dependency level of the step graph)",
+        "flop_per_step": flop_step,
+        "launches_per_step": launches,
+        "avg_launch_us": round(per_launch_s * 1e6, 3),
+        "hbm_bytes_per_step_algorithmic": round(bytes_step),
+        "hbm_achieved_GBs": round(bytes_step * steps / gpu_s / 1e9, 2),
+    }
+    return {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "gradient-steps/s",
+        "n_gpus": n_gpus,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(wall / steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic",
+        "config": {"workload": "TD7 Humanoid-v4 gradient step, LAP over 1M HBM replay",
+                   "algo": "td7", "obs_dim": S, "act_dim": A, "hidden": H, "batch": B,
+                   "replay": N_REPLAY, "lap": True, "policy_freq": 2, "target_update_rate": 250,
+                   "parallelism": f"replicas x{n_gpus} (one seed per GPU, no collective)"},
+        "roofline": roofline,
+        "gpu_event_s": round(gpu_s, 6),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -162,61 +233,14 @@ def main():
     torch.cuda.synchronize(local)
     t1 = time.perf_counter()
     wall = t1 - t0
-    if dist:
-        t = torch.tensor([wall, gpu_ms / 1e3], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall, gpu_s = float(t[0]), float(t[1])
-    else:
-        gpu_s = gpu_ms / 1e3
+    wall, gpu_s = max_over_ranks([wall, gpu_ms / 1e3], dist)
 
     if rank != 0:
         if dist:
             dist.barrier()
         return
-    n_gpus = world
-    value = n_gpus * args.steps / wall
-    macs = SURVEY_MACS_PER_SAMPLE  # the §8(d) contract figure (own derivation: td7_macs_per_sample)
-    flop_step = 2.0 * macs * B
-    bytes_step = td7_bytes_per_step(S, A, H, B, N_REPLAY)
-    # launches per step: average over the policy / non-policy graphs (+ hard update amortised)
-    launches = (lv_policy + lv_plain) / 2.0
-    per_launch_s = gpu_s / (args.steps * launches)
-    achieved = flop_step / launches / per_launch_s / 1e12
-    roofline = {
-        "bound": "mfma",
-        "achieved": round(achieved, 3),
-        "peak": PEAK_FP32_TFLOPS,
-        "unit": "TFLOP/s",
-        "frac": round(achieved / PEAK_FP32_TFLOPS, 5),
-        "traffic": None,
-        "kernel": "rle_level (one launch per dependency level of the step graph)",
-        "flop_per_step": flop_step,
-        "launches_per_step": launches,
-        "avg_launch_us": round(per_launch_s * 1e6, 3),
-        "hbm_bytes_per_step_algorithmic": round(bytes_step),
-        "hbm_achieved_GBs": round(bytes_step * args.steps / gpu_s / 1e9, 2),
-    }
-    out = {
-        "metric": METRIC,
-        "value": round(value, 2),
-        "unit": "gradient-steps/s",
-        "n_gpus": n_gpus,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "fp32",
-        "data": "synthetic",
-        "config": {"workload": "TD7 Humanoid-v4 gradient step, LAP over 1M HBM replay",
-                   "algo": "td7", "obs_dim": S, "act_dim": A, "hidden": H, "batch": B,
-                   "replay": N_REPLAY, "lap": True, "policy_freq": 2, "target_update_rate": 250,
-                   "parallelism": f"replicas x{n_gpus} (one seed per GPU, no collective)"},
-        "roofline": roofline,
-        "gpu_event_s": round(gpu_s, 6),
-    }
-    if n_gpus == 1 and not args.no_cpu_baseline:
+    out = summarize(world, args.steps, args.warmup, wall, gpu_s, lv_policy, lv_plain)
+    if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     print(json.dumps(out), flush=True)
     if dist:

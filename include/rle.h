@@ -111,10 +111,12 @@ int rle_step(rle_engine* e, int n_steps, float* info_out);
 /* Benchmark form of rle_step: n_steps without info readback, bracketed by HIP events recorded
  * on the engine's own stream; *gpu_ms = elapsed event time.  Syncs once at the end. */
 int rle_step_timed(rle_engine* e, int n_steps, float* gpu_ms);
-/* Parity mode: replace the Philox draws of the next n_steps with tapes.
- * u [n][B] (torch.rand in sample), eps [n][B][A] (randn_like target noise, or SAC next-state
- * rsample noise), eps_pi [n][B][A] (SAC policy rsample noise, may be NULL), ind [n][B]
- * (optional explicit indices; overrides u).  Pass n_steps = 0 to return to Philox. */
+/* Parity / explicit-batch mode: replace draws of the next n_steps with tapes; each tape
+ * is optional and a NULL one keeps its Philox stream.  u [n][B] (torch.rand in sample),
+ * eps [n][B][A] (randn_like target noise, or SAC next-state rsample noise), eps_pi [n][B][A]
+ * (SAC policy rsample noise; SAC takes eps and eps_pi together), ind [n][B] (explicit
+ * indices, e.g. the batch a replay's sample() drew; overrides u).  At least one of u / ind.
+ * Pass n_steps = 0 to return to Philox; stepping past the tape's end is an error. */
 int rle_set_tapes(rle_engine* e, int n_steps, const float* u, const float* eps, const float* eps_pi,
                   const long long* ind);
 /* Last sampled indices (LAPReplayMemory.ind) [B]. */

@@ -1918,7 +1918,7 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     s.eps = timg(n, r.Ap);
     long long* cnt = tmp.make<long long>(2);
     int* mode = tmp.make<int>(1);
-    const int one = 1;
+    const int one = rle::kTapeU;
     HIPCHK(hipMemcpy(mode, &one, 4, hipMemcpyHostToDevice));
     s.ctrl_rng = cnt;
     s.tape_mode = mode;
@@ -2203,7 +2203,8 @@ int rle_set_tapes(rle_engine* h, int n, const float* u, const float* eps, const 
       if (eps_pi) HIPCHK(hipMemcpy(e.t_eps2, eps_pi, na * 4, hipMemcpyHostToDevice));
       if (ind) HIPCHK(hipMemcpy(e.t_ind, ind, nb * 8, hipMemcpyHostToDevice));
       REQUIRE(u || ind, "set_tapes: need u or ind");
-      mode = ind ? 2 : 1;
+      REQUIRE(e.algo != RLE_SAC || !eps == !eps_pi, "set_tapes: SAC takes eps and eps_pi together");
+      mode = (u ? rle::kTapeU : 0) | (ind ? rle::kTapeInd : 0) | (eps ? rle::kTapeEps : 0);
     }
     rle::Ctrl c;
     HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));

@@ -840,7 +840,7 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
   // noise tensors for this row (T images)
   for (int j = tid; j < s.A; j += kThreads) {
     float e, e2 = 0.f;
-    if (tape) {
+    if (tape & kTapeEps) {
       e = G(s.tape_eps)[((size_t)pos * s.B + b) * s.A + j];
       if (s.eps2.t) e2 = G(s.tape_eps2)[((size_t)pos * s.B + b) * s.A + j];
     } else {
@@ -853,11 +853,11 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
   }
   long long* found = reinterpret_cast<long long*>(smem);  // [1]
   long long ind;
-  if (tape == 2) {
+  if (tape & kTapeInd) {
     ind = G(s.tape_ind)[(size_t)pos * s.B + b];
   } else {
     float u;
-    if (tape) u = G(s.tape_u)[(size_t)pos * s.B + b];
+    if (tape & kTapeU) u = G(s.tape_u)[(size_t)pos * s.B + b];
     else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
     if (tid == 0) GW(s.u_out)[b] = u;
     if (!s.lap) {

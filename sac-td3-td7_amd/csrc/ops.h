@@ -174,6 +174,8 @@ struct HeadArgs {                   // 4 rows per workgroup (1 per wave)
   float inv_b;                       // 1/B (policy loss scale)
 };
 
+enum { kTapeU = 1, kTapeInd = 2, kTapeEps = 4 };
+
 struct SampleArgs {
   // replay
   const float* state; const float* next_state; const float* action;
@@ -195,7 +197,7 @@ struct SampleArgs {
   // randomness
   const long long* ctrl_rng;         // step counter for Philox
   unsigned long long seed;
-  const int* tape_mode;              // 0: Philox, 1: tapes, 2: tapes incl. indices
+  const int* tape_mode;              // kTape* bits: which draws come from tapes (others: Philox)
   const long long* tape_pos;
   const float* tape_u; const float* tape_eps; const float* tape_eps2; const long long* tape_ind;
 };

@@ -1,0 +1,236 @@
+"""Shared machinery of the engine-backed TD7 / TD3 / SAC agents.
+
+Each agent owns one ``rle_engine`` (include/rle.h): all networks, target copies,
+Adam moments and step counters live in HBM and a gradient step is one replay of
+a captured HIP graph.  The Python side keeps the reference's interface
+(rl/agent/abc.py:16-55, rl/sampler.py:14-19): construction arguments,
+``train_ops(batch, replay_buffer)`` returning the same info dict, ``sample``,
+``to``, ``load_state_dict``, pickling (``save``/``load``/``deepcopy``).
+
+There is no CPU path: constructing an agent without the HIP library raises.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from rl import _engine as E
+from rl.agent.abc import Agent
+from rl.nn.layout import AGENT_COPIES, AGENT_NETS, init_agent, layers
+from rl.replay_memory.base import BaseReplayMemory, DeviceBatch
+from rl.sampler import Sampler
+from rl.utils.envs import get_action_bias_scale, get_state_action_dims
+
+
+def _device_index(device) -> int:
+    if device is None:
+        return 0
+    if isinstance(device, int):
+        return device
+    s = str(device)
+    if s == "cpu":
+        return -1
+    if s.startswith("cuda") or s.startswith("hip"):
+        return int(s.split(":")[1]) if ":" in s else 0
+    raise ValueError(f"unsupported device {device!r}")
+
+
+class EngineAgent(Agent, Sampler):
+    ALG = ""          # "td7" | "td3" | "sac"
+    ALGO = -1         # RLE_TD7 / RLE_TD3 / RLE_SAC
+    OPTIM_NETS: tuple = ()
+    NULLABLE: tuple = ()  # info keys the reference sets to None on non-policy steps
+
+    def _setup(self, env_id, *, hidden, batch_size, seed, device, make_nn, make_nn_kwargs, cfg):
+        if make_nn is not None:
+            raise NotImplementedError("engine agents build the reference's default nets; pass hidden= for width")
+        hdim = make_nn_kwargs.pop("hdim", None) or make_nn_kwargs.pop("zs_dim", None)
+        hs = make_nn_kwargs.pop("hidden_sizes", None)
+        if make_nn_kwargs:
+            raise TypeError(f"unsupported arguments {sorted(make_nn_kwargs)}")
+        if hs is not None:
+            if len(set(hs)) != 1 or len(hs) != 2:
+                raise NotImplementedError("make_mlp with two equal hidden layers only (mlp.py:45)")
+            hidden = hs[0]
+        if hdim is not None:
+            hidden = hdim
+        self.env_id = env_id
+        self.state_dim, self.action_dim = get_state_action_dims(env_id)
+        self.action_bias, self.action_scale = get_action_bias_scale(env_id)
+        self.hidden = int(hidden)
+        if seed is None:
+            import torch
+
+            seed = torch.initial_seed() & 0x7FFFFFFF
+        self.seed = int(seed)
+        self._cfg = dict(cfg)
+        self._device = max(_device_index(device), 0)
+        self.device = device if device is not None else "cuda:0"
+        self._replay = None
+        self.engine = self._new_engine(int(batch_size))
+        nets = init_agent(self.ALG, self.state_dim, self.action_dim, self.hidden, self.seed)
+        self._import({"params": nets})
+
+    # ---- engine lifecycle ----------------------------------------------------
+    def _new_engine(self, batch):
+        c = E.make_config(self.ALGO, self.state_dim, self.action_dim, self.hidden, batch, seed=self.seed,
+                          device=self._device, **self._cfg)
+        return E.Engine(c)
+
+    @property
+    def batch_size(self) -> int:
+        return self.engine.cfg.batch
+
+    def _rebuild(self, batch=None, device=None):
+        st = self._export()
+        if device is not None:
+            self._device = device
+        self.engine.close()
+        self.engine = self._new_engine(self.batch_size if batch is None else batch)
+        self._import(st)
+        self._replay = None
+
+    def _prepare(self, replay: BaseReplayMemory, batch: int):
+        if not isinstance(replay, BaseReplayMemory):
+            raise TypeError("engine agents train from rl.replay_memory device replays")
+        if self._cfg.get("use_lap") and not replay.LAP:
+            raise AssertionError("use_lap=True needs a LAPReplayMemory (td7.py:307-309)")
+        if replay.device != self._device:
+            raise ValueError(f"replay on device {replay.device}, agent on {self._device}")
+        if batch != self.batch_size or (self._replay is not None and self._replay is not replay):
+            self._rebuild(batch)
+        if self._replay is not replay:
+            self.engine.bind(replay.dev)
+            self._replay = replay
+        replay.flush()
+
+    # ---- parameters / state ---------------------------------------------------
+    def _param_names(self):
+        out = []
+        for net, kind in AGENT_NETS[self.ALG].items():
+            o = 2 * self.action_dim if (self.ALG == "sac" and net == "policy") else None
+            names = []
+            for prefix, fin, fout in layers(kind, self.state_dim, self.action_dim, self.hidden, o):
+                names += [(prefix + ".weight", (fout, fin)), (prefix + ".bias", (fout,))]
+            out.append((net, names))
+            for copy, src in AGENT_COPIES[self.ALG].items():
+                if src == net:
+                    out.append((copy, names))
+        return out
+
+    def _export(self):
+        e = self.engine
+        params = {net: {n: e.get_param(net, n, shp) for n, shp in names} for net, names in self._param_names()}
+        adam = {}
+        for net, names in self._param_names():
+            if net in self.OPTIM_NETS:
+                adam[net] = {n: (e.get_adam(net, n, 0, shp), e.get_adam(net, n, 1, shp)) for n, shp in names}
+        if self.ALG == "sac":
+            params["tmp"] = {"log_alpha": e.get_param("tmp", "log_alpha")}
+            adam["tmp"] = {"log_alpha": (e.get_adam("tmp", "log_alpha", 0), e.get_adam("tmp", "log_alpha", 1))}
+        return {"params": params, "adam": adam, "counters": e.counters(), "vbounds": e.value_bounds()}
+
+    def _import(self, st):
+        e = self.engine
+        for net, d in st["params"].items():
+            for n, v in d.items():
+                e.set_param(net, n, np.asarray(v, np.float32))
+        for net, d in st.get("adam", {}).items():
+            for n, (m, v) in d.items():
+                e.set_adam(net, n, 0, m)
+                e.set_adam(net, n, 1, v)
+        if "counters" in st:
+            e.set_counters(st["counters"])
+        if "vbounds" in st:
+            e.set_value_bounds(st["vbounds"])
+
+    def state_dict(self):
+        """{net: {param name: ndarray}} in the reference's state_dict naming."""
+        return self._export()["params"]
+
+    def load_params(self, params):
+        self._import({"params": params})
+
+    def __getstate__(self):
+        d = {k: v for k, v in self.__dict__.items() if k not in ("engine", "_replay")}
+        d["_engine_state"] = self._export()
+        d["_batch"] = self.batch_size
+        return d
+
+    def __setstate__(self, d):
+        st = d.pop("_engine_state")
+        batch = d.pop("_batch")
+        self.__dict__.update(d)
+        self._replay = None
+        self.engine = self._new_engine(batch)
+        self._import(st)
+
+    def to(self, device):
+        """td7.py:101-112: move to a device.  'cpu' is accepted as a no-op (pickling exports
+        the HBM state; there is no CPU execution path); cuda:k moves the engine to GPU k."""
+        k = _device_index(device)
+        if k >= 0 and k != self._device:
+            self._rebuild(device=k)
+        self.device = device
+        return self
+
+    def load_state_dict(self, agent: "EngineAgent"):
+        """td7.py:114-125 / td3.py:94-100 / sac.py:101-107: copy every network (not the
+        optimiser state, counters or SAC temperature)."""
+        if type(agent) is not type(self):
+            raise TypeError("load_state_dict needs an agent of the same class")
+        for net, names in self._param_names():
+            for n, _ in names:
+                self.engine.set_param(net, n, agent.engine.get_param(net, n))
+        return self
+
+    @property
+    def n_runs(self) -> int:
+        return int(self.engine.counters()[3])
+
+    # ---- training ----------------------------------------------------------
+    def _info(self, row):
+        out = {}
+        for k, v in zip(self._info_keys(), row):
+            v = float(v)
+            out[k] = None if (k in self.NULLABLE and math.isnan(v)) else v
+        return out
+
+    def train_ops(self, batch, replay_buffer=None, *args, **kwargs):
+        """One gradient step on ``batch`` (td7.py:287-332 / td3.py:206-242 / sac.py:251-295).
+
+        ``batch`` must come from ``replay_buffer.sample(B)`` of a device replay: the step
+        reads rows ``batch.ind`` in HBM (the host tensors in the dict are not re-uploaded).
+        Target-policy / rsample noise comes from the engine's Philox stream."""
+        if not isinstance(batch, DeviceBatch):
+            raise ValueError("engine train_ops needs the DeviceBatch returned by a device replay's sample()")
+        rep = replay_buffer if replay_buffer is not None else batch.replay
+        if batch.replay is not rep:
+            raise ValueError("batch was drawn from a different replay than replay_buffer")
+        ind = np.ascontiguousarray(batch.ind, np.int64).reshape(1, -1)
+        self._prepare(rep, ind.shape[1])
+        self.engine.set_tapes(ind=ind)
+        try:
+            row = self.engine.step(1)[0]
+        finally:
+            self.engine.set_tapes()
+        return self._info(row)
+
+    def train_n(self, replay_buffer: BaseReplayMemory, batch_size: int, n_ops: int):
+        """n_ops x (sample + train_ops) fused on the device (run_train_ops, run.py:87-96)."""
+        self._prepare(replay_buffer, batch_size)
+        rows = self.engine.step(n_ops) if n_ops > 0 else []
+        if n_ops > 0:
+            replay_buffer._mark_engine_indices(self.engine)
+        return [self._info(r) for r in rows]
+
+    # ---- acting --------------------------------------------------------------
+    def _forward(self, state, width):
+        if hasattr(state, "detach"):
+            state = state.detach().cpu().numpy()
+        x = np.asarray(state, np.float32)
+        if x.ndim == 1:
+            x = x[None]
+        return self.engine.act(x, width)

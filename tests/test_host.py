@@ -1,0 +1,129 @@
+"""Host-side logic of the reference-interface mirror and the bench (no GPU calls)."""
+
+import json
+import math
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from rl import _engine as E
+from rl.agent import SAC, TD3, TD7
+from rl.replay_memory import DeviceBatch, LAPReplayMemory
+from rl.sampler import RandomSampler
+from rl.utils import get_action_bias_scale, get_state_action_dims, register_env
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_env_table_matches_mujoco_v4_spaces():
+    # SURVEY.md §8 dims table (miscellaneous.py:50-66 on the real gym spaces)
+    assert get_state_action_dims("Humanoid-v4") == (376, 17)
+    assert get_state_action_dims("Ant-v4") == (27, 8)
+    assert get_state_action_dims("HalfCheetah-v4") == (17, 6)
+    bias, scale = get_action_bias_scale("Humanoid-v4")
+    assert bias.dtype == np.float32 and np.all(bias == 0) and np.all(scale == np.float32(0.4))
+    register_env("Odd-v0", 5, 2, [-1.0, 0.0], [3.0, 1.0])
+    bias, scale = get_action_bias_scale("Odd-v0")
+    np.testing.assert_array_equal(bias, [1.0, 0.5])
+    np.testing.assert_array_equal(scale, [2.0, 0.5])
+    with pytest.raises(KeyError):
+        get_state_action_dims("NoSuchEnv-v9")
+
+
+def test_random_sampler_stays_in_box():
+    rs = RandomSampler("Humanoid-v4")
+    a = np.stack([rs.sample() for _ in range(200)])
+    assert a.shape == (200, 17) and np.all(np.abs(a) <= 0.4)
+
+
+def test_append_normalisation_uses_reference_dtypes():
+    # lap.py:35: action / scale - bias in the operands' NumPy dtypes, stored then cast to fp32
+    rep = LAPReplayMemory.__new__(LAPReplayMemory)
+    rep.action_bias, rep.action_scale = get_action_bias_scale("Humanoid-v4")
+    a64 = np.linspace(-0.4, 0.4, 17)
+    np.testing.assert_array_equal(rep._normalise(a64), a64 / np.float32(0.4) - 0.0)
+    a32 = a64.astype(np.float32)
+    out = rep._normalise(a32)
+    assert out.dtype == np.float32
+
+
+def test_info_rows_map_to_reference_keys():
+    td7 = TD7.__new__(TD7)
+    row = np.array([1.0, 2.0, np.nan, 0, 0, 0, 0, 0], np.float32)
+    assert td7._info(row) == {"train/encoder": 1.0, "train/q_fn": 2.0, "train/policy": None}
+    td3 = TD3.__new__(TD3)
+    assert td3._info(np.array([0.5, np.nan, np.nan], np.float32)) == {
+        "train/q_fn": 0.5, "train/policy": None, "norm/policy": None}
+    sac = SAC.__new__(SAC)
+    sac.auto_tmp_mode = True
+    got = sac._info(np.arange(8, dtype=np.float32))
+    assert list(got) == ["train/q_fn", "tmp", "norm/tmp", "train/policy", "train/tmp", "entropy"]
+    sac.auto_tmp_mode = False
+    nan_loss = sac._info(np.array([np.nan, 1.0, 2.0], np.float32))
+    assert math.isnan(nan_loss["train/q_fn"])  # a diverged loss stays NaN, only policy keys go None
+
+
+def test_train_ops_rejects_batches_not_drawn_from_a_device_replay():
+    td7 = TD7.__new__(TD7)
+    with pytest.raises(ValueError):
+        td7.train_ops({"state": np.zeros((4, 3))}, None)
+    rep_a, rep_b = object(), object()
+    batch = DeviceBatch({}, np.zeros(4, np.int64), rep_a)
+    with pytest.raises(ValueError):
+        td7.train_ops(batch, rep_b)
+
+
+def test_engine_agents_reject_custom_nets():
+    with pytest.raises(NotImplementedError):
+        TD3("HalfCheetah-v4", make_nn=lambda **k: None)
+
+
+def test_missing_library_fails_loudly(tmp_path, monkeypatch):
+    monkeypatch.setattr(E, "LIB_PATH", str(tmp_path / "librle.so"))
+    monkeypatch.setattr(E, "_lib", None)
+    with pytest.raises(RuntimeError, match="not built"):
+        E.Replay(16, 3, 1, False)
+
+
+def test_bench_workload_figures_match_survey():
+    sys.path.insert(0, REPO)
+    import bench
+
+    # 6,217,088 MAC/sample, 3.183 GFLOP/step, 41.37 MB/step for TD7 Humanoid B=256
+    assert bench.SURVEY_MACS_PER_SAMPLE == 6_217_088
+    # own derivation (bench.td7_macs_per_sample) agrees within 2%; the bench uses the §8(d) figure
+    assert abs(bench.td7_macs_per_sample(376, 17, 256) / bench.SURVEY_MACS_PER_SAMPLE - 1) < 0.02
+    assert abs(2 * bench.SURVEY_MACS_PER_SAMPLE * 256 / 1e9 - 3.183) < 1e-3
+    assert abs(bench.td7_bytes_per_step(376, 17, 256, 256, 1_000_000) / 1e6 - 41.4) < 0.1
+    out = bench.summarize(2, 1000, 10, wall=0.5, gpu_s=0.45, lv_policy=30, lv_plain=20)
+    assert out["value"] == 4000.0 and out["n_gpus"] == 2 and out["scaling"] == "weak"
+    assert out["roofline"]["launches_per_step"] == 25.0
+    assert abs(out["roofline"]["avg_launch_us"] - 0.45 / (1000 * 25) * 1e6) < 1e-3
+    json.dumps(out)
+
+
+def test_bench_max_over_ranks_gloo_world2(tmp_path):
+    """The N>1 bench path: two gloo ranks, the job time is the slowest rank's."""
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import os, sys, json\n"
+        f"sys.path.insert(0, {REPO!r})\n"
+        "import torch.distributed as dist\n"
+        "import bench\n"
+        "dist.init_process_group('gloo')\n"
+        "r = dist.get_rank()\n"
+        "wall, gpu = bench.max_over_ranks([1.0 + r, 0.5 * (2 - r)], dist)\n"
+        "out = bench.summarize(dist.get_world_size(), 100, 5, wall, gpu, 30, 20)\n"
+        "if r == 0: print(json.dumps([wall, gpu, out['value']]))\n"
+        "dist.barrier(); dist.destroy_process_group()\n")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29517", str(script)],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert res.returncode == 0, res.stderr[-2000:]
+    wall, gpu, value = json.loads(res.stdout.strip().splitlines()[-1])
+    assert (wall, gpu) == (2.0, 1.0)
+    assert value == 2 * 100 / 2.0
