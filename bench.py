@@ -30,6 +30,13 @@ sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd")]
 
 S, A, H, B, N_REPLAY = 376, 17, 256, 256, 1_000_000
 METRIC = "gradient-steps/sec (whole node), TD7 Humanoid-v4 batch=256 at 1/2/4/8 GPUs"
+TASKS = {"Humanoid-v4": (376, 17, 0.4), "Ant-v4": (27, 8, 1.0), "HalfCheetah-v4": (17, 6, 1.0)}
+# SURVEY.md §8(d) algorithmic work per step: (algo, env, B) -> (GFLOP/step, HBM MB/step).
+# The headline (default) config is TD7 Humanoid B=256; the others are BASELINE.json's
+# secondary configs, run with --algo/--env/--batch (not part of the default JSON line).
+WORK = {("td7", "Humanoid-v4", 256): (3.183, 41.37), ("td7", "Humanoid-v4", 1024): (12.733, 43.74),
+        ("td7", "Ant-v4", 256): (2.502, 31.66), ("sac", "Humanoid-v4", 256): (1.121, 18.93),
+        ("td3", "HalfCheetah-v4", 256): (0.449, 6.39)}
 PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 MFMA dense (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 # SURVEY.md §8(d) algorithmic work for TD7 Humanoid B=256: 6,217,088 MAC/sample (3.183 GFLOP/step).
@@ -78,34 +85,40 @@ def td7_bytes_per_step(S, A, H, B, N, target_update_rate=250, policy_freq=2):
     return gather + B * 8 + 4 * N + adam + hard
 
 
-def cpu_baseline(seconds=12.0):
-    """Oracle (torch-CPU restatement of td7.py train_ops + lap.py sample) on host cores."""
+def cpu_baseline(seconds=12.0, algo="td7", env="Humanoid-v4", batch=B, lap=True):
+    """Oracle (torch-CPU restatement of train_ops + replay sample) on host cores, same
+    synthetic workload as the GPU run (full 1M replay)."""
     import torch
 
     from oracle import agents, replay, spec
 
+    s_dim, a_dim, hi = TASKS[env]
     threads = torch.get_num_threads()
     rng = np.random.default_rng(0)
-    nets = spec.agent_params("td7", S, A, H, 123)
-    orc = agents.TD7Oracle(nets, use_lap=True)
-    rep = replay.Replay(N_REPLAY, S, A, np.full(A, 0.4, np.float32), np.zeros(A, np.float32), True)
+    nets = spec.agent_params(algo, s_dim, a_dim, H, 123)
+    orc = agents.make_oracle(algo, nets, a_dim, lap)
+    rep = replay.Replay(N_REPLAY, s_dim, a_dim, np.full(a_dim, hi, np.float32), np.zeros(a_dim, np.float32), lap)
     blk = 4096
-    base_s = rng.standard_normal((blk, S), dtype=np.float32)
-    base_s2 = rng.standard_normal((blk, S), dtype=np.float32)
+    base_s = rng.standard_normal((blk, s_dim), dtype=np.float32)
+    base_s2 = rng.standard_normal((blk, s_dim), dtype=np.float32)
     for i in range(0, N_REPLAY, blk):
         n = min(blk, N_REPLAY - i)
         rep.state[i:i + n] = base_s[:n]
         rep.next_state[i:i + n] = base_s2[:n]
-    rep.action[:] = rng.uniform(-1, 1, (N_REPLAY, A)).astype(np.float32)
+    rep.action[:] = rng.uniform(-1, 1, (N_REPLAY, a_dim)).astype(np.float32)
     rep.reward[:, 0] = rng.standard_normal(N_REPLAY).astype(np.float32)
     rep.done[:, 0] = (rng.random(N_REPLAY) < 0.99).astype(np.float32)
     rep.priority[:] = 1.0
     rep.size, rep.ptr = N_REPLAY, 0
 
     def one():
-        u = rng.random(B, dtype=np.float32)
-        batch = rep.gather(rep.sample_indices(u))
-        orc.step(batch, rep, rng.standard_normal((B, A), dtype=np.float32))
+        u = rng.random(batch, dtype=np.float32)
+        batch_d = rep.gather(rep.sample_indices(u))
+        eps = rng.standard_normal((batch, a_dim), dtype=np.float32)
+        if algo == "sac":
+            orc.step(batch_d, rep, eps, rng.standard_normal((batch, a_dim), dtype=np.float32))
+        else:
+            orc.step(batch_d, rep, eps)
 
     for _ in range(3):
         one()
@@ -116,7 +129,7 @@ def cpu_baseline(seconds=12.0):
         n += 1
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 3), "unit": "gradient-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} TD7 Humanoid B=256 steps (LAP over 1M priorities, policy every 2nd step) "
+            "sample": f"{n} {algo.upper()} {env} B={batch} steps ({'LAP' if lap else 'uniform'} over a 1M replay) "
                       f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads}"}
 
 
@@ -144,12 +157,19 @@ def pmc_traffic():
     return round((2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0)
 
 
-def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain):
+def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7", env="Humanoid-v4",
+              batch=B, lap=True):
     """The bench JSON line (everything but cpu_baseline) from the max-over-ranks timings."""
     value = n_gpus * steps / wall
-    macs = SURVEY_MACS_PER_SAMPLE  # the §8(d) contract figure (own derivation: td7_macs_per_sample)
-    flop_step = 2.0 * macs * B
-    bytes_step = td7_bytes_per_step(S, A, H, B, N_REPLAY)
+    headline = (algo, env, batch) == ("td7", "Humanoid-v4", B)
+    if headline:
+        macs = SURVEY_MACS_PER_SAMPLE  # the §8(d) contract figure (own derivation: td7_macs_per_sample)
+        flop_step = 2.0 * macs * B
+        bytes_step = td7_bytes_per_step(S, A, H, B, N_REPLAY)
+    else:
+        gflop, mb = WORK[(algo, env, batch)]
+        flop_step, bytes_step = gflop * 1e9, mb * 1e6
+    s_dim, a_dim, _ = TASKS[env]
     # launches per step: average over the policy / non-policy graphs (+ hard update amortised)
     launches = (lv_policy + lv_plain) / 2.0
     per_launch_s = gpu_s / (steps * launches)
@@ -160,7 +180,7 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain):
         "peak": PEAK_FP32_TFLOPS,
         "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_FP32_TFLOPS, 5),
-        "traffic": pmc_traffic(),
+        "traffic": pmc_traffic() if headline else None,
         "traffic_algorithmic": round(bytes_step / launches),
         "kernel": "rle_level (one launch per dependency level of the step graph)",
         "flop_per_step": flop_step,
@@ -169,8 +189,10 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain):
         "hbm_bytes_per_step_algorithmic": round(bytes_step),
         "hbm_achieved_GBs": round(bytes_step * steps / gpu_s / 1e9, 2),
     }
+    metric = METRIC if headline else (f"gradient-steps/sec, {algo.upper()} {env} batch={batch}"
+                                      f"{' LAP' if lap else ''} (secondary config)")
     return {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(value, 2),
         "unit": "gradient-steps/s",
         "n_gpus": n_gpus,
@@ -182,9 +204,9 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain):
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic",
-        "config": {"workload": "TD7 Humanoid-v4 gradient step, LAP over 1M HBM replay",
-                   "algo": "td7", "obs_dim": S, "act_dim": A, "hidden": H, "batch": B,
-                   "replay": N_REPLAY, "lap": True, "policy_freq": 2, "target_update_rate": 250,
+        "config": {"workload": f"{algo.upper()} {env} gradient step, {'LAP' if lap else 'uniform'} over 1M HBM replay",
+                   "algo": algo, "obs_dim": s_dim, "act_dim": a_dim, "hidden": H, "batch": batch,
+                   "replay": N_REPLAY, "lap": lap, "policy_freq": 2, "target_update_rate": 250,
                    "parallelism": f"replicas x{n_gpus} (one seed per GPU, no collective)"},
         "roofline": roofline,
         "gpu_event_s": round(gpu_s, 6),
@@ -198,7 +220,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--algo", choices=("td7", "td3", "sac"), default="td7")
+    ap.add_argument("--env", choices=tuple(TASKS), default="Humanoid-v4")
+    ap.add_argument("--batch", type=int, default=B)
     args = ap.parse_args()
+    if (args.algo, args.env, args.batch) not in WORK:
+        ap.error(f"no SURVEY §8(d) work figures for {args.algo} {args.env} B={args.batch}")
+    lap = args.algo == "td7"  # TD7 runs LAP (td7_exp.sh); SAC / TD3 the uniform replay
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -214,12 +242,14 @@ def main():
     from rl.nn.layout import init_agent
 
     # --- engine: one independent seed per GPU (seed 111, 222, ... as scripts/td7_exp.sh)
-    cfg = E.make_config(E.RLE_TD7, S, A, H, B, use_lap=True, seed=111 * (rank + 1), device=local)
+    s_dim, a_dim, _ = TASKS[args.env]
+    algo_id = {"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[args.algo]
+    cfg = E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=111 * (rank + 1), device=local)
     eng = E.Engine(cfg)
-    for net, params in init_agent("td7", S, A, H, 123 + rank).items():
+    for net, params in init_agent(args.algo, s_dim, a_dim, H, 123 + rank).items():
         for name, v in params.items():
             eng.set_param(net, name, v)
-    rep = E.Replay(N_REPLAY, S, A, True, device=local)
+    rep = E.Replay(N_REPLAY, s_dim, a_dim, lap, device=local)
     rep.fill_random(N_REPLAY, seed=rank)
     eng.bind(rep)
     lv_policy, lv_plain = eng.graph_stats()
@@ -239,9 +269,10 @@ def main():
         if dist:
             dist.barrier()
         return
-    out = summarize(world, args.steps, args.warmup, wall, gpu_s, lv_policy, lv_plain)
+    out = summarize(world, args.steps, args.warmup, wall, gpu_s, lv_policy, lv_plain, args.algo, args.env,
+                    args.batch, lap)
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.algo, args.env, args.batch, lap)
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

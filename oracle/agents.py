@@ -264,7 +264,7 @@ class SACOracle:
         obj += tmp_obj  # in place: logged policy loss includes the temperature loss (Q15)
         keys = list(self.pi.keys())
         gs = torch.autograd.grad(obj, [self.pi[k] for k in keys] + [self.log_alpha])
-        info["tmp"] = float(self.log_alpha.exp())
+        info["tmp"] = float(self.log_alpha.detach().exp())
         info["norm/tmp"] = float(gs[-1])
         self.opt_pi.step(gs[:-1])
         self.opt_t.step([gs[-1]])

@@ -140,3 +140,45 @@ def test_step_trajectory_matches_reference(name):
             d = np.abs(v - g[key])
             assert d.max() <= tol, (key, d.max())
             assert (d <= 1e-5).mean() >= 0.99, (key, (d <= 1e-5).mean())
+
+
+def _synthetic_golden(alg, env, H, B, ncap, n_fill, n_steps, use_lap, seed):
+    S, A, _ = spec.TASKS[env]
+    g = {"meta_alg": np.array(alg), "meta_env": np.array(env),
+         "meta": np.array([H, B, ncap, n_fill, n_steps, int(use_lap), seed]),
+         "meta_extra_keys": np.array([], dtype="<U1"), "meta_extra_vals": np.array([], np.float64)}
+    for k, v in spec.tapes(alg, B, A, n_steps, seed + 3).items():
+        g["tape_" + k] = v
+    return g
+
+
+def test_td7_humanoid_b1024_matches_oracle():
+    """BASELINE config 4 (TD7 Humanoid, LAP, B=1024): the oracle (pinned at B=256 by the
+    goldens) runs the same tapes on the host; the engine must agree step by step."""
+    from oracle import agents
+    from test_oracle import build_from_golden
+
+    g = _synthetic_golden("td7", "Humanoid-v4", 256, 1024, 8192, 8192, 2, True, 77)
+    alg, orc, orep, tp, n_steps, B = build_from_golden(g)
+    eng, rep, tp2 = engine_from_golden(g)
+    infos_ref, inds_ref = [], []
+    prios = []
+
+    def per_step(t):
+        np.testing.assert_array_equal(eng.last_indices(), inds_ref[t])
+        np.testing.assert_allclose(rep.get_priority(8192), prios[t], rtol=1e-4, atol=1e-5)
+
+    for t in range(n_steps):
+        i1, n1 = agents.run_steps(orc, alg, orep, {k: v[t:t + 1] for k, v in tp.items()}, 1, B)
+        infos_ref += i1
+        inds_ref += n1
+        prios.append(orep.priority.copy())
+    infos = run_with_tapes(eng, tp2, n_steps, per_step)
+    keys = ["train/encoder", "train/q_fn", "train/policy"]
+    ref = np.array([[np.nan if i[k] is None else i[k] for k in keys] for i in infos_ref])
+    np.testing.assert_allclose(infos[:, :3], ref, rtol=2e-3, atol=1e-4, equal_nan=True)
+    tol = 2 * 3e-4 * n_steps + 1e-4
+    for net, d in orc.nets().items():
+        for name, v in d.items():
+            got = eng.get_param(net, name, tuple(v.shape))
+            assert np.abs(got - v.detach().numpy()).max() <= tol, (net, name)
