@@ -30,7 +30,8 @@ int level_capacity();
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count,
-                         int Sp, int Ap, const float* max_priority, int lap, hipStream_t st);
+                         int Sp, int Ap, const float* max_priority, int lap, double* bsum,
+                         long long size_before, hipStream_t st);
 hipError_t launch_fill(float* state, float* next_state, float* action, float* reward, float* notdone,
                        float* priority, long long n, int S, int Sp, int A, int Ap, unsigned long long seed,
                        hipStream_t st);
@@ -811,14 +812,7 @@ struct Engine {
 
   // ---------------------------------------------------------------- step programs
   void add_sampling(Prog& pg, bool sac) {
-    Replay& rp = *replay;
-    if (rp.lap) {
-      Op op{};
-      op.kind = OP_SAMPLE_REDUCE;
-      fill_sample_args(op.sample, sac);
-      op.wg_count = rp.nblk;
-      pg.add(op, {R_PRIO}, {bsum_id});
-    }
+    // LAP block sums are maintained by every priority write (OP_PRIORITY, appends)
     Op op{};
     op.kind = OP_SAMPLE_GATHER;
     fill_sample_args(op.sample, sac);
@@ -1077,8 +1071,9 @@ struct Engine {
       op.prio.p = prio.p;
       op.prio.B = B;
       op.prio.max_priority = replay->maxp_d;
+      op.prio.bsum = replay->lap ? replay->bsum : nullptr;
       op.wg_count = 1;
-      pg.add(op, {prio.id, ind_id, bsum_id}, {R_PRIO, R_MAXP});
+      pg.add(op, {prio.id, ind_id}, {R_PRIO, R_MAXP, bsum_id});
     }
     for (int n = 0; n < 2; ++n) {  // critic backward + Adam (optim_q_fns spans q1 + q2)
       Net& Q = *q[n];
@@ -1298,8 +1293,9 @@ struct Engine {
       op.prio.p = prio.p;
       op.prio.B = B;
       op.prio.max_priority = replay->maxp_d;
+      op.prio.bsum = replay->lap ? replay->bsum : nullptr;
       op.wg_count = 1;
-      pg.add(op, {prio.id, ind_id, bsum_id}, {R_PRIO, R_MAXP});
+      pg.add(op, {prio.id, ind_id}, {R_PRIO, R_MAXP, bsum_id});
     }
     for (int n = 0; n < 2; ++n) {
       Net& Q = *q[n];
@@ -1809,7 +1805,7 @@ int rle_replay_append(rle_replay* h, const float* state, const float* action, co
       HIPCHK(rle::launch_append(r.state, r.next_state, r.action, r.reward, r.notdone, r.priority, ds,
                                 ds + (size_t)c * r.Sp, ds + 2 * (size_t)c * r.Sp, ds + 2 * (size_t)c * r.Sp + c * r.Ap,
                                 ds + 2 * (size_t)c * r.Sp + c * r.Ap + c, r.ptr, r.cap, (int)c, r.Sp, r.Ap, r.maxp_d,
-                                r.lap, r.stream));
+                                r.lap, r.bsum, r.size, r.stream));
       r.ptr = (r.ptr + c) % r.cap;
       r.size = std::min(r.size + c, r.cap);
       HIPCHK(hipMemcpyAsync(r.size_d, &r.size, sizeof(long long), hipMemcpyHostToDevice, r.stream));
@@ -1832,6 +1828,8 @@ int rle_replay_state(rle_replay* h, long long* ptr, long long* size, float* max_
   });
 }
 
+static void recompute_bsum(Replay& r);
+
 int rle_replay_fill_random(rle_replay* h, long long count, unsigned long long seed) {
   return guard([&] {
     Replay& r = h->r;
@@ -1843,6 +1841,7 @@ int rle_replay_fill_random(rle_replay* h, long long count, unsigned long long se
     r.ptr = count % r.cap;
     HIPCHK(hipMemcpyAsync(r.size_d, &r.size, sizeof(long long), hipMemcpyHostToDevice, r.stream));
     HIPCHK(hipStreamSynchronize(r.stream));
+    if (r.lap) recompute_bsum(r);
   });
 }
 
@@ -1860,6 +1859,7 @@ int rle_replay_set_priority(rle_replay* h, const float* p, long long n, float ma
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(h->r.priority, p, n * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->r.maxp_d, &max_priority, 4, hipMemcpyHostToDevice));
+    if (h->r.lap) recompute_bsum(h->r);
   });
 }
 
@@ -1876,6 +1876,19 @@ static void run_eager(Replay& r, rle::DevMem& tmp, std::vector<std::vector<rle::
     HIPCHK(rle::launch_level(d, lv.data(), (int)lv.size(), wg, r.stream));
   }
   HIPCHK(hipStreamSynchronize(r.stream));
+}
+
+// Full recompute of the LAP block sums (after bulk priority writes).  In-step and
+// eager priority scatters and appends keep them exact incrementally.
+static void recompute_bsum(Replay& r) {
+  rle::DevMem tmp;
+  rle::Op a{};
+  a.kind = rle::OP_SAMPLE_REDUCE;
+  a.sample.priority = r.priority;
+  a.sample.size = r.size_d;
+  a.sample.bsum = r.bsum;
+  a.wg_count = r.nblk;
+  run_eager(r, tmp, {{a}});
 }
 
 int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* ind_out) {
@@ -1928,13 +1941,6 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     s.tape_u = du;
     s.tape_eps = tmp.make<float>((size_t)n * r.A);
     std::vector<std::vector<rle::Op>> lv;
-    if (r.lap) {
-      rle::Op a{};
-      a.kind = rle::OP_SAMPLE_REDUCE;
-      a.sample = s;
-      a.wg_count = r.nblk;
-      lv.push_back({a});
-    }
     rle::Op b{};
     b.kind = rle::OP_SAMPLE_GATHER;
     b.sample = s;
@@ -1961,6 +1967,7 @@ int rle_replay_update_priority(rle_replay* h, int n, const long long* ind, const
     op.prio.p = dp;
     op.prio.B = n;
     op.prio.max_priority = r.maxp_d;
+    op.prio.bsum = r.lap ? r.bsum : nullptr;
     op.wg_count = 1;
     run_eager(r, tmp, {{op}});
   });

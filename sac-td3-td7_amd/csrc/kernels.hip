@@ -996,7 +996,14 @@ __device__ __forceinline__ void op_priority(const CAS PriorityArgs& a, float* sm
     const int b = threadIdx.x + u * kThreads;
     if (b >= a.B) continue;
     const float pv = G(a.p)[b];
-    if (last[myslot[u & 3]] == b) GW(a.priority)[mine[u & 3]] = pv;
+    if (last[myslot[u & 3]] == b) {
+      // the block sums follow every priority write exactly: fp64 differences of fp32
+      // priorities (>= 1, lap.py) and their sums are exact, so any order gives the sums
+      // a full recompute would (op_sample_reduce)
+      const int key = mine[u & 3];
+      if (a.bsum) atomicAdd(&a.bsum[key / kBlk], (double)pv - (double)G(a.priority)[key]);
+      GW(a.priority)[key] = pv;
+    }
     mx = fmaxf(mx, pv);
   }
 #pragma unroll
@@ -1294,7 +1301,8 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
 __global__ void rle_append_kernel(float* state, float* next_state, float* action, float* reward, float* notdone,
                                   float* priority, const float* st_s, const float* st_ns, const float* st_a,
                                   const float* st_r, const float* st_d, long long ptr, long long cap, int count,
-                                  int Sp, int Ap, const float* max_priority, int lap) {
+                                  int Sp, int Ap, const float* max_priority, int lap, double* bsum,
+                                  long long size_before) {
   const int i = blockIdx.x;
   if (i >= count) return;
   const long long row = (ptr + i) % cap;
@@ -1306,7 +1314,12 @@ __global__ void rle_append_kernel(float* state, float* next_state, float* action
   if (threadIdx.x == 0) {
     reward[row] = st_r[i];
     notdone[row] = st_d[i];
-    if (lap) priority[row] = *max_priority;
+    if (lap) {  // lap.py:41, with the block sum following the write (rows past size count as 0)
+      const float nv = *max_priority;
+      const float old = row < size_before ? priority[row] : 0.f;
+      priority[row] = nv;
+      atomicAdd(&bsum[row / kBlk], (double)nv - (double)old);
+    }
   }
 }
 
@@ -1362,9 +1375,11 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count, int Sp,
-                         int Ap, const float* max_priority, int lap, hipStream_t st) {
+                         int Ap, const float* max_priority, int lap, double* bsum, long long size_before,
+                         hipStream_t st) {
   hipLaunchKernelGGL(rle_append_kernel, dim3(count), dim3(256), 0, st, state, next_state, action, reward, notdone,
-                     priority, st_s, st_ns, st_a, st_r, st_d, ptr, cap, count, Sp, Ap, max_priority, lap);
+                     priority, st_s, st_ns, st_a, st_r, st_d, ptr, cap, count, Sp, Ap, max_priority, lap, bsum,
+                     size_before);
   return hipGetLastError();
 }
 hipError_t launch_fill(float* state, float* next_state, float* action, float* reward, float* notdone,

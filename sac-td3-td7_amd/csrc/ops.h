@@ -205,6 +205,7 @@ struct SampleArgs {
 struct PriorityArgs {
   float* priority; const long long* ind; const float* p; int B;
   float* max_priority;
+  double* bsum;          // LAP block sums kept in step with the scatter (nullptr: none)
 };
 
 struct SacActorArgs {
