@@ -123,7 +123,7 @@ __device__ __forceinline__ int fkey(float f) {
 __device__ __forceinline__ float unkey(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
 
 // Philox4x32-10 counter-based RNG.
-__device__ __attribute__((noinline)) uint4 philox(uint2 key, uint4 c) {
+__device__ __forceinline__ uint4 philox(uint2 key, uint4 c) {
 #pragma unroll 1
   for (int i = 0; i < 10; ++i) {
     unsigned hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
@@ -246,15 +246,13 @@ __device__ __forceinline__ void mat_st4(const CAS Mat& m, int r, int c, float4 v
 __device__ __forceinline__ void trace_mark(unsigned long long* tr, int slot) {
   if (tr && threadIdx.x == 0) tr[slot] = __builtin_amdgcn_s_memrealtime();
 }
+// Diagnostics builds (-DRLE_TRACE_FINE, tools only): 12 more stamps per workgroup
+// in the same trace buffer (SGPR pointer: a stamp never waits on a load).
 #ifdef RLE_TRACE_FINE
-constexpr int kTraceSlots = 8;
-__device__ unsigned long long* g_fine;
-#define FINE_MARK(slot)                                                                       \
-  do {                                                                                        \
-    if (g_fine && threadIdx.x == 0)                                                           \
-      g_fine[(size_t)blockIdx.x * kTraceSlots + (slot)] = __builtin_amdgcn_s_memrealtime();   \
-  } while (0)
+constexpr int kTraceStride = 16;
+#define FINE_MARK(slot) trace_mark(tr, 4 + (slot))
 #else
+constexpr int kTraceStride = 4;
 #define FINE_MARK(slot) \
   do {                  \
   } while (0)
@@ -818,13 +816,13 @@ __device__ __forceinline__ double wave_scan_incl_d(double v) {
 // Exclusive scan of one double per thread over the workgroup (fixed order; the
 // priority sums are exact in fp64, so the order does not change a value, Q8).
 __device__ __forceinline__ double wg_scan_excl_d(double v, double* wtot, double& total) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const double inc = wave_scan_incl_d(v);
   if (lane == 63) wtot[wave] = inc;
   __syncthreads();
-  double before = 0.0;
-  for (int w = 0; w < wave; ++w) before += wtot[w];
-  total = ((wtot[0] + wtot[1]) + wtot[2]) + wtot[3];
+  const double w0 = wtot[0], w1 = wtot[1], w2 = wtot[2], w3 = wtot[3];
+  const double before = (wave > 0 ? w0 : 0.0) + (wave > 1 ? w1 : 0.0) + (wave > 2 ? w2 : 0.0);
+  total = ((w0 + w1) + w2) + w3;
   return before + (inc - v);
 }
 
@@ -837,6 +835,22 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
   const long long pos = sload(s.tape_pos);
   const uint2 key = make_uint2((unsigned)s.seed, (unsigned)(s.seed >> 32));
   const unsigned long long step = (unsigned long long)sload(s.ctrl_rng);
+  FINE_MARK(0);
+  const bool tind = tape & kTapeInd;
+  float u = 0.f;
+  if (!tind) {
+    if (tape & kTapeU) u = G(s.tape_u)[(size_t)pos * s.B + b];
+    else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
+  }
+  // LAP: the block-sum loads go out first and the noise below runs while they are in
+  // flight.  Thread tid owns blocks [tid*per, tid*per + per), per <= 8 (capacity <= 8M).
+  const int nb = (int)((size + kBlk - 1) / kBlk);
+  const int per = (nb + kThreads - 1) / kThreads;
+  double bs[8];
+  if (!tind && s.lap) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bs[q] = G(s.bsum)[min(tid * per + q, nb - 1)];
+  }
   // noise tensors for this row (T images)
   for (int j = tid; j < s.A; j += kThreads) {
     float e, e2 = 0.f;
@@ -851,14 +865,11 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
     mat_st(s.eps, b, j, e);
     if (s.eps2.t) mat_st(s.eps2, b, j, e2);
   }
-  long long* found = reinterpret_cast<long long*>(smem);  // [1]
+  FINE_MARK(1);
   long long ind;
-  if (tape & kTapeInd) {
+  if (tind) {
     ind = G(s.tape_ind)[(size_t)pos * s.B + b];
   } else {
-    float u;
-    if (tape & kTapeU) u = G(s.tape_u)[(size_t)pos * s.B + b];
-    else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
     if (tid == 0) GW(s.u_out)[b] = u;
     if (!s.lap) {
       // searchsorted(cumsum(ones(size)), u*size): first j in 1..size with j >= v
@@ -866,25 +877,22 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
       const long long k = (long long)ceilf(v) - 1;
       ind = k < 0 ? 0 : (k > size - 1 ? size - 1 : k);
     } else {
-      // exact fp64 prefix over block sums, rounded to fp32 per element (Q8); thread
-      // tid owns blocks [tid*per, tid*per + per), per <= 8 (capacity <= 8M)
-      const int nb = (int)((size + kBlk - 1) / kBlk);
-      const int per = (nb + kThreads - 1) / kThreads;
-      double* wtot = reinterpret_cast<double*>(smem) + 2;  // [4]
-      int* fblk = reinterpret_cast<int*>(smem + 24);        // [1]
-      double* fbase = reinterpret_cast<double*>(smem) + 10;  // [1]
-      double bs[8];
+      // exact fp64 prefix over block sums, rounded to fp32 per element (Q8)
+      const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+      double* wtot = reinterpret_cast<double*>(smem) + 2;  // [8]: two scans
+      int* wm = reinterpret_cast<int*>(smem + 32);          // [4] per-wave first block
+      double* wb = reinterpret_cast<double*>(smem) + 18;    // [4] its prefix base
+      int* wh = reinterpret_cast<int*>(smem + 48);          // [4] per-wave first hit
       double loc = 0.0;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int k = tid * per + q;
-        bs[q] = G(s.bsum)[min(k, nb - 1)];
-        if (q >= per || k >= nb) bs[q] = 0.0;
+        if (q >= per || tid * per + q >= nb) bs[q] = 0.0;
         loc += bs[q];
       }
-      if (tid == 0) *fblk = 0x7FFFFFFF;
+      FINE_MARK(2);
       double total;
       double run = wg_scan_excl_d(loc, wtot, total);
+      FINE_MARK(3);
       const float v = u * (float)total;
       // first block whose rounded inclusive prefix >= v (the last block if none)
       int mine = 0x7FFFFFFF;
@@ -900,13 +908,35 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
           run += bs[q];
         }
       }
-      if (mine != 0x7FFFFFFF) atomicMin(fblk, mine);
+      // the qualifying blocks form a suffix in thread order (monotone prefix), so the
+      // answer is the first qualifying lane of the first wave that has one: ballot +
+      // readlane per wave, no atomics (whose per-lane loops cost microseconds here)
+      {
+        const unsigned long long bal = __ballot(mine != 0x7FFFFFFF);
+        int m = 0x7FFFFFFF;
+        double mb = 0.0;
+        if (bal) {
+          const int fl = __builtin_ffsll((long long)bal) - 1;
+          m = __builtin_amdgcn_readlane(mine, fl);
+          mb = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(mbase), fl),
+                                __builtin_amdgcn_readlane(__double2loint(mbase), fl));
+        }
+        if (lane == 0) {
+          wm[wave] = m;
+          wb[wave] = mb;
+        }
+      }
       __syncthreads();
-      const int lo = *fblk;
+      int lo = 0x7FFFFFFF;
+      double base = 0.0;
+#pragma unroll
+      for (int w = 3; w >= 0; --w) {
+        if (wm[w] != 0x7FFFFFFF) {
+          lo = wm[w];
+          base = wb[w];
+        }
+      }
       trace_mark(tr, 1);
-      if (mine == lo) *fbase = mbase;
-      __syncthreads();
-      const double base = *fbase;
       const long long e0 = (long long)lo * kBlk + (long long)tid * 16;
       // 16 priorities per thread: four 16-byte buffer loads (past the capacity read 0)
       const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
@@ -927,36 +957,57 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
         if (e0 + q >= size) pv[q] = 0.f;
         tl += (double)pv[q];
       }
-      if (tid == 0) *found = 0x7FFFFFFFFFFFFFFFll;
+      FINE_MARK(4);
       double btot;
       run = base + wg_scan_excl_d(tl, wtot + 4, btot);
-      long long hit = 0x7FFFFFFFFFFFFFFFll;
+      FINE_MARK(5);
+      int hit = 0x7FFFFFFF;  // offset in the block
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         run += (double)pv[q];
-        if (hit == 0x7FFFFFFFFFFFFFFFll && e0 + q < size && (float)run >= v) hit = e0 + q;
+        if (hit == 0x7FFFFFFF && e0 + q < size && (float)run >= v) hit = tid * 16 + q;
       }
-      if (hit != 0x7FFFFFFFFFFFFFFFll) atomicMin((unsigned long long*)found, (unsigned long long)hit);
+      {
+        const unsigned long long bal = __ballot(hit != 0x7FFFFFFF);
+        const int h = bal ? __builtin_amdgcn_readlane(hit, __builtin_ffsll((long long)bal) - 1) : 0x7FFFFFFF;
+        if (lane == 0) wh[wave] = h;
+      }
       __syncthreads();
-      ind = *found;
+      int off = 0x7FFFFFFF;
+#pragma unroll
+      for (int w = 3; w >= 0; --w)
+        if (wh[w] != 0x7FFFFFFF) off = wh[w];
+      ind = off == 0x7FFFFFFF ? size - 1 : (long long)lo * kBlk + off;
       if (ind >= size) ind = size - 1;
     }
   }
   trace_mark(tr, 2);
   // gather the transition into the batch images (rows b and B + b of ss): thread
-  // tid moves columns 4 tid .. 4 tid + 3 (rows are 16-float aligned)
+  // tid moves columns 4 tid .. 4 tid + 3 (rows are 16-float aligned); every load is
+  // issued before any store (one memory round trip)
   const int c = 4 * tid;
+  float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0, va = v0;
+  float rv = 0.f, dv = 0.f;
   if (c < s.Sp) {
-    const float4 v0 = ld4g(G(s.state) + (size_t)ind * s.Sp + c), v1 = ld4g(G(s.next_state) + (size_t)ind * s.Sp + c);
+    v0 = ld4g(G(s.state) + (size_t)ind * s.Sp + c);
+    v1 = ld4g(G(s.next_state) + (size_t)ind * s.Sp + c);
+  }
+  if (c < s.Ap) va = ld4g(G(s.action) + (size_t)ind * s.Ap + c);
+  if (tid == 0) {
+    rv = G(s.reward)[ind];
+    dv = G(s.notdone)[ind];
+  }
+  if (c < s.Sp) {
     mat_str4(s.ss, b, c, v0);
     mat_str4(s.ss, s.B + b, c, v1);
   }
-  if (c < s.Ap) mat_str4(s.a, b, c, ld4g(G(s.action) + (size_t)ind * s.Ap + c));
+  if (c < s.Ap) mat_str4(s.a, b, c, va);
   if (tid == 0) {
-    GW(s.r)[b] = G(s.reward)[ind];
-    GW(s.nd)[b] = G(s.notdone)[ind];
+    GW(s.r)[b] = rv;
+    GW(s.nd)[b] = dv;
     GW(s.ind)[b] = ind;
   }
+  FINE_MARK(6);
 }
 
 // LAPReplayMemory.update_priority (lap.py:66-69): last duplicate wins (Q9).
@@ -1249,7 +1300,7 @@ __device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
 
 __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
   __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
-  unsigned long long* tr = la.trace ? la.trace + (size_t)blockIdx.x * 4 : nullptr;
+  unsigned long long* tr = la.trace ? la.trace + (size_t)blockIdx.x * kTraceStride : nullptr;
   trace_mark(tr, 0);
   const CAS Op* ops = (const CAS Op*)la.ops;
   const int wg = blockIdx.x;
@@ -1278,7 +1329,12 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
 #ifndef RLE_EXP_GEMM_ONLY
     RLE_OP(OP_NORMBWD, op_normbwd(op.nb, t))
     RLE_OP(OP_SAMPLE_REDUCE, op_sample_reduce(op.sample, t, smem))
+#ifdef RLE_EXP_TWICE  // diagnostics: the stamps of a second, cache-warm pass overwrite the first
+    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather(op.sample, t, smem, tr); __syncthreads();
+           op_sample_gather(op.sample, t, smem, tr))
+#else
     RLE_OP(OP_SAMPLE_GATHER, op_sample_gather(op.sample, t, smem, tr))
+#endif
     RLE_OP(OP_HEAD, op_head(op.head, t, smem, tr))
     RLE_OP(OP_PRIORITY, op_priority(op.prio, smem))
     RLE_OP(OP_SAC_ACTOR, op_sac_actor(op.sac, t))

@@ -106,9 +106,6 @@ static void phases(const char* name, int nwg) {
          med(epi));
 }
 
-#ifdef RLE_TRACE_FINE
-namespace rle { extern __device__ unsigned long long* g_fine; }
-#endif
 
 int main() {
   hipStream_t st;
@@ -178,27 +175,6 @@ int main() {
   }
   CK(hipFree(g_trace));
   g_trace = nullptr;
-#ifdef RLE_TRACE_FINE
-  {
-    unsigned long long* fine;
-    CK(hipMalloc(&fine, 8 * 8 * 4096));
-    CK(hipMemcpyToSymbol(HIP_SYMBOL(rle::g_fine), &fine, 8));
-    CK(hipMalloc(&g_trace, 8 * 4 * 4096));
-    for (int Kk : {16, 256}) {
-      Op o = fwd_op(X, W, bb, Y, 16, 64, Kk);
-      time_level({o}, 20, st);
-      unsigned long long t[4], f[8];
-      CK(hipMemcpy(t, g_trace, 32, hipMemcpyDeviceToHost));
-      CK(hipMemcpy(f, fine, 64, hipMemcpyDeviceToHost));
-      printf("fine 1WG K=%d: entry->mark1 %.2f | ->lane_op %.2f ->seek %.2f ->issue %.2f ->loop end %.2f ->ret %.2f "
-             "->splitK %.2f ->exit %.2f us\n", Kk, (t[1] - t[0]) * 0.01, (f[0] - t[1]) * 0.01, (f[1] - f[0]) * 0.01,
-             (f[2] - f[1]) * 0.01, (f[3] - f[2]) * 0.01, (f[4] - f[3]) * 0.01, (f[5] - f[4]) * 0.01,
-             (t[3] - f[5]) * 0.01);
-    }
-    CK(hipFree(g_trace));
-    g_trace = nullptr;
-  }
-#endif
   for (int M : {256, 512}) {
     Op o = fwd_op(X, W, bb, Y, M, N, K);
     printf("fwd %dx%dx%d (%d WG): %8.2f us\n", M, N, K, o.wg_count, time_level({o}, reps, st));
