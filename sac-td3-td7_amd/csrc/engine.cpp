@@ -110,6 +110,9 @@ struct Replay {
   // append staging
   float* stage = nullptr;
   long long stage_rows = 0;
+  // bumped by every change of what sampling draws from (appends, priority writes):
+  // an engine's batch prefetched under another version is stale
+  unsigned long long version = 0;
 };
 
 // ------------------------------------------------------------------ programs
@@ -309,14 +312,44 @@ struct Engine {
   std::vector<float> info_host;
   Replay* replay = nullptr;
   int next_id = R_FIRST_DYNAMIC;
-  Graph g_policy, g_plain, g_hard;
+  // Graphs per batch-buffer parity p: g_prime[p] samples batch p (draws of the next
+  // step); g_pol[p] / g_pln[p] run a (policy / plain) step on batch p and, once its
+  // priority update is done, prefetch the next step's batch into 1 - p.
+  Graph g_prime[2], g_pol[2], g_pln[2], g_hard;
+  // (diagnostics: the parity that last ran; with policy_freq 2 policy and plain steps
+  // alternate, so each kind always runs on the same parity)
+  int pol_set = 0, pln_set = 0;
+  const Graph& policy_graph() const { return g_pol[pol_set]; }
+  const Graph& plain_graph() const { return algo == RLE_SAC ? g_pol[pol_set] : g_pln[pln_set]; }  // SAC: every step
   bool built = false;
   long long n_runs = 0;  // host mirror of the agent's step counter
-  // step buffers
-  View ss, act_in, rw, nd, eps, eps2;
+  int cur_set = 0, last_set = 0;       // batch the next step runs on / the last step ran on
+  bool primed = false;                 // batch cur_set holds the next step's draws
+  unsigned long long primed_ver = 0;   // replay version it was drawn under
+  // step buffers: two batch sets (the running step's and the prefetched next one)
+  struct BatchSet {
+    View ss, act_in, rw, nd, eps, eps2;
+    long long* ind = nullptr;
+    float* u_buf = nullptr;
+    int ind_id = -1;
+  };
+  BatchSet bsets[2];
+  View ss, act_in, rw, nd, eps, eps2;  // the set a program is being built on (use_set)
   long long* ind = nullptr;
   float* u_buf = nullptr;
   double* bsum = nullptr;
+  void use_set(int k) {
+    const BatchSet& b = bsets[k];
+    ss = b.ss;
+    act_in = b.act_in;
+    rw = b.rw;
+    nd = b.nd;
+    eps = b.eps;
+    eps2 = b.eps2;
+    ind = b.ind;
+    u_buf = b.u_buf;
+    ind_id = b.ind_id;
+  }
   // tapes
   float *t_u = nullptr, *t_eps = nullptr, *t_eps2 = nullptr;
   long long* t_ind = nullptr;
@@ -811,15 +844,21 @@ struct Engine {
   }
 
   // ---------------------------------------------------------------- step programs
-  void add_sampling(Prog& pg, bool sac) {
+  void add_sampling(Prog& pg, bool sac, int ahead) {
     // LAP block sums are maintained by every priority write (OP_PRIORITY, appends)
     Op op{};
     op.kind = OP_SAMPLE_GATHER;
     fill_sample_args(op.sample, sac);
+    op.sample.ahead = ahead;
     op.wg_count = B;
     // reads the RNG step / tape position counters -> ordered before STEP_END (WAR)
-    pg.add(op, {bsum_id, R_PRIO, R_REPLAY, R_CNT},
-           {ss.id, act_in.id, rw.id, nd.id, eps.id, ind_id, sac ? eps2.id : -1});
+    pg.add(op, {bsum_id, R_PRIO, R_REPLAY, R_CNT}, {ss.id, act_in.id, rw.id, nd.id, ind_id});
+    Op nz{};
+    nz.kind = OP_NOISE;
+    fill_sample_args(nz.sample, sac);
+    nz.sample.ahead = ahead;
+    nz.wg_count = cdiv(B * A, kThreads);
+    pg.add(nz, {R_CNT}, {eps.id, sac ? eps2.id : -1});
   }
   int bsum_id = -1, ind_id = -1;
 
@@ -917,7 +956,19 @@ struct Engine {
   }
 
   // TD7 (td7.py:287-332)
-  void build_td7(Prog& pg, bool policy) {
+  // Next step's batch into the other buffer set, after this step's priority update
+  // (RAW on the priorities) and before STEP_END bumps the counters (WAR).
+  void add_prefetch(Prog& pg, bool sac, int set) {
+    use_set(1 - set);
+    add_sampling(pg, sac, 1);
+    use_set(set);
+  }
+  void build_prime(Prog& pg, bool sac, int set) {
+    use_set(set);
+    add_sampling(pg, sac, 0);
+  }
+
+  void build_td7(Prog& pg, bool policy, int set) {
     const int B2 = 2 * B;
     Net& enc = net("encoder");
     Net& fe = net("fixed_encoder");
@@ -926,8 +977,8 @@ struct Engine {
     Net* q[2] = {&net("q1"), &net("q2")};
     Net* tq[2] = {&net("target_q1"), &net("target_q2")};
     const bool lap = cfg.use_lap;
+    use_set(set);
     add_adam_scalars(pg);
-    add_sampling(pg, false);
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
     // ---- encoder phase (td7.py:246-257): online encoder on [s; s'] (one GEMM per layer)
     View ez1, ez2;
@@ -1075,6 +1126,7 @@ struct Engine {
       op.wg_count = 1;
       pg.add(op, {prio.id, ind_id}, {R_PRIO, R_MAXP, bsum_id});
     }
+    add_prefetch(pg, false, set);
     for (int n = 0; n < 2; ++n) {  // critic backward + Adam (optim_q_fns spans q1 + q2)
       Net& Q = *q[n];
       dw(pg, Q.layers[3], dq[n], {c2[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
@@ -1200,15 +1252,15 @@ struct Engine {
   }
 
   // TD3 (td3.py:206-242) and SAC (sac.py:251-295)
-  void build_mlp(Prog& pg, bool policy) {
+  void build_mlp(Prog& pg, bool policy, int set) {
     const bool sac = algo == RLE_SAC;
     const int B2 = 2 * B;
     Net& pi = net("policy");
     Net* q[2] = {&net("q1"), &net("q2")};
     Net* tq[2] = {&net("target_q1"), &net("target_q2")};
     const bool lap = cfg.use_lap && !sac;
+    use_set(set);
     add_adam_scalars(pg);
-    add_sampling(pg, sac);
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
     // actor on [s; s'] (target policy aliases the policy, Q1; SAC policy unchanged until its step)
     View h0 = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_RELU, nullptr, false);
@@ -1297,6 +1349,7 @@ struct Engine {
       op.wg_count = 1;
       pg.add(op, {prio.id, ind_id}, {R_PRIO, R_MAXP, bsum_id});
     }
+    add_prefetch(pg, sac, set);
     for (int n = 0; n < 2; ++n) {
       Net& Q = *q[n];
       dw(pg, Q.layers[2], dq[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
@@ -1467,7 +1520,7 @@ struct Engine {
       total += lv.size();
     }
     static const char* kname[] = {"?", "gemm", "normbwd", "sreduce", "sgather", "head", "prio",
-                                  "sacfwd", "sacbwd", "end", "polyak", "copy", "maxred", "ctrl"};
+                                  "sacfwd", "sacbwd", "end", "polyak", "copy", "maxred", "ctrl", "noise"};
     for (size_t l = 0; l < levels.size(); ++l) {
       G.desc += "L" + std::to_string(l) + " wg=" + std::to_string(G.nwg[l]) + ":";
       for (auto& op : levels[l]) {
@@ -1509,15 +1562,18 @@ struct Engine {
   }
 
   void alloc_step_buffers() {
-    ss = buf(2 * B, S);
-    act_in = buf(B, A);
-    rw = vec(B);
-    nd = vec(B);
-    eps = buf(B, A, false, true);
-    eps2 = buf(B, A, false, true);
-    ind = mem.make<long long>(B);
-    u_buf = mem.make<float>(B);
-    ind_id = next_id++;
+    for (BatchSet& b : bsets) {
+      b.ss = buf(2 * B, S);
+      b.act_in = buf(B, A);
+      b.rw = vec(B);
+      b.nd = vec(B);
+      b.eps = buf(B, A, false, true);
+      b.eps2 = buf(B, A, false, true);
+      b.ind = mem.make<long long>(B);
+      b.u_buf = mem.make<float>(B);
+      b.ind_id = next_id++;
+    }
+    use_set(0);
     bsum_id = next_id++;
   }
 
@@ -1526,10 +1582,11 @@ struct Engine {
     // tapes are referenced by captured graphs: allocate once at a generous size
     REQUIRE(!built || n <= tape_cap, "tape larger than the capacity fixed at first use");
     tape_cap = std::max<long long>(n, 1024);
-    t_u = mem.make<float>((size_t)tape_cap * B);
-    t_eps = mem.make<float>((size_t)tape_cap * B * A);
-    t_eps2 = mem.make<float>((size_t)tape_cap * B * A);
-    t_ind = mem.make<long long>((size_t)tape_cap * B);
+    // + 1 row: the last taped step prefetches (and the host discards) one row past the end
+    t_u = mem.make<float>((size_t)(tape_cap + 1) * B);
+    t_eps = mem.make<float>((size_t)(tape_cap + 1) * B * A);
+    t_eps2 = mem.make<float>((size_t)(tape_cap + 1) * B * A);
+    t_ind = mem.make<long long>((size_t)(tape_cap + 1) * B);
   }
 
   // Builds a step program twice: the first pass fixes the level schedule, then
@@ -1543,11 +1600,13 @@ struct Engine {
     Prog p0;
     f(p0);
     std::vector<int> plan(tn_seq, 16);
+    const char* tmin = std::getenv("RLE_TN_MIN");  // tuning experiments
     auto levels = p0.schedule();
     for (auto& lv : levels)
       for (auto& op : lv)
-        if (op.kind == OP_GEMM) plan[op.seq] = op.gemm.tn;
-    const int cap = std::max(256, level_capacity());
+        if (op.kind == OP_GEMM) plan[op.seq] = std::max(op.gemm.tn, tmin ? std::atoi(tmin) : 16);
+    int cap = std::max(256, level_capacity());
+    if (const char* e = std::getenv("RLE_LEVEL_CAP")) cap = std::max(1, std::atoi(e));  // tuning experiments
     auto wg_of = [&](const Op& op) {
       if (op.kind != OP_GEMM) return op.wg_count;
       const GemmArgs& g = op.gemm;
@@ -1579,24 +1638,31 @@ struct Engine {
   void build() {
     REQUIRE(replay, "no replay bound");
     ensure_tapes(1024);
+    const bool sac = algo == RLE_SAC;
+    for (int set = 0; set < 2; ++set) {
+      Prog pp;
+      build_prime(pp, sac, set);
+      g_prime[set] = capture(pp);
+      if (algo == RLE_TD7) {
+        Prog p1 = plan_build([&](Prog& p) { build_td7(p, true, set); });
+        g_pol[set] = capture(p1);
+        Prog p2 = plan_build([&](Prog& p) { build_td7(p, false, set); });
+        g_pln[set] = capture(p2);
+      } else {
+        Prog p1 = plan_build([&](Prog& p) { build_mlp(p, true, set); });
+        g_pol[set] = capture(p1);
+        if (!sac) {
+          Prog p2 = plan_build([&](Prog& p) { build_mlp(p, false, set); });
+          g_pln[set] = capture(p2);
+        }
+      }
+    }
     if (algo == RLE_TD7) {
-      Prog p1 = plan_build([&](Prog& p) { build_td7(p, true); });
-      g_policy = capture(p1);
-      Prog p2 = plan_build([&](Prog& p) { build_td7(p, false); });
-      g_plain = capture(p2);
       Prog ph;
       build_td7_hard(ph);
       g_hard = capture(ph);
-    } else if (algo == RLE_TD3) {
-      Prog p1 = plan_build([&](Prog& p) { build_mlp(p, true); });
-      g_policy = capture(p1);
-      Prog p2 = plan_build([&](Prog& p) { build_mlp(p, false); });
-      g_plain = capture(p2);
-    } else {
-      Prog p1 = plan_build([&](Prog& p) { build_mlp(p, true); });
-      g_policy = capture(p1);
-      g_plain = g_policy;
     }
+    use_set(0);
     built = true;
   }
 
@@ -1660,17 +1726,29 @@ struct Engine {
           REQUIRE(tape_left > 0, "tape exhausted");
           --tape_left;
         }
+        // the batch of this step: prefetched by the previous step, unless anything it was
+        // drawn from has changed since (appends, other writers of the priorities, tapes)
+        if (!primed || primed_ver != replay->version) HIPCHK(hipGraphLaunch(g_prime[cur_set].x, stream));
+        const int p = cur_set;
         if (algo == RLE_TD7) {
           ++n_runs;  // td7.py:295 (increment first)
-          HIPCHK(hipGraphLaunch((n_runs % pf == 0) ? g_policy.x : g_plain.x, stream));
+          (n_runs % pf == 0 ? pol_set : pln_set) = p;
+          HIPCHK(hipGraphLaunch((n_runs % pf == 0) ? g_pol[p].x : g_pln[p].x, stream));
           if (n_runs % std::max(1, cfg.target_update_rate) == 0) HIPCHK(hipGraphLaunch(g_hard.x, stream));
         } else if (algo == RLE_TD3) {
-          HIPCHK(hipGraphLaunch((n_runs % pf == 0) ? g_policy.x : g_plain.x, stream));  // td3.py:231
+          (n_runs % pf == 0 ? pol_set : pln_set) = p;
+          HIPCHK(hipGraphLaunch((n_runs % pf == 0) ? g_pol[p].x : g_pln[p].x, stream));  // td3.py:231
           ++n_runs;
         } else {
-          HIPCHK(hipGraphLaunch(g_policy.x, stream));
+          pol_set = p;
+          HIPCHK(hipGraphLaunch(g_pol[p].x, stream));
           ++n_runs;
         }
+        last_set = p;
+        cur_set = 1 - p;
+        if (cfg.use_lap && algo != RLE_SAC) ++replay->version;  // this step wrote priorities
+        primed = true;
+        primed_ver = replay->version;
       }
       if (info_out) {
         HIPCHK(hipMemcpyAsync(info_out + (size_t)done * kInfoMax, info, (size_t)chunk * kInfoMax * sizeof(float),
@@ -1808,6 +1886,7 @@ int rle_replay_append(rle_replay* h, const float* state, const float* action, co
                                 r.lap, r.bsum, r.size, r.stream));
       r.ptr = (r.ptr + c) % r.cap;
       r.size = std::min(r.size + c, r.cap);
+      ++r.version;
       HIPCHK(hipMemcpyAsync(r.size_d, &r.size, sizeof(long long), hipMemcpyHostToDevice, r.stream));
       HIPCHK(hipStreamSynchronize(r.stream));
       done += c;
@@ -1839,6 +1918,7 @@ int rle_replay_fill_random(rle_replay* h, long long count, unsigned long long se
                             r.Ap, seed, r.stream));
     r.size = std::max(r.size, count);
     r.ptr = count % r.cap;
+    ++r.version;
     HIPCHK(hipMemcpyAsync(r.size_d, &r.size, sizeof(long long), hipMemcpyHostToDevice, r.stream));
     HIPCHK(hipStreamSynchronize(r.stream));
     if (r.lap) recompute_bsum(r);
@@ -1860,6 +1940,7 @@ int rle_replay_set_priority(rle_replay* h, const float* p, long long n, float ma
     HIPCHK(hipMemcpy(h->r.priority, p, n * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->r.maxp_d, &max_priority, 4, hipMemcpyHostToDevice));
     if (h->r.lap) recompute_bsum(h->r);
+    ++h->r.version;
   });
 }
 
@@ -1970,6 +2051,7 @@ int rle_replay_update_priority(rle_replay* h, int n, const long long* ind, const
     op.prio.bsum = r.lap ? r.bsum : nullptr;
     op.wg_count = 1;
     run_eager(r, tmp, {{op}});
+    ++r.version;
   });
 }
 
@@ -2077,9 +2159,10 @@ int rle_destroy(rle_engine* h) {
     if (!h) return;
     Engine& e = *h->e;
     (void)hipStreamSynchronize(e.stream);
-    for (rle::Graph* g : {&e.g_policy, &e.g_plain, &e.g_hard}) {
-      if (g->x && !(g == &e.g_plain && e.algo == RLE_SAC)) (void)hipGraphExecDestroy(g->x);
-      if (g->g && !(g == &e.g_plain && e.algo == RLE_SAC)) (void)hipGraphDestroy(g->g);
+    for (rle::Graph* g : {&e.g_prime[0], &e.g_prime[1], &e.g_pol[0], &e.g_pol[1], &e.g_pln[0], &e.g_pln[1],
+                          &e.g_hard}) {
+      if (g->x) (void)hipGraphExecDestroy(g->x);
+      if (g->g) (void)hipGraphDestroy(g->g);
     }
     for (auto& kv : e.act_graphs) {
       if (kv.second.first.x) (void)hipGraphExecDestroy(kv.second.first.x);
@@ -2098,6 +2181,7 @@ int rle_bind_replay(rle_engine* h, rle_replay* r) {
     if (e.replay == &r->r) return;
     REQUIRE(!e.built, "bind: engine already bound to another replay");
     e.replay = &r->r;
+    e.primed = false;
   });
 }
 
@@ -2144,6 +2228,7 @@ int rle_set_counters(rle_engine* h, const long long* in6) {
     for (int i = 0; i < 5; ++i) c.counters[i] = in6[i];
     c.la_t = in6[5];
     e.n_runs = in6[3];
+    e.primed = false;  // the RNG position changed
     HIPCHK(hipMemcpy(e.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
     e.refresh_adam_scalars();
   });
@@ -2208,7 +2293,12 @@ int rle_set_tapes(rle_engine* h, int n, const float* u, const float* eps, const 
       if (u) HIPCHK(hipMemcpy(e.t_u, u, nb * 4, hipMemcpyHostToDevice));
       if (eps) HIPCHK(hipMemcpy(e.t_eps, eps, na * 4, hipMemcpyHostToDevice));
       if (eps_pi) HIPCHK(hipMemcpy(e.t_eps2, eps_pi, na * 4, hipMemcpyHostToDevice));
-      if (ind) HIPCHK(hipMemcpy(e.t_ind, ind, nb * 8, hipMemcpyHostToDevice));
+      if (ind) {
+        const long long size = e.replay ? e.replay->size : 0;
+        for (size_t i = 0; i < nb; ++i)
+          REQUIRE(ind[i] >= 0 && ind[i] < size, "set_tapes: index outside the bound replay's size");
+        HIPCHK(hipMemcpy(e.t_ind, ind, nb * 8, hipMemcpyHostToDevice));
+      }
       REQUIRE(u || ind, "set_tapes: need u or ind");
       REQUIRE(e.algo != RLE_SAC || !eps == !eps_pi, "set_tapes: SAC takes eps and eps_pi together");
       mode = (u ? rle::kTapeU : 0) | (ind ? rle::kTapeInd : 0) | (eps ? rle::kTapeEps : 0);
@@ -2220,6 +2310,7 @@ int rle_set_tapes(rle_engine* h, int n, const float* u, const float* eps, const 
     HIPCHK(hipMemcpy(e.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
     e.ctrl_tape_mode_host = mode;
     e.tape_left = n;
+    e.primed = false;  // a prefetched batch was drawn from the previous draws
   });
 }
 
@@ -2227,7 +2318,7 @@ int rle_last_indices(rle_engine* h, long long* out) {
   return guard([&] {
     Engine& e = *h->e;
     HIPCHK(hipStreamSynchronize(e.stream));
-    HIPCHK(hipMemcpy(out, e.ind, e.B * sizeof(long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, e.bsets[e.last_set].ind, e.B * sizeof(long long), hipMemcpyDeviceToHost));
   });
 }
 
@@ -2283,8 +2374,8 @@ int rle_graph_stats(rle_engine* h, int* lp, int* lplain) {
   return guard([&] {
     Engine& e = *h->e;
     if (!e.built) e.build();
-    if (lp) *lp = e.g_policy.levels();
-    if (lplain) *lplain = e.g_plain.levels();
+    if (lp) *lp = e.policy_graph().levels();
+    if (lplain) *lplain = e.plain_graph().levels();
   });
 }
 
@@ -2292,7 +2383,7 @@ int rle_graph_describe(rle_engine* h, int which, char* buf, int len) {
   return guard([&] {
     Engine& e = *h->e;
     if (!e.built) e.build();
-    const rle::Graph& G = which == 0 ? e.g_policy : (which == 1 ? e.g_plain : e.g_hard);
+    const rle::Graph& G = which == 0 ? e.policy_graph() : (which == 1 ? e.plain_graph() : e.g_hard);
     REQUIRE(buf && len > 0, "describe: bad buffer");
     std::snprintf(buf, (size_t)len, "%s", G.desc.c_str());
   });
@@ -2303,7 +2394,7 @@ int rle_graph_trace(rle_engine* h, int which, unsigned long long* out, long long
     Engine& e = *h->e;
     REQUIRE(n_out, "trace: null n_out");
     if (!e.built) e.build();
-    const rle::Graph& G = which == 0 ? e.g_policy : (which == 1 ? e.g_plain : e.g_hard);
+    const rle::Graph& G = which == 0 ? e.policy_graph() : (which == 1 ? e.plain_graph() : e.g_hard);
     *n_out = G.trace ? G.trace_n : 0;
     if (!G.trace || !out) return;
     REQUIRE(cap >= G.trace_n * 4, "trace: buffer too small");
@@ -2324,6 +2415,7 @@ int rle_copy_state(rle_engine* dst, rle_engine* src) {
     HIPCHK(hipMemcpy(&c, s.ctrl, sizeof(c), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(d.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
     d.n_runs = s.n_runs;
+    d.primed = false;
   });
 }
 

@@ -314,25 +314,30 @@ __device__ __forceinline__ float act_b(float saved) {  // see act_bwd
 }
 
 // Reduction over chunks [k0, k1) of one operand pair: A from (ra, va), B from
-// (rb, vb) (byte offsets of chunk k0, +1 KB per chunk); 4 chunks in flight.
+// (rb, vb) (byte offsets of chunk k0, +1 KB per chunk); kRing chunks in flight.
 // SA / SB: per-chunk scaling (deferred AvgL1Norm) by a lane constant (N image)
 // or an LDS table of 4 rows (T image, tab = float offset of chunk k0's rows).
+#ifndef RLE_RING
+#define RLE_RING 4
+#endif
+constexpr int kRing = RLE_RING;  // chunks in flight per wave
+
 template <int SA, int SB>
 __device__ __forceinline__ f32x4 chunk_loop(__amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rb, int vb,
                                             int n, f32x4 acc, float inva, const float* taba, const float* tabb,
                                             bool bias_ones) {
   const int rl = ((threadIdx.x & 63) >> 4) << 2;
-  float4 a[4], b[4];
+  float4 a[kRing], b[kRing];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < kRing; ++r) {
     a[r] = bload(ra, r < n ? va + r * 1024 : kOOB);
     b[r] = bias_ones ? make_float4(1.f, 1.f, 1.f, 1.f) : bload(rb, r < n ? vb + r * 1024 : kOOB);
   }
   f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-  for (int c = 0; c < n; c += 4) {
+  for (int c = 0; c < n; c += kRing) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < kRing; ++r) {
       float4 x = a[r], y = b[r];
       if constexpr (SA == 1) x = scale4(x, inva);
       // (table rows past n are not built: clamp; their chunks load as zeros anyway)
@@ -340,7 +345,7 @@ __device__ __forceinline__ f32x4 chunk_loop(__amdgpu_buffer_rsrc_t ra, int va, _
       if constexpr (SB == 2) y = mul4(y, *(const float4*)(tabb + min(c + r, n - 1) * 16 + rl));
       if (r & 1) acc1 = mfma4(x, y, acc1);
       else acc = mfma4(x, y, acc);
-      const int nx = c + r + 4;
+      const int nx = c + r + kRing;
       a[r] = bload(ra, nx < n ? va + nx * 1024 : kOOB);
       if (!bias_ones) b[r] = bload(rb, nx < n ? vb + nx * 1024 : kOOB);
     }
@@ -826,15 +831,39 @@ __device__ __forceinline__ double wg_scan_excl_d(double v, double* wtot, double&
   return before + (inc - v);
 }
 
+// Noise of the batch (its own op so that the sampler's search does not wait on it):
+// element e = (b, j) of the [B][A] target-smoothing noise (td7.py:188, td3.py:154) or
+// SAC next-state rsample noise, and the SAC policy rsample noise in eps2.
+__device__ __forceinline__ void op_noise(const CAS SampleArgs& s, int t) {
+  const int e = t * kThreads + threadIdx.x;
+  if (e >= s.B * s.A) return;
+  const int b = e / s.A, j = e - b * s.A;
+  const int tape = sload(s.tape_mode);
+  const long long pos = sload(s.tape_pos) + s.ahead;
+  const unsigned long long step = (unsigned long long)sload(s.ctrl_rng) + s.ahead;
+  float v, v2 = 0.f;
+  if (tape & kTapeEps) {
+    v = G(s.tape_eps)[(size_t)pos * s.B * s.A + e];
+    if (s.eps2.t) v2 = G(s.tape_eps2)[(size_t)pos * s.B * s.A + e];
+  } else {
+    const uint2 key = make_uint2((unsigned)s.seed, (unsigned)(s.seed >> 32));
+    const uint4 r = philox(key, make_uint4((unsigned)e, 1u, (unsigned)step, (unsigned)(step >> 32)));
+    v = normal_from(r.x, r.y);
+    v2 = normal_from(r.z, r.w);
+  }
+  mat_st(s.eps, b, j, v);
+  if (s.eps2.t) mat_st(s.eps2, b, j, v2);
+}
+
 // One workgroup per query: uniform / LAP index search (searchsorted left over the
 // fp32-rounded exact prefix), noise for this row, then the coalesced row gather.
 __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b, float* smem, unsigned long long* tr) {
   const int tid = threadIdx.x;
   const long long size = sload(s.size);
   const int tape = sload(s.tape_mode);
-  const long long pos = sload(s.tape_pos);
+  const long long pos = sload(s.tape_pos) + s.ahead;
   const uint2 key = make_uint2((unsigned)s.seed, (unsigned)(s.seed >> 32));
-  const unsigned long long step = (unsigned long long)sload(s.ctrl_rng);
+  const unsigned long long step = (unsigned long long)sload(s.ctrl_rng) + s.ahead;
   FINE_MARK(0);
   const bool tind = tape & kTapeInd;
   float u = 0.f;
@@ -842,8 +871,7 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
     if (tape & kTapeU) u = G(s.tape_u)[(size_t)pos * s.B + b];
     else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
   }
-  // LAP: the block-sum loads go out first and the noise below runs while they are in
-  // flight.  Thread tid owns blocks [tid*per, tid*per + per), per <= 8 (capacity <= 8M).
+  // LAP block sums: thread tid owns blocks [tid*per, tid*per + per), per <= 8 (capacity <= 8M)
   const int nb = (int)((size + kBlk - 1) / kBlk);
   const int per = (nb + kThreads - 1) / kThreads;
   double bs[8];
@@ -851,24 +879,13 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
 #pragma unroll
     for (int q = 0; q < 8; ++q) bs[q] = G(s.bsum)[min(tid * per + q, nb - 1)];
   }
-  // noise tensors for this row (T images)
-  for (int j = tid; j < s.A; j += kThreads) {
-    float e, e2 = 0.f;
-    if (tape & kTapeEps) {
-      e = G(s.tape_eps)[((size_t)pos * s.B + b) * s.A + j];
-      if (s.eps2.t) e2 = G(s.tape_eps2)[((size_t)pos * s.B + b) * s.A + j];
-    } else {
-      const uint4 r = philox(key, make_uint4((unsigned)(b * s.A + j), 1u, (unsigned)step, (unsigned)(step >> 32)));
-      e = normal_from(r.x, r.y);
-      e2 = normal_from(r.z, r.w);
-    }
-    mat_st(s.eps, b, j, e);
-    if (s.eps2.t) mat_st(s.eps2, b, j, e2);
-  }
   FINE_MARK(1);
   long long ind;
   if (tind) {
+    // (host-checked in range; the clamp only guards a prefetch past a tape's end,
+    // whose batch the host discards)
     ind = G(s.tape_ind)[(size_t)pos * s.B + b];
+    ind = ind < 0 ? 0 : (ind > size - 1 ? size - 1 : ind);
   } else {
     if (tid == 0) GW(s.u_out)[b] = u;
     if (!s.lap) {
@@ -1344,6 +1361,7 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
     RLE_OP(OP_COPY, op_copy(op.flat, t))
     RLE_OP(OP_MAXRED, op_maxred(op.flat, t, smem))
     RLE_OP(OP_CTRL, op_ctrl(op.ctrl))
+    RLE_OP(OP_NOISE, op_noise(op.sample, t))
 #endif
 #undef RLE_OP
     default: break;

@@ -27,6 +27,7 @@ enum OpKind : int {
   OP_COPY = 11,
   OP_MAXRED = 12,
   OP_CTRL = 13,
+  OP_NOISE = 14,        // target-smoothing / rsample noise of the batch (SampleArgs)
 };
 
 // ---------------------------------------------------------------- tensor images
@@ -200,6 +201,7 @@ struct SampleArgs {
   const int* tape_mode;              // kTape* bits: which draws come from tapes (others: Philox)
   const long long* tape_pos;
   const float* tape_u; const float* tape_eps; const float* tape_eps2; const long long* tape_ind;
+  int ahead;                         // 1: draws of the NEXT step (prefetch at the end of a step)
 };
 
 struct PriorityArgs {

@@ -182,3 +182,25 @@ def test_td7_humanoid_b1024_matches_oracle():
         for name, v in d.items():
             got = eng.get_param(net, name, tuple(v.shape))
             assert np.abs(got - v.detach().numpy()).max() <= tol, (net, name)
+
+
+@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny"])
+def test_prefetched_batches_equal_fresh_draws(name):
+    """Each step's graph prefetches the next step's batch (after its priority update);
+    a run that re-draws every batch from scratch must be bit-identical."""
+    g = load_golden(name)
+    n = 6
+    e1, r1, _ = engine_from_golden(g)
+    e2, r2, _ = engine_from_golden(g)
+    info1 = e1.step(n)
+    info2 = []
+    for _ in range(n):
+        e2.set_counters(e2.counters())  # invalidates the prefetched batch
+        info2.append(e2.step(1)[0])
+    np.testing.assert_array_equal(info1, np.array(info2))
+    np.testing.assert_array_equal(e1.last_indices(), e2.last_indices())
+    np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
+    alg = parse(g)[0]
+    for net, params in spec.agent_params(alg, *spec.TASKS[parse(g)[1]][:2], parse(g)[2], 0).items():
+        for pname in params:
+            np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
