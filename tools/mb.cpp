@@ -175,6 +175,31 @@ int main() {
   }
   CK(hipFree(g_trace));
   g_trace = nullptr;
+  {  // contention: copies of the same-shaped GEMM in one level (tn 16 -> 256 WG each)
+    CK(hipMalloc(&g_trace, 8 * 4 * 8192));
+    for (int Kk : {256, 768}) {
+      for (int copies : {1, 2, 4, 8}) {
+        std::vector<Op> v;
+        for (int i = 0; i < copies; ++i) {
+          Op o = fwd_op(X, W + (size_t)i * 256 * 800, bb, Y + (size_t)i * 2048 * 256, 256, N, Kk);
+          o.gemm.tn = 16;
+          o.gemm.tiles_n = 16;
+          o.gemm.ks_log = 2;
+          o.gemm.inv_tiles_n = 1.f / 16.f;
+          o.wg_count = 256;
+          v.push_back(o);
+        }
+        const double us = time_level(v, 50, st);
+        char nm[64];
+        snprintf(nm, sizeof nm, "%dx fwd 256x256x%d (%d WG)", copies, Kk, 256 * copies);
+        printf("%-34s %8.2f us\n", nm, us);
+        time_level(v, 5, st);
+        phases(nm, 256 * copies);
+      }
+    }
+    CK(hipFree(g_trace));
+    g_trace = nullptr;
+  }
   for (int M : {256, 512}) {
     Op o = fwd_op(X, W, bb, Y, M, N, K);
     printf("fwd %dx%dx%d (%d WG): %8.2f us\n", M, N, K, o.wg_count, time_level({o}, reps, st));
