@@ -137,6 +137,9 @@ int rle_graph_describe(rle_engine* e, int which, char* buf, int len);
  * end (GEMM ops) and exit of workgroup w, levels concatenated in order; *n_out = number
  * of workgroups written (0 when tracing is off). */
 int rle_graph_trace(rle_engine* e, int which, unsigned long long* out, long long cap, long long* n_out);
+/* Timestamps per workgroup in rle_graph_trace rows: 4, or 16 in diagnostics builds
+ * (-DRLE_TRACE_FINE: slots 4.. are finer in-op stamps). */
+int rle_trace_stride(void);
 /* Copy all weights/optimizer state/counters of src into dst (checkpoint agent,
  * ckpt_agent.load_state_dict(agent), run_w_checkpoint.py:140). Same config required. */
 int rle_copy_state(rle_engine* dst, rle_engine* src);

@@ -27,6 +27,7 @@ namespace rle {
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
                         unsigned long long* trace = nullptr);
 int level_capacity();
+int trace_stride();
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count,
@@ -1542,13 +1543,13 @@ struct Engine {
     const char* tr_env = std::getenv("RLE_TRACE");
     if (tr_env && tr_env[0] == '1') {
       for (int w : G.nwg) G.trace_n += w;
-      G.trace = mem.make<unsigned long long>((size_t)G.trace_n * 4);
+      G.trace = mem.make<unsigned long long>((size_t)G.trace_n * trace_stride());
     }
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     long long tr_off = 0;
     for (size_t l = 0; l < levels.size(); ++l) {
       hipError_t e = launch_level(G.d_ops + G.off[l], levels[l].data(), G.nops[l], G.nwg[l], stream,
-                                  G.trace ? G.trace + tr_off * 4 : nullptr);
+                                  G.trace ? G.trace + tr_off * trace_stride() : nullptr);
       tr_off += G.nwg[l];
       if (e != hipSuccess) {
         hipGraph_t tmp;
@@ -2397,12 +2398,15 @@ int rle_graph_trace(rle_engine* h, int which, unsigned long long* out, long long
     const rle::Graph& G = which == 0 ? e.policy_graph() : (which == 1 ? e.plain_graph() : e.g_hard);
     *n_out = G.trace ? G.trace_n : 0;
     if (!G.trace || !out) return;
-    REQUIRE(cap >= G.trace_n * 4, "trace: buffer too small");
+    const int st = rle::trace_stride();
+    REQUIRE(cap >= G.trace_n * st, "trace: buffer too small");
     HIPCHK(hipStreamSynchronize(e.stream));
-    HIPCHK(hipMemcpy(out, G.trace, (size_t)G.trace_n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, G.trace, (size_t)G.trace_n * st * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     *n_out = G.trace_n;
   });
 }
+
+int rle_trace_stride(void) { return rle::trace_stride(); }
 
 int rle_copy_state(rle_engine* dst, rle_engine* src) {
   return guard([&] {

@@ -326,6 +326,9 @@ template <int SA, int SB>
 __device__ __forceinline__ f32x4 chunk_loop(__amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rb, int vb,
                                             int n, f32x4 acc, float inva, const float* taba, const float* tabb,
                                             bool bias_ones) {
+#ifdef RLE_EXP_NOLOOP  // timing experiment only: no main-loop loads / MFMAs
+  n = 0;
+#endif
   const int rl = ((threadIdx.x & 63) >> 4) << 2;
   float4 a[kRing], b[kRing];
 #pragma unroll
@@ -373,6 +376,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   const int nch = g.R >> 4;
   const int per = (nch + (1 << ksl) - 1) >> ksl;
   const int c0 = kp * per, c1 = min(nch, c0 + per);
+  FINE_MARK(8);
 
   // ---- epilogue operands fetched ahead of the main loop
   float pre_b = 0.f;
@@ -467,6 +471,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       for (int q = 1; q < (1 << ksl); ++q) acc += *(const f32x4*)(part + ((wave + q) * 64 + lane) * 4);
     }
   }
+  FINE_MARK(9);
 
   // ---- epilogue
   if constexpr (EPI == EPI_STORE) {
@@ -1336,6 +1341,7 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
   }
   const CAS Op& op = ops[k];
   const int t = wg - (la.nops <= kLevelOps ? la.wg_begin[k] : op.wg_begin);
+  FINE_MARK(7);
   switch (kind) {
 #define RLE_OP(K, call)                       \
   case K:                                     \
@@ -1424,6 +1430,9 @@ __global__ void rle_fill_kernel(float* state, float* next_state, float* action, 
 // ---------------------------------------------------------------- host launchers
 
 // Workgroups of rle_level resident at once on the current device.
+// Timestamps per workgroup in trace buffers (4; 16 in -DRLE_TRACE_FINE builds).
+int trace_stride() { return kTraceStride; }
+
 int level_capacity() {
   int per_cu = 0, cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;

@@ -16,7 +16,7 @@ RLE_TD7, RLE_TD3, RLE_SAC = 0, 1, 2
 INFO_MAX = 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librle.so")
+LIB_PATH = os.environ.get("RLE_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "librle.so")  # RLE_LIB: experiment builds
 
 _lib = None
 
@@ -76,6 +76,7 @@ SIGNATURES = {
     "rle_graph_stats": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "rle_graph_describe": (_int, [_vp, _int, ctypes.c_char_p, _int]),
     "rle_graph_trace": (_int, [_vp, _int, ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)]),
+    "rle_trace_stride": (_int, []),
     "rle_copy_state": (_int, [_vp, _vp]),
     "rle_synchronize": (_int, [_vp]),
 }
@@ -300,12 +301,14 @@ class Engine:
         return buf.value.decode()
 
     def trace(self, which=0):
-        """Per-workgroup phase timestamps of the last replay of graph `which` (RLE_TRACE=1)."""
+        """Per-workgroup phase timestamps of the last replay of graph `which` (RLE_TRACE=1):
+        (workgroups, 4) -- or 16 columns from a -DRLE_TRACE_FINE build."""
         n = ctypes.c_longlong()
         _check(lib().rle_graph_trace(self.h, which, None, 0, ctypes.byref(n)))
+        stride = lib().rle_trace_stride()
         if n.value == 0:
-            return np.zeros((0, 4), np.uint64)
-        out = np.zeros((n.value, 4), np.uint64)
+            return np.zeros((0, stride), np.uint64)
+        out = np.zeros((n.value, stride), np.uint64)
         _check(lib().rle_graph_trace(self.h, which, out.ctypes.data, out.size, ctypes.byref(n)))
         return out
 

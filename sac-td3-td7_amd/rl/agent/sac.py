@@ -37,6 +37,17 @@ class SAC(EngineAgent):
         if self.auto_tmp_mode:
             self.target_entropy = -self.action_dim
 
+    def train_ops(self, batch, replay_buffer=None, *args, **kwargs):
+        if self.use_lap:
+            # sac.py:199-203 calls self._lap_huber, which SAC does not define
+            raise AttributeError("'SAC' object has no attribute '_lap_huber' (reference sac.py:202)")
+        return super().train_ops(batch, replay_buffer, *args, **kwargs)
+
+    def train_n(self, replay_buffer, batch_size, n_ops):
+        if self.use_lap:
+            raise AttributeError("'SAC' object has no attribute '_lap_huber' (reference sac.py:202)")
+        return super().train_n(replay_buffer, batch_size, n_ops)
+
     def _info_keys(self):
         if self.auto_tmp_mode:  # sac.py:268-290
             return ("train/q_fn", "tmp", "norm/tmp", "train/policy", "train/tmp", "entropy")

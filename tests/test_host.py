@@ -127,3 +127,11 @@ def test_bench_max_over_ranks_gloo_world2(tmp_path):
     wall, gpu, value = json.loads(res.stdout.strip().splitlines()[-1])
     assert (wall, gpu) == (2.0, 1.0)
     assert value == 2 * 100 / 2.0
+
+
+def test_sac_lap_fails_like_the_reference():
+    # sac.py:202 calls an undefined _lap_huber: train_ops raises before any engine call
+    sac = SAC.__new__(SAC)
+    sac.use_lap = True
+    with pytest.raises(AttributeError, match="_lap_huber"):
+        sac.train_ops(DeviceBatch({}, np.zeros(4, np.int64), None), None)

@@ -48,3 +48,9 @@ for which in (0, 1):
         tot = (t[:, 3] - t[:, 0]) * 10 / 1000
         print(f"gap {gap:5.2f} span {span:6.2f} | disp max {disp.max():5.2f} | wg med {np.median(tot):5.2f} max {tot.max():5.2f}"
               f" | pro {np.median(pro):5.2f} loop {np.median(loop):5.2f} epi {np.median(epi):5.2f} | {line[:90]}")
+        if tr.shape[1] == 16 and "gemm" in line:  # fine build: GEMM prologue / epilogue split
+            gm = g & (t[:, 11] > 0) & (t[:, 12] > 0)
+            if gm.any():
+                med = lambda a, b: np.median((t[gm, b] - t[gm, a]) * 10 / 1000)
+                print(f"      gemm: decode {med(0, 11):5.2f} desc {med(11, 12):5.2f} prefetch {med(12, 1):5.2f}"
+                      f" | loop {med(1, 2):5.2f} | splitK {med(2, 13):5.2f} epi {med(13, 3):5.2f}")
