@@ -1320,27 +1320,31 @@ __device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
 
 // ---------------------------------------------------------------- dispatch
 
+// TRACE: compiled with the phase stamps (RLE_TRACE=1 runs); the production instance has
+// none, so nothing but the op table is read before the op body starts.
+template <bool TRACE>
 __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
   __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
-  unsigned long long* tr = la.trace ? la.trace + (size_t)blockIdx.x * kTraceStride : nullptr;
-  trace_mark(tr, 0);
-  const CAS Op* ops = (const CAS Op*)la.ops;
+  // op of this workgroup from the kernel-argument table: straight-line selects over
+  // SGPRs, so all kernel-argument loads go out in one batch (one round trip) and no
+  // descriptor is read before the op is known
   const int wg = blockIdx.x;
-  // op of this workgroup: from the kernel-argument table (SGPRs, no dependent
-  // descriptor loads), or by scanning descriptors for an oversized level
-  int k = 0, kind, vid;
-  if (la.nops <= kLevelOps) {
+  int k = 0;
+  unsigned e = la.entry[0];
 #pragma unroll
-    for (int q = 1; q < kLevelOps; ++q) k = (q < la.nops && la.wg_begin[q] <= wg) ? q : k;
-    kind = la.kind[k];
-    vid = la.vid[k];
-  } else {
-    while (k + 1 < la.nops && ops[k + 1].wg_begin <= wg) ++k;
-    kind = ops[k].kind;
-    vid = ops[k].gemm.vid;
+  for (int q = 1; q < kLevelOps; ++q) {
+    const unsigned x = la.entry[q];
+    const bool in = (int)(x & 0xffffu) <= wg;
+    e = in ? x : e;
+    k = in ? q : k;
   }
+  const int kind = (e >> 16) & 0xff, vid = e >> 24;
+  const CAS Op* ops = (const CAS Op*)la.ops;
   const CAS Op& op = ops[k];
-  const int t = wg - (la.nops <= kLevelOps ? la.wg_begin[k] : op.wg_begin);
+  const int t = wg - (int)(e & 0xffffu);
+  // (stamp 0 follows the decode: its kernel-argument loads share one round trip)
+  unsigned long long* tr = TRACE ? la.trace + (size_t)wg * kTraceStride : nullptr;
+  trace_mark(tr, 0);
   FINE_MARK(7);
   switch (kind) {
 #define RLE_OP(K, call)                       \
@@ -1436,24 +1440,39 @@ int trace_stride() { return kTraceStride; }
 int level_capacity() {
   int per_cu = 0, cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level, kThreads, 0) != hipSuccess) return 1024;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false>, kThreads, 0) != hipSuccess)
+    return 1024;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
   return per_cu * cus;
 }
 
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
                         unsigned long long* trace) {
-  LevelArgs la{};
-  la.ops = d_ops;
-  la.trace = trace;
-  la.nops = nops;
-  for (int q = 0; q < nops && q < kLevelOps; ++q) {
-    la.wg_begin[q] = h_ops[q].wg_begin;
-    la.kind[q] = (unsigned char)h_ops[q].kind;
-    la.vid[q] = (unsigned char)(h_ops[q].kind == OP_GEMM ? h_ops[q].gemm.vid : 0);
+  // a level of more than kLevelOps ops runs as consecutive launches of kLevelOps (its
+  // ops are independent, so any split is correct)
+  for (int q0 = 0; q0 < nops; q0 += kLevelOps) {
+    const int n = nops - q0 < kLevelOps ? nops - q0 : kLevelOps;
+    const int w0 = h_ops[q0].wg_begin;
+    const int w1 = q0 + n < nops ? h_ops[q0 + n].wg_begin : nwg;
+    if (w1 - w0 > kMaxLevelWG) return hipErrorInvalidValue;
+    LevelArgs la{};
+    la.ops = d_ops + q0;
+    la.trace = trace ? trace + (size_t)w0 * kTraceStride : nullptr;
+    for (int q = 0; q < kLevelOps; ++q) {
+      if (q < n) {
+        const Op& o = h_ops[q0 + q];
+        const unsigned vid = o.kind == OP_GEMM ? (unsigned)o.gemm.vid : 0u;
+        la.entry[q] = (unsigned)(o.wg_begin - w0) | ((unsigned)o.kind << 16) | (vid << 24);
+      } else {
+        la.entry[q] = 0xffffu;
+      }
+    }
+    if (trace) hipLaunchKernelGGL(rle_level<true>, dim3(w1 - w0), dim3(kThreads), 0, st, la);
+    else hipLaunchKernelGGL(rle_level<false>, dim3(w1 - w0), dim3(kThreads), 0, st, la);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(rle_level, dim3(nwg), dim3(kThreads), 0, st, la);
-  return hipGetLastError();
+  return hipSuccess;
 }
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,

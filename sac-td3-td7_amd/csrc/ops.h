@@ -282,15 +282,15 @@ struct Op {
 
 // Kernel argument of one level launch: the workgroup -> op table travels in the
 // kernarg segment (one scalar load burst) instead of being searched in memory.
-constexpr int kLevelOps = 24;
+constexpr int kLevelOps = 16;
 struct LevelArgs {
   const Op* ops;
   unsigned long long* trace;  // optional phase timestamps [wg][4] (s_memrealtime, 100 MHz)
-  int nops;
-  int wg_begin[kLevelOps];
-  unsigned char kind[kLevelOps];
-  unsigned char vid[kLevelOps];  // GemmArgs::vid of GEMM ops (variant chosen before any descriptor load)
+  // op q: first workgroup (bits 0-15; 0xffff past the last op) | kind << 16 | GEMM variant
+  // id << 24 (GemmArgs::vid: the variant is chosen before any descriptor load)
+  unsigned entry[kLevelOps];
 };
+constexpr int kMaxLevelWG = 0xfffe;  // workgroups per launch (16-bit entry field)
 
 // Device control block.
 struct Ctrl {
