@@ -202,6 +202,23 @@ static void gemm_finalize(GemmArgs& g) {
   REQUIRE(g.R % 16 == 0, "gemm: reduction length must be a multiple of 16");
   REQUIRE((long long)g.tiles_m * g.tiles_n < 65536, "gemm: too many tiles");
   g.inv_tiles_n = 1.f / (float)g.tiles_n;
+  GemmHot& h = g.hot;
+  h.ks_log = g.ks_log;
+  h.tiles_n = g.tiles_n;
+  h.tn = g.tn;
+  h.N = g.N;
+  h.R = g.R;
+  h.inv_tiles_n = g.inv_tiles_n;
+  h.bias_col = g.epi == EPI_ADAM ? g.adam.bias_col : 0;
+  h.nseg_a = g.A.nseg;
+  h.nseg_b = g.B.nseg;
+  h.a0xs = g.A.seg[0].xs;
+  h.a0r0 = g.A.seg[0].r0;
+  h.a0r1 = g.A.seg[0].r1;
+  h.b0xs = g.B.seg[0].xs;
+  h.a0p = g.A.seg[0].p;
+  h.b0p = g.B.seg[0].p;
+  h.bias = g.epi == EPI_ADAM ? nullptr : g.bias;
 }
 
 struct Prog {

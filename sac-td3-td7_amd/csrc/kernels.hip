@@ -275,6 +275,7 @@ constexpr int kTraceStride = 4;
 // are walked by an outer loop), and no normalisation code in the plain case.
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x16 __attribute__((ext_vector_type(16)));
 constexpr int kOOB = 0x7ffffff0;  // voffset beyond num_records: the load returns 0
 
 __device__ __forceinline__ float4 as_f4(u32x4 v) {
@@ -360,20 +361,38 @@ template <int MODE, int EPI, int ACT, bool NORM>
 __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ksl = g.ks_log;
+  // ---- every descriptor field the prologue and the first operand segment need (GemmHot)
+  // in ONE batch of scalar loads.  Left to the compiler, each load is issued next to its
+  // use, behind branches: one dependent round trip each, ~6 before the first operand load.
+  u32x16 h0;
+  u32x4 h1;
+  asm volatile(
+      "s_load_dwordx16 %0, %2, 0x0\n\t"
+      "s_load_dwordx4 %1, %2, 0x40\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=s"(h0), "=s"(h1)
+      : "s"(&g.hot));
+  auto ptr = [](unsigned lo, unsigned hi) { return (const float*)(((unsigned long long)hi << 32) | lo); };
+  const int ksl = (int)h0[0], tiles_n = (int)h0[1], tn = (int)h0[2], gN = (int)h0[3], gR = (int)h0[4];
+  const float inv_tn = __uint_as_float(h0[5]);
+  const int bias_col = (int)h0[6], nseg_a = (int)h0[7], nseg_b = (int)h0[8];
+  const int a0xs = (int)h0[9], a0r0 = (int)h0[10], a0r1 = (int)h0[11], b0xs = (int)h0[12];
+  const float* a0p = ptr(h0[14], h0[15]);
+  const float* b0p = ptr(h1[0], h1[1]);
+  const float* biasp = ptr(h1[2], h1[3]);
   const int cg = wave >> ksl, kp = wave & ((1 << ksl) - 1);
-  const int it = (int)(((float)t + 0.5f) * g.inv_tiles_n);
-  const int jt = t - it * g.tiles_n;
-  const int i0 = it << 4, j0 = jt * g.tn + (cg << 4);
-  const bool bias_tile = EPI == EPI_ADAM && jt * g.tn >= g.adam.bias_col;
+  const int it = (int)(((float)t + 0.5f) * inv_tn);
+  const int jt = t - it * tiles_n;
+  const int i0 = it << 4, j0 = jt * tn + (cg << 4);
+  const bool bias_tile = EPI == EPI_ADAM && jt * tn >= bias_col;
   const bool lead = kp == 0;
-  const bool active = bias_tile ? cg == 0 : j0 < g.N;  // wave-uniform
+  const bool active = bias_tile ? cg == 0 : j0 < gN;  // wave-uniform
   const int j = j0 + (lane & 15), ib = i0 + ((lane >> 4) << 2);
-  const bool jok = active && lead && (bias_tile ? j == g.adam.bias_col : j < g.N);
+  const bool jok = active && lead && (bias_tile ? j == bias_col : j < gN);
   float* red = smem;               // [64] reduction scratch
   float* part = smem + 64;         // [4 waves][64][4] split-K partials
   float* tabs = smem + 64 + 1024;  // AvgL1Norm 1/m tables (T-image operands)
-  const int nch = g.R >> 4;
+  const int nch = gR >> 4;
   const int per = (nch + (1 << ksl) - 1) >> ksl;
   const int c0 = kp * per, c1 = min(nch, c0 + per);
   FINE_MARK(8);
@@ -383,7 +402,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   float4 ds = make_float4(1.f, 1.f, 1.f, 1.f), pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
   size_t wt = 0;
   if constexpr (EPI != EPI_ADAM) {
-    if (jok && g.bias) pre_b = G(g.bias)[j];
+    if (jok && biasp) pre_b = G(biasp)[j];
     if constexpr (MODE == GEMM_DX && ACT != ACT_NONE) {
       if (jok) ds = mat_ld4(g.dsrc, ib, j);
     }
@@ -410,41 +429,42 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   if constexpr (MODE != GEMM_DW) {
     // A: N image, segments along the reduction; B: W (FWD: N image, one segment over
     // the whole reduction; DX: T image, one segment per A segment)
-    const CAS Seg& w0 = g.B.seg[0];
-    for (int q = 0; q < g.A.nseg; ++q) {
-      const CAS Seg& sa = g.A.seg[q];
-      const int s0 = sa.r0 >> 4;
-      const int k0 = max(c0, s0), k1 = min(c1, (sa.r1 + 15) >> 4);
-      if (!active || k0 >= k1) continue;
+    // (segment 0 from the hot header; later segments load their own fields)
+    auto seg = [&](const float* sap, int sxs, int sr0, int sr1, const float* sbp, int bxs, float inva) {
+      const int s0 = sr0 >> 4;
+      const int k0 = max(c0, s0), k1 = min(c1, (sr1 + 15) >> 4);
+      if (!active || k0 >= k1) return;
+      const int va = ((i0 >> 4) * sxs + (k0 - s0)) * 1024 + lb;
+      const int vb = ((j0 >> 4) * bxs + (MODE == GEMM_FWD ? k0 : k0 - s0)) * 1024 + lb;
+      acc = chunk_loop<NORM ? 1 : 0, 0>(rsrc(sap), va, rsrc(sbp), vb, k1 - k0, acc, inva, nullptr, nullptr, false);
+    };
+    auto inv_of = [&](int q) {
       float inva = 1.f;
       if constexpr (NORM) {
-        if (sa.norm.part) inva = norm_inv(sa.norm, i0 + (lane & 15));
+        if (g.A.seg[q].norm.part) inva = norm_inv(g.A.seg[q].norm, i0 + (lane & 15));
       }
-      const int va = ((i0 >> 4) * sa.xs + (k0 - s0)) * 1024 + lb;
-      if constexpr (MODE == GEMM_FWD) {
-        const int vb = ((j0 >> 4) * w0.xs + k0) * 1024 + lb;
-        acc = chunk_loop<NORM ? 1 : 0, 0>(rsrc(sa.p), va, rsrc(w0.p), vb, k1 - k0, acc, inva, nullptr, nullptr,
-                                          false);
-      } else {
-        const CAS Seg& sb = g.B.seg[q];
-        const int vb = ((j0 >> 4) * sb.xs + (k0 - s0)) * 1024 + lb;
-        acc = chunk_loop<0, 0>(rsrc(sa.p), va, rsrc(sb.p), vb, k1 - k0, acc, 1.f, nullptr, nullptr, false);
-      }
+      return inva;
+    };
+    seg(a0p, a0xs, a0r0, a0r1, b0p, b0xs, inv_of(0));
+    for (int q = 1; q < nseg_a; ++q) {
+      const CAS Seg& sa = g.A.seg[q];
+      // FWD: one W segment over the whole reduction; DX: W segment q pairs with A segment q
+      const CAS Seg& sb = g.B.seg[MODE == GEMM_FWD ? 0 : q];
+      seg(sa.p, sa.xs, sa.r0, sa.r1, MODE == GEMM_FWD ? b0p : sb.p, MODE == GEMM_FWD ? b0xs : sb.xs, inv_of(q));
     }
   } else {
     // DW: A = dZ (T image, x = output row), B = X (T image, x = output column; the
     // wave's 16 columns lie in one column segment); both reduce over batch rows
-    const CAS Seg& sa = g.A.seg[0];
     int qb = 0;
 #pragma unroll
     for (int q = 1; q < kMaxSeg; ++q)
-      if (q < g.B.nseg && j0 >= g.B.seg[q].x0) qb = q;
+      if (q < nseg_b && j0 >= g.B.seg[q].x0) qb = q;
     const CAS Seg& sb = g.B.seg[qb];
     const float* tb = nullptr;
     if constexpr (NORM) {
       // 1/m of every reduction row of every normed B segment, segment by segment
       int off = 0, mine = -1;
-      for (int q = 0; q < g.B.nseg; ++q) {
+      for (int q = 0; q < nseg_b; ++q) {
         const CAS Seg& s = g.B.seg[q];
         if (!s.norm.part) continue;
         build_norm_tab(s.norm, s.r1 - s.r0, tabs + off);
@@ -455,12 +475,12 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       if (mine >= 0) tb = tabs + mine + c0 * 16;
     }
     if (active && c0 < c1) {
-      const int va = ((i0 >> 4) * sa.xs + c0) * 1024 + lb;
+      const int va = ((i0 >> 4) * a0xs + c0) * 1024 + lb;
       const int vb = (((j0 - sb.x0) >> 4) * sb.xs + c0) * 1024 + lb;
       if (NORM && tb && !bias_tile)  // the bias column's B is ones: never scaled
-        acc = chunk_loop<0, 2>(rsrc(sa.p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, tb, bias_tile);
+        acc = chunk_loop<0, 2>(rsrc(a0p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, tb, bias_tile);
       else
-        acc = chunk_loop<0, 0>(rsrc(sa.p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, nullptr, bias_tile);
+        acc = chunk_loop<0, 0>(rsrc(a0p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, nullptr, bias_tile);
     }
   }
   trace_mark(tr, 2);
@@ -567,7 +587,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       gg = wg_sum(gg, red);
       if (tid == 0) {
         if (bias_tile) GW(ad.gsq_b)[it] = gg;
-        else GW(ad.gsq)[it * (g.tiles_n - 1) + jt] = gg;
+        else GW(ad.gsq)[it * (tiles_n - 1) + jt] = gg;
       }
     }
   }
@@ -1328,6 +1348,7 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
   // op of this workgroup from the kernel-argument table: straight-line selects over
   // SGPRs, so all kernel-argument loads go out in one batch (one round trip) and no
   // descriptor is read before the op is known
+  const unsigned long long t_in = TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;  // before any load
   const int wg = blockIdx.x;
   int k = 0;
   unsigned e = la.entry[0];
@@ -1342,9 +1363,9 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
   const CAS Op* ops = (const CAS Op*)la.ops;
   const CAS Op& op = ops[k];
   const int t = wg - (int)(e & 0xffffu);
-  // (stamp 0 follows the decode: its kernel-argument loads share one round trip)
+  // (stamp 0 is taken on entry, before the kernel-argument loads)
   unsigned long long* tr = TRACE ? la.trace + (size_t)wg * kTraceStride : nullptr;
-  trace_mark(tr, 0);
+  if (TRACE && threadIdx.x == 0) tr[0] = t_in;
   FINE_MARK(7);
   switch (kind) {
 #define RLE_OP(K, call)                       \

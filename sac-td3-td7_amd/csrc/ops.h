@@ -109,7 +109,22 @@ enum GemmMode : int {
   GEMM_DW = 2,    // A strided (dZ^T), B strided (X):                     dW = dZ^T X
 };
 
+// Copies of every field the GEMM prologue and the first operand segment need, packed
+// at the start of GemmArgs so the kernel reads them in ONE scalar-load batch
+// (filled by the host from the fields below; kernels.hip gemm_v).
+struct GemmHot {
+  int ks_log, tiles_n, tn, N, R;
+  float inv_tiles_n;
+  int bias_col, nseg_a, nseg_b;
+  int a0xs, a0r0, a0r1, b0xs, pad_;
+  const float* a0p;
+  const float* b0p;
+  const float* bias;
+};
+static_assert(sizeof(GemmHot) == 80, "GemmHot is loaded as 16 + 4 dwords");
+
 struct GemmArgs {
+  GemmHot hot;           // (first: one s_load_dwordx16 + one s_load_dwordx4)
   int mode;              // GemmMode (operand layouts; every segment of an operand shares it)
   int M, N, R;           // output rows, output cols (x-extent of B), reduction length
   int tn;                // tile width: 16 x tn output tile; the 4 waves are tn/16 column groups
