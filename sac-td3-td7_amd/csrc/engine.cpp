@@ -925,8 +925,21 @@ struct Engine {
     h.H = H;
     h.gamma = cfg.discount;
     h.inv_b = 1.f / (float)B;
+    h.tgt_mode = -1;
     op.wg_count = cdiv(rows, 4);
     return op;
+  }
+
+  // The target twins' last layer fused into a *_LOSS head (HeadArgs::tgt_mode).
+  void set_head_target(HeadArgs& h, int mode, const View& t1, const View& t2, const Layer& l1, const Layer& l2) {
+    REQUIRE(t1.m.n && t2.m.n && l1.out == 1 && l2.out == 1 && l1.cb == h.w_cbn, "head: target operand layout");
+    h.tgt_mode = mode;
+    h.th[0] = t1.m;
+    h.th[1] = t2.m;
+    h.tw[0] = P + l1.wn_off;
+    h.tw[1] = P + l2.wn_off;
+    h.tb[0] = bias(l1);
+    h.tb[1] = bias(l2);
   }
 
   void set_head_twin(HeadArgs& h, const View& h1, const View& h2, const Layer& l1, const Layer& l2) {
@@ -1089,20 +1102,6 @@ struct Engine {
       View t1 = fwd(pg, tq[n]->layers[1], {{t01}, {tzsa}, {tzs}}, B, ACT_ELU, nullptr, false);
       th[n] = fwd(pg, tq[n]->layers[2], {{t1}}, B, ACT_ELU, nullptr, false);
     }
-    View y = vec(B);
-    {
-      Op op = head_op(HEAD_TD7_TARGET, B);
-      HeadArgs& h = op.head;
-      set_head_twin(h, th[0], th[1], tq[0]->layers[3], tq[1]->layers[3]);
-      h.reward = rw.p;
-      h.notdone = nd.p;
-      h.y = y.p;
-      h.vmax_key = &ctrl->vmax_key;
-      h.vmin_key = &ctrl->vmin_key;
-      h.vt = ctrl->vt;
-      pg.add(op, {th[0].id, th[1].id, tq[0]->layers[3].res, tq[1]->layers[3].res, rw.id, nd.id, R_VT},
-             {y.id, R_VKEYS});
-    }
     // ---- online critics on (s, a, zsa_f, zs_f)
     View c01[2], c1[2], c2[2], c1z[2], c2z[2];
     for (int n = 0; n < 2; ++n) {
@@ -1115,22 +1114,30 @@ struct Engine {
     const int hw = cdiv(B, 4);
     qloss_part = mem.make<float>((size_t)hw * 4);
     {
+      // target head (td7.py:211-218) fused: y per row from the target twins, then the loss
       Op op = head_op(HEAD_TD7_LOSS, B);
       HeadArgs& h = op.head;
       set_head_twin(h, c2[0], c2[1], q[0]->layers[3], q[1]->layers[3]);
+      set_head_target(h, HEAD_TD7_TARGET, th[0], th[1], tq[0]->layers[3], tq[1]->layers[3]);
+      h.reward = rw.p;
+      h.notdone = nd.p;
+      h.vmax_key = &ctrl->vmax_key;
+      h.vmin_key = &ctrl->vmin_key;
+      h.vt = ctrl->vt;
       h.dsrc[0] = c2z[0].m;
       h.dsrc[1] = c2z[1].m;
       h.dact = ACT_ELU;
       h.lap = lap;
-      h.y = y.p;
       h.dz[0] = dz2[0].m;
       h.dz[1] = dz2[1].m;
       h.dq[0] = dq[0].m;
       h.dq[1] = dq[1].m;
       h.loss_part = qloss_part;
       h.prio = prio.p;
-      pg.add(op, {c2[0].id, c2[1].id, c2z[0].id, c2z[1].id, q[0]->layers[3].res, q[1]->layers[3].res, y.id},
-             {dz2[0].id, dz2[1].id, dq[0].id, dq[1].id, prio.id, qloss_id = next_id++});
+      pg.add(op,
+             {c2[0].id, c2[1].id, c2z[0].id, c2z[1].id, q[0]->layers[3].res, q[1]->layers[3].res, th[0].id, th[1].id,
+              tq[0]->layers[3].res, tq[1]->layers[3].res, rw.id, nd.id, R_VT},
+             {dz2[0].id, dz2[1].id, dq[0].id, dq[1].id, prio.id, qloss_id = next_id++, R_VKEYS});
     }
     if (lap) {
       Op op{};
@@ -1312,24 +1319,6 @@ struct Engine {
     // target critics + y
     View th0[2], th1[2];
     for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n]);
-    View y = vec(B);
-    {
-      Op op = head_op(HEAD_MLP_TARGET, B);
-      HeadArgs& h = op.head;
-      set_head_twin(h, th1[0], th1[1], tq[0]->layers[2], tq[1]->layers[2]);
-      h.reward = rw.p;
-      h.notdone = nd.p;
-      h.y = y.p;
-      std::vector<int> rd{th1[0].id, th1[1].id, tq[0]->layers[2].res, tq[1]->layers[2].res, rw.id, nd.id};
-      if (sac) {
-        h.sac = 1;
-        h.logpi = logpi.p + B;
-        h.log_alpha = P + (nP - 4);
-        rd.push_back(logpi.id);
-        rd.push_back(R_LA);
-      }
-      pg.add(op, rd, {y.id});
-    }
     // online critics
     View c0[2], c1[2];
     for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c0[n], c1[n]);
@@ -1338,22 +1327,33 @@ struct Engine {
     const int hw = cdiv(B, 4);
     qloss_part = mem.make<float>((size_t)hw * 4);
     {
+      // target head (td3.py:160-164, sac.py:188-193) fused: y per row, then the loss
       Op op = head_op(HEAD_MLP_LOSS, B);
       HeadArgs& h = op.head;
       set_head_twin(h, c1[0], c1[1], q[0]->layers[2], q[1]->layers[2]);
+      set_head_target(h, HEAD_MLP_TARGET, th1[0], th1[1], tq[0]->layers[2], tq[1]->layers[2]);
+      h.reward = rw.p;
+      h.notdone = nd.p;
+      std::vector<int> rd{c1[0].id, c1[1].id, q[0]->layers[2].res, q[1]->layers[2].res, th1[0].id, th1[1].id,
+                          tq[0]->layers[2].res, tq[1]->layers[2].res, rw.id, nd.id};
+      if (sac) {
+        h.sac = 1;
+        h.logpi = logpi.p + B;  // next-state rows
+        h.log_alpha = P + (nP - 4);
+        rd.push_back(logpi.id);
+        rd.push_back(R_LA);
+      }
       h.dsrc[0] = c1[0].m;
       h.dsrc[1] = c1[1].m;
       h.dact = ACT_RELU;
       h.lap = lap;
-      h.y = y.p;
       h.dz[0] = dz1[0].m;
       h.dz[1] = dz1[1].m;
       h.dq[0] = dq[0].m;
       h.dq[1] = dq[1].m;
       h.loss_part = qloss_part;
       h.prio = prio.p;
-      pg.add(op, {c1[0].id, c1[1].id, q[0]->layers[2].res, q[1]->layers[2].res, y.id},
-             {dz1[0].id, dz1[1].id, dq[0].id, dq[1].id, prio.id, qloss_id = next_id++});
+      pg.add(op, rd, {dz1[0].id, dz1[1].id, dq[0].id, dq[1].id, prio.id, qloss_id = next_id++});
     }
     if (lap) {
       Op op{};

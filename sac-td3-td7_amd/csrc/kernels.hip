@@ -672,7 +672,8 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
     const bool in0 = c0 < h.H, in1 = c1 < h.H;
     const int k0 = in0 ? c0 : 0, k1 = in1 ? c1 : 0;
     const bool dz = h.mode != HEAD_TD7_TARGET && h.mode != HEAD_MLP_TARGET;
-    float4 hv[2][2], wv[2][2], dv[2][2];
+    const bool fused = h.tgt_mode >= 0;  // target twins in this op too (wave-uniform)
+    float4 hv[2][2], wv[2][2], dv[2][2], tv[2][2], twv[2][2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       hv[n][0] = mat_ldr4(h.h[n], b, k0);
@@ -683,20 +684,36 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
         dv[n][0] = mat_ldr4(h.dsrc[n], b, k0);
         dv[n][1] = mat_ldr4(h.dsrc[n], b, k1);
       }
+      if (fused) {
+        tv[n][0] = mat_ldr4(h.th[n], b, k0);
+        tv[n][1] = mat_ldr4(h.th[n], b, k1);
+        twv[n][0] = ld4g(G(h.tw[n]) + nidx(h.w_cbn, 0, k0));
+        twv[n][1] = ld4g(G(h.tw[n]) + nidx(h.w_cbn, 0, k1));
+      }
     }
     const float rw = h.reward ? sload(h.reward + b) : 0.f, ndn = h.notdone ? sload(h.notdone + b) : 0.f;
-    const float yv = (h.mode == HEAD_TD7_LOSS || h.mode == HEAD_MLP_LOSS) ? sload(h.y + b) : 0.f;
+    float yv = ((h.mode == HEAD_TD7_LOSS || h.mode == HEAD_MLP_LOSS) && !fused) ? sload(h.y + b) : 0.f;
     const float lp = h.sac ? sload(h.logpi + b) : 0.f;
     const float alpha = h.sac ? expf(sload(h.log_alpha)) : 0.f;
     const float bias0 = sload(h.b[0]), bias1 = sload(h.b[1]);
     const float vtmax = h.vt ? sload(h.vt) : 0.f, vtmin = h.vt ? sload(h.vt + 1) : 0.f;
+    auto dot2 = [&](const float4 (&x)[2], const float4 (&w)[2]) {
+      float s = 0.f;
+      if (in0) s += (x[0].x * w[0].x + x[0].y * w[0].y) + (x[0].z * w[0].z + x[0].w * w[0].w);
+      if (in1) s += (x[1].x * w[1].x + x[1].y * w[1].y) + (x[1].z * w[1].z + x[1].w * w[1].w);
+      return wave_sum(s);
+    };
     float q[2];
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      float s = 0.f;
-      if (in0) s += (hv[n][0].x * wv[n][0].x + hv[n][0].y * wv[n][0].y) + (hv[n][0].z * wv[n][0].z + hv[n][0].w * wv[n][0].w);
-      if (in1) s += (hv[n][1].x * wv[n][1].x + hv[n][1].y * wv[n][1].y) + (hv[n][1].z * wv[n][1].z + hv[n][1].w * wv[n][1].w);
-      q[n] = wave_sum(s) + (n ? bias1 : bias0);
+    for (int n = 0; n < 2; ++n) q[n] = dot2(hv[n], wv[n]) + (n ? bias1 : bias0);
+    if (fused) {  // the TD target of this row (as HEAD_TD7_TARGET / HEAD_MLP_TARGET below)
+      const float qt0 = dot2(tv[0], twv[0]) + sload(h.tb[0]), qt1 = dot2(tv[1], twv[1]) + sload(h.tb[1]);
+      float v = fminf(qt0, qt1);
+      if (h.tgt_mode == HEAD_TD7_TARGET) v = fminf(fmaxf(v, vtmin), vtmax);
+      else if (h.sac) v = v - alpha * lp;
+      yv = rw + (h.gamma * v) * ndn;
+      if (h.y && lane == 0) GW(h.y)[b] = yv;
+      if (h.tgt_mode == HEAD_TD7_TARGET) kmax = kmin = fkey(yv);
     }
     trace_mark(tr, 1);
     float dq[2] = {0.f, 0.f};
@@ -788,7 +805,7 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
       lp[t * 4 + 2] = 0.f;
       lp[t * 4 + 3] = 0.f;
     }
-    if (h.mode == HEAD_TD7_TARGET) {  // value_max / value_min tracking (td7.py:217-218)
+    if (h.mode == HEAD_TD7_TARGET || h.tgt_mode == HEAD_TD7_TARGET) {  // value_max / value_min (td7.py:217-218)
       int mx = ired[0], mn = ired[1];
       for (int w = 1; w < 4; ++w) {
         mx = max(mx, ired[2 * w]);

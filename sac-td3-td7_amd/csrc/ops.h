@@ -188,6 +188,14 @@ struct HeadArgs {                   // 4 rows per workgroup (1 per wave)
   int* vmax_key; int* vmin_key;      // TD7 value tracking (ordered-int keys)
   const float* vt;                   // TD7 [vt_max, vt_min]
   float inv_b;                       // 1/B (policy loss scale)
+  // *_LOSS with the target head fused in (one level fewer): tgt_mode is HEAD_TD7_TARGET or
+  // HEAD_MLP_TARGET and y is computed per row from the target twins' last hidden layer
+  // (th / tw / tb, as h / w / b), reward, notdone, vt (TD7) or alpha * logpi (SAC);
+  // -1: y is read from the `y` vector written by a separate *_TARGET head.
+  int tgt_mode;
+  Mat th[2];
+  const float* tw[2];
+  const float* tb[2];
 };
 
 enum { kTapeU = 1, kTapeInd = 2, kTapeEps = 4 };
