@@ -182,6 +182,11 @@ static void check_gemm(const GemmArgs& g) {
   };
   chk(g.A, false, g.M);
   chk(g.B, g.mode == GEMM_DW, g.N);
+  if (g.mode == GEMM_DX || (g.mode == GEMM_FWD && g.B.nseg > 1)) {  // W segment q pairs with A segment q
+    REQUIRE(g.B.nseg == g.A.nseg, "gemm: one W segment per A segment");
+    for (int q = 0; q < g.A.nseg; ++q)
+      REQUIRE(g.B.seg[q].r0 == g.A.seg[q].r0 && g.B.seg[q].r1 == g.A.seg[q].r1, "gemm: W / A segment mismatch");
+  }
   REQUIRE(g.R <= 16 * 1024, "gemm: reduction too long");
 }
 
@@ -495,6 +500,7 @@ struct Engine {
     REQUIRE(n == numel(netn, name), "size mismatch for " + netn + "." + name);
     const size_t base = (size_t)which * nP;
     HIPCHK(hipStreamSynchronize(stream));
+    if (to_dev) fold_dirty = true;
     if (netn == "tmp") {
       float* d = P + base + (nP - 4);
       if (to_dev) HIPCHK(hipMemcpy(d, host, 4, hipMemcpyHostToDevice));
@@ -596,11 +602,37 @@ struct Engine {
   // The GEMM kernel wants every A segment to span the op's whole row range, so
   // row pieces split the op into one sub-op per row range (same level, disjoint
   // output rows).
+  // A weight block for fwd(): N image of a [out][segment width] matrix (a column block
+  // of a layer's weights, or a folded product) and the resource it belongs to.
+  struct WSeg {
+    const float* p;
+    int xs, res;
+  };
+  WSeg wblock(const Layer& L, int col0) const {
+    return {P + L.wn_off + (size_t)(col0 / 16) * 256, L.cb, L.res};
+  }
+  // Columns [col0, col0 + width) of a layer's weights as a GEMM A operand (N image).
+  View wview_n(const Layer& L, int col0, int width) const {
+    View v;
+    v.m.n = P + L.wn_off + (size_t)(col0 / 16) * 256;
+    v.m.cbn = L.cb;
+    v.m.rbs = L.rb;
+    v.rows = L.out;
+    v.cols = r16(width);
+    v.id = L.res;
+    return v;
+  }
+
   View fwd(Prog& pg, const Layer& L, const std::vector<std::vector<View>>& ins, int M, int act, View* pre_out,
-           bool normed, const View* noise = nullptr, int noise_row0 = 0) {
+           bool normed, const View* noise = nullptr, int noise_row0 = 0, const std::vector<WSeg>* wsegs = nullptr,
+           const View* bias_ovr = nullptr) {
     REQUIRE(ins.size() == L.seg_p.size(), "fwd: input segment count mismatch for " + L.wname);
     REQUIRE(M % kTileM == 0, "fwd: rows must be a multiple of 16");
+    REQUIRE(!wsegs || wsegs->size() == ins.size(), "fwd: one weight block per input segment");
     std::vector<int> rd{L.res}, wr;
+    if (wsegs)
+      for (const WSeg& w : *wsegs) rd.push_back(w.res);
+    if (bias_ovr) rd.push_back(bias_ovr->id);
     std::vector<int> cuts{0, M};
     for (size_t s = 0; s < ins.size(); ++s) {
       int xo = 0;
@@ -658,15 +690,29 @@ struct Engine {
         koff += L.seg_p[s];
       }
       g.A.nseg = (int)ins.size();
-      Seg w{};
-      w.p = P + L.wn_off;
-      w.xs = L.cb;
-      w.x0 = 0;
-      w.x1 = L.out;
-      w.r0 = 0;
-      w.r1 = L.K;
-      g.B.seg[0] = w;
-      g.B.nseg = 1;
+      if (!wsegs) {
+        Seg w{};
+        w.p = P + L.wn_off;
+        w.xs = L.cb;
+        w.x0 = 0;
+        w.x1 = L.out;
+        w.r0 = 0;
+        w.r1 = L.K;
+        g.B.seg[0] = w;
+        g.B.nseg = 1;
+      } else {  // one weight block per input segment, paired like a DX operand
+        for (size_t q = 0; q < ins.size(); ++q) {
+          Seg w{};
+          w.p = (*wsegs)[q].p;
+          w.xs = (*wsegs)[q].xs;
+          w.x0 = 0;
+          w.x1 = L.out;
+          w.r0 = g.A.seg[q].r0;
+          w.r1 = g.A.seg[q].r1;
+          g.B.seg[q] = w;
+        }
+        g.B.nseg = (int)ins.size();
+      }
       g.M = m;
       g.N = L.out;
       g.R = L.K;
@@ -676,7 +722,7 @@ struct Engine {
       g.epi = EPI_STORE;
       g.act = act;
       g.out = out.sub(ra, m).m;
-      g.bias = bias(L);
+      g.bias = bias_ovr ? bias_ovr->p : bias(L);
       if (pre_out) g.pre = pre_out->sub(ra, m).m;
       if (normed) {
         g.norm_out = part + ra;
@@ -699,12 +745,14 @@ struct Engine {
 
   struct DxTerm {
     View dz;
-    const Layer* L;
+    const Layer* L;  // weights of a layer (T image) ...
     int col0;
+    const View* wv = nullptr;  // ... or of a derived [out][in] matrix (T image) when L is null
   };
 
   // dX[:, 0:ncols] = sum_t dZ_t W_t[:, col0_t : col0_t + ncols]  (* act'(saved))
-  View dx(Prog& pg, const std::vector<DxTerm>& terms, int ncols, int M, int dact, const View* saved) {
+  View dx(Prog& pg, const std::vector<DxTerm>& terms, int ncols, int M, int dact, const View* saved,
+          const View* into = nullptr) {
     Op op{};
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
@@ -714,19 +762,25 @@ struct Engine {
     int roff = 0;
     for (size_t t = 0; t < terms.size(); ++t) {
       const DxTerm& tm = terms[t];
-      REQUIRE(tm.dz.m.n && tm.col0 % 16 == 0, "dx: operand layout");
-      g.A.seg[t] = seg_n(tm.dz, roff, roff + tm.L->out);
+      REQUIRE(tm.dz.m.n && tm.col0 % 16 == 0 && (tm.L || (tm.wv && tm.wv->m.t)), "dx: operand layout");
+      const int wout = tm.L ? tm.L->out : tm.wv->rows;
+      g.A.seg[t] = seg_n(tm.dz, roff, roff + wout);
       Seg b{};  // W[:, col0 : col0 + ncols] through the T image
-      b.p = P + tm.L->wt_off + (size_t)(tm.col0 / 16) * tm.L->rb * 256;
-      b.xs = tm.L->rb;
+      if (tm.L) {
+        b.p = P + tm.L->wt_off + (size_t)(tm.col0 / 16) * tm.L->rb * 256;
+        b.xs = tm.L->rb;
+      } else {
+        b.p = tm.wv->m.t + (size_t)(tm.col0 / 16) * tm.wv->m.rbs * 256;
+        b.xs = tm.wv->m.rbs;
+      }
       b.x0 = 0;
       b.x1 = ncols;
       b.r0 = roff;
-      b.r1 = roff + tm.L->out;
+      b.r1 = roff + wout;
       g.B.seg[t] = b;
-      roff += r16(tm.L->out);
+      roff += r16(wout);
       rd.push_back(tm.dz.id);
-      rd.push_back(tm.L->res);
+      rd.push_back(tm.L ? tm.L->res : tm.wv->id);
     }
     g.A.nseg = g.B.nseg = (int)terms.size();
     g.M = M;
@@ -739,7 +793,8 @@ struct Engine {
     g.tiles_n = cdiv(ncols, g.tn);
     g.epi = EPI_STORE;
     g.act = ACT_NONE;
-    View out = buf(M, ncols);
+    View out = into ? *into : buf(M, ncols);
+    REQUIRE(!into || (into->rows == M && into->cols == r16(ncols)), "dx: output view shape");
     g.out = out.m;
     if (saved) {
       REQUIRE(saved->m.t, "dx: derivative source needs a T image");
@@ -1095,11 +1150,24 @@ struct Engine {
     // ---- target: zsa' and target critics
     View ta1 = fwd(pg, fet.layers[3], {{tzs}, {a_next}}, B, ACT_ELU, nullptr, false);
     View ta2 = fwd(pg, fet.layers[4], {{ta1}}, B, ACT_ELU, nullptr, false);
-    View tzsa = fwd(pg, fet.layers[5], {{ta2}}, B, ACT_NONE, nullptr, false);
+    // zsa' = zsa3(ta2) only feeds the target critics' first hidden layer, a linear map:
+    // with `fold`, tq.q1[:, zsa block] x fet.zsa3 is precomputed (add_target_fold) and the
+    // target critics read ta2 directly (one dependent level fewer)
+    const bool fold = td7_fold();
+    View tzsa;
+    if (!fold) tzsa = fwd(pg, fet.layers[5], {{ta2}}, B, ACT_NONE, nullptr, false);
     View th[2];
     for (int n = 0; n < 2; ++n) {
       View t01 = fwd(pg, tq[n]->layers[0], {{s2}, {a_next}}, B, ACT_NONE, nullptr, true);
-      View t1 = fwd(pg, tq[n]->layers[1], {{t01}, {tzsa}, {tzs}}, B, ACT_ELU, nullptr, false);
+      View t1;
+      if (fold) {  // fixed_encoder_target.zsa3 folded into the zsa block (tfold_w / tfold_b)
+        const Layer& L1 = tq[n]->layers[1];
+        const std::vector<WSeg> ws{wblock(L1, 0), {tfold_w[n].m.n, tfold_w[n].m.cbn, tfold_w[n].id},
+                                   wblock(L1, L1.seg_p[0] + L1.seg_p[1])};
+        t1 = fwd(pg, L1, {{t01}, {ta2}, {tzs}}, B, ACT_ELU, nullptr, false, nullptr, 0, &ws, &tfold_b[n]);
+      } else {
+        t1 = fwd(pg, tq[n]->layers[1], {{t01}, {tzsa}, {tzs}}, B, ACT_ELU, nullptr, false);
+      }
       th[n] = fwd(pg, tq[n]->layers[2], {{t1}}, B, ACT_ELU, nullptr, false);
     }
     // ---- online critics on (s, a, zsa_f, zs_f)
@@ -1196,9 +1264,17 @@ struct Engine {
         dxp01[n] = normbwd(pg, g, p01[n]);
       }
       // grad wrt zsa from both critics (q1 input columns [H, 2H))
-      View gzsa = dx(pg, {{dzp1[0], &q[0]->layers[1], Hp}, {dzp1[1], &q[1]->layers[1], Hp}}, H, B, ACT_NONE,
-                     nullptr);
-      View dpa2 = dx(pg, {{gzsa, &fe.layers[5], 0}}, H, B, ACT_ELU, &pa2z);
+      View dpa2;
+      if (fold) {  // d zsa -> d pa2 through zsa3 folded: G_n = q_n.q1[:, zsa block] x fe.zsa3 (updated critics)
+        View G[2];
+        for (int n = 0; n < 2; ++n)
+          G[n] = dx(pg, {{wview_n(q[n]->layers[1], Hp, H), &fe.layers[5], 0}}, H, H, ACT_NONE, nullptr);
+        dpa2 = dx(pg, {{dzp1[0], nullptr, 0, &G[0]}, {dzp1[1], nullptr, 0, &G[1]}}, H, B, ACT_ELU, &pa2z);
+      } else {
+        View gzsa = dx(pg, {{dzp1[0], &q[0]->layers[1], Hp}, {dzp1[1], &q[1]->layers[1], Hp}}, H, B, ACT_NONE,
+                       nullptr);
+        dpa2 = dx(pg, {{gzsa, &fe.layers[5], 0}}, H, B, ACT_ELU, &pa2z);
+      }
       View dpa1 = dx(pg, {{dpa2, &fe.layers[4], 0}}, H, B, ACT_ELU, &pa1z);
       // d action = sum of three paths, then tanh' (actor output)
       View dl3 = dx(pg,
@@ -1235,11 +1311,51 @@ struct Engine {
   float* qloss_part = nullptr;
   float* ploss_part = nullptr;
 
+  // Algebraic folds of TD7's linear zsa3 layer into its consumers (build_td7): on when
+  // every block is 16-aligned.  RLE_NO_FOLD=1 keeps the unfolded programs (tests).
+  bool td7_fold() const {
+    const char* e = std::getenv("RLE_NO_FOLD");
+    return algo == RLE_TD7 && H % 16 == 0 && !(e && e[0] == '1');
+  }
+  View tfold_w[2], tfold_b[2];  // per target critic: q1[:, zsa block] x fet.zsa3, folded q1 bias
+  bool fold_dirty = true;       // parameters written from the host since the last fold
+  Graph g_fold;
+  void alloc_folds() {
+    if (!td7_fold()) return;
+    for (int n = 0; n < 2; ++n) {
+      tfold_w[n] = buf(H, H);
+      tfold_b[n] = vec(H);
+    }
+  }
+  // tq_n.q1 applied to zsa3(x) = (W1[:, zsa] W3) x + (b1 + W1[:, zsa] b3): the target
+  // critics and the fixed target encoder change only at hard updates (and host loads)
+  void add_target_fold(Prog& pg) {
+    Net& fet = net("fixed_encoder_target");
+    for (int n = 0; n < 2; ++n) {
+      const Layer& L1 = net(n ? "target_q2" : "target_q1").layers[1];
+      const Layer& L3 = fet.layers[5];
+      dx(pg, {{wview_n(L1, L1.seg_p[0], H), &L3, 0}}, H, H, ACT_NONE, nullptr, &tfold_w[n]);
+      Op op{};
+      op.kind = OP_FOLDBIAS;
+      FoldBiasArgs& f = op.fb;
+      f.wn = P + L1.wn_off;
+      f.cbn = L1.cb;
+      f.col0 = L1.seg_p[0];
+      f.H = H;
+      f.bin = bias(L3);
+      f.bbase = bias(L1);
+      f.bout = tfold_b[n].p;
+      op.wg_count = 1;
+      pg.add(op, {L1.res, L3.res}, {tfold_b[n].id});
+    }
+  }
+
   void build_td7_hard(Prog& pg) {  // td7.py:278-285, 325-331
     flat(pg, OP_COPY, net("target_q1"), &net("q1"), 0.f, false);
     flat(pg, OP_COPY, net("target_q2"), &net("q2"), 0.f, false);
     flat(pg, OP_COPY, net("fixed_encoder_target"), &net("fixed_encoder"), 0.f, false);
     flat(pg, OP_COPY, net("fixed_encoder"), &net("encoder"), 0.f, false);
+    if (td7_fold()) add_target_fold(pg);
     Op c{};
     c.kind = OP_CTRL;
     c.ctrl.mode = 0;
@@ -1538,7 +1654,8 @@ struct Engine {
       total += lv.size();
     }
     static const char* kname[] = {"?", "gemm", "normbwd", "sreduce", "sgather", "head", "prio",
-                                  "sacfwd", "sacbwd", "end", "polyak", "copy", "maxred", "ctrl", "noise"};
+                                  "sacfwd", "sacbwd", "end", "polyak", "copy", "maxred", "ctrl", "noise",
+                                  "foldbias"};
     for (size_t l = 0; l < levels.size(); ++l) {
       G.desc += "L" + std::to_string(l) + " wg=" + std::to_string(G.nwg[l]) + ":";
       for (auto& op : levels[l]) {
@@ -1657,6 +1774,7 @@ struct Engine {
     REQUIRE(replay, "no replay bound");
     ensure_tapes(1024);
     const bool sac = algo == RLE_SAC;
+    alloc_folds();
     for (int set = 0; set < 2; ++set) {
       Prog pp;
       build_prime(pp, sac, set);
@@ -1679,6 +1797,11 @@ struct Engine {
       Prog ph;
       build_td7_hard(ph);
       g_hard = capture(ph);
+      if (td7_fold()) {
+        Prog pf;
+        add_target_fold(pf);
+        g_fold = capture(pf);
+      }
     }
     use_set(0);
     built = true;
@@ -1728,6 +1851,8 @@ struct Engine {
     REQUIRE(replay->size > 0, "replay is empty");
     if (!built) build();
     const int pf = std::max(1, cfg.policy_freq);
+    if (fold_dirty && g_fold.x) HIPCHK(hipGraphLaunch(g_fold.x, stream));
+    fold_dirty = false;
     int done = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (gpu_ms) {
@@ -2437,6 +2562,7 @@ int rle_copy_state(rle_engine* dst, rle_engine* src) {
     HIPCHK(hipMemcpy(d.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
     d.n_runs = s.n_runs;
     d.primed = false;
+    d.fold_dirty = true;
   });
 }
 

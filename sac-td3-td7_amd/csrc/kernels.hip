@@ -430,12 +430,16 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     // A: N image, segments along the reduction; B: W (FWD: N image, one segment over
     // the whole reduction; DX: T image, one segment per A segment)
     // (segment 0 from the hot header; later segments load their own fields)
+    // FWD with one W segment: W spans the whole reduction (absolute chunk index);
+    // DX, or FWD with one W segment per A segment (folded weight blocks): each W
+    // segment starts at its own reduction offset (relative chunk index)
+    const bool wabs = MODE == GEMM_FWD && nseg_b == 1;
     auto seg = [&](const float* sap, int sxs, int sr0, int sr1, const float* sbp, int bxs, float inva) {
       const int s0 = sr0 >> 4;
       const int k0 = max(c0, s0), k1 = min(c1, (sr1 + 15) >> 4);
       if (!active || k0 >= k1) return;
       const int va = ((i0 >> 4) * sxs + (k0 - s0)) * 1024 + lb;
-      const int vb = ((j0 >> 4) * bxs + (MODE == GEMM_FWD ? k0 : k0 - s0)) * 1024 + lb;
+      const int vb = ((j0 >> 4) * bxs + (wabs ? k0 : k0 - s0)) * 1024 + lb;
       acc = chunk_loop<NORM ? 1 : 0, 0>(rsrc(sap), va, rsrc(sbp), vb, k1 - k0, acc, inva, nullptr, nullptr, false);
     };
     auto inv_of = [&](int q) {
@@ -449,8 +453,8 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     for (int q = 1; q < nseg_a; ++q) {
       const CAS Seg& sa = g.A.seg[q];
       // FWD: one W segment over the whole reduction; DX: W segment q pairs with A segment q
-      const CAS Seg& sb = g.B.seg[MODE == GEMM_FWD ? 0 : q];
-      seg(sa.p, sa.xs, sa.r0, sa.r1, MODE == GEMM_FWD ? b0p : sb.p, MODE == GEMM_FWD ? b0xs : sb.xs, inv_of(q));
+      const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
+      seg(sa.p, sa.xs, sa.r0, sa.r1, wabs ? b0p : sb.p, wabs ? b0xs : sb.xs, inv_of(q));
     }
   } else {
     // DW: A = dZ (T image, x = output row), B = X (T image, x = output column; the
@@ -1355,6 +1359,16 @@ __device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
   }
 }
 
+// ---------------------------------------------------------------- folded bias
+// (runs at hard updates / parameter loads only: plain loads, one thread per output)
+__device__ __forceinline__ void op_foldbias(const CAS FoldBiasArgs& f) {
+  for (int o = threadIdx.x; o < f.H; o += kThreads) {
+    float acc = 0.f;
+    for (int z = 0; z < f.H; ++z) acc += f.wn[nidx(f.cbn, o, f.col0 + z)] * f.bin[z];
+    f.bout[o] = f.bbase[o] + acc;
+  }
+}
+
 // ---------------------------------------------------------------- dispatch
 
 // TRACE: compiled with the phase stamps (RLE_TRACE=1 runs); the production instance has
@@ -1410,6 +1424,7 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
     RLE_OP(OP_MAXRED, op_maxred(op.flat, t, smem))
     RLE_OP(OP_CTRL, op_ctrl(op.ctrl))
     RLE_OP(OP_NOISE, op_noise(op.sample, t))
+    RLE_OP(OP_FOLDBIAS, op_foldbias(op.fb))
 #endif
 #undef RLE_OP
     default: break;

@@ -28,6 +28,7 @@ enum OpKind : int {
   OP_MAXRED = 12,
   OP_CTRL = 13,
   OP_NOISE = 14,        // target-smoothing / rsample noise of the batch (SampleArgs)
+  OP_FOLDBIAS = 15,     // bias of a folded weight block (FoldBiasArgs)
 };
 
 // ---------------------------------------------------------------- tensor images
@@ -272,6 +273,17 @@ enum InfoKind : int {
   INFO_SAC_ENT = 7,   // -mean(logpi)
 };
 
+// Bias of a layer whose input block [col0, col0 + H) is fed by a linear layer folded
+// into it (y = W[:, blk] (V x + c) = (W[:, blk] V) x + W[:, blk] c):
+// bout[o] = bbase[o] + sum_z W[o][col0 + z] * bin[z], o < H.  One workgroup.
+struct FoldBiasArgs {
+  const float* wn; int cbn; int col0;  // W: N image, column blocks per row block
+  int H;                               // outputs (rows of W) = width of the block
+  const float* bin;                    // bias of the folded-in layer [H]
+  const float* bbase;                  // bias of the consuming layer [H]
+  float* bout;                         // [H]
+};
+
 struct FlatArgs {   // POLYAK / COPY / MAXRED
   float* dst; const float* src; long long n;
   float tau, omt; int self_alias;     // self_alias: p <- tau*p + p*(1-tau) (TD3 quirk Q2)
@@ -300,6 +312,7 @@ struct Op {
     StepEndArgs end;
     FlatArgs flat;
     CtrlArgs ctrl;
+    FoldBiasArgs fb;
   };
 };
 
