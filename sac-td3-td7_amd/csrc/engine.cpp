@@ -1236,26 +1236,21 @@ struct Engine {
       View pa1 = fwd(pg, fe.layers[3], {{fzs}, {a_pi}}, B, ACT_ELU, &pa1z, false);
       View pa2 = fwd(pg, fe.layers[4], {{pa1}}, B, ACT_ELU, &pa2z, false);
       View pzsa = fwd(pg, fe.layers[5], {{pa2}}, B, ACT_NONE, nullptr, false);
-      View p01[2], p1[2], p2[2], p1z[2], p2z[2];
+      View p01[2], p1[2], p1z[2], dzp2[2];
       for (int n = 0; n < 2; ++n) {
         p01[n] = fwd(pg, q[n]->layers[0], {{s}, {a_pi}}, B, ACT_NONE, nullptr, true);
         p1[n] = fwd(pg, q[n]->layers[1], {{p01[n]}, {pzsa}, {fzs}}, B, ACT_ELU, &p1z[n], false);
-        p2[n] = fwd(pg, q[n]->layers[2], {{p1[n]}}, B, ACT_ELU, &p2z[n], false);
       }
-      View dzp2[2] = {buf(B, H), buf(B, H)};
-      ploss_part = mem.make<float>((size_t)hw * 4);
-      {
-        Op op = head_op(HEAD_TD7_POLICY, B);
-        HeadArgs& h = op.head;
-        set_head_twin(h, p2[0], p2[1], q[0]->layers[3], q[1]->layers[3]);
-        h.dsrc[0] = p2z[0].m;
-        h.dsrc[1] = p2z[1].m;
-        h.dact = ACT_ELU;
-        h.dz[0] = dzp2[0].m;
-        h.dz[1] = dzp2[1].m;
-        h.loss_part = ploss_part;
-        pg.add(op, {p2[0].id, p2[1].id, p2z[0].id, p2z[1].id, q[0]->layers[3].res, q[1]->layers[3].res},
-               {dzp2[0].id, dzp2[1].id, ploss_id = next_id++});
+      // q2 + q3 + dL/dQ = -1/(2B) fused (EPI_QHEAD): dZ of q2 straight from the GEMM
+      ploss_id = next_id++;  // one loss resource per critic: the two heads share a level
+      ploss_id2 = next_id++;
+      ploss_part = mem.make<float>((size_t)(qhead_tiles(q[0]->layers[2]) + qhead_tiles(q[1]->layers[2])));
+      ploss_n = 0;
+      for (int n = 0; n < 2; ++n) {
+        int nt = 0;
+        dzp2[n] = fwd_qhead(pg, q[n]->layers[2], q[n]->layers[3], p1[n], B, -0.5f / (float)B, ploss_part + ploss_n,
+                            &nt, n ? ploss_id2 : ploss_id);
+        ploss_n += nt;
       }
       View dzp1[2], dxp01[2];
       for (int n = 0; n < 2; ++n) {
@@ -1298,16 +1293,64 @@ struct Engine {
     StepEndArgs& a = op.end;
     info_sum(a, 0, enc_loss, enc_tiles, 1, 1.f / (float)((long long)B * H));
     info_sum(a, 1, qloss_part, hw * 4, 1, (lap ? 1.f : 0.5f) / (float)B);
-    if (policy) info_sum(a, 2, ploss_part, hw, 4, -0.5f / (float)B);
+    if (policy) info_sum(a, 2, ploss_part, ploss_n, 1, -0.5f / (float)B);
     else a.kind[2] = INFO_NAN;
     a.ninfo = 3;
     std::vector<int> rd{loss_id_enc, qloss_id};
-    if (policy) rd.push_back(ploss_id);
+    if (policy) {
+      rd.push_back(ploss_id);
+      rd.push_back(ploss_id2);
+    }
     std::vector<int> cn{CNT_ADAM_Q, CNT_ADAM_ENC, 3, CNT_RNG, CNT_TAPE};
     if (policy) cn.push_back(CNT_ADAM_PI);
     add_step_end(pg, op, rd, cn);
   }
-  int loss_id_enc = -1, qloss_id = -1, ploss_id = -1;
+  int loss_id_enc = -1, qloss_id = -1, ploss_id = -1, ploss_id2 = -1, ploss_n = 0;
+
+  // Upper bound on the tiles of a fwd_qhead GEMM over B rows (its loss partial slots).
+  int qhead_tiles(const Layer& L) const { return cdiv(B, kTileM) * cdiv(L.out, kTileM); }
+  // dZ of a critic's last hidden layer L (input x, activation ELU) under a constant dL/dq
+  // through the head layer Lq (H -> 1), and per-tile sums of Q - b3 (+ B b3 on tile 0)
+  // into part[0, *ntiles).
+  View fwd_qhead(Prog& pg, const Layer& L, const Layer& Lq, const View& x, int M, float dq, float* part,
+                 int* ntiles, int loss_id) {
+    REQUIRE(L.seg_p.size() == 1 && x.cols == L.seg_p[0] && x.m.n && Lq.out == 1, "qhead: operand layout");
+    Op op{};
+    op.kind = OP_GEMM;
+    GemmArgs& g = op.gemm;
+    g.mode = GEMM_FWD;
+    g.A.seg[0] = seg_n(x, 0, L.K);
+    g.A.nseg = 1;
+    Seg w{};
+    w.p = P + L.wn_off;
+    w.xs = L.cb;
+    w.x1 = L.out;
+    w.r1 = L.K;
+    g.B.seg[0] = w;
+    g.B.nseg = 1;
+    g.M = M;
+    g.N = L.out;
+    g.R = L.K;
+    const auto tq = choose_tn(M, L.out);
+    g.tn = tq.first;
+    op.seq = tq.second;
+    g.tiles_m = cdiv(M, kTileM);
+    g.tiles_n = cdiv(L.out, g.tn);
+    *ntiles = g.tiles_m * g.tiles_n;
+    g.epi = EPI_QHEAD;
+    g.act = ACT_ELU;
+    g.bias = bias(L);
+    View dz = buf(M, L.out);
+    g.out = dz.m;
+    g.loss_part = part;
+    g.qw = P + Lq.wn_off;
+    g.qw_cbn = Lq.cb;
+    g.qb = bias(Lq);
+    g.qscale = dq;
+    op.wg_count = g.tiles_m * g.tiles_n;
+    pg.add(op, {x.id, L.res, Lq.res}, {dz.id, loss_id});
+    return dz;
+  }
   float* qloss_part = nullptr;
   float* ploss_part = nullptr;
 
@@ -1661,7 +1704,7 @@ struct Engine {
       for (auto& op : levels[l]) {
         G.desc += std::string(" ") + kname[op.kind];
         if (op.kind == OP_GEMM) {
-          const char* ep = op.gemm.epi == EPI_ADAM ? "adam" : (op.gemm.epi == EPI_MSE ? "mse" : "st");
+          const char* ep = op.gemm.epi == EPI_ADAM ? "adam" : (op.gemm.epi == EPI_MSE ? "mse" : (op.gemm.epi == EPI_QHEAD ? "qhead" : "st"));
           G.desc += "[" + std::to_string(op.gemm.M) + "x" + std::to_string(op.gemm.N) + "x" +
                     std::to_string(op.gemm.R) + " " + ep + "]";
         }

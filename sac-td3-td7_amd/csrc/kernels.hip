@@ -401,6 +401,10 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   float pre_b = 0.f;
   float4 ds = make_float4(1.f, 1.f, 1.f, 1.f), pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
   size_t wt = 0;
+  float qwj = 0.f;
+  if constexpr (EPI == EPI_QHEAD) {
+    if (jok) qwj = G(g.qw)[nidx(g.qw_cbn, 0, j)];
+  }
   if constexpr (EPI != EPI_ADAM) {
     if (jok && biasp) pre_b = G(biasp)[j];
     if constexpr (MODE == GEMM_DX && ACT != ACT_NONE) {
@@ -540,6 +544,20 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
               (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
       }
     }
+  } else if constexpr (EPI == EPI_QHEAD) {  // td7.py:268-275: Q = w3 . act(z) + b3, L = -mean(cat Q)
+    float ls = 0.f;
+    if (jok) {
+      float dz[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float z = acc[q] + pre_b, y = act_f<ACT>(z);
+        ls += y * qwj;
+        dz[q] = (g.qscale * qwj) * act_b<ACT>(ACT == ACT_RELU ? y : z);
+      }
+      mat_st4(g.out, ib, j, make_float4(dz[0], dz[1], dz[2], dz[3]));
+    }
+    ls = wg_sum(ls, red);
+    if (tid == 0) GW(g.loss_part)[t] = t == 0 ? ls + (float)g.M * sload(g.qb) : ls;
   } else if constexpr (EPI == EPI_MSE) {  // td7.py:256 encoder loss, grad wrt zsa
     float d2 = 0.f;
     if (jok) {
@@ -612,6 +630,7 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_V(GEMM_FWD, EPI_STORE, ACT_ELU, true)
     RLE_V(GEMM_FWD, EPI_STORE, ACT_TANH, false)
     RLE_V(GEMM_FWD, EPI_STORE, ACT_TANH, true)
+    RLE_V(GEMM_FWD, EPI_QHEAD, ACT_ELU, false)
     RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, false)
     RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, true)
     RLE_V(GEMM_DX, EPI_STORE, ACT_NONE, false)

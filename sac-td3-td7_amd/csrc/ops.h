@@ -84,6 +84,8 @@ enum Epi : int {
   EPI_STORE = 0,   // out = act(acc + bias); optional pre-act store, |y| partials, derivative mask, tanh-noise
   EPI_ADAM = 1,    // acc is dL/dW (or dL/db on the bias tile column): Adam in place
   EPI_MSE = 2,     // acc (+bias) = zsa; grad = 2 (zsa - tgt) / n ; loss partial sum of squares
+  EPI_QHEAD = 3,   // critic's last hidden layer with its H -> 1 head and a constant dL/dq fused:
+                   // out = qscale * w3 * act'(z) (= dZ), loss partial sum of act(z) * w3 (+ M b3)
 };
 
 struct AdamArgs {
@@ -145,8 +147,10 @@ struct GemmArgs {
   Mat dsrc;                        // T image
   Mat noise; int noise_row0; float noise_sigma, noise_clip;  // tanh-noise (T image)
   Mat tgt; NormRef tgt_norm;       // EPI_MSE target (T image of a normed view)
-  float* loss_part;                // EPI_MSE per-tile partial sums
+  float* loss_part;                // EPI_MSE / EPI_QHEAD per-tile partial sums
   float mse_scale;                 // 1/n
+  const float* qw; const float* qb; int qw_cbn;  // EPI_QHEAD: head weight row (N image of [1][N]), bias
+  float qscale;                    // EPI_QHEAD: dL/dq
   int pad_;
   AdamArgs adam;
 };
