@@ -127,6 +127,10 @@ struct View {
   int id = -1;
   const float* norm = nullptr;  // AvgL1Norm partials (producer |x| column-tile sums)
   int norm_ld = 0, norm_row0 = 0, nparts = 0, width = 0, norm_id = -1;
+  // EPI_NBDOT output (the gradient g of an AvgL1Norm output whose backward is deferred
+  // into the consuming DW, kDwNb): row partials of sum_j g x
+  const float* nbdot = nullptr;
+  int nbdot_ld = 0, nbdot_n = 0, nbdot_id = -1;
   View sub(int r0, int n) const {
     View v = *this;
     if (m.n || m.t) {
@@ -196,9 +200,14 @@ static void gemm_finalize(GemmArgs& g) {
   int norm = 0;
   for (int q = 0; q < g.A.nseg; ++q) norm |= g.A.seg[q].norm.part != nullptr;
   for (int q = 0; q < g.B.nseg; ++q) norm |= g.B.seg[q].norm.part != nullptr;
-  const int act = g.mode == GEMM_FWD ? g.act : (g.mode == GEMM_DX ? g.dact : ACT_NONE);
+  const int act = g.mode == GEMM_FWD ? g.act : (g.mode == GEMM_DX ? g.dact : g.act);
   REQUIRE(g.mode != GEMM_DX || !norm, "gemm: no DX variant with normed operands");
   REQUIRE(g.mode != GEMM_DW || g.epi == EPI_ADAM, "gemm: DW is always fused with Adam");
+  REQUIRE(g.mode != GEMM_DW || act == ACT_NONE || (act == kDwNb && !norm && g.nbx.t && g.nbm.part && g.nbdot &&
+                                                   g.R <= 1024),
+          "gemm: deferred AvgL1Norm backward operands");
+  REQUIRE(g.epi != EPI_NBDOT || (g.mode == GEMM_DX && act == ACT_NONE && g.nbx.t && g.norm_out),
+          "gemm: EPI_NBDOT is a plain DX with x and partials");
   REQUIRE(g.epi != EPI_MSE || act == ACT_NONE, "gemm: MSE epilogue takes no activation");
   REQUIRE((g.dact == ACT_NONE) == (g.dsrc.t == nullptr) || g.mode != GEMM_DX, "gemm: DX derivative source");
   g.vid = gemm_vid(g.mode, g.epi, act, norm);
@@ -752,7 +761,7 @@ struct Engine {
 
   // dX[:, 0:ncols] = sum_t dZ_t W_t[:, col0_t : col0_t + ncols]  (* act'(saved))
   View dx(Prog& pg, const std::vector<DxTerm>& terms, int ncols, int M, int dact, const View* saved,
-          const View* into = nullptr) {
+          const View* into = nullptr, const View* nb_x = nullptr) {
     Op op{};
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
@@ -794,6 +803,21 @@ struct Engine {
     g.epi = EPI_STORE;
     g.act = ACT_NONE;
     View out = into ? *into : buf(M, ncols);
+    if (nb_x) {  // out = g of AvgL1Norm(x): row partials of sum_j g x for the consuming DW (kDwNb)
+      REQUIRE(!saved && nb_x->norm && nb_x->m.t && nb_x->rows == M && nb_x->cols == r16(ncols),
+              "dx: deferred AvgL1Norm backward operands");
+      g.epi = EPI_NBDOT;
+      g.nbx = nb_x->m;
+      float* part = mem.make<float>((size_t)cdiv(ncols, kTileM) * M);  // any tile plan fits
+      g.norm_out = part;
+      g.norm_ld = M;
+      out.nbdot = part;
+      out.nbdot_ld = M;
+      out.nbdot_n = g.tiles_n;
+      out.nbdot_id = next_id++;
+      wr.push_back(out.nbdot_id);
+      rd.push_back(nb_x->id);
+    }
     REQUIRE(!into || (into->rows == M && into->cols == r16(ncols)), "dx: output view shape");
     g.out = out.m;
     if (saved) {
@@ -825,7 +849,7 @@ struct Engine {
 
   // dW = dZ^T [X], db = sum dZ, fused Adam (torch.optim.Adam law).
   void dw(Prog& pg, const Layer& L, const View& dz, const std::vector<View>& X, int Brows, int cnt, float lr,
-          float* gsq = nullptr, float* gsq_b = nullptr) {
+          float* gsq = nullptr, float* gsq_b = nullptr, const View* nb_x = nullptr) {
     REQUIRE(X.size() == L.seg_p.size(), "dw: input count mismatch for " + L.wname);
     REQUIRE(dz.m.t, "dw: dZ needs a T image");
     Op op{};
@@ -870,6 +894,19 @@ struct Engine {
     ad.bias_col = cdiv(L.K, g.tn) * g.tn;
     ad.gsq = gsq;
     ad.gsq_b = gsq_b;
+    if (nb_x) {  // dZ = AvgL1Norm backward of (dz = g, x), applied on load (kDwNb)
+      REQUIRE(dz.nbdot && nb_x->norm && nb_x->m.t && nb_x->rows >= Brows, "dw: deferred AvgL1Norm backward operands");
+      g.act = kDwNb;
+      g.nbx = nb_x->m;
+      g.nbx_xs = nb_x->m.rbs;
+      g.nbm = nb_x->nref();
+      g.nbdot = dz.nbdot;
+      g.nbdot_ld = dz.nbdot_ld;
+      g.nbdot_n = dz.nbdot_n;
+      rd.push_back(nb_x->id);
+      rd.push_back(nb_x->norm_id);
+      rd.push_back(dz.nbdot_id);
+    }
     op.wg_count = g.tiles_m * g.tiles_n;
     pg.add(op, rd, wr);
   }
@@ -1063,6 +1100,7 @@ struct Engine {
     Net* q[2] = {&net("q1"), &net("q2")};
     Net* tq[2] = {&net("target_q1"), &net("target_q2")};
     const bool lap = cfg.use_lap;
+    const bool nbd = td7_nb_defer();
     use_set(set);
     add_adam_scalars(pg);
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
@@ -1225,10 +1263,14 @@ struct Engine {
       dw(pg, Q.layers[3], dq[n], {c2[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
       View d1 = dx(pg, {{dz2[n], &Q.layers[2], 0}}, H, B, ACT_ELU, &c1z[n]);
       dw(pg, Q.layers[2], dz2[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
-      View g01 = dx(pg, {{d1, &Q.layers[1], 0}}, H, B, ACT_NONE, nullptr);
+      View g01 = dx(pg, {{d1, &Q.layers[1], 0}}, H, B, ACT_NONE, nullptr, nullptr, nbd ? &c01[n] : nullptr);
       dw(pg, Q.layers[1], d1, {c01[n], fzsa, fzs}, B, CNT_ADAM_Q, cfg.critic_lr);
-      View dx01 = normbwd(pg, g01, c01[n]);
-      dw(pg, Q.layers[0], dx01, {s, act_in}, B, CNT_ADAM_Q, cfg.critic_lr);
+      if (nbd) {  // AvgL1Norm backward deferred into the weight-gradient GEMM (kDwNb)
+        dw(pg, Q.layers[0], g01, {s, act_in}, B, CNT_ADAM_Q, cfg.critic_lr, nullptr, nullptr, &c01[n]);
+      } else {
+        View dx01 = normbwd(pg, g01, c01[n]);
+        dw(pg, Q.layers[0], dx01, {s, act_in}, B, CNT_ADAM_Q, cfg.critic_lr);
+      }
     }
     ploss_part = nullptr;
     if (policy) {  // td7.py:259-276 with the updated critics
@@ -1283,10 +1325,15 @@ struct Engine {
       dw(pg, pi.layers[3], dl3, {ap2s}, B, CNT_ADAM_PI, cfg.policy_lr);
       View dl1 = dx(pg, {{dl2, &pi.layers[2], 0}}, H, B, ACT_RELU, &ap1s);
       dw(pg, pi.layers[2], dl2, {ap1s}, B, CNT_ADAM_PI, cfg.policy_lr);
-      View gl0 = dx(pg, {{dl1, &pi.layers[1], 0}}, H, B, ACT_NONE, nullptr);
-      dw(pg, pi.layers[1], dl1, {ap0.sub(0, B), fzs}, B, CNT_ADAM_PI, cfg.policy_lr);
-      View dl0 = normbwd(pg, gl0, ap0.sub(0, B));
-      dw(pg, pi.layers[0], dl0, {s}, B, CNT_ADAM_PI, cfg.policy_lr);
+      const View ap0s = ap0.sub(0, B);
+      View gl0 = dx(pg, {{dl1, &pi.layers[1], 0}}, H, B, ACT_NONE, nullptr, nullptr, nbd ? &ap0s : nullptr);
+      dw(pg, pi.layers[1], dl1, {ap0s, fzs}, B, CNT_ADAM_PI, cfg.policy_lr);
+      if (nbd) {
+        dw(pg, pi.layers[0], gl0, {s}, B, CNT_ADAM_PI, cfg.policy_lr, nullptr, nullptr, &ap0s);
+      } else {
+        View dl0 = normbwd(pg, gl0, ap0s);
+        dw(pg, pi.layers[0], dl0, {s}, B, CNT_ADAM_PI, cfg.policy_lr);
+      }
     }
     // ---- step end: info row [encoder, q_fn, policy]
     Op op = step_end_op();
@@ -1359,6 +1406,13 @@ struct Engine {
   bool td7_fold() const {
     const char* e = std::getenv("RLE_NO_FOLD");
     return algo == RLE_TD7 && H % 16 == 0 && !(e && e[0] == '1');
+  }
+  // AvgL1Norm backwards that feed only a weight-gradient GEMM are applied inside it
+  // (EPI_NBDOT producer + kDwNb consumer: one level fewer).  RLE_NO_NBDEFER=1: separate
+  // OP_NORMBWD (tests).
+  bool td7_nb_defer() const {
+    const char* e = std::getenv("RLE_NO_NBDEFER");
+    return B <= 1024 && !(e && e[0] == '1');
   }
   View tfold_w[2], tfold_b[2];  // per target critic: q1[:, zsa block] x fet.zsa3, folded q1 bias
   bool fold_dirty = true;       // parameters written from the host since the last fold
@@ -1704,7 +1758,8 @@ struct Engine {
       for (auto& op : levels[l]) {
         G.desc += std::string(" ") + kname[op.kind];
         if (op.kind == OP_GEMM) {
-          const char* ep = op.gemm.epi == EPI_ADAM ? "adam" : (op.gemm.epi == EPI_MSE ? "mse" : (op.gemm.epi == EPI_QHEAD ? "qhead" : "st"));
+          static const char* kepi[] = {"st", "adam", "mse", "qhead", "nbdot"};
+          const char* ep = op.gemm.mode == GEMM_DW && op.gemm.act == kDwNb ? "adam+nb" : kepi[op.gemm.epi];
           G.desc += "[" + std::to_string(op.gemm.M) + "x" + std::to_string(op.gemm.N) + "x" +
                     std::to_string(op.gemm.R) + " " + ep + "]";
         }

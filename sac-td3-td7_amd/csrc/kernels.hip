@@ -357,6 +357,57 @@ __device__ __forceinline__ f32x4 chunk_loop(__amdgpu_buffer_rsrc_t ra, int va, _
   return acc + acc1;
 }
 
+__device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
+
+// DW reduction whose A operand (dZ, T image) is an AvgL1Norm backward applied on load
+// (kDwNb, sale.py:11-13): a = g * inv[r] + sign(x) * gm[r] for the chunk's rows r, with
+// x read from (rx, vx) in the same T-image layout as g and inv / gm from LDS tables
+// (ti / tg: float offset of chunk k0's first row).  Same ring as chunk_loop.
+__device__ __forceinline__ f32x4 chunk_loop_nb(__amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rx, int vx,
+                                               __amdgpu_buffer_rsrc_t rb, int vb, int n, f32x4 acc, const float* ti,
+                                               const float* tg, bool bias_ones) {
+  const int rl = ((threadIdx.x & 63) >> 4) << 2;
+  float4 a[kRing], x[kRing], b[kRing];
+#pragma unroll
+  for (int r = 0; r < kRing; ++r) {
+    a[r] = bload(ra, r < n ? va + r * 1024 : kOOB);
+    x[r] = bload(rx, r < n ? vx + r * 1024 : kOOB);
+    b[r] = bias_ones ? make_float4(1.f, 1.f, 1.f, 1.f) : bload(rb, r < n ? vb + r * 1024 : kOOB);
+  }
+  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int c = 0; c < n; c += kRing) {
+#pragma unroll
+    for (int r = 0; r < kRing; ++r) {
+      const int k = min(c + r, n - 1);
+      const float4 iv = *(const float4*)(ti + k * 16 + rl), gv = *(const float4*)(tg + k * 16 + rl);
+      const float4 y = make_float4(a[r].x * iv.x + sgnf(x[r].x) * gv.x, a[r].y * iv.y + sgnf(x[r].y) * gv.y,
+                                   a[r].z * iv.z + sgnf(x[r].z) * gv.z, a[r].w * iv.w + sgnf(x[r].w) * gv.w);
+      if (r & 1) acc1 = mfma4(y, b[r], acc1);
+      else acc = mfma4(y, b[r], acc);
+      const int nx = c + r + kRing;
+      a[r] = bload(ra, nx < n ? va + nx * 1024 : kOOB);
+      x[r] = bload(rx, nx < n ? vx + nx * 1024 : kOOB);
+      if (!bias_ones) b[r] = bload(rb, nx < n ? vb + nx * 1024 : kOOB);
+    }
+  }
+  return acc + acc1;
+}
+
+// kDwNb tables for the n reduction rows: 1/m and the sign coefficient
+// gm = -(sum_j g x) / (n_x m^2) (0 when m is clamped), exactly as op_normbwd.
+__device__ __forceinline__ void build_nb_tab(const CAS GemmArgs& g, int n, float* ti, float* tg) {
+#pragma unroll 1
+  for (int i = threadIdx.x; i < n; i += kThreads) {
+    const float mean = norm_mean(g.nbm.part, g.nbm.ld, i + g.nbm.row0, g.nbm.nparts, g.nbm.width);
+    const bool clamped = mean < 1e-8f;
+    const float inv = 1.f / (clamped ? 1e-8f : mean);
+    const float dot = norm_mean(g.nbdot, g.nbdot_ld, i, g.nbdot_n, 1);
+    ti[i] = inv;
+    tg[i] = clamped ? 0.f : (-dot * inv * inv) / (float)g.nbm.width;
+  }
+}
+
 template <int MODE, int EPI, int ACT, bool NORM>
 __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -404,6 +455,10 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   float qwj = 0.f;
   if constexpr (EPI == EPI_QHEAD) {
     if (jok) qwj = G(g.qw)[nidx(g.qw_cbn, 0, j)];
+  }
+  float4 nbxv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (EPI == EPI_NBDOT) {
+    if (jok) nbxv = mat_ld4(g.nbx, ib, j);
   }
   if constexpr (EPI != EPI_ADAM) {
     if (jok && biasp) pre_b = G(biasp)[j];
@@ -482,10 +537,20 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       __syncthreads();
       if (mine >= 0) tb = tabs + mine + c0 * 16;
     }
+    int tgo = 0;
+    if constexpr (ACT == kDwNb) {
+      tgo = (gR + 15) & ~15;
+      build_nb_tab(g, gR, tabs, tabs + tgo);
+      __syncthreads();
+    }
     if (active && c0 < c1) {
       const int va = ((i0 >> 4) * a0xs + c0) * 1024 + lb;
       const int vb = (((j0 - sb.x0) >> 4) * sb.xs + c0) * 1024 + lb;
-      if (NORM && tb && !bias_tile)  // the bias column's B is ones: never scaled
+      if constexpr (ACT == kDwNb) {
+        const int vx = ((i0 >> 4) * g.nbx_xs + c0) * 1024 + lb;
+        acc = chunk_loop_nb(rsrc(a0p), va, rsrc(g.nbx.t), vx, rsrc(sb.p), vb, c1 - c0, acc, tabs + c0 * 16,
+                            tabs + tgo + c0 * 16, bias_tile);
+      } else if (NORM && tb && !bias_tile)  // the bias column's B is ones: never scaled
         acc = chunk_loop<0, 2>(rsrc(a0p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, tb, bias_tile);
       else
         acc = chunk_loop<0, 0>(rsrc(a0p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, nullptr, bias_tile);
@@ -558,6 +623,20 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     }
     ls = wg_sum(ls, red);
     if (tid == 0) GW(g.loss_part)[t] = t == 0 ? ls + (float)g.M * sload(g.qb) : ls;
+  } else if constexpr (EPI == EPI_NBDOT) {  // sale.py:11-13 backward, first half (the rest: kDwNb)
+    float rd[4] = {0.f, 0.f, 0.f, 0.f};
+    if (jok) {
+      const float xq[4] = {nbxv.x, nbxv.y, nbxv.z, nbxv.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rd[q] = acc[q] * xq[q];
+      mat_st4(g.out, ib, j, make_float4(acc[0], acc[1], acc[2], acc[3]));
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rd[q] = row16_sum(rd[q]);
+    if ((lane & 15) == 0) *(float4*)(red + wave * 16 + ((lane >> 4) << 2)) = make_float4(rd[0], rd[1], rd[2], rd[3]);
+    __syncthreads();
+    if (tid < 16)
+      GW(g.norm_out)[(size_t)jt * g.norm_ld + i0 + tid] = (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
   } else if constexpr (EPI == EPI_MSE) {  // td7.py:256 encoder loss, grad wrt zsa
     float d2 = 0.f;
     if (jok) {
@@ -637,8 +716,10 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_V(GEMM_DX, EPI_STORE, ACT_RELU, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_ELU, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_TANH, false)
+    RLE_V(GEMM_DX, EPI_NBDOT, ACT_NONE, false)
     RLE_V(GEMM_DW, EPI_ADAM, ACT_NONE, false)
     RLE_V(GEMM_DW, EPI_ADAM, ACT_NONE, true)
+    RLE_V(GEMM_DW, EPI_ADAM, kDwNb, false)
     default: break;
   }
 #undef RLE_V

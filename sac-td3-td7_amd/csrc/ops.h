@@ -86,7 +86,12 @@ enum Epi : int {
   EPI_MSE = 2,     // acc (+bias) = zsa; grad = 2 (zsa - tgt) / n ; loss partial sum of squares
   EPI_QHEAD = 3,   // critic's last hidden layer with its H -> 1 head and a constant dL/dq fused:
                    // out = qscale * w3 * act'(z) (= dZ), loss partial sum of act(z) * w3 (+ M b3)
+  EPI_NBDOT = 4,   // DX whose output g feeds an AvgL1Norm backward deferred into its consumer:
+                   // out = g, per-tile row partials of sum_j g x (x: nbx) into norm_out
 };
+// GEMM_DW variant whose A operand (dZ) is an AvgL1Norm backward applied on load:
+// a = g / m + sign(x) * gm, gm = -(sum_j g x) / (n m^2) (0 when m is clamped), rows by LDS table
+constexpr int kDwNb = 1;  // (in the act slot of a DW variant id)
 
 struct AdamArgs {
   Mat w;                 // weight images [N out rows][K cols] (both kept: FWD reads N, DX reads T)
@@ -101,10 +106,10 @@ struct AdamArgs {
   float* gsq_b;          // optional: per-tile sum of squared grads (bias), [tiles_m]
 };
 
-// Variant id of a GEMM op = mode * 32 + epi * 8 + act * 2 + norm (act: the forward
-// activation for GEMM_FWD, the derivative mask for GEMM_DX; norm: some operand
+// Variant id of a GEMM op = mode * 64 + epi * 8 + act * 2 + norm (act: the forward
+// activation for GEMM_FWD, the derivative mask for GEMM_DX, kDwNb or 0 for GEMM_DW; norm: some operand
 // segment carries a deferred AvgL1Norm).
-constexpr int gemm_vid(int mode, int epi, int act, int norm) { return mode * 32 + epi * 8 + act * 2 + norm; }
+constexpr int gemm_vid(int mode, int epi, int act, int norm) { return mode * 64 + epi * 8 + act * 2 + norm; }
 
 enum GemmMode : int {
   GEMM_FWD = 0,   // A contiguous (activations), B contiguous (W rows):  Y = X W^T
@@ -151,6 +156,9 @@ struct GemmArgs {
   float mse_scale;                 // 1/n
   const float* qw; const float* qb; int qw_cbn;  // EPI_QHEAD: head weight row (N image of [1][N]), bias
   float qscale;                    // EPI_QHEAD: dL/dq
+  Mat nbx; int nbx_xs;             // EPI_NBDOT / kDwNb: x of the AvgL1Norm (T image; DW: its x-block step)
+  NormRef nbm;                     // kDwNb: m of x's rows (producer |x| partials)
+  const float* nbdot; int nbdot_ld, nbdot_n;  // kDwNb: the EPI_NBDOT producer's row partials of sum g x
   int pad_;
   AdamArgs adam;
 };
