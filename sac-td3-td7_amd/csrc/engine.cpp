@@ -210,7 +210,11 @@ static void gemm_finalize(GemmArgs& g) {
           "gemm: EPI_NBDOT is a plain DX with x and partials");
   REQUIRE(g.epi != EPI_MSE || act == ACT_NONE, "gemm: MSE epilogue takes no activation");
   REQUIRE((g.dact == ACT_NONE) == (g.dsrc.t == nullptr) || g.mode != GEMM_DX, "gemm: DX derivative source");
-  g.vid = gemm_vid(g.mode, g.epi, act, norm);
+  REQUIRE(!g.has_pre || ((g.mode == GEMM_FWD || g.mode == GEMM_DX) && g.prea.N <= 32 && g.prea.seg < g.A.nseg &&
+                          g.A.seg[g.prea.seg].r1 - g.A.seg[g.prea.seg].r0 <= 32 && g.prea.mode == g.mode &&
+                          g.prea.R % 16 == 0),
+          "gemm: pre-GEMM layout");
+  g.vid = gemm_vid(g.mode, g.epi, act, norm, g.has_pre ? 1 : 0);
   REQUIRE(g.tn == 16 || g.tn == 32 || g.tn == 64, "gemm: tile width");
   g.ks_log = g.tn == 16 ? 2 : (g.tn == 32 ? 1 : 0);
   REQUIRE(g.R % 16 == 0, "gemm: reduction length must be a multiple of 16");
@@ -632,9 +636,83 @@ struct Engine {
     return v;
   }
 
+  struct DxTerm {
+    View dz;
+    const Layer* L;  // weights of a layer (T image) ...
+    int col0;
+    const View* wv = nullptr;  // ... or of a derived [out][in] matrix (T image) when L is null
+  };
+
+  // A pre-GEMM (PreArgs) and the resources it reads, for fwd() / dx(): the consumer's A segment
+  // a.seg is computed in-tile, so the view passed for that segment only gives its layout.
+  struct PreUse {
+    PreArgs a;
+    std::vector<int> rd;
+  };
+  // The actor's tanh output layer L over rows x (+ target smoothing noise) as a pre-GEMM
+  // (sale.py:77-83 / mlp.py:55-62, td7.py:188-194, td3.py:154-158).
+  PreUse pre_actor_fwd(const Layer& L, const View& x, const View* noise, int seg) {
+    REQUIRE(L.out <= 32 && L.seg_p.size() == 1 && x.m.n && !x.norm, "pre: actor output layer operands");
+    PreUse u{};
+    PreArgs& p = u.a;
+    p.mode = GEMM_FWD;
+    p.A.seg[0] = seg_n(x, 0, L.K);
+    p.A.nseg = 1;
+    Seg w{};
+    w.p = P + L.wn_off;
+    w.xs = L.cb;
+    w.x1 = L.out;
+    w.r1 = L.K;
+    p.B.seg[0] = w;
+    p.B.nseg = 1;
+    p.N = L.out;
+    p.R = L.K;
+    p.seg = seg;
+    p.bias = bias(L);
+    u.rd = {x.id, L.res};
+    if (noise) {
+      p.noise = noise->m;
+      p.noise_sigma = cfg.target_policy_noise;
+      p.noise_clip = cfg.noise_clip;
+      u.rd.push_back(noise->id);
+    }
+    return u;
+  }
+  // The gradient wrt the actor's tanh input, sum_t dZ_t W_t[:, col0_t ..] * (1 - a^2), as a
+  // pre-GEMM (the DX op dx(terms, ncols, ..., ACT_TANH, &a) would compute).
+  PreUse pre_actor_dx(const std::vector<DxTerm>& terms, int ncols, const View& a, int seg) {
+    REQUIRE(ncols <= 32 && a.m.t && (int)terms.size() <= kMaxSeg, "pre: actor output gradient operands");
+    PreUse u{};
+    PreArgs& p = u.a;
+    p.mode = GEMM_DX;
+    int roff = 0;
+    for (size_t t = 0; t < terms.size(); ++t) {
+      const DxTerm& tm = terms[t];
+      REQUIRE(tm.L && tm.dz.m.n && tm.col0 % 16 == 0, "pre: dx term layout");
+      p.A.seg[t] = seg_n(tm.dz, roff, roff + tm.L->out);
+      Seg b{};
+      b.p = P + tm.L->wt_off + (size_t)(tm.col0 / 16) * tm.L->rb * 256;
+      b.xs = tm.L->rb;
+      b.x1 = ncols;
+      b.r0 = roff;
+      b.r1 = roff + tm.L->out;
+      p.B.seg[t] = b;
+      roff += r16(tm.L->out);
+      u.rd.push_back(tm.dz.id);
+      u.rd.push_back(tm.L->res);
+    }
+    p.A.nseg = p.B.nseg = (int)terms.size();
+    p.N = ncols;
+    p.R = roff;
+    p.seg = seg;
+    p.dsrc = a.m;
+    u.rd.push_back(a.id);
+    return u;
+  }
+
   View fwd(Prog& pg, const Layer& L, const std::vector<std::vector<View>>& ins, int M, int act, View* pre_out,
            bool normed, const View* noise = nullptr, int noise_row0 = 0, const std::vector<WSeg>* wsegs = nullptr,
-           const View* bias_ovr = nullptr) {
+           const View* bias_ovr = nullptr, const PreUse* pre = nullptr) {
     REQUIRE(ins.size() == L.seg_p.size(), "fwd: input segment count mismatch for " + L.wname);
     REQUIRE(M % kTileM == 0, "fwd: rows must be a multiple of 16");
     REQUIRE(!wsegs || wsegs->size() == ins.size(), "fwd: one weight block per input segment");
@@ -649,6 +727,7 @@ struct Engine {
         REQUIRE(v.cols == L.seg_p[s] && v.m.n, "fwd: segment width / image mismatch for " + L.wname);
         xo += v.rows;
         if (xo < M) cuts.push_back(xo);
+        if (pre && (int)s == pre->a.seg) continue;  // computed in-tile
         rd.push_back(v.id);
         if (v.norm) rd.push_back(v.norm_id);
       }
@@ -657,6 +736,10 @@ struct Engine {
     std::sort(cuts.begin(), cuts.end());
     cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
     REQUIRE((int)ins.size() <= kMaxSeg, "fwd: too many operand segments");
+    if (pre) {
+      REQUIRE(cuts.size() == 2 && !noise, "fwd: a pre-GEMM consumer is one row piece");
+      rd.insert(rd.end(), pre->rd.begin(), pre->rd.end());
+    }
     const auto tq = choose_tn(M, L.out);
     const int tn = tq.first;
     const int tiles_n = cdiv(L.out, tn);
@@ -744,6 +827,10 @@ struct Engine {
         g.noise_sigma = cfg.target_policy_noise;
         g.noise_clip = cfg.noise_clip;
       }
+      if (pre) {
+        g.has_pre = 1;
+        g.prea = pre->a;
+      }
       op.wg_count = g.tiles_m * g.tiles_n;
       op.seq = tq.second;
       ops.push_back(op);
@@ -752,16 +839,10 @@ struct Engine {
     return out;
   }
 
-  struct DxTerm {
-    View dz;
-    const Layer* L;  // weights of a layer (T image) ...
-    int col0;
-    const View* wv = nullptr;  // ... or of a derived [out][in] matrix (T image) when L is null
-  };
 
   // dX[:, 0:ncols] = sum_t dZ_t W_t[:, col0_t : col0_t + ncols]  (* act'(saved))
   View dx(Prog& pg, const std::vector<DxTerm>& terms, int ncols, int M, int dact, const View* saved,
-          const View* into = nullptr, const View* nb_x = nullptr) {
+          const View* into = nullptr, const View* nb_x = nullptr, const PreUse* pre = nullptr) {
     Op op{};
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
@@ -788,7 +869,7 @@ struct Engine {
       b.r1 = roff + wout;
       g.B.seg[t] = b;
       roff += r16(wout);
-      rd.push_back(tm.dz.id);
+      if (!(pre && (int)t == pre->a.seg)) rd.push_back(tm.dz.id);  // (else computed in-tile)
       rd.push_back(tm.L ? tm.L->res : tm.wv->id);
     }
     g.A.nseg = g.B.nseg = (int)terms.size();
@@ -827,6 +908,11 @@ struct Engine {
       rd.push_back(saved->id);
     }
     wr.push_back(out.id);
+    if (pre) {
+      g.has_pre = 1;
+      g.prea = pre->a;
+      rd.insert(rd.end(), pre->rd.begin(), pre->rd.end());
+    }
     op.wg_count = g.tiles_m * g.tiles_n;
     pg.add(op, rd, wr);
     return out;
@@ -1183,10 +1269,17 @@ struct Engine {
     View ap0 = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_NONE, nullptr, true);
     View ap1 = fwd(pg, pi.layers[1], {{ap0}, {fzs, tzs}}, B2, ACT_RELU, nullptr, false);
     View ap2 = fwd(pg, pi.layers[2], {{ap1}}, B2, ACT_RELU, nullptr, false);
-    View actv = fwd(pg, pi.layers[3], {{ap2}}, B2, ACT_TANH, nullptr, false, &eps, B);
-    View a_pi = actv.sub(0, B), a_next = actv.sub(B, B);
+    // a' = clamp(pi(s', zs') + noise) only feeds the target branch's first layers, which
+    // recompute it in-tile (pre-GEMM): the actor output layer runs on the s rows alone
+    const bool prea = actor_pre();
+    View actv = prea ? fwd(pg, pi.layers[3], {{ap2.sub(0, B)}}, B, ACT_TANH, nullptr, false)
+                     : fwd(pg, pi.layers[3], {{ap2}}, B2, ACT_TANH, nullptr, false, &eps, B);
+    View a_pi = actv.sub(0, B), a_next = prea ? a_pi : actv.sub(B, B);  // (pre: layout only)
+    const View ap2n = ap2.sub(B, B);
+    const PreUse pn1 = prea ? pre_actor_fwd(pi.layers[3], ap2n, &eps, 1) : PreUse{};
+    const PreUse* pnext = prea ? &pn1 : nullptr;
     // ---- target: zsa' and target critics
-    View ta1 = fwd(pg, fet.layers[3], {{tzs}, {a_next}}, B, ACT_ELU, nullptr, false);
+    View ta1 = fwd(pg, fet.layers[3], {{tzs}, {a_next}}, B, ACT_ELU, nullptr, false, nullptr, 0, nullptr, nullptr, pnext);
     View ta2 = fwd(pg, fet.layers[4], {{ta1}}, B, ACT_ELU, nullptr, false);
     // zsa' = zsa3(ta2) only feeds the target critics' first hidden layer, a linear map:
     // with `fold`, tq.q1[:, zsa block] x fet.zsa3 is precomputed (add_target_fold) and the
@@ -1196,7 +1289,8 @@ struct Engine {
     if (!fold) tzsa = fwd(pg, fet.layers[5], {{ta2}}, B, ACT_NONE, nullptr, false);
     View th[2];
     for (int n = 0; n < 2; ++n) {
-      View t01 = fwd(pg, tq[n]->layers[0], {{s2}, {a_next}}, B, ACT_NONE, nullptr, true);
+      View t01 = fwd(pg, tq[n]->layers[0], {{s2}, {a_next}}, B, ACT_NONE, nullptr, true, nullptr, 0, nullptr, nullptr,
+                     pnext);
       View t1;
       if (fold) {  // fixed_encoder_target.zsa3 folded into the zsa block (tfold_w / tfold_b)
         const Layer& L1 = tq[n]->layers[1];
@@ -1314,14 +1408,14 @@ struct Engine {
       }
       View dpa1 = dx(pg, {{dpa2, &fe.layers[4], 0}}, H, B, ACT_ELU, &pa1z);
       // d action = sum of three paths, then tanh' (actor output)
-      View dl3 = dx(pg,
-                    {{dxp01[0], &q[0]->layers[0], Sp}, {dxp01[1], &q[1]->layers[0], Sp},
-                     {dpa1, &fe.layers[3], Hp}},
-                    A, B, ACT_TANH, &a_pi);
+      const std::vector<DxTerm> t3{
+          {dxp01[0], &q[0]->layers[0], Sp}, {dxp01[1], &q[1]->layers[0], Sp}, {dpa1, &fe.layers[3], Hp}};
+      View dl3 = dx(pg, t3, A, B, ACT_TANH, &a_pi);
+      const PreUse p3 = prea ? pre_actor_dx(t3, A, a_pi, 0) : PreUse{};  // dl2 recomputes dl3 in-tile
       // input-grads through a layer are emitted BEFORE its Adam update so the
       // scheduler orders them against the pre-update weights (as autograd does)
       View ap2s = ap2.sub(0, B), ap1s = ap1.sub(0, B);
-      View dl2 = dx(pg, {{dl3, &pi.layers[3], 0}}, H, B, ACT_RELU, &ap2s);
+      View dl2 = dx(pg, {{dl3, &pi.layers[3], 0}}, H, B, ACT_RELU, &ap2s, nullptr, nullptr, prea ? &p3 : nullptr);
       dw(pg, pi.layers[3], dl3, {ap2s}, B, CNT_ADAM_PI, cfg.policy_lr);
       View dl1 = dx(pg, {{dl2, &pi.layers[2], 0}}, H, B, ACT_RELU, &ap1s);
       dw(pg, pi.layers[2], dl2, {ap1s}, B, CNT_ADAM_PI, cfg.policy_lr);
@@ -1407,6 +1501,12 @@ struct Engine {
     const char* e = std::getenv("RLE_NO_FOLD");
     return algo == RLE_TD7 && H % 16 == 0 && !(e && e[0] == '1');
   }
+  // The actor's tanh output layer (N = act_dim <= 32) recomputed in-tile by the consumers on
+  // the critical path (PreArgs).  RLE_NO_PRE=1: separate ops (tests).
+  bool actor_pre() const {
+    const char* e = std::getenv("RLE_NO_PRE");
+    return A <= 32 && !(e && e[0] == '1');
+  }
   // AvgL1Norm backwards that feed only a weight-gradient GEMM are applied inside it
   // (EPI_NBDOT producer + kDwNb consumer: one level fewer).  RLE_NO_NBDEFER=1: separate
   // OP_NORMBWD (tests).
@@ -1484,8 +1584,9 @@ struct Engine {
   }
 
   // MLP critic stack forward: returns (h0, h1)
-  void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, View& h0, View& h1) {
-    h0 = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false);
+  void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, View& h0, View& h1,
+                      const PreUse* pre = nullptr) {
+    h0 = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pre);
     h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false);
   }
 
@@ -1504,8 +1605,13 @@ struct Engine {
     View h0 = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_RELU, nullptr, false);
     View h1 = fwd(pg, pi.layers[1], {{h0}}, B2, ACT_RELU, nullptr, false);
     View actv, raw, logpi;
+    // TD3: the target critics' first layer recomputes a' in-tile (pre-GEMM, as TD7)
+    const bool prea = !sac && actor_pre();
+    const View h1n = h1.sub(B, B);
+    const PreUse pn1 = prea ? pre_actor_fwd(pi.layers[2], h1n, &eps, 1) : PreUse{};
     if (!sac) {
-      actv = fwd(pg, pi.layers[2], {{h1}}, B2, ACT_TANH, nullptr, false, &eps, B);
+      actv = prea ? fwd(pg, pi.layers[2], {{h1.sub(0, B)}}, B, ACT_TANH, nullptr, false)
+                  : fwd(pg, pi.layers[2], {{h1}}, B2, ACT_TANH, nullptr, false, &eps, B);
     } else {
       raw = fwd(pg, pi.layers[2], {{h1}}, B2, ACT_NONE, nullptr, false);
       actv = buf(B2, A);
@@ -1528,10 +1634,10 @@ struct Engine {
       op.wg_count = cdiv(B2, kThreads);
       pg.add(op, {raw.id, eps.id, eps2.id}, {actv.id, logpi.id});
     }
-    View a_pi = actv.sub(0, B), a_next = actv.sub(B, B);
+    View a_pi = actv.sub(0, B), a_next = prea ? a_pi : actv.sub(B, B);  // (pre: layout only)
     // target critics + y
     View th0[2], th1[2];
-    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n]);
+    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n], prea ? &pn1 : nullptr);
     // online critics
     View c0[2], c1[2];
     for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c0[n], c1[n]);
@@ -1619,8 +1725,10 @@ struct Engine {
       View dzp0[2];
       for (int n = 0; n < 2; ++n) dzp0[n] = dx(pg, {{dzp1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &p0[n]);
       View dout;
+      PreUse pdout{};  // TD3: d1 recomputes dout in-tile
       if (!sac) {
         dout = dx(pg, {{dzp0[0], &q[0]->layers[0], Sp}, {dzp0[1], &q[1]->layers[0], Sp}}, A, B, ACT_TANH, &a_pi);
+        if (prea) pdout = pre_actor_dx({{dzp0[0], &q[0]->layers[0], Sp}, {dzp0[1], &q[1]->layers[0], Sp}}, A, a_pi, 0);
       } else {
         View da = dx(pg, {{dzp0[0], &q[0]->layers[0], Sp}, {dzp0[1], &q[1]->layers[0], Sp}}, A, B, ACT_NONE,
                      nullptr);
@@ -1665,7 +1773,7 @@ struct Engine {
       auto g1 = gsq_for(pi.layers[1], 2, 3);
       auto g2 = gsq_for(pi.layers[2], 4, 5);
       View h1s = h1.sub(0, B), h0s = h0.sub(0, B);
-      View d1 = dx(pg, {{dout, &pi.layers[2], 0}}, H, B, ACT_RELU, &h1s);
+      View d1 = dx(pg, {{dout, &pi.layers[2], 0}}, H, B, ACT_RELU, &h1s, nullptr, nullptr, prea ? &pdout : nullptr);
       dw(pg, pi.layers[2], dout, {h1s}, B, CNT_ADAM_PI, cfg.policy_lr, g2.first, g2.second);
       View d0 = dx(pg, {{d1, &pi.layers[1], 0}}, H, B, ACT_RELU, &h0s);
       dw(pg, pi.layers[1], d1, {h0s}, B, CNT_ADAM_PI, cfg.policy_lr, g1.first, g1.second);

@@ -408,7 +408,158 @@ __device__ __forceinline__ void build_nb_tab(const CAS GemmArgs& g, int n, float
   }
 }
 
-template <int MODE, int EPI, int ACT, bool NORM>
+// chunk_loop over one A stream and two B streams (two 16-column blocks sharing A).
+__device__ __forceinline__ void chunk_loop2(__amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rb, int vb0,
+                                            int vb1, int n, f32x4& acc0, f32x4& acc1) {
+  float4 a[kRing], b0[kRing], b1[kRing];
+#pragma unroll
+  for (int r = 0; r < kRing; ++r) {
+    a[r] = bload(ra, r < n ? va + r * 1024 : kOOB);
+    b0[r] = bload(rb, r < n ? vb0 + r * 1024 : kOOB);
+    b1[r] = bload(rb, r < n ? vb1 + r * 1024 : kOOB);
+  }
+#pragma unroll 1
+  for (int c = 0; c < n; c += kRing) {
+#pragma unroll
+    for (int r = 0; r < kRing; ++r) {
+      acc0 = mfma4(a[r], b0[r], acc0);
+      acc1 = mfma4(a[r], b1[r], acc1);
+      const int nx = c + r + kRing;
+      a[r] = bload(ra, nx < n ? va + nx * 1024 : kOOB);
+      b0[r] = bload(rb, nx < n ? vb0 + nx * 1024 : kOOB);
+      b1[r] = bload(rb, nx < n ? vb1 + nx * 1024 : kOOB);
+    }
+  }
+}
+
+// A chunks from an LDS fragment image (pre-GEMM output), B from memory.
+__device__ __forceinline__ f32x4 chunk_loop_lds(const float* la, __amdgpu_buffer_rsrc_t rb, int vb, int n, f32x4 acc) {
+  const int lane = threadIdx.x & 63;
+  for (int c = 0; c < n; ++c) acc = mfma4(*(const float4*)(la + c * 256 + lane * 4), bload(rb, vb + c * 1024), acc);
+  return acc;
+}
+
+// Pre-GEMM (PreArgs): the actor's tanh output layer for the 16 rows at i0 into pimg[2][256]
+// (N-image fragment blocks, columns >= N zero).  Each wave reduces a quarter of the chunks
+// for both column blocks; the quarters are summed in fixed wave order by wave 0, which
+// also runs the epilogue.  Two phases, so that one memory round trip serves both the
+// pre-GEMM and the consumer's own segments: pre_issue puts the wave's first kPreRing chunks
+// and the epilogue operands in flight; pre_finish (after the consumer's other segments)
+// reduces, applies the epilogue and publishes pimg.
+constexpr int kPreRing = 2;  // pre-GEMM chunks prefetched per wave (registers held across the
+                             // consumer's own segments: more would cost occupancy)
+struct PreRing {
+  float4 a[kPreRing], b0[kPreRing], b1[kPreRing];
+  float4 e[2];   // FWD: noise, DX: saved tanh output (4 rows, per column block)
+  float bj[2];   // FWD: bias per column block
+  int c0, c1, cp;
+};
+
+template <int MODE>
+__device__ __forceinline__ void pre_issue(const CAS PreArgs& p, int i0, PreRing& R) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nch = p.R >> 4, per = (nch + 3) >> 2;
+  R.c0 = wave * per;
+  R.c1 = min(nch, R.c0 + per);
+  R.cp = min(R.c1, R.c0 + kPreRing);
+  const bool wabs = MODE == GEMM_FWD && p.B.nseg == 1;
+  const int lb = lane * 16;
+#pragma unroll
+  for (int r = 0; r < kPreRing; ++r) {
+    const int k = R.c0 + r;
+    int q = 0;  // segment of chunk k (wave-uniform)
+#pragma unroll
+    for (int u = 1; u < kMaxSeg; ++u)
+      if (u < p.A.nseg && k >= (p.A.seg[u].r0 >> 4)) q = u;
+    const CAS Seg& sa = p.A.seg[q];
+    const CAS Seg& sb = p.B.seg[wabs ? 0 : q];
+    const int s0 = sa.r0 >> 4, kb = wabs ? k : k - s0;
+    const bool ok = k < R.cp;
+    R.a[r] = bload(rsrc(sa.p), ok ? ((i0 >> 4) * sa.xs + (k - s0)) * 1024 + lb : kOOB);
+    R.b0[r] = bload(rsrc(sb.p), ok ? kb * 1024 + lb : kOOB);
+    R.b1[r] = bload(rsrc(sb.p), ok && p.N > 16 ? (sb.xs + kb) * 1024 + lb : kOOB);
+  }
+  const int rb = (lane >> 4) << 2;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int j = cb * 16 + (lane & 15);
+    const bool jok = wave == 0 && j < p.N;
+    R.e[cb] = make_float4(0.f, 0.f, 0.f, 0.f);
+    R.bj[cb] = 0.f;
+    if constexpr (MODE == GEMM_FWD) {
+      if (jok && p.bias) R.bj[cb] = G(p.bias)[j];
+      if (jok && p.noise.t) R.e[cb] = mat_ld4(p.noise, i0 + rb, j);
+    } else {
+      if (jok) R.e[cb] = mat_ld4(p.dsrc, i0 + rb, j);
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void pre_finish(const CAS PreArgs& p, int i0, PreRing& R, float* part, float* part2,
+                                           float* pimg) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool two = p.N > 16, wabs = MODE == GEMM_FWD && p.B.nseg == 1;
+  const int lb = lane * 16;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+  for (int r = 0; r < kPreRing; ++r) {  // (chunks past cp loaded as zeros)
+    acc0 = mfma4(R.a[r], R.b0[r], acc0);
+    if (two) acc1 = mfma4(R.a[r], R.b1[r], acc1);
+  }
+  for (int q = 0; q < p.A.nseg; ++q) {  // the rest of the wave's chunks
+    const CAS Seg& sa = p.A.seg[q];
+    const CAS Seg& sb = p.B.seg[wabs ? 0 : q];
+    const int s0 = sa.r0 >> 4;
+    const int k0 = max(R.cp, s0), k1 = min(R.c1, (sa.r1 + 15) >> 4);
+    if (k0 >= k1) continue;
+    const int va = ((i0 >> 4) * sa.xs + (k0 - s0)) * 1024 + lb;
+    const int kb = wabs ? k0 : k0 - s0;
+    if (two) chunk_loop2(rsrc(sa.p), va, rsrc(sb.p), kb * 1024 + lb, (sb.xs + kb) * 1024 + lb, k1 - k0, acc0, acc1);
+    else acc0 = chunk_loop<0, 0>(rsrc(sa.p), va, rsrc(sb.p), kb * 1024 + lb, k1 - k0, acc0, 1.f, nullptr, nullptr, false);
+  }
+  if (wave) {
+    *(f32x4*)(part + (wave * 64 + lane) * 4) = acc0;
+    *(f32x4*)(part2 + (wave * 64 + lane) * 4) = acc1;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    for (int w = 1; w < 4; ++w) {
+      acc0 += *(const f32x4*)(part + (w * 64 + lane) * 4);
+      acc1 += *(const f32x4*)(part2 + (w * 64 + lane) * 4);
+    }
+    const int rb = (lane >> 4) << 2;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const f32x4 acc = cb ? acc1 : acc0;
+      const int j = cb * 16 + (lane & 15);
+      const bool jok = j < p.N;
+      const float ev[4] = {R.e[cb].x, R.e[cb].y, R.e[cb].z, R.e[cb].w};
+      float y[4];
+      if constexpr (MODE == GEMM_FWD) {  // tanh (+ target smoothing), as the EPI_STORE tanh path
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] = act_f<ACT_TANH>(acc[q] + R.bj[cb]);
+        if (p.noise.t) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float nz = fminf(fmaxf(ev[q] * p.noise_sigma, -p.noise_clip), p.noise_clip);
+            y[q] = fminf(fmaxf(y[q] + nz, -1.f), 1.f);
+          }
+        }
+      } else {  // grad wrt the tanh input: * (1 - a^2)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] = acc[q] * act_b<ACT_TANH>(ev[q]);
+      }
+      float* dst = pimg + cb * 256 + ((lane & 15) >> 2) * 64 + rb * 4 + (lane & 3);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[q * 4] = jok ? y[q] : 0.f;
+    }
+  }
+  __syncthreads();
+}
+
+template <int MODE, int EPI, int ACT, bool NORM, bool PRE = false>
 __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -508,12 +659,33 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       }
       return inva;
     };
-    seg(a0p, a0xs, a0r0, a0r1, b0p, b0xs, inv_of(0));
-    for (int q = 1; q < nseg_a; ++q) {
-      const CAS Seg& sa = g.A.seg[q];
-      // FWD: one W segment over the whole reduction; DX: W segment q pairs with A segment q
-      const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
-      seg(sa.p, sa.xs, sa.r0, sa.r1, wabs ? b0p : sb.p, wabs ? b0xs : sb.xs, inv_of(q));
+    if constexpr (PRE) {  // segment g.prea.seg comes from the pre-GEMM in LDS
+      float* pimg = smem + 64 + 2048;
+      PreRing pr;
+      pre_issue<MODE>(g.prea, i0, pr);
+      const int pseg = g.prea.seg;
+      for (int q = 0; q < nseg_a; ++q) {
+        if (q == pseg) continue;
+        const CAS Seg& sa = g.A.seg[q];
+        const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
+        seg(sa.p, sa.xs, sa.r0, sa.r1, sb.p, sb.xs, inv_of(q));
+      }
+      pre_finish<MODE>(g.prea, i0, pr, part, smem + 64 + 1024, pimg);
+      const CAS Seg& sa = g.A.seg[pseg];
+      const CAS Seg& sb = g.B.seg[wabs ? 0 : pseg];
+      const int s0 = sa.r0 >> 4;
+      const int k0 = max(c0, s0), k1 = min(c1, (sa.r1 + 15) >> 4);
+      if (active && k0 < k1)
+        acc = chunk_loop_lds(pimg + (k0 - s0) * 256, rsrc(sb.p), ((j0 >> 4) * sb.xs + (wabs ? k0 : k0 - s0)) * 1024 + lb,
+                             k1 - k0, acc);
+    } else {
+      seg(a0p, a0xs, a0r0, a0r1, b0p, b0xs, inv_of(0));
+      for (int q = 1; q < nseg_a; ++q) {
+        const CAS Seg& sa = g.A.seg[q];
+        // FWD: one W segment over the whole reduction; DX: W segment q pairs with A segment q
+        const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
+        seg(sa.p, sa.xs, sa.r0, sa.r1, wabs ? b0p : sb.p, wabs ? b0xs : sb.xs, inv_of(q));
+      }
     }
   } else {
     // DW: A = dZ (T image, x = output row), B = X (T image, x = output column; the
@@ -700,6 +872,11 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     asm volatile("; gemm variant " #mode #epi #act #norm ::); \
     gemm_v<mode, epi, act, norm>(g, t, smem, tr);        \
     break;
+#define RLE_VP(mode, epi, act, norm)                                  \
+  case gemm_vid(mode, epi, act, norm, 1):                            \
+    asm volatile("; gemm variant pre " #mode #epi #act #norm ::);    \
+    gemm_v<mode, epi, act, norm, true>(g, t, smem, tr);              \
+    break;
   switch (vid) {
     RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, false)
     RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, true)
@@ -720,9 +897,14 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_V(GEMM_DW, EPI_ADAM, ACT_NONE, false)
     RLE_V(GEMM_DW, EPI_ADAM, ACT_NONE, true)
     RLE_V(GEMM_DW, EPI_ADAM, kDwNb, false)
+    RLE_VP(GEMM_FWD, EPI_STORE, ACT_NONE, false)
+    RLE_VP(GEMM_FWD, EPI_STORE, ACT_RELU, false)
+    RLE_VP(GEMM_FWD, EPI_STORE, ACT_ELU, true)
+    RLE_VP(GEMM_DX, EPI_STORE, ACT_RELU, false)
     default: break;
   }
 #undef RLE_V
+#undef RLE_VP
 }
 
 // ---------------------------------------------------------------- AvgL1Norm backward
@@ -1490,7 +1672,7 @@ __global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
     e = in ? x : e;
     k = in ? q : k;
   }
-  const int kind = (e >> 16) & 0xff, vid = e >> 24;
+  const int kind = (e >> 16) & 0xf, vid = e >> 20;
   const CAS Op* ops = (const CAS Op*)la.ops;
   const CAS Op& op = ops[k];
   const int t = wg - (int)(e & 0xffffu);
@@ -1615,7 +1797,7 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
       if (q < n) {
         const Op& o = h_ops[q0 + q];
         const unsigned vid = o.kind == OP_GEMM ? (unsigned)o.gemm.vid : 0u;
-        la.entry[q] = (unsigned)(o.wg_begin - w0) | ((unsigned)o.kind << 16) | (vid << 24);
+        la.entry[q] = (unsigned)(o.wg_begin - w0) | ((unsigned)o.kind << 16) | (vid << 20);
       } else {
         la.entry[q] = 0xffffu;
       }

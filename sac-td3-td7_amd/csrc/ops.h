@@ -106,10 +106,13 @@ struct AdamArgs {
   float* gsq_b;          // optional: per-tile sum of squared grads (bias), [tiles_m]
 };
 
-// Variant id of a GEMM op = mode * 64 + epi * 8 + act * 2 + norm (act: the forward
+// Variant id of a GEMM op = pre * 256 + mode * 64 + epi * 8 + act * 2 + norm (pre: one A
+// segment is the actor's tanh output layer recomputed in the workgroup, PreArgs; act: the forward
 // activation for GEMM_FWD, the derivative mask for GEMM_DX, kDwNb or 0 for GEMM_DW; norm: some operand
 // segment carries a deferred AvgL1Norm).
-constexpr int gemm_vid(int mode, int epi, int act, int norm) { return mode * 64 + epi * 8 + act * 2 + norm; }
+constexpr int gemm_vid(int mode, int epi, int act, int norm, int pre = 0) {
+  return pre * 256 + mode * 64 + epi * 8 + act * 2 + norm;
+}
 
 enum GemmMode : int {
   GEMM_FWD = 0,   // A contiguous (activations), B contiguous (W rows):  Y = X W^T
@@ -130,6 +133,23 @@ struct GemmHot {
   const float* bias;
 };
 static_assert(sizeof(GemmHot) == 80, "GemmHot is loaded as 16 + 4 dwords");
+
+// The actor's output layer (rl/nn/sale.py:77-83 / mlp.py:55-68, N = act_dim <= 32) recomputed
+// by a consuming GEMM for its own 16 rows into an LDS fragment block, so the consumer does not
+// wait a level for it ("pre-GEMM"):
+//   FWD: a = clamp(tanh(X W^T + b) + clamp(sigma * eps, +-c), +-1)   (target policy smoothing)
+//   DX:  a = (sum_t dZ_t W_t) * (1 - act^2)                           (grad wrt the tanh input)
+// The result replaces the consumer's A segment `seg` (reduction width <= 32).
+struct PreArgs {
+  Operand A, B;        // operands in the conventions of GemmArgs A / B for `mode`
+  int mode;            // GEMM_FWD or GEMM_DX
+  int N, R;            // output columns (<= 32), reduction length
+  int seg;             // consumer A segment produced
+  int pad_;
+  const float* bias;   // FWD
+  Mat noise; float noise_sigma, noise_clip;  // FWD: smoothing noise (T image, consumer rows)
+  Mat dsrc;            // DX: saved tanh output (T image, consumer rows)
+};
 
 struct GemmArgs {
   GemmHot hot;           // (first: one s_load_dwordx16 + one s_load_dwordx4)
@@ -159,6 +179,8 @@ struct GemmArgs {
   Mat nbx; int nbx_xs;             // EPI_NBDOT / kDwNb: x of the AvgL1Norm (T image; DW: its x-block step)
   NormRef nbm;                     // kDwNb: m of x's rows (producer |x| partials)
   const float* nbdot; int nbdot_ld, nbdot_n;  // kDwNb: the EPI_NBDOT producer's row partials of sum g x
+  int has_pre;                     // pre-GEMM (PreArgs) in use
+  PreArgs prea;
   int pad_;
   AdamArgs adam;
 };
@@ -334,8 +356,8 @@ constexpr int kLevelOps = 16;
 struct LevelArgs {
   const Op* ops;
   unsigned long long* trace;  // optional phase timestamps [wg][4] (s_memrealtime, 100 MHz)
-  // op q: first workgroup (bits 0-15; 0xffff past the last op) | kind << 16 | GEMM variant
-  // id << 24 (GemmArgs::vid: the variant is chosen before any descriptor load)
+  // op q: first workgroup (bits 0-15; 0xffff past the last op) | kind << 16 (4 bits) | GEMM
+  // variant id << 20 (GemmArgs::vid: the variant is chosen before any descriptor load)
   unsigned entry[kLevelOps];
 };
 constexpr int kMaxLevelWG = 0xfffe;  // workgroups per launch (16-bit entry field)
