@@ -160,6 +160,21 @@ __device__ __attribute__((noinline)) float norm_mean(const float* part, int ld, 
   }
   return s / (float)width;
 }
+// Inline copy for operand scaling that must overlap loads already in flight (a call would
+// make the caller wait for them).
+__device__ __forceinline__ float norm_mean_i(const float* part, int ld, int row, int nparts, int width) {
+  const GAS float* p = G(part) + row;
+  float s = 0.f;
+  for (int q0 = 0; q0 < nparts; q0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = p[(size_t)min(q0 + q, nparts - 1) * ld];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (q0 + q < nparts) s += v[q];
+  }
+  return s / (float)width;
+}
 // Denominator m = clamp(mean, min=1e-8) (rl/nn/sale.py:11-13).
 __device__ __forceinline__ float norm_m(const float* part, int ld, int row, int nparts, int width) {
   const float m = norm_mean(part, ld, row, nparts, width);
@@ -189,11 +204,15 @@ __device__ __forceinline__ float act_bwd(int act, float saved) {
 __device__ __forceinline__ float norm_inv(const CAS NormRef& nr, int row) {
   return 1.f / norm_m(nr.part, nr.ld, row + nr.row0, nr.nparts, nr.width);
 }
+__device__ __forceinline__ float norm_inv_i(const CAS NormRef& nr, int row) {
+  const float m = norm_mean_i(nr.part, nr.ld, row + nr.row0, nr.nparts, nr.width);
+  return 1.f / (m < 1e-8f ? 1e-8f : m);
+}
 
 // LDS table of 1/m for n consecutive rows of a normed tensor (16-padded with 0).
 __device__ __forceinline__ void build_norm_tab(const CAS NormRef& nr, int n, float* dst) {
 #pragma unroll 1
-  for (int i = threadIdx.x; i < n; i += kThreads) dst[i] = norm_inv(nr, i);
+  for (int i = threadIdx.x; i < n; i += kThreads) dst[i] = norm_inv_i(nr, i);
 #pragma unroll 1
   for (int i = n + threadIdx.x; i < ((n + 15) & ~15); i += kThreads) dst[i] = 0.f;
 }
@@ -323,20 +342,21 @@ __device__ __forceinline__ float act_b(float saved) {  // see act_bwd
 #endif
 constexpr int kRing = RLE_RING;  // chunks in flight per wave
 
-template <int SA, int SB>
-__device__ __forceinline__ f32x4 chunk_loop(__amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rb, int vb,
-                                            int n, f32x4 acc, float inva, const float* taba, const float* tabb,
-                                            bool bias_ones) {
-#ifdef RLE_EXP_NOLOOP  // timing experiment only: no main-loop loads / MFMAs
-  n = 0;
-#endif
-  const int rl = ((threadIdx.x & 63) >> 4) << 2;
-  float4 a[kRing], b[kRing];
+// The ring in two halves, so that work with its own memory round trip (AvgL1Norm scalars
+// and tables) can run between issuing the first kRing chunks and consuming them.
+__device__ __forceinline__ void ring_issue(float4 (&a)[kRing], float4 (&b)[kRing], __amdgpu_buffer_rsrc_t ra, int va,
+                                           __amdgpu_buffer_rsrc_t rb, int vb, int n, bool bias_ones) {
 #pragma unroll
   for (int r = 0; r < kRing; ++r) {
     a[r] = bload(ra, r < n ? va + r * 1024 : kOOB);
     b[r] = bias_ones ? make_float4(1.f, 1.f, 1.f, 1.f) : bload(rb, r < n ? vb + r * 1024 : kOOB);
   }
+}
+template <int SA, int SB>
+__device__ __forceinline__ f32x4 ring_run(float4 (&a)[kRing], float4 (&b)[kRing], __amdgpu_buffer_rsrc_t ra, int va,
+                                          __amdgpu_buffer_rsrc_t rb, int vb, int n, f32x4 acc, float inva,
+                                          const float* taba, const float* tabb, bool bias_ones) {
+  const int rl = ((threadIdx.x & 63) >> 4) << 2;
   f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int c = 0; c < n; c += kRing) {
@@ -356,6 +376,17 @@ __device__ __forceinline__ f32x4 chunk_loop(__amdgpu_buffer_rsrc_t ra, int va, _
   }
   return acc + acc1;
 }
+template <int SA, int SB>
+__device__ __forceinline__ f32x4 chunk_loop(__amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rb, int vb,
+                                            int n, f32x4 acc, float inva, const float* taba, const float* tabb,
+                                            bool bias_ones) {
+#ifdef RLE_EXP_NOLOOP  // timing experiment only: no main-loop loads / MFMAs
+  n = 0;
+#endif
+  float4 a[kRing], b[kRing];
+  ring_issue(a, b, ra, va, rb, vb, n, bias_ones);
+  return ring_run<SA, SB>(a, b, ra, va, rb, vb, n, acc, inva, taba, tabb, bias_ones);
+}
 
 __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
 
@@ -363,17 +394,12 @@ __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f
 // (kDwNb, sale.py:11-13): a = g * inv[r] + sign(x) * gm[r] for the chunk's rows r, with
 // x read from (rx, vx) in the same T-image layout as g and inv / gm from LDS tables
 // (ti / tg: float offset of chunk k0's first row).  Same ring as chunk_loop.
-__device__ __forceinline__ f32x4 chunk_loop_nb(__amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rx, int vx,
-                                               __amdgpu_buffer_rsrc_t rb, int vb, int n, f32x4 acc, const float* ti,
-                                               const float* tg, bool bias_ones) {
+// (x ring issued by the caller together with ring_issue for a / b, ahead of the tables)
+__device__ __forceinline__ f32x4 ring_run_nb(float4 (&a)[kRing], float4 (&x)[kRing], float4 (&b)[kRing],
+                                             __amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rx, int vx,
+                                             __amdgpu_buffer_rsrc_t rb, int vb, int n, f32x4 acc, const float* ti,
+                                             const float* tg, bool bias_ones) {
   const int rl = ((threadIdx.x & 63) >> 4) << 2;
-  float4 a[kRing], x[kRing], b[kRing];
-#pragma unroll
-  for (int r = 0; r < kRing; ++r) {
-    a[r] = bload(ra, r < n ? va + r * 1024 : kOOB);
-    x[r] = bload(rx, r < n ? vx + r * 1024 : kOOB);
-    b[r] = bias_ones ? make_float4(1.f, 1.f, 1.f, 1.f) : bload(rb, r < n ? vb + r * 1024 : kOOB);
-  }
   f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int c = 0; c < n; c += kRing) {
@@ -399,10 +425,10 @@ __device__ __forceinline__ f32x4 chunk_loop_nb(__amdgpu_buffer_rsrc_t ra, int va
 __device__ __forceinline__ void build_nb_tab(const CAS GemmArgs& g, int n, float* ti, float* tg) {
 #pragma unroll 1
   for (int i = threadIdx.x; i < n; i += kThreads) {
-    const float mean = norm_mean(g.nbm.part, g.nbm.ld, i + g.nbm.row0, g.nbm.nparts, g.nbm.width);
+    const float mean = norm_mean_i(g.nbm.part, g.nbm.ld, i + g.nbm.row0, g.nbm.nparts, g.nbm.width);
+    const float dot = norm_mean_i(g.nbdot, g.nbdot_ld, i, g.nbdot_n, 1);
     const bool clamped = mean < 1e-8f;
     const float inv = 1.f / (clamped ? 1e-8f : mean);
-    const float dot = norm_mean(g.nbdot, g.nbdot_ld, i, g.nbdot_n, 1);
     ti[i] = inv;
     tg[i] = clamped ? 0.f : (-dot * inv * inv) / (float)g.nbm.width;
   }
@@ -644,20 +670,24 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     // DX, or FWD with one W segment per A segment (folded weight blocks): each W
     // segment starts at its own reduction offset (relative chunk index)
     const bool wabs = MODE == GEMM_FWD && nseg_b == 1;
-    auto seg = [&](const float* sap, int sxs, int sr0, int sr1, const float* sbp, int bxs, float inva) {
+    auto inv_of = [&](int q) {
+      float inva = 1.f;
+      if constexpr (NORM) {
+        if (g.A.seg[q].norm.part) inva = norm_inv_i(g.A.seg[q].norm, i0 + (lane & 15));
+      }
+      return inva;
+    };
+    // (the segment's deferred-AvgL1Norm scale is fetched while its first chunks are in flight)
+    auto seg = [&](const float* sap, int sxs, int sr0, int sr1, const float* sbp, int bxs, int q) {
       const int s0 = sr0 >> 4;
       const int k0 = max(c0, s0), k1 = min(c1, (sr1 + 15) >> 4);
       if (!active || k0 >= k1) return;
       const int va = ((i0 >> 4) * sxs + (k0 - s0)) * 1024 + lb;
       const int vb = ((j0 >> 4) * bxs + (wabs ? k0 : k0 - s0)) * 1024 + lb;
-      acc = chunk_loop<NORM ? 1 : 0, 0>(rsrc(sap), va, rsrc(sbp), vb, k1 - k0, acc, inva, nullptr, nullptr, false);
-    };
-    auto inv_of = [&](int q) {
-      float inva = 1.f;
-      if constexpr (NORM) {
-        if (g.A.seg[q].norm.part) inva = norm_inv(g.A.seg[q].norm, i0 + (lane & 15));
-      }
-      return inva;
+      float4 ra[kRing], rb[kRing];
+      ring_issue(ra, rb, rsrc(sap), va, rsrc(sbp), vb, k1 - k0, false);
+      const float inva = inv_of(q);
+      acc = ring_run<NORM ? 1 : 0, 0>(ra, rb, rsrc(sap), va, rsrc(sbp), vb, k1 - k0, acc, inva, nullptr, nullptr, false);
     };
     if constexpr (PRE) {  // segment g.prea.seg comes from the pre-GEMM in LDS
       float* pimg = smem + 64 + 2048;
@@ -668,7 +698,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         if (q == pseg) continue;
         const CAS Seg& sa = g.A.seg[q];
         const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
-        seg(sa.p, sa.xs, sa.r0, sa.r1, sb.p, sb.xs, inv_of(q));
+        seg(sa.p, sa.xs, sa.r0, sa.r1, sb.p, sb.xs, q);
       }
       pre_finish<MODE>(g.prea, i0, pr, part, smem + 64 + 1024, pimg);
       const CAS Seg& sa = g.A.seg[pseg];
@@ -679,12 +709,12 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         acc = chunk_loop_lds(pimg + (k0 - s0) * 256, rsrc(sb.p), ((j0 >> 4) * sb.xs + (wabs ? k0 : k0 - s0)) * 1024 + lb,
                              k1 - k0, acc);
     } else {
-      seg(a0p, a0xs, a0r0, a0r1, b0p, b0xs, inv_of(0));
+      seg(a0p, a0xs, a0r0, a0r1, b0p, b0xs, 0);
       for (int q = 1; q < nseg_a; ++q) {
         const CAS Seg& sa = g.A.seg[q];
         // FWD: one W segment over the whole reduction; DX: W segment q pairs with A segment q
         const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
-        seg(sa.p, sa.xs, sa.r0, sa.r1, wabs ? b0p : sb.p, wabs ? b0xs : sb.xs, inv_of(q));
+        seg(sa.p, sa.xs, sa.r0, sa.r1, wabs ? b0p : sb.p, wabs ? b0xs : sb.xs, q);
       }
     }
   } else {
@@ -695,6 +725,18 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     for (int q = 1; q < kMaxSeg; ++q)
       if (q < nseg_b && j0 >= g.B.seg[q].x0) qb = q;
     const CAS Seg& sb = g.B.seg[qb];
+    // first chunks in flight before the AvgL1Norm tables are built (their loads overlap)
+    const bool run = active && c0 < c1;
+    const int va = ((i0 >> 4) * a0xs + c0) * 1024 + lb;
+    const int vb = (((j0 - sb.x0) >> 4) * sb.xs + c0) * 1024 + lb;
+    const int vx = ACT == kDwNb ? ((i0 >> 4) * g.nbx_xs + c0) * 1024 + lb : 0;
+    const int nrun = run ? c1 - c0 : 0;
+    float4 ra[kRing], rb[kRing], rx[kRing];
+    ring_issue(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, bias_tile);
+    if constexpr (ACT == kDwNb) {
+#pragma unroll
+      for (int r = 0; r < kRing; ++r) rx[r] = bload(rsrc(g.nbx.t), r < nrun ? vx + r * 1024 : kOOB);
+    }
     const float* tb = nullptr;
     if constexpr (NORM) {
       // 1/m of every reduction row of every normed B segment, segment by segment
@@ -715,17 +757,14 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       build_nb_tab(g, gR, tabs, tabs + tgo);
       __syncthreads();
     }
-    if (active && c0 < c1) {
-      const int va = ((i0 >> 4) * a0xs + c0) * 1024 + lb;
-      const int vb = (((j0 - sb.x0) >> 4) * sb.xs + c0) * 1024 + lb;
+    if (run) {
       if constexpr (ACT == kDwNb) {
-        const int vx = ((i0 >> 4) * g.nbx_xs + c0) * 1024 + lb;
-        acc = chunk_loop_nb(rsrc(a0p), va, rsrc(g.nbx.t), vx, rsrc(sb.p), vb, c1 - c0, acc, tabs + c0 * 16,
-                            tabs + tgo + c0 * 16, bias_tile);
+        acc = ring_run_nb(ra, rx, rb, rsrc(a0p), va, rsrc(g.nbx.t), vx, rsrc(sb.p), vb, nrun, acc, tabs + c0 * 16,
+                          tabs + tgo + c0 * 16, bias_tile);
       } else if (NORM && tb && !bias_tile)  // the bias column's B is ones: never scaled
-        acc = chunk_loop<0, 2>(rsrc(a0p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, tb, bias_tile);
+        acc = ring_run<0, 2>(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, acc, 1.f, nullptr, tb, bias_tile);
       else
-        acc = chunk_loop<0, 0>(rsrc(a0p), va, rsrc(sb.p), vb, c1 - c0, acc, 1.f, nullptr, nullptr, bias_tile);
+        acc = ring_run<0, 0>(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, acc, 1.f, nullptr, nullptr, bias_tile);
     }
   }
   trace_mark(tr, 2);
@@ -1656,7 +1695,7 @@ __device__ __forceinline__ void op_foldbias(const CAS FoldBiasArgs& f) {
 // TRACE: compiled with the phase stamps (RLE_TRACE=1 runs); the production instance has
 // none, so nothing but the op table is read before the op body starts.
 template <bool TRACE>
-__global__ __launch_bounds__(kThreads) void rle_level(const LevelArgs la) {
+__global__ __launch_bounds__(kThreads, 4) void rle_level(const LevelArgs la) {
   __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
   // op of this workgroup from the kernel-argument table: straight-line selects over
   // SGPRs, so all kernel-argument loads go out in one batch (one round trip) and no
