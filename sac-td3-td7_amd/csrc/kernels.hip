@@ -1695,7 +1695,10 @@ __device__ __forceinline__ void op_foldbias(const CAS FoldBiasArgs& f) {
 // TRACE: compiled with the phase stamps (RLE_TRACE=1 runs); the production instance has
 // none, so nothing but the op table is read before the op body starts.
 template <bool TRACE>
-__global__ __launch_bounds__(kThreads, 4) void rle_level(const LevelArgs la) {
+#ifndef RLE_WAVES
+#define RLE_WAVES 4  // waves per SIMD the register allocation must allow (4 workgroups per CU)
+#endif
+__global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(const LevelArgs la) {
   __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
   // op of this workgroup from the kernel-argument table: straight-line selects over
   // SGPRs, so all kernel-argument loads go out in one batch (one round trip) and no
