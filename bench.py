@@ -213,6 +213,69 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
     }
 
 
+def multi_seed(args, K, world, rank, local, dist, algo_id, lap, chunk=25):
+    """K independent seeds per GPU: K engines, each with its own replay,
+    weights, Philox stream and HIP stream, stepped round-robin in chunks without host syncs.
+    value = steps of all seeds on all ranks / max-rank wall time."""
+    import torch
+
+    from rl import _engine as E
+    from rl.nn.layout import init_agent
+
+    s_dim, a_dim, _ = TASKS[args.env]
+    engs = []
+    for k in range(K):
+        seed = 111 * (rank * K + k + 1)
+        eng = E.Engine(E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=seed, device=local))
+        for net, params in init_agent(args.algo, s_dim, a_dim, H, 123 + rank * K + k).items():
+            for name, v in params.items():
+                eng.set_param(net, name, v)
+        rep = E.Replay(N_REPLAY, s_dim, a_dim, lap, device=local)
+        rep.fill_random(N_REPLAY, seed=rank * K + k)
+        eng.bind(rep)
+        engs.append((eng, rep))
+
+    def run(n):
+        done = 0
+        while done < n:
+            c = min(chunk, n - done)
+            for eng, _ in engs:
+                eng.step_async(c)
+            done += c
+        for eng, _ in engs:
+            eng.synchronize()
+
+    run(args.warmup)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(local)
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize(local)
+    wall = max_over_ranks([time.perf_counter() - t0], dist)[0]
+    if rank == 0:
+        gflop, mb = (SURVEY_MACS_PER_SAMPLE * 2.0 * B / 1e9, None) if (args.algo, args.env, args.batch) == (
+            "td7", "Humanoid-v4", B) else WORK[(args.algo, args.env, args.batch)]
+        value = world * K * args.steps / wall
+        out = {
+            "metric": f"gradient-steps/sec, {K} independent seeds per GPU, {args.algo.upper()} {args.env} "
+                      f"batch={args.batch} (secondary: SURVEY §8(f) rank 4)",
+            "value": round(value, 2), "unit": "gradient-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"{K} x {args.algo.upper()} {args.env} gradient step per GPU",
+                       "seeds_per_gpu": K, "batch": args.batch, "replay": N_REPLAY, "lap": lap,
+                       "parallelism": f"replicas x{world * K} ({K} seeds per GPU, one HIP stream each)"},
+            "roofline": {"bound": "mfma", "achieved": round(gflop * 1e9 * value / world / 1e12, 3),
+                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(gflop * 1e9 * value / world / 1e12 / PEAK_FP32_TFLOPS, 5),
+                         "traffic": None, "note": "device aggregate over the K seeds (wall clock)"},
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,6 +286,8 @@ def main():
     ap.add_argument("--algo", choices=("td7", "td3", "sac"), default="td7")
     ap.add_argument("--env", choices=tuple(TASKS), default="Humanoid-v4")
     ap.add_argument("--batch", type=int, default=B)
+    ap.add_argument("--seeds-per-gpu", type=int, default=1,
+                    help="independent seeds (engines, one stream each) sharing each GPU (SURVEY §8(f) rank 4)")
     args = ap.parse_args()
     if (args.algo, args.env, args.batch) not in WORK:
         ap.error(f"no SURVEY §8(d) work figures for {args.algo} {args.env} B={args.batch}")
@@ -244,6 +309,9 @@ def main():
     # --- engine: one independent seed per GPU (seed 111, 222, ... as scripts/td7_exp.sh)
     s_dim, a_dim, _ = TASKS[args.env]
     algo_id = {"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[args.algo]
+    K = max(1, args.seeds_per_gpu)
+    if K > 1:
+        return multi_seed(args, K, world, rank, local, dist, algo_id, lap)
     cfg = E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=111 * (rank + 1), device=local)
     eng = E.Engine(cfg)
     for net, params in init_agent(args.algo, s_dim, a_dim, H, 123 + rank).items():

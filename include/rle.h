@@ -111,6 +111,11 @@ int rle_step(rle_engine* e, int n_steps, float* info_out);
 /* Benchmark form of rle_step: n_steps without info readback, bracketed by HIP events recorded
  * on the engine's own stream; *gpu_ms = elapsed event time.  Syncs once at the end. */
 int rle_step_timed(rle_engine* e, int n_steps, float* gpu_ms);
+/* Enqueue n_steps as rle_step does, without any host sync or info readback (the device info
+ * ring keeps the last rows); rle_synchronize waits.  Lets one host thread drive several
+ * independent seeds (engines, each on its own stream) on one GPU concurrently -- SURVEY
+ * §8(f) rank 4, beyond the reference's one agent per process (scripts/td7_exp.sh:1-4). */
+int rle_step_async(rle_engine* e, int n_steps);
 /* Parity / explicit-batch mode: replace draws of the next n_steps with tapes; each tape
  * is optional and a NULL one keeps its Philox stream.  u [n][B] (torch.rand in sample),
  * eps [n][B][A] (randn_like target noise, or SAC next-state rsample noise), eps_pi [n][B][A]

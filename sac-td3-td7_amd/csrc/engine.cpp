@@ -2052,7 +2052,7 @@ struct Engine {
   Op* ctrl_op = nullptr;
 
   // ---------------------------------------------------------------- run
-  void step(int n, float* info_out, float* gpu_ms = nullptr) {
+  void step(int n, float* info_out, float* gpu_ms = nullptr, bool async = false) {
     REQUIRE(replay, "no replay bound");
     REQUIRE(replay->size > 0, "replay is empty");
     if (!built) build();
@@ -2103,7 +2103,7 @@ struct Engine {
         HIPCHK(hipMemcpyAsync(info_out + (size_t)done * kInfoMax, info, (size_t)chunk * kInfoMax * sizeof(float),
                               hipMemcpyDeviceToHost, stream));
       }
-      if (!gpu_ms) HIPCHK(hipStreamSynchronize(stream));
+      if (!gpu_ms && !async) HIPCHK(hipStreamSynchronize(stream));
       done += chunk;
     }
     if (gpu_ms) {
@@ -2627,6 +2627,16 @@ int rle_step_timed(rle_engine* h, int n_steps, float* gpu_ms) {
     HIPCHK(hipSetDevice(e.cfg.device));
     if (e.replay) HIPCHK(hipStreamSynchronize(e.replay->stream));
     e.step(n_steps, nullptr, gpu_ms);
+  });
+}
+
+int rle_step_async(rle_engine* h, int n_steps) {
+  return guard([&] {
+    REQUIRE(n_steps >= 0, "step_async: n < 0");
+    Engine& e = *h->e;
+    HIPCHK(hipSetDevice(e.cfg.device));
+    if (e.replay) HIPCHK(hipStreamSynchronize(e.replay->stream));
+    e.step(n_steps, nullptr, nullptr, true);
   });
 }
 

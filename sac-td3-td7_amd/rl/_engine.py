@@ -70,6 +70,7 @@ SIGNATURES = {
     "rle_set_value_bounds": (_int, [_vp, _f32p]),
     "rle_step": (_int, [_vp, _int, _f32p]),
     "rle_step_timed": (_int, [_vp, _int, _f32p]),
+    "rle_step_async": (_int, [_vp, _int]),
     "rle_set_tapes": (_int, [_vp, _int, _f32p, _f32p, _f32p, _i64p]),
     "rle_last_indices": (_int, [_vp, _i64p]),
     "rle_act": (_int, [_vp, _f32p, _int, _f32p]),
@@ -265,6 +266,10 @@ class Engine:
         ms = ctypes.c_float()
         _check(lib().rle_step_timed(self.h, n, ctypes.byref(ms)))
         return ms.value
+
+    def step_async(self, n):
+        """Enqueue n steps on the engine's stream; no host sync, no info readback."""
+        _check(lib().rle_step_async(self.h, n))
 
     def set_tapes(self, u=None, eps=None, eps_pi=None, ind=None):
         if u is None and ind is None:

@@ -204,3 +204,31 @@ def test_prefetched_batches_equal_fresh_draws(name):
     for net, params in spec.agent_params(alg, *spec.TASKS[parse(g)[1]][:2], parse(g)[2], 0).items():
         for pname in params:
             np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
+
+
+@pytest.mark.gpu
+def test_step_async_equals_step_and_seeds_overlap():
+    """rle_step_async (several seeds per GPU, one stream each) enqueues the
+    same steps as rle_step: two engines stepped concurrently end bit-identical to a
+    synchronous run of each."""
+    g = load_golden("td7_tiny")
+    runs = []
+    for mode in ("sync", "async"):
+        pair = [engine_from_golden(g) for _ in range(2)]
+        if mode == "sync":
+            for eng, _, _ in pair:
+                eng.step(5)
+        else:
+            for _ in range(5):
+                for eng, _, _ in pair:
+                    eng.step_async(1)
+            for eng, _, _ in pair:
+                eng.synchronize()
+        runs.append(pair)
+    alg = parse(g)[0]
+    for (e1, r1, _), (e2, r2, _) in zip(runs[0], runs[1]):
+        np.testing.assert_array_equal(e1.last_indices(), e2.last_indices())
+        np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
+        for net, params in spec.agent_params(alg, *spec.TASKS[parse(g)[1]][:2], parse(g)[2], 0).items():
+            for pname in params:
+                np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
