@@ -263,6 +263,7 @@ struct Prog {
   std::vector<std::vector<Op>> schedule() {
     std::map<int, int> lw, lr;
     int maxl = -1;
+    std::vector<int> nops;
     for (auto& it : items) {
       int l = 0;
       for (int r : it.rd)
@@ -272,6 +273,11 @@ struct Prog {
         if (lw.count(w)) l = std::max(l, lw[w] + 1);
         if (lr.count(w)) l = std::max(l, lr[w] + 1);
       }
+      // a level of more than kLevelOps ops would take two launches: defer to the next level
+      // with room (every dependence is still met at a later level)
+      while (l < (int)nops.size() && nops[l] + (int)it.ops.size() > kLevelOps) ++l;
+      if (l >= (int)nops.size()) nops.resize(l + 1, 0);
+      nops[l] += (int)it.ops.size();
       it.level = l;
       for (int w : it.wr)
         if (w >= 0) lw[w] = l;
@@ -330,6 +336,7 @@ enum Res : int {
   R_MAXP,
   R_REPLAY,
   R_ADAMSC,  // Ctrl::adam_step / adam_bc2s (Adam bias corrections of this step)
+  R_ADAMSC1, // their copy for steps on batch set 1 (two steps in one graph: g_pair)
   R_FIRST_DYNAMIC = 100,
 };
 
@@ -352,6 +359,15 @@ struct Engine {
   // step); g_pol[p] / g_pln[p] run a (policy / plain) step on batch p and, once its
   // priority update is done, prefetch the next step's batch into 1 - p.
   Graph g_prime[2], g_pol[2], g_pln[2], g_hard;
+  // g_pair[p]: a policy step on batch p then a plain step on 1 - p as ONE program, so
+  // the scheduler overlaps the second step's early levels (encoder phase, fixed
+  // encoders) with the first step's policy-phase tail.  Each step of the pair keeps
+  // its own Adam scalars (asc_set) so only true data dependencies order the two.
+  Graph g_pair[2];
+  int asc_set = 0;
+  float* adamsc1 = nullptr;  // [step[4], bc2s[4]] of steps built on set 1
+  float* adam_step_of(int set) { return set ? adamsc1 : ctrl->adam_step; }
+  float* adam_bc2s_of(int set) { return set ? adamsc1 + 4 : ctrl->adam_bc2s; }
   // (diagnostics: the parity that last ran; with policy_freq 2 policy and plain steps
   // alternate, so each kind always runs on the same parity)
   int pol_set = 0, pln_set = 0;
@@ -942,7 +958,7 @@ struct Engine {
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
     g.mode = GEMM_DW;
-    std::vector<int> rd{dz.id, L.res, R_ADAMSC}, wr{L.res};
+    std::vector<int> rd{dz.id, L.res, asc_set ? R_ADAMSC1 : R_ADAMSC}, wr{L.res};
     g.A.seg[0] = seg_t(dz, 0, 0, Brows);
     g.A.nseg = 1;
     int koff = 0;
@@ -969,8 +985,8 @@ struct Engine {
     ad.b = bias(L);
     ad.mo = (long long)nP;
     ad.vo = 2LL * (long long)nP;
-    ad.step = &ctrl->adam_step[cnt];
-    ad.bc2s = &ctrl->adam_bc2s[cnt];
+    ad.step = adam_step_of(asc_set) + cnt;
+    ad.bc2s = adam_bc2s_of(asc_set) + cnt;
     ad.lr = lr;
     ad.beta1 = 0.9f;
     ad.beta2 = 0.999f;
@@ -1188,6 +1204,7 @@ struct Engine {
     const bool lap = cfg.use_lap;
     const bool nbd = td7_nb_defer();
     use_set(set);
+    asc_set = set;
     add_adam_scalars(pg);
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
     // ---- encoder phase (td7.py:246-257): online encoder on [s; s'] (one GEMM per layer)
@@ -1599,6 +1616,7 @@ struct Engine {
     Net* tq[2] = {&net("target_q1"), &net("target_q2")};
     const bool lap = cfg.use_lap && !sac;
     use_set(set);
+    asc_set = set;
     add_adam_scalars(pg);
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
     // actor on [s; s'] (target policy aliases the policy, Q1; SAC policy unchanged until its step)
@@ -1976,6 +1994,11 @@ struct Engine {
     return p;
   }
 
+  static bool pair_on() {
+    const char* e = std::getenv("RLE_PAIR");  // A/B experiments
+    return !(e && e[0] == '0');
+  }
+
   void build() {
     REQUIRE(replay, "no replay bound");
     ensure_tapes(1024);
@@ -1990,12 +2013,26 @@ struct Engine {
         g_pol[set] = capture(p1);
         Prog p2 = plan_build([&](Prog& p) { build_td7(p, false, set); });
         g_pln[set] = capture(p2);
+        if (pair_on()) {
+          Prog p3 = plan_build([&](Prog& p) {
+            build_td7(p, true, set);
+            build_td7(p, false, 1 - set);
+          });
+          g_pair[set] = capture(p3);
+        }
       } else {
         Prog p1 = plan_build([&](Prog& p) { build_mlp(p, true, set); });
         g_pol[set] = capture(p1);
         if (!sac) {
           Prog p2 = plan_build([&](Prog& p) { build_mlp(p, false, set); });
           g_pln[set] = capture(p2);
+        }
+        if (pair_on()) {  // TD3: policy step then plain step; SAC: two (policy) steps
+          Prog p3 = plan_build([&](Prog& p) {
+            build_mlp(p, true, set);
+            build_mlp(p, sac, 1 - set);
+          });
+          g_pair[set] = capture(p3);
         }
       }
     }
@@ -2015,16 +2052,16 @@ struct Engine {
 
   // Adam bias-correction scalars of this step from the completed-step counters; the
   // op has no producers, so it runs in level 0 beside the LAP block sums.
-  void add_adam_scalars(Prog& pg) { pg.add(adam_scalars_op(), {R_CNT}, {R_ADAMSC}); }
-  Op adam_scalars_op() {
+  void add_adam_scalars(Prog& pg) { pg.add(adam_scalars_op(asc_set), {R_CNT}, {asc_set ? R_ADAMSC1 : R_ADAMSC}); }
+  Op adam_scalars_op(int set) {
     Op op{};
     op.kind = OP_CTRL;
     op.wg_count = 1;
     CtrlArgs& c = op.ctrl;
     c.mode = 1;
     c.counters = ctrl->counters;
-    c.adam_step = ctrl->adam_step;
-    c.adam_bc2s = ctrl->adam_bc2s;
+    c.adam_step = adam_step_of(set);
+    c.adam_bc2s = adam_bc2s_of(set);
     c.adam_lr[CNT_ADAM_Q] = cfg.critic_lr;
     c.adam_lr[CNT_ADAM_PI] = cfg.policy_lr;
     c.adam_lr[CNT_ADAM_ENC] = cfg.policy_lr;
@@ -2033,20 +2070,12 @@ struct Engine {
 
   // The same computed eagerly (creation / counters set), for readers outside a step.
   void refresh_adam_scalars() {
-    Op op{};
-    op.kind = OP_CTRL;
-    op.wg_count = 1;
-    CtrlArgs& c = op.ctrl;
-    c.mode = 1;
-    c.counters = ctrl->counters;
-    c.adam_step = ctrl->adam_step;
-    c.adam_bc2s = ctrl->adam_bc2s;
-    c.adam_lr[CNT_ADAM_Q] = cfg.critic_lr;
-    c.adam_lr[CNT_ADAM_PI] = cfg.policy_lr;
-    c.adam_lr[CNT_ADAM_ENC] = cfg.policy_lr;
-    if (!ctrl_op) ctrl_op = mem.make<Op>(1);
-    HIPCHK(hipMemcpyAsync(ctrl_op, &op, sizeof(Op), hipMemcpyHostToDevice, stream));
-    HIPCHK(launch_level(ctrl_op, &op, 1, 1, stream));
+    if (!adamsc1) adamsc1 = mem.make<float>(8);
+    if (!ctrl_op) ctrl_op = mem.make<Op>(2);
+    Op ops[2] = {adam_scalars_op(0), adam_scalars_op(1)};
+    ops[1].wg_begin = 1;
+    HIPCHK(hipMemcpyAsync(ctrl_op, ops, sizeof(ops), hipMemcpyHostToDevice, stream));
+    HIPCHK(launch_level(ctrl_op, ops, 2, 2, stream));
     HIPCHK(hipStreamSynchronize(stream));
   }
   Op* ctrl_op = nullptr;
@@ -2079,6 +2108,27 @@ struct Engine {
         // drawn from has changed since (appends, other writers of the priorities, tapes)
         if (!primed || primed_ver != replay->version) HIPCHK(hipGraphLaunch(g_prime[cur_set].x, stream));
         const int p = cur_set;
+        const int tur = std::max(1, cfg.target_update_rate);
+        // TD7 (counter bumped first, td7.py:295) / TD3 (td3.py:231): policy step on p, plain
+        // step on 1 - p, one graph (TD7: neither needs a hard update); SAC: any two steps
+        const long long k1 = algo == RLE_TD7 ? n_runs + 1 : n_runs;
+        const bool pair_ok = algo == RLE_SAC ? true
+                                              : k1 % pf == 0 && (k1 + 1) % pf != 0 &&
+                                                    (algo != RLE_TD7 || (k1 % tur != 0 && (k1 + 1) % tur != 0));
+        if (g_pair[p].x && i + 1 < chunk && pair_ok && (!ctrl_tape_mode_host || tape_left > 0)) {
+          if (ctrl_tape_mode_host) --tape_left;
+          n_runs += 2;
+          HIPCHK(hipGraphLaunch(g_pair[p].x, stream));
+          pol_set = p;
+          if (algo != RLE_SAC) pln_set = 1 - p;
+          last_set = 1 - p;
+          cur_set = p;
+          ++i;
+          if (cfg.use_lap && algo != RLE_SAC) replay->version += 2;
+          primed = true;
+          primed_ver = replay->version;
+          continue;
+        }
         if (algo == RLE_TD7) {
           ++n_runs;  // td7.py:295 (increment first)
           (n_runs % pf == 0 ? pol_set : pln_set) = p;
@@ -2509,7 +2559,7 @@ int rle_destroy(rle_engine* h) {
     Engine& e = *h->e;
     (void)hipStreamSynchronize(e.stream);
     for (rle::Graph* g : {&e.g_prime[0], &e.g_prime[1], &e.g_pol[0], &e.g_pol[1], &e.g_pln[0], &e.g_pln[1],
-                          &e.g_hard}) {
+                          &e.g_pair[0], &e.g_pair[1], &e.g_hard, &e.g_fold}) {
       if (g->x) (void)hipGraphExecDestroy(g->x);
       if (g->g) (void)hipGraphDestroy(g->g);
     }
@@ -2742,7 +2792,10 @@ int rle_graph_describe(rle_engine* h, int which, char* buf, int len) {
   return guard([&] {
     Engine& e = *h->e;
     if (!e.built) e.build();
-    const rle::Graph& G = which == 0 ? e.policy_graph() : (which == 1 ? e.plain_graph() : e.g_hard);
+    const rle::Graph& G = which == 0 ? e.policy_graph()
+                          : which == 1 ? e.plain_graph()
+                          : which == 3 ? e.g_pair[e.pol_set]
+                                       : e.g_hard;
     REQUIRE(buf && len > 0, "describe: bad buffer");
     std::snprintf(buf, (size_t)len, "%s", G.desc.c_str());
   });
@@ -2753,7 +2806,10 @@ int rle_graph_trace(rle_engine* h, int which, unsigned long long* out, long long
     Engine& e = *h->e;
     REQUIRE(n_out, "trace: null n_out");
     if (!e.built) e.build();
-    const rle::Graph& G = which == 0 ? e.policy_graph() : (which == 1 ? e.plain_graph() : e.g_hard);
+    const rle::Graph& G = which == 0 ? e.policy_graph()
+                          : which == 1 ? e.plain_graph()
+                          : which == 3 ? e.g_pair[e.pol_set]
+                                       : e.g_hard;
     *n_out = G.trace ? G.trace_n : 0;
     if (!G.trace || !out) return;
     const int st = rle::trace_stride();

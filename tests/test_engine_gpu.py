@@ -104,8 +104,12 @@ TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny"]
 FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid"]
 
 
+@pytest.mark.parametrize("burst", [False, True], ids=["per_step", "burst"])
 @pytest.mark.parametrize("name", TINY + FULL)
-def test_step_trajectory_matches_reference(name):
+def test_step_trajectory_matches_reference(name, burst):
+    """per_step: one rle_step(1) per step (single-step graphs), checked after every step.
+    burst: the whole taped trajectory in one rle_step(n) (two-step graphs g_pair wherever a
+    policy step is followed by a plain step, or any two SAC steps), checked at the end."""
     g = load_golden(name)
     alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
     eng, rep, tp = engine_from_golden(g)
@@ -118,7 +122,14 @@ def test_step_trajectory_matches_reference(name):
             np.testing.assert_allclose(eng.value_bounds(), g[f"vbounds_{t}"].astype(np.float32),
                                        rtol=1e-4, atol=1e-4)
 
-    infos = run_with_tapes(eng, tp, n_steps, check)
+    if burst:
+        eng.set_tapes(u=tp["u"][:n_steps], eps=tp["eps"][:n_steps],
+                      eps_pi=tp.get("eps_pi", None) if "eps_pi" in tp else None)
+        infos = np.array(eng.step(n_steps))
+        eng.set_tapes()
+        check(n_steps - 1)
+    else:
+        infos = run_with_tapes(eng, tp, n_steps, check)
     ref = g["info"]
     k = ref.shape[1]
     np.testing.assert_array_equal(np.isnan(infos[:, :k]), np.isnan(ref))

@@ -16,6 +16,6 @@ for net, params in init_agent(algo, S, A, H, 1).items():
 rep = E.Replay(1000000, S, A, algo == "td7")
 rep.fill_random(1000000, 1)
 eng.bind(rep)
-for w in (0, 1):
+for w in (0, 1, 3):
     print(f"=== graph {w}")
     print(eng.describe(w))
