@@ -359,11 +359,13 @@ struct Engine {
   // step); g_pol[p] / g_pln[p] run a (policy / plain) step on batch p and, once its
   // priority update is done, prefetch the next step's batch into 1 - p.
   Graph g_prime[2], g_pol[2], g_pln[2], g_hard;
-  // g_pair[p]: a policy step on batch p then a plain step on 1 - p as ONE program, so
-  // the scheduler overlaps the second step's early levels (encoder phase, fixed
-  // encoders) with the first step's policy-phase tail.  Each step of the pair keeps
-  // its own Adam scalars (asc_set) so only true data dependencies order the two.
+  // g_pair[p]: multi_k consecutive steps as ONE program, starting on batch p (policy,
+  // plain, policy, ... with policy_freq 2; SAC: every step), so the scheduler overlaps
+  // each step's early levels (encoder phase, fixed encoders, online critic forward) with
+  // the previous step's policy-phase tail and last Adam level.  Steps on the two batch
+  // sets keep their own Adam scalars (asc_set) so only true data dependencies order them.
   Graph g_pair[2];
+  int multi_k = 0;
   int asc_set = 0;
   float* adamsc1 = nullptr;  // [step[4], bc2s[4]] of steps built on set 1
   float* adam_step_of(int set) { return set ? adamsc1 : ctrl->adam_step; }
@@ -1994,9 +1996,14 @@ struct Engine {
     return p;
   }
 
-  static bool pair_on() {
+  // steps per multi-step graph: RLE_PAIR=K (even; 0 = single-step graphs only)
+  int pair_k() const {
     const char* e = std::getenv("RLE_PAIR");  // A/B experiments
-    return !(e && e[0] == '0');
+    // measured on MI355X (tools/abk.sh): TD7 Humanoid K=2/4/6/8 -> 6370/6513/6440/6290
+    // steps/s, TD3 HalfCheetah K=2/4/8 -> 14072/14885/15408, SAC Humanoid flat from K=2
+    int k = e ? std::atoi(e) : (algo == RLE_TD3 ? 8 : 4);
+    if (algo != RLE_SAC && cfg.policy_freq != 2) k = 0;  // the pattern assumes policy_freq 2
+    return k >= 2 ? k & ~1 : 0;
   }
 
   void build() {
@@ -2004,6 +2011,7 @@ struct Engine {
     ensure_tapes(1024);
     const bool sac = algo == RLE_SAC;
     alloc_folds();
+    multi_k = pair_k();
     for (int set = 0; set < 2; ++set) {
       Prog pp;
       build_prime(pp, sac, set);
@@ -2013,10 +2021,9 @@ struct Engine {
         g_pol[set] = capture(p1);
         Prog p2 = plan_build([&](Prog& p) { build_td7(p, false, set); });
         g_pln[set] = capture(p2);
-        if (pair_on()) {
+        if (multi_k) {
           Prog p3 = plan_build([&](Prog& p) {
-            build_td7(p, true, set);
-            build_td7(p, false, 1 - set);
+            for (int j = 0; j < multi_k; ++j) build_td7(p, j % 2 == 0, (set + j) % 2);
           });
           g_pair[set] = capture(p3);
         }
@@ -2027,10 +2034,9 @@ struct Engine {
           Prog p2 = plan_build([&](Prog& p) { build_mlp(p, false, set); });
           g_pln[set] = capture(p2);
         }
-        if (pair_on()) {  // TD3: policy step then plain step; SAC: two (policy) steps
+        if (multi_k) {  // TD3: policy, plain, ...; SAC: every step is a policy step
           Prog p3 = plan_build([&](Prog& p) {
-            build_mlp(p, true, set);
-            build_mlp(p, sac, 1 - set);
+            for (int j = 0; j < multi_k; ++j) build_mlp(p, sac || j % 2 == 0, (set + j) % 2);
           });
           g_pair[set] = capture(p3);
         }
@@ -2109,22 +2115,25 @@ struct Engine {
         if (!primed || primed_ver != replay->version) HIPCHK(hipGraphLaunch(g_prime[cur_set].x, stream));
         const int p = cur_set;
         const int tur = std::max(1, cfg.target_update_rate);
-        // TD7 (counter bumped first, td7.py:295) / TD3 (td3.py:231): policy step on p, plain
-        // step on 1 - p, one graph (TD7: neither needs a hard update); SAC: any two steps
+        // multi-step graph: TD7 (counter bumped first, td7.py:295) / TD3 (td3.py:231) when
+        // its first step is a policy step (and, TD7, no step of it needs a hard update);
+        // SAC any multi_k steps
+        const int K = multi_k;
         const long long k1 = algo == RLE_TD7 ? n_runs + 1 : n_runs;
-        const bool pair_ok = algo == RLE_SAC ? true
-                                              : k1 % pf == 0 && (k1 + 1) % pf != 0 &&
-                                                    (algo != RLE_TD7 || (k1 % tur != 0 && (k1 + 1) % tur != 0));
-        if (g_pair[p].x && i + 1 < chunk && pair_ok && (!ctrl_tape_mode_host || tape_left > 0)) {
-          if (ctrl_tape_mode_host) --tape_left;
-          n_runs += 2;
+        bool pair_ok = K && i + K - 1 < chunk && (!ctrl_tape_mode_host || tape_left >= K - 1);
+        if (pair_ok && algo != RLE_SAC) pair_ok = k1 % 2 == 0;
+        if (pair_ok && algo == RLE_TD7)
+          for (long long k = k1; k < k1 + K; ++k) pair_ok = pair_ok && k % tur != 0;
+        if (pair_ok && g_pair[p].x) {
+          if (ctrl_tape_mode_host) tape_left -= K - 1;
+          n_runs += K;
           HIPCHK(hipGraphLaunch(g_pair[p].x, stream));
           pol_set = p;
           if (algo != RLE_SAC) pln_set = 1 - p;
           last_set = 1 - p;
           cur_set = p;
-          ++i;
-          if (cfg.use_lap && algo != RLE_SAC) replay->version += 2;
+          i += K - 1;
+          if (cfg.use_lap && algo != RLE_SAC) replay->version += K;
           primed = true;
           primed_ver = replay->version;
           continue;
