@@ -259,11 +259,13 @@ struct Prog {
     it.wr = std::move(wr);
     items.push_back(std::move(it));
   }
-  // Lowest level respecting RAW / WAR / WAW against all earlier ops.
-  std::vector<std::vector<Op>> schedule() {
+  // Lowest level respecting RAW / WAR / WAW against all earlier ops (program order), and
+  // (wg_cap) holding no more workgroups than are resident on the device at once unless
+  // the op alone exceeds that: a second dispatch wave costs more than a later level.
+  std::vector<std::vector<Op>> schedule(int wg_cap = 1 << 30) {
     std::map<int, int> lw, lr;
     int maxl = -1;
-    std::vector<int> nops;
+    std::vector<int> nops, nwg;
     for (auto& it : items) {
       int l = 0;
       for (int r : it.rd)
@@ -275,9 +277,17 @@ struct Prog {
       }
       // a level of more than kLevelOps ops would take two launches: defer to the next level
       // with room (every dependence is still met at a later level)
-      while (l < (int)nops.size() && nops[l] + (int)it.ops.size() > kLevelOps) ++l;
-      if (l >= (int)nops.size()) nops.resize(l + 1, 0);
+      int wg = 0;
+      for (auto& op : it.ops) wg += op.wg_count;
+      while (l < (int)nops.size() &&
+             (nops[l] + (int)it.ops.size() > kLevelOps || (nwg[l] > 0 && nwg[l] + wg > wg_cap)))
+        ++l;
+      if (l >= (int)nops.size()) {
+        nops.resize(l + 1, 0);
+        nwg.resize(l + 1, 0);
+      }
       nops[l] += (int)it.ops.size();
+      nwg[l] += wg;
       it.level = l;
       for (int w : it.wr)
         if (w >= 0) lw[w] = l;
@@ -1866,8 +1876,14 @@ struct Engine {
   std::vector<int> gsq_offs;
 
   // ---------------------------------------------------------------- graphs
+  int sched_cap() const {
+    int cap = std::max(256, level_capacity());
+    if (const char* e = std::getenv("RLE_LEVEL_CAP")) cap = std::max(1, std::atoi(e));  // tuning experiments
+    if (const char* e = std::getenv("RLE_SCHED_CAP")) if (e[0] == '0') cap = 1 << 30;   // A/B
+    return cap;
+  }
   Graph capture(Prog& pg) {
-    auto levels = pg.schedule();
+    auto levels = pg.schedule(sched_cap());
     Graph G;
     size_t total = 0;
     for (auto& lv : levels) {
@@ -1891,6 +1907,7 @@ struct Engine {
           G.desc += "[" + std::to_string(op.gemm.M) + "x" + std::to_string(op.gemm.N) + "x" +
                     std::to_string(op.gemm.R) + " " + ep + "]";
         }
+        if (std::getenv("RLE_DESC_WG")) G.desc += "/" + std::to_string(op.wg_count);  // trace tools
       }
       G.desc += "\n";
     }

@@ -6,11 +6,13 @@ entry), prologue (entry -> main loop), main loop, epilogue (-> exit); the level 
 first entry -> last exit.
 """
 import os
+import re
 import sys
 
 import numpy as np
 
 os.environ.setdefault("RLE_TRACE", "1")
+os.environ.setdefault("RLE_DESC_WG", "1")
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd")]
 from rl import _engine as E  # noqa: E402
@@ -26,8 +28,12 @@ rep.fill_random(1000000, 1)
 eng.bind(rep)
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 eng.step_timed(steps)
-for which in (0, 1):
+graphs = [int(w) for w in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 3]
+for which in graphs:
     tr = eng.trace(which).astype(np.int64)
+    if tr.size == 0:
+        continue
+    tot_t = 0.0
     desc = [l for l in eng.describe(which).splitlines() if l.startswith("L")]
     print(f"=== graph {which}")
     off = 0
@@ -40,6 +46,7 @@ for which in (0, 1):
         span = (t[:, 3].max() - t0) * 10 / 1000
         gap = (t0 - prev_end) * 10 / 1000 if prev_end is not None else 0.0
         prev_end = t[:, 3].max()
+        tot_t += gap + span
         disp = (t[:, 0] - t0) * 10 / 1000
         g = t[:, 1] > 0
         pro = ((t[g, 1] - t[g, 0]) * 10 / 1000) if g.any() else np.zeros(1)
@@ -48,9 +55,20 @@ for which in (0, 1):
         tot = (t[:, 3] - t[:, 0]) * 10 / 1000
         print(f"gap {gap:5.2f} span {span:6.2f} | disp max {disp.max():5.2f} | wg med {np.median(tot):5.2f} max {tot.max():5.2f}"
               f" | pro {np.median(pro):5.2f} loop {np.median(loop):5.2f} epi {np.median(epi):5.2f} | {line[:90]}")
+        if os.environ.get("RLE_DESC_WG") and span > 6.0:  # per-op longest workgroup
+            o = 0
+            parts = []
+            for name, w in re.findall(r"([a-z]+(?:\[[^\]]*\])?)/(\d+)", line.split(":", 1)[1]):
+                w = int(w)
+                tt = t[o:o + w]
+                o += w
+                parts.append(f"{name.replace(' ', '_')}:{(tt[:, 3] - tt[:, 0]).max() * 10 / 1000:.1f}"
+                             f"@{(tt[:, 0].min() - t0) * 10 / 1000:.1f}")
+            print("      ops: " + " ".join(parts))
         if tr.shape[1] == 16 and "gemm" in line:  # fine build: GEMM prologue / epilogue split
             gm = g & (t[:, 11] > 0) & (t[:, 12] > 0)
             if gm.any():
                 med = lambda a, b: np.median((t[gm, b] - t[gm, a]) * 10 / 1000)
                 print(f"      gemm: decode {med(0, 11):5.2f} desc {med(11, 12):5.2f} prefetch {med(12, 1):5.2f}"
                       f" | loop {med(1, 2):5.2f} | splitK {med(2, 13):5.2f} epi {med(13, 3):5.2f}")
+    print(f"total (gaps + spans) {tot_t:7.2f} us over {len(desc)} levels")
