@@ -158,7 +158,7 @@ def pmc_traffic():
 
 
 def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7", env="Humanoid-v4",
-              batch=B, lap=True):
+              batch=B, lap=True, launches=None):
     """The bench JSON line (everything but cpu_baseline) from the max-over-ranks timings."""
     value = n_gpus * steps / wall
     headline = (algo, env, batch) == ("td7", "Humanoid-v4", B)
@@ -170,8 +170,10 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
         gflop, mb = WORK[(algo, env, batch)]
         flop_step, bytes_step = gflop * 1e9, mb * 1e6
     s_dim, a_dim, _ = TASKS[env]
-    # launches per step: average over the policy / non-policy graphs (+ hard update amortised)
-    launches = (lv_policy + lv_plain) / 2.0
+    # launches per step: counted by the engine over the timed steps (rle_launch_count: single-
+    # and multi-step graphs, batch primes, hard updates); else the single-step graph average
+    if launches is None:
+        launches = (lv_policy + lv_plain) / 2.0
     per_launch_s = gpu_s / (steps * launches)
     achieved = flop_step / launches / per_launch_s / 1e12
     roofline = {
@@ -184,7 +186,7 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
         "traffic_algorithmic": round(bytes_step / launches),
         "kernel": "rle_level (one launch per dependency level of the step graph)",
         "flop_per_step": flop_step,
-        "launches_per_step": launches,
+        "launches_per_step": round(launches, 4),
         "avg_launch_us": round(per_launch_s * 1e6, 3),
         "hbm_bytes_per_step_algorithmic": round(bytes_step),
         "hbm_achieved_GBs": round(bytes_step * steps / gpu_s / 1e9, 2),
@@ -326,10 +328,12 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize(local)
+    n_l0 = eng.launch_count()
     t0 = time.perf_counter()
     gpu_ms = eng.step_timed(args.steps)
     torch.cuda.synchronize(local)
     t1 = time.perf_counter()
+    launches = (eng.launch_count() - n_l0) / args.steps
     wall = t1 - t0
     wall, gpu_s = max_over_ranks([wall, gpu_ms / 1e3], dist)
 
@@ -338,7 +342,7 @@ def main():
             dist.barrier()
         return
     out = summarize(world, args.steps, args.warmup, wall, gpu_s, lv_policy, lv_plain, args.algo, args.env,
-                    args.batch, lap)
+                    args.batch, lap, launches)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.algo, args.env, args.batch, lap)
     print(json.dumps(out), flush=True)

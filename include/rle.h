@@ -131,6 +131,10 @@ int rle_last_indices(rle_engine* e, long long* ind_out);
  * before tanh (W = A); SAC raw (mean | log_std) head (W = 2A).  Exploration noise, clipping and
  * scale/bias stay on the host as in the reference. */
 int rle_act(rle_engine* e, const float* obs, int n, float* out);
+/* rle_level dispatches enqueued so far by rle_step* (every step graph replay: single-step,
+ * multi-step, batch prime, hard update, fold refresh); differences over a timed burst give
+ * the exact launches per gradient step (roofline accounting).  Engine-side, no sync. */
+int rle_launch_count(rle_engine* e, long long* n);
 /* Launches per gradient step of each captured graph kind (for roofline accounting). */
 int rle_graph_stats(rle_engine* e, int* levels_policy_step, int* levels_plain_step);
 /* Human-readable description of a captured graph (which: 0 policy step, 1 plain step,

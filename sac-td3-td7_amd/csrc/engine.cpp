@@ -317,6 +317,7 @@ struct Graph {
   long long trace_n = 0;
   std::vector<int> nops, nwg, off;
   std::string desc;
+  int nlaunch = 0;  // rle_level dispatches per replay (a level of > kLevelOps ops takes several)
   int levels() const { return (int)nops.size(); }
 };
 
@@ -1887,6 +1888,7 @@ struct Engine {
     Graph G;
     size_t total = 0;
     for (auto& lv : levels) {
+      G.nlaunch += (int)((lv.size() + kLevelOps - 1) / kLevelOps);
       G.off.push_back((int)total);
       G.nops.push_back((int)lv.size());
       int wg = 0;
@@ -2104,12 +2106,17 @@ struct Engine {
   Op* ctrl_op = nullptr;
 
   // ---------------------------------------------------------------- run
+  long long launches = 0;  // rle_level dispatches enqueued by step graphs (rle_launch_count)
+  void launch_graph(const Graph& G) {
+    HIPCHK(hipGraphLaunch(G.x, stream));
+    launches += G.nlaunch;
+  }
   void step(int n, float* info_out, float* gpu_ms = nullptr, bool async = false) {
     REQUIRE(replay, "no replay bound");
     REQUIRE(replay->size > 0, "replay is empty");
     if (!built) build();
     const int pf = std::max(1, cfg.policy_freq);
-    if (fold_dirty && g_fold.x) HIPCHK(hipGraphLaunch(g_fold.x, stream));
+    if (fold_dirty && g_fold.x) launch_graph(g_fold);
     fold_dirty = false;
     int done = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -2129,7 +2136,7 @@ struct Engine {
         }
         // the batch of this step: prefetched by the previous step, unless anything it was
         // drawn from has changed since (appends, other writers of the priorities, tapes)
-        if (!primed || primed_ver != replay->version) HIPCHK(hipGraphLaunch(g_prime[cur_set].x, stream));
+        if (!primed || primed_ver != replay->version) launch_graph(g_prime[cur_set]);
         const int p = cur_set;
         const int tur = std::max(1, cfg.target_update_rate);
         // multi-step graph: TD7 (counter bumped first, td7.py:295) / TD3 (td3.py:231) when
@@ -2144,7 +2151,7 @@ struct Engine {
         if (pair_ok && g_pair[p].x) {
           if (ctrl_tape_mode_host) tape_left -= K - 1;
           n_runs += K;
-          HIPCHK(hipGraphLaunch(g_pair[p].x, stream));
+          launch_graph(g_pair[p]);
           pol_set = p;
           if (algo != RLE_SAC) pln_set = 1 - p;
           last_set = 1 - p;
@@ -2158,15 +2165,15 @@ struct Engine {
         if (algo == RLE_TD7) {
           ++n_runs;  // td7.py:295 (increment first)
           (n_runs % pf == 0 ? pol_set : pln_set) = p;
-          HIPCHK(hipGraphLaunch((n_runs % pf == 0) ? g_pol[p].x : g_pln[p].x, stream));
-          if (n_runs % std::max(1, cfg.target_update_rate) == 0) HIPCHK(hipGraphLaunch(g_hard.x, stream));
+          launch_graph((n_runs % pf == 0) ? g_pol[p] : g_pln[p]);
+          if (n_runs % std::max(1, cfg.target_update_rate) == 0) launch_graph(g_hard);
         } else if (algo == RLE_TD3) {
           (n_runs % pf == 0 ? pol_set : pln_set) = p;
-          HIPCHK(hipGraphLaunch((n_runs % pf == 0) ? g_pol[p].x : g_pln[p].x, stream));  // td3.py:231
+          launch_graph((n_runs % pf == 0) ? g_pol[p] : g_pln[p]);  // td3.py:231
           ++n_runs;
         } else {
           pol_set = p;
-          HIPCHK(hipGraphLaunch(g_pol[p].x, stream));
+          launch_graph(g_pol[p]);
           ++n_runs;
         }
         last_set = p;
@@ -2802,6 +2809,13 @@ int rle_act(rle_engine* h, const float* obs, int n, float* out) {
     HIPCHK(hipStreamSynchronize(e.stream));
     for (int i = 0; i < n; ++i)
       for (int c = 0; c < W; ++c) out[(size_t)i * W + c] = res[Engine::h_tidx(o.m.rbs, i, c)];
+  });
+}
+
+int rle_launch_count(rle_engine* h, long long* n) {
+  return guard([&] {
+    REQUIRE(n, "launch_count: null out");
+    *n = h->e->launches;
   });
 }
 

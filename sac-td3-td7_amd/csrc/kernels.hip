@@ -472,8 +472,12 @@ __device__ __forceinline__ f32x4 chunk_loop_lds(const float* la, __amdgpu_buffer
 // pre-GEMM and the consumer's own segments: pre_issue puts the wave's first kPreRing chunks
 // and the epilogue operands in flight; pre_finish (after the consumer's other segments)
 // reduces, applies the epilogue and publishes pimg.
-constexpr int kPreRing = 2;  // pre-GEMM chunks prefetched per wave (registers held across the
-                             // consumer's own segments: more would cost occupancy)
+#ifndef RLE_PRE_RING
+#define RLE_PRE_RING 4  // MI355X A/B (K=4 step graphs): 2/3/4 -> 6509/6476/6540 steps/s; 125 VGPRs, no spills
+#endif
+// pre-GEMM chunks prefetched per wave, i.e. all of a wave's quarter of K = 256: registers held
+// across the consumer's own segments (within the 4-waves/SIMD budget)
+constexpr int kPreRing = RLE_PRE_RING;
 struct PreRing {
   float4 a[kPreRing], b0[kPreRing], b1[kPreRing];
   float4 e[2];   // FWD: noise, DX: saved tanh output (4 rows, per column block)

@@ -74,6 +74,7 @@ SIGNATURES = {
     "rle_set_tapes": (_int, [_vp, _int, _f32p, _f32p, _f32p, _i64p]),
     "rle_last_indices": (_int, [_vp, _i64p]),
     "rle_act": (_int, [_vp, _f32p, _int, _f32p]),
+    "rle_launch_count": (_int, [_vp, ctypes.POINTER(ctypes.c_longlong)]),
     "rle_graph_stats": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "rle_graph_describe": (_int, [_vp, _int, ctypes.c_char_p, _int]),
     "rle_graph_trace": (_int, [_vp, _int, ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)]),
@@ -294,6 +295,11 @@ class Engine:
         out = np.empty((n, width), np.float32)
         _check(lib().rle_act(self.h, _fp(obs), n, _fp(out)))
         return out
+
+    def launch_count(self):
+        n = ctypes.c_longlong()
+        _check(lib().rle_launch_count(self.h, ctypes.byref(n)))
+        return n.value
 
     def graph_stats(self):
         a, b = _int(), _int()
