@@ -1020,6 +1020,7 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
         twv[n][1] = ld4g(G(h.tw[n]) + nidx(h.w_cbn, 0, k1));
       }
     }
+    FINE_MARK(0);
     const float rw = h.reward ? sload(h.reward + b) : 0.f, ndn = h.notdone ? sload(h.notdone + b) : 0.f;
     float yv = ((h.mode == HEAD_TD7_LOSS || h.mode == HEAD_MLP_LOSS) && !fused) ? sload(h.y + b) : 0.f;
     const float lp = h.sac ? sload(h.logpi + b) : 0.f;
@@ -1035,6 +1036,7 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
     float q[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) q[n] = dot2(hv[n], wv[n]) + (n ? bias1 : bias0);
+    FINE_MARK(1);
     if (fused) {  // the TD target of this row (as HEAD_TD7_TARGET / HEAD_MLP_TARGET below)
       const float qt0 = dot2(tv[0], twv[0]) + sload(h.tb[0]), qt1 = dot2(tv[1], twv[1]) + sload(h.tb[1]);
       float v = fminf(qt0, qt1);
@@ -1081,7 +1083,9 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
             dq[n] = -e * h.inv_b;
           }
         }
+        FINE_MARK(2);
         if (h.lap && lane == 0) GW(h.prio)[b] = lap_priority(dmax);
+        FINE_MARK(3);
         break;
       }
       case HEAD_TD7_POLICY:  // td7.py:274-275
@@ -1115,6 +1119,7 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
         if (in1) mat_str4(h.dz[n], b, c1, g4(wv[n][1], dv[n][1]));
       }
     }
+    FINE_MARK(4);
   }
   // workgroup partials (fixed order) + value tracking
   float* red = smem;
@@ -1126,6 +1131,7 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
     ired[wave * 2 + 1] = kmin;
   }
   __syncthreads();
+  FINE_MARK(5);
   if (threadIdx.x == 0) {
     if (h.loss_part) {
       GAS float* lp = GW(h.loss_part);

@@ -65,6 +65,11 @@ for which in graphs:
                 parts.append(f"{name.replace(' ', '_')}:{(tt[:, 3] - tt[:, 0]).max() * 10 / 1000:.1f}"
                              f"@{(tt[:, 0].min() - t0) * 10 / 1000:.1f}")
             print("      ops: " + " ".join(parts))
+        if tr.shape[1] == 16 and line.rstrip().endswith("head/64"):  # fine build: loss head phases
+            med = lambda a, b: np.median((t[:, b] - t[:, a]) * 10 / 1000)
+            print(f"      head: issue {med(0, 4):5.2f} loads+q {med(4, 5):5.2f} target {med(5, 1):5.2f}"
+                  f" | loss {med(1, 6):5.2f} prio {med(6, 7):5.2f} | dz {med(2, 8):5.2f} sync {med(8, 9):5.2f}"
+                  f" tail {med(9, 3):5.2f}")
         if tr.shape[1] == 16 and "gemm" in line:  # fine build: GEMM prologue / epilogue split
             gm = g & (t[:, 11] > 0) & (t[:, 12] > 0)
             if gm.any():
