@@ -262,6 +262,80 @@ struct Prog {
   // Lowest level respecting RAW / WAR / WAW against all earlier ops (program order), and
   // (wg_cap) holding no more workgroups than are resident on the device at once unless
   // the op alone exceeds that: a second dispatch wave costs more than a later level.
+  int balance = 0;  // 0 off, 1 any item, 2 no Adam items, 3 no Adam items + only into levels
+                    // whose longest op is at least twice as long
+  // Relative per-workgroup duration of an item (its longest op): a GEMM workgroup's
+  // dependent MFMA chain grows with reduction length x tile width (4 waves share it); Adam
+  // epilogues, the loss head and the sampler are long for their size (level traces).
+  static int item_weight(const Item& it) {
+    int w = 0;
+    for (const Op& op : it.ops) {
+      int x = 8;
+      if (op.kind == OP_GEMM) x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? 8 : 0);
+      else if (op.kind == OP_HEAD || op.kind == OP_SAMPLE_GATHER) x = 60;
+      w = std::max(w, x);
+    }
+    return w;
+  }
+  // After the ASAP pass: in reverse program order, move each item with slack (every
+  // successor at least two levels later) to the lightest level of its window where it is
+  // not the longest op, so wide ASAP levels (contended CUs) shed work into thin levels of
+  // the critical chain.  Dependencies are the RAW / WAW / WAR edges of the ASAP pass.
+  void rebalance(int maxl, std::vector<int>& nops, std::vector<int>& nwg, int wg_cap) {
+    const int n = (int)items.size();
+    std::vector<std::vector<int>> succ(n);
+    std::map<int, int> lastw;
+    std::map<int, std::vector<int>> readers;
+    for (int i = 0; i < n; ++i) {
+      const Item& it = items[i];
+      auto edge = [&](int from) {
+        if (from >= 0) succ[from].push_back(i);
+      };
+      for (int r : it.rd)
+        if (r >= 0 && lastw.count(r)) edge(lastw[r]);
+      for (int w : it.wr) {
+        if (w < 0) continue;
+        if (lastw.count(w)) edge(lastw[w]);
+        for (int j : readers[w]) edge(j);
+      }
+      for (int w : it.wr)
+        if (w >= 0) {
+          lastw[w] = i;
+          readers[w].clear();
+        }
+      for (int r : it.rd)
+        if (r >= 0) readers[r].push_back(i);
+    }
+    std::vector<int> wmax(maxl + 1, 0);
+    for (auto& it : items) wmax[it.level] = std::max(wmax[it.level], item_weight(it));
+    const int cap = std::min(wg_cap, 1024);
+    for (int i = n - 1; i >= 0; --i) {
+      Item& it = items[i];
+      int hi = maxl;
+      for (int s : succ[i]) hi = std::min(hi, items[s].level - 1);
+      const int cur = it.level;
+      if (hi <= cur) continue;
+      int wg = 0;
+      for (auto& op : it.ops) wg += op.wg_count;
+      const int wt = item_weight(it);
+      bool adam = false;
+      for (auto& op : it.ops) adam = adam || (op.kind == OP_GEMM && op.gemm.epi == EPI_ADAM);
+      if (balance >= 2 && adam) continue;
+      const int wfac = balance >= 3 ? 2 : 1;
+      int best = -1;
+      for (int l = cur + 1; l <= hi; ++l) {
+        if (nops[l] + (int)it.ops.size() > kLevelOps || wt * wfac > wmax[l] || nwg[l] + wg > cap) continue;
+        if (nwg[l] + wg >= nwg[cur]) continue;
+        if (best < 0 || nwg[l] < nwg[best]) best = l;
+      }
+      if (best < 0) continue;
+      nops[cur] -= (int)it.ops.size();
+      nwg[cur] -= wg;
+      nops[best] += (int)it.ops.size();
+      nwg[best] += wg;
+      it.level = best;
+    }
+  }
   std::vector<std::vector<Op>> schedule(int wg_cap = 1 << 30) {
     std::map<int, int> lw, lr;
     int maxl = -1;
@@ -295,6 +369,7 @@ struct Prog {
         if (r >= 0) lr[r] = std::max(lr.count(r) ? lr[r] : -1, l);
       maxl = std::max(maxl, l);
     }
+    if (balance) rebalance(maxl, nops, nwg, wg_cap);
     std::vector<std::vector<Op>> levels(maxl + 1);
     for (auto& it : items)
       for (auto& op : it.ops) levels[it.level].push_back(op);
@@ -1888,6 +1963,10 @@ struct Engine {
     return cap;
   }
   Graph capture(Prog& pg) {
+    const char* eb = std::getenv("RLE_BALANCE");  // A/B
+    // measured on MI355X (tools/abk.sh, RLE_BALANCE 0/1/2/3): TD3 HalfCheetah 15481/16050/15911/
+    // 15637, SAC Humanoid 7674/8025/7997/7801, TD7 Humanoid 6532/6478/6498/6517 steps/s
+    pg.balance = eb ? std::atoi(eb) : (algo == RLE_TD7 ? 0 : 1);
     auto levels = pg.schedule(sched_cap());
     Graph G;
     size_t total = 0;
