@@ -243,3 +243,60 @@ def test_step_async_equals_step_and_seeds_overlap():
         for net, params in spec.agent_params(alg, *spec.TASKS[parse(g)[1]][:2], parse(g)[2], 0).items():
             for pname in params:
                 np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
+
+
+@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny", "sac_tiny"])
+def test_multistep_graphs_equal_single_steps(name):
+    """rle_step(12) replays the K-step graphs (TD7/SAC K=4, TD3 K=8, plus single-step graphs
+    around them); twelve rle_step(1) calls replay single-step graphs only.  Same ops on the
+    same data, only grouped into other levels: bit-identical end state."""
+    g = load_golden(name)
+    n = 12
+    e1, r1, _ = engine_from_golden(g)
+    e2, r2, _ = engine_from_golden(g)
+    info1 = e1.step(n)
+    info2 = np.array([e2.step(1)[0] for _ in range(n)])
+    np.testing.assert_array_equal(info1, info2)
+    np.testing.assert_array_equal(e1.last_indices(), e2.last_indices())
+    np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
+    np.testing.assert_array_equal(e1.counters(), e2.counters())
+    alg, env, H = parse(g)[:3]
+    for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
+        for pname in params:
+            np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
+
+
+@pytest.mark.parametrize("alg,env,n", [("td3", "HalfCheetah-v4", 10), ("sac", "Humanoid-v4", 5),
+                                       ("td7", "Ant-v4", 6)])
+def test_multistep_burst_matches_oracle(alg, env, n):
+    """Full-size burst through the multi-step graphs (TD3: one 8-step graph + 2 single steps;
+    SAC: one 4-step graph + 1; TD7: 1 single + one 4-step graph + 1) against the oracle
+    stepped one taped step at a time on the same draws."""
+    from oracle import agents
+    from test_oracle import build_from_golden
+
+    g = _synthetic_golden(alg, env, 256, 256, 4096, 4096, n, alg == "td7", 91)
+    _, orc, orep, tp, n_steps, B = build_from_golden(g)
+    eng, rep, tp2 = engine_from_golden(g)
+    infos_ref = []
+    for t in range(n_steps):
+        i1, n1 = agents.run_steps(orc, alg, orep, {k: v[t:t + 1] for k, v in tp.items()}, 1, B)
+        infos_ref += i1
+    eng.set_tapes(u=tp2["u"][:n_steps], eps=tp2["eps"][:n_steps],
+                  eps_pi=tp2.get("eps_pi", None) if "eps_pi" in tp2 else None)
+    infos = np.array(eng.step(n_steps))
+    eng.set_tapes()
+    np.testing.assert_array_equal(eng.last_indices(), n1[-1])
+    keys = {"td7": ["train/encoder", "train/q_fn", "train/policy"],
+            "td3": ["train/q_fn", "train/policy", "norm/policy"],
+            "sac": ["train/q_fn", "tmp", "norm/tmp", "train/policy", "train/tmp", "entropy"]}[alg]
+    ref = np.array([[np.nan if i[k] is None else i[k] for k in keys] for i in infos_ref], np.float64)
+    k = ref.shape[1]
+    np.testing.assert_allclose(infos[:, :k], ref, rtol=2e-3, atol=1e-4, equal_nan=True)
+    if alg == "td7":
+        np.testing.assert_allclose(rep.get_priority(4096), orep.priority, rtol=1e-4, atol=1e-5)
+    tol = 2 * 3e-4 * n_steps + 1e-4
+    for net, d in orc.nets().items():
+        for name, v in d.items():
+            got = eng.get_param(net, name, tuple(v.shape))
+            assert np.abs(got - v.detach().numpy()).max() <= tol, (net, name)
