@@ -2102,8 +2102,9 @@ struct Engine {
   int pair_k() const {
     const char* e = std::getenv("RLE_PAIR");  // A/B experiments
     // measured on MI355X (tools/abk.sh): TD7 Humanoid K=2/4/6/8 -> 6370/6513/6440/6290
-    // steps/s, TD3 HalfCheetah K=2/4/8 -> 14072/14885/15408, SAC Humanoid flat from K=2
-    int k = e ? std::atoi(e) : (algo == RLE_TD3 ? 8 : 4);
+    // steps/s; TD3 HalfCheetah K=2/4/8/12/16 -> 14072/14885/16066/16203/16348 and SAC
+    // Humanoid K=2/4/8 -> 7874/7977/8052 (with the rebalance pass)
+    int k = e ? std::atoi(e) : (algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 4);
     if (algo != RLE_SAC && cfg.policy_freq != 2) k = 0;  // the pattern assumes policy_freq 2
     return k >= 2 ? k & ~1 : 0;
   }
