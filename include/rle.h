@@ -70,7 +70,9 @@ int rle_replay_get_priority(rle_replay* r, float* out, long long n);
 int rle_replay_set_priority(rle_replay* r, const float* p, long long n, float max_priority);
 /* Device LAP/uniform index search with given uniforms (lap.py:47-54, simple.py:45-54). */
 int rle_replay_sample_indices(rle_replay* r, int n, const float* u, long long* ind_out);
-/* LAPReplayMemory.update_priority (lap.py:66-69) with explicit indices. */
+/* LAPReplayMemory.update_priority (lap.py:66-69) with explicit indices (any values; with a
+ * priority below 1 the block sums are recomputed instead of updated in place).  Every replay
+ * operation waits for the steps already enqueued by engines bound to the replay. */
 int rle_replay_update_priority(rle_replay* r, int n, const long long* ind, const float* p);
 /* LAPReplayMemory.reset_max_priority (lap.py:71-73). */
 int rle_replay_reset_max_priority(rle_replay* r);
@@ -131,6 +133,29 @@ int rle_last_indices(rle_engine* e, long long* ind_out);
  * before tanh (W = A); SAC raw (mean | log_std) head (W = 2A).  Exploration noise, clipping and
  * scale/bias stay on the host as in the reference. */
 int rle_act(rle_engine* e, const float* obs, int n, float* out);
+/* Forward diagnostics on a given batch (host rows s [n][S], a [n][A], n <= 1024), for parity
+ * checks of the nets the step trains:
+ *   RLE_EVAL_Q:   critic `net`'s estimate_q_value -> out [n].  TD7 (SALECritic, sale.py:106-121)
+ *                 on zs = encode_state(s), zsa = encode_state_action(zs, a) of encoder `enc`
+ *                 (online critics use "fixed_encoder", target critics "fixed_encoder_target",
+ *                 td7.py:175-230); TD3/SAC (MLPCritic, mlp.py:98-101) ignore `enc`.
+ *   RLE_EVAL_ZS:  encoder `net`'s encode_state(s) (sale.py:41-46) -> out [n][hidden] (a unused).
+ *   RLE_EVAL_ZSA: encoder `net`'s encode_state_action(encode_state(s), a) (sale.py:48-55)
+ *                 -> out [n][hidden].
+ * Runs on the engine's stream after any enqueued step; syncs. */
+#define RLE_EVAL_Q 0
+#define RLE_EVAL_ZS 1
+#define RLE_EVAL_ZSA 2
+int rle_eval(rle_engine* e, int what, const char* net, const char* enc, const float* s, const float* a, int n,
+             float* out);
+/* SAC._rsample (sac.py:164-172) on given distribution parameters through the step's own
+ * squashed-Gaussian op: log_std clamped to [min_log_std, max_log_std] (sac.py:154-159),
+ * u = mean + eps * exp(log_std), action = tanh(u), log_pi [n] (annotation.py:12 EPS). */
+int rle_sac_rsample(rle_engine* e, const float* mean, const float* log_std, const float* eps, int n, float* action,
+                    float* log_pi);
+/* Info rows [n][RLE_INFO_MAX] of the last rle_step / rle_step_async call (its first n steps;
+ * n <= 4096).  Syncs the engine stream. */
+int rle_get_info(rle_engine* e, int n, float* out);
 /* rle_level dispatches enqueued so far by rle_step* (every step graph replay: single-step,
  * multi-step, batch prime, hard update, fold refresh); differences over a timed burst give
  * the exact launches per gradient step (roofline accounting).  Engine-side, no sync. */

@@ -296,6 +296,29 @@ def _nets(self):
 TD7Oracle.nets = _nets
 TD3Oracle.nets = _nets
 
+# optimizer -> the nets whose parameters it holds, in parameter order (td7.py:127-133,
+# td3.py:102-107, sac.py:109-123)
+_OPT_NETS = {"opt_pi": ("policy",), "opt_q": ("q1", "q2"), "opt_enc": ("encoder",)}
+
+
+def moments(oracle):
+    """Adam exp_avg / exp_avg_sq keyed "{net}.{param}:m|v" (the engine's rle_get_adam layout);
+    only optimizers that have stepped (torch creates the state at the first step)."""
+    out = {}
+    nets = oracle.nets()
+    for attr, owners in _OPT_NETS.items():
+        opt = getattr(oracle, attr, None)
+        if opt is None or opt.t == 0:
+            continue
+        keys = [f"{n}.{k}" for n in owners for k in nets[n]]
+        for key, m, v in zip(keys, opt.m, opt.v):
+            out[key + ":m"] = m.detach().numpy().copy()
+            out[key + ":v"] = v.detach().numpy().copy()
+    if isinstance(oracle, SACOracle) and oracle.opt_t.t:
+        out["tmp.log_alpha:m"] = oracle.opt_t.m[0].detach().numpy().copy()
+        out["tmp.log_alpha:v"] = oracle.opt_t.v[0].detach().numpy().copy()
+    return out
+
 
 def make_oracle(alg, nets, A, use_lap, **hp):
     if alg == "td7":

@@ -94,6 +94,8 @@ struct DevMem {
 
 // ------------------------------------------------------------------ replay
 
+struct Engine;
+
 struct Replay {
   int device;
   long long cap;
@@ -114,6 +116,13 @@ struct Replay {
   // bumped by every change of what sampling draws from (appends, priority writes):
   // an engine's batch prefetched under another version is stale
   unsigned long long version = 0;
+  // engines bound to this replay, each with an event recorded on its stream after every
+  // enqueued step: replay operations on `stream` wait for them first (an append after
+  // rle_step_async must not race the step's priority scatter and block sums)
+  std::vector<std::pair<Engine*, hipEvent_t>> users;
+  void wait_users() {
+    for (auto& u : users) HIPCHK(hipStreamWaitEvent(stream, u.second, 0));
+  }
 };
 
 // ------------------------------------------------------------------ programs
@@ -440,6 +449,7 @@ struct Engine {
   int info_cap = 4096;
   std::vector<float> info_host;
   Replay* replay = nullptr;
+  hipEvent_t done_ev = nullptr;  // recorded after every enqueued step (Replay::users)
   int next_id = R_FIRST_DYNAMIC;
   // Graphs per batch-buffer parity p: g_prime[p] samples batch p (draws of the next
   // step); g_pol[p] / g_pln[p] run a (policy / plain) step on batch p and, once its
@@ -1118,6 +1128,75 @@ struct Engine {
     pg.add(op, {gv.id, x.id, x.norm_id}, {out.id});
     return out;
   }
+
+  // AvgL1Norm itself (sale.py:11-13) applied to a normed view: out = x / m (OP_NORMBWD with
+  // fwd = 1).  Only diagnostics read a normed tensor explicitly; the step defers the norm.
+  View normfwd(Prog& pg, const View& x) {
+    REQUIRE(x.norm && x.m.n && x.rows % 16 == 0, "normfwd: x is not a normed view");
+    Op op{};
+    op.kind = OP_NORMBWD;
+    NormBwdArgs& a = op.nb;
+    View out = buf(x.rows, x.width);
+    a.g = x.m;
+    a.x = x.m;
+    a.dx = out.m;
+    a.rows = x.rows;
+    a.width = x.width;
+    a.norm = x.nref();
+    a.fwd = 1;
+    op.wg_count = cdiv(x.rows, 4);
+    pg.add(op, {x.id, x.norm_id}, {out.id});
+    return out;
+  }
+
+  // SALEEncoder.encode_state (sale.py:41-46): a normed view (consumers apply the norm).
+  View enc_zs(Prog& pg, Net& E, const View& s, int M) {
+    View h1 = fwd(pg, E.layers[0], {{s}}, M, ACT_ELU, nullptr, false);
+    View h2 = fwd(pg, E.layers[1], {{h1}}, M, ACT_ELU, nullptr, false);
+    return fwd(pg, E.layers[2], {{h2}}, M, ACT_NONE, nullptr, true);
+  }
+  // SALEEncoder.encode_state_action (sale.py:48-55).
+  View enc_zsa(Prog& pg, Net& E, const View& zs, const View& a, int M) {
+    View a1 = fwd(pg, E.layers[3], {{zs}, {a}}, M, ACT_ELU, nullptr, false);
+    View a2 = fwd(pg, E.layers[4], {{a1}}, M, ACT_ELU, nullptr, false);
+    return fwd(pg, E.layers[5], {{a2}}, M, ACT_NONE, nullptr, false);
+  }
+
+  // Host rows [n][w] into every kept image of v (rows past n and columns past w stay zero).
+  void upload(const View& v, const float* host, int n, int w) {
+    const size_t img = (size_t)v.m.rbs * 16 * v.m.cbn * 16;
+    if (v.m.n) {
+      std::vector<float> buf_n(img, 0.f);
+      for (int i = 0; i < n; ++i)
+        for (int c = 0; c < w; ++c) buf_n[h_nidx(v.m.cbn, i, c)] = host[(size_t)i * w + c];
+      HIPCHK(hipMemcpyAsync(v.m.n, buf_n.data(), img * 4, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+    if (v.m.t) {
+      std::vector<float> buf_t(img, 0.f);
+      for (int i = 0; i < n; ++i)
+        for (int c = 0; c < w; ++c) buf_t[h_tidx(v.m.rbs, i, c)] = host[(size_t)i * w + c];
+      HIPCHK(hipMemcpyAsync(v.m.t, buf_t.data(), img * 4, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+  }
+  // Rows [n][w] of v's T image to the host (syncs the engine stream).
+  void download(const View& v, float* host, int n, int w) {
+    std::vector<float> res((size_t)v.m.rbs * 16 * v.m.cbn * 16);
+    HIPCHK(hipMemcpyAsync(res.data(), v.m.t, res.size() * 4, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    for (int i = 0; i < n; ++i)
+      for (int c = 0; c < w; ++c) host[(size_t)i * w + c] = res[h_tidx(v.m.rbs, i, c)];
+  }
+
+  // Diagnostic forward programs (rle_eval, rle_sac_rsample), captured once per shape.
+  struct EvalGraph {
+    Graph G;
+    View in0, in1, out;
+    float* out_vec = nullptr;
+    int width = 0;
+  };
+  std::map<std::string, EvalGraph> eval_graphs;
 
   // polyak / copy over a whole net range
   void flat(Prog& pg, int kind, Net& dst, Net* src, float tau, bool self_alias) {
@@ -2273,6 +2352,7 @@ struct Engine {
       if (!gpu_ms && !async) HIPCHK(hipStreamSynchronize(stream));
       done += chunk;
     }
+    HIPCHK(hipEventRecord(done_ev, stream));  // replay operations wait for this (Replay::wait_users)
     if (gpu_ms) {
       HIPCHK(hipEventRecord(ev1, stream));
       HIPCHK(hipEventSynchronize(ev1));
@@ -2358,6 +2438,10 @@ int rle_replay_create(int device, long long capacity, int state_dim, int action_
 int rle_replay_destroy(rle_replay* r) {
   return guard([&] {
     if (!r) return;
+    for (auto& u : r->r.users) {  // engines still bound: unbind (their steps now fail: "no replay bound")
+      (void)hipEventSynchronize(u.second);
+      u.first->replay = nullptr;
+    }
     (void)hipStreamSynchronize(r->r.stream);
     (void)hipStreamDestroy(r->r.stream);
     delete r;
@@ -2370,6 +2454,7 @@ int rle_replay_append(rle_replay* h, const float* state, const float* action, co
     REQUIRE(h && count >= 0, "append: bad args");
     Replay& r = h->r;
     HIPCHK(hipSetDevice(r.device));
+    r.wait_users();
     long long done = 0;
     // a chunk never wraps onto itself (rows i and i+cap would race; the later must win)
     const long long chunk_max = std::min<long long>(65536, r.cap);
@@ -2430,6 +2515,7 @@ int rle_replay_fill_random(rle_replay* h, long long count, unsigned long long se
     Replay& r = h->r;
     REQUIRE(count > 0 && count <= r.cap, "fill: bad count");
     HIPCHK(hipSetDevice(r.device));
+    r.wait_users();
     HIPCHK(rle::launch_fill(r.state, r.next_state, r.action, r.reward, r.notdone, r.priority, count, r.S, r.Sp, r.A,
                             r.Ap, seed, r.stream));
     r.size = std::max(r.size, count);
@@ -2493,6 +2579,7 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     Replay& r = h->r;
     REQUIRE(n > 0 && r.size > 0, "sample_indices: bad args / empty replay");
     HIPCHK(hipSetDevice(r.device));
+    r.wait_users();
     rle::DevMem tmp;
     rle::SampleArgs s{};
     s.state = r.state;
@@ -2552,6 +2639,13 @@ int rle_replay_update_priority(rle_replay* h, int n, const long long* ind, const
   return guard([&] {
     Replay& r = h->r;
     REQUIRE(n > 0 && n <= 1024, "update_priority: 0 < n <= 1024");
+    HIPCHK(hipSetDevice(r.device));
+    r.wait_users();
+    for (int i = 0; i < n; ++i) REQUIRE(ind[i] >= 0 && ind[i] < r.cap, "update_priority: index out of range");
+    // The incremental fp64 block-sum update is exact for priorities >= 1 (integer multiples of
+    // 2^-23 summing below 2^30); any smaller value -> full recompute of the block sums instead.
+    bool small = false;
+    for (int i = 0; i < n; ++i) small = small || !(p[i] >= 1.f);
     rle::DevMem tmp;
     long long* di = tmp.make<long long>(n);
     float* dp = tmp.make<float>(n);
@@ -2564,9 +2658,10 @@ int rle_replay_update_priority(rle_replay* h, int n, const long long* ind, const
     op.prio.p = dp;
     op.prio.B = n;
     op.prio.max_priority = r.maxp_d;
-    op.prio.bsum = r.lap ? r.bsum : nullptr;
+    op.prio.bsum = r.lap && !small ? r.bsum : nullptr;
     op.wg_count = 1;
     run_eager(r, tmp, {{op}});
+    if (r.lap && small) recompute_bsum(r);
     ++r.version;
   });
 }
@@ -2575,6 +2670,8 @@ int rle_replay_reset_max_priority(rle_replay* h) {
   return guard([&] {
     Replay& r = h->r;
     REQUIRE(r.size > 0, "reset_max_priority: empty");
+    HIPCHK(hipSetDevice(r.device));
+    r.wait_users();
     rle::DevMem tmp;
     rle::Op a{};
     a.kind = rle::OP_MAXRED;
@@ -2675,6 +2772,15 @@ int rle_destroy(rle_engine* h) {
     if (!h) return;
     Engine& e = *h->e;
     (void)hipStreamSynchronize(e.stream);
+    if (e.replay) {
+      auto& us = e.replay->users;
+      for (size_t i = 0; i < us.size(); ++i)
+        if (us[i].first == &e) {
+          us.erase(us.begin() + i);
+          break;
+        }
+    }
+    if (e.done_ev) (void)hipEventDestroy(e.done_ev);
     for (rle::Graph* g : {&e.g_prime[0], &e.g_prime[1], &e.g_pol[0], &e.g_pol[1], &e.g_pln[0], &e.g_pln[1],
                           &e.g_pair[0], &e.g_pair[1], &e.g_hard, &e.g_fold}) {
       if (g->x) (void)hipGraphExecDestroy(g->x);
@@ -2683,6 +2789,10 @@ int rle_destroy(rle_engine* h) {
     for (auto& kv : e.act_graphs) {
       if (kv.second.first.x) (void)hipGraphExecDestroy(kv.second.first.x);
       if (kv.second.first.g) (void)hipGraphDestroy(kv.second.first.g);
+    }
+    for (auto& kv : e.eval_graphs) {
+      if (kv.second.G.x) (void)hipGraphExecDestroy(kv.second.G.x);
+      if (kv.second.G.g) (void)hipGraphDestroy(kv.second.G.g);
     }
     (void)hipStreamDestroy(e.stream);
     delete h;
@@ -2696,8 +2806,18 @@ int rle_bind_replay(rle_engine* h, rle_replay* r) {
     REQUIRE(r->r.S == e.S && r->r.A == e.A, "bind: replay dims differ from agent dims");
     if (e.replay == &r->r) return;
     REQUIRE(!e.built, "bind: engine already bound to another replay");
+    if (e.replay) {  // not built yet: move to the new replay
+      auto& us = e.replay->users;
+      for (size_t i = 0; i < us.size(); ++i)
+        if (us[i].first == &e) {
+          us.erase(us.begin() + i);
+          break;
+        }
+    }
     e.replay = &r->r;
     e.primed = false;
+    if (!e.done_ev) HIPCHK(hipEventCreateWithFlags(&e.done_ev, hipEventDisableTiming));
+    r->r.users.push_back({&e, e.done_ev});
   });
 }
 
@@ -2959,6 +3079,124 @@ int rle_copy_state(rle_engine* dst, rle_engine* src) {
     d.n_runs = s.n_runs;
     d.primed = false;
     d.fold_dirty = true;
+  });
+}
+
+int rle_eval(rle_engine* h, int what, const char* net, const char* enc, const float* s, const float* a, int n,
+             float* out) {
+  return guard([&] {
+    REQUIRE(h && net && s && out && n > 0 && n <= 1024, "eval: bad args (0 < n <= 1024)");
+    REQUIRE(what == RLE_EVAL_Q || what == RLE_EVAL_ZS || what == RLE_EVAL_ZSA, "eval: bad `what`");
+    REQUIRE(what == RLE_EVAL_ZS || a, "eval: needs actions");
+    Engine& e = *h->e;
+    const bool td7 = e.algo == RLE_TD7;
+    REQUIRE(what == RLE_EVAL_Q || td7, "eval: encoder outputs exist for TD7 only");
+    REQUIRE(!(td7 && what == RLE_EVAL_Q) || enc, "eval: TD7 critics need the encoder of their embeddings");
+    HIPCHK(hipSetDevice(e.cfg.device));
+    const std::string key = std::to_string(what) + "|" + net + "|" + (enc ? enc : "") + "|" + std::to_string(n);
+    auto it = e.eval_graphs.find(key);
+    if (it == e.eval_graphs.end()) {
+      rle::Net& N = e.net(net);
+      rle::Prog pg;
+      const int M = rle::r16(n);
+      Engine::EvalGraph eg;
+      eg.in0 = e.buf(M, e.S, true, false);
+      eg.in1 = e.buf(M, e.A, true, false);
+      if (what == RLE_EVAL_Q) {
+        if (td7) {  // SALECritic.estimate_q_value (sale.py:106-121) on (s, a, zsa, zs) of `enc`
+          rle::Net& E = e.net(enc);
+          REQUIRE(N.kind == "sale_critic" && E.kind == "sale_enc", "eval: Q needs a critic net and an encoder");
+          rle::View zs = e.enc_zs(pg, E, eg.in0, M);
+          rle::View zsa = e.enc_zsa(pg, E, zs, eg.in1, M);
+          rle::View c01 = e.fwd(pg, N.layers[0], {{eg.in0}, {eg.in1}}, M, rle::ACT_NONE, nullptr, true);
+          rle::View c1 = e.fwd(pg, N.layers[1], {{c01}, {zsa}, {zs}}, M, rle::ACT_ELU, nullptr, false);
+          rle::View c2 = e.fwd(pg, N.layers[2], {{c1}}, M, rle::ACT_ELU, nullptr, false);
+          eg.out = e.fwd(pg, N.layers[3], {{c2}}, M, rle::ACT_NONE, nullptr, false);
+        } else {  // MLPCritic.estimate_q_value (mlp.py:98-101)
+          REQUIRE(N.kind == "mlp_critic", "eval: Q needs a critic net");
+          rle::View h0 = e.fwd(pg, N.layers[0], {{eg.in0}, {eg.in1}}, M, rle::ACT_RELU, nullptr, false);
+          rle::View h1 = e.fwd(pg, N.layers[1], {{h0}}, M, rle::ACT_RELU, nullptr, false);
+          eg.out = e.fwd(pg, N.layers[2], {{h1}}, M, rle::ACT_NONE, nullptr, false);
+        }
+        eg.width = 1;
+      } else {
+        REQUIRE(N.kind == "sale_enc", "eval: ZS / ZSA need an encoder net");
+        rle::View zs = e.enc_zs(pg, N, eg.in0, M);
+        eg.out = what == RLE_EVAL_ZS ? e.normfwd(pg, zs) : e.enc_zsa(pg, N, zs, eg.in1, M);
+        eg.width = e.H;
+      }
+      eg.G = e.capture(pg);
+      it = e.eval_graphs.emplace(key, eg).first;
+    }
+    Engine::EvalGraph& eg = it->second;
+    e.upload(eg.in0, s, n, e.S);
+    if (a) e.upload(eg.in1, a, n, e.A);
+    HIPCHK(hipGraphLaunch(eg.G.x, e.stream));
+    e.download(eg.out, out, n, eg.width);
+  });
+}
+
+int rle_sac_rsample(rle_engine* h, const float* mean, const float* log_std, const float* eps, int n, float* action,
+                    float* log_pi) {
+  return guard([&] {
+    REQUIRE(h && mean && log_std && eps && action && log_pi && n > 0 && n <= 1024, "sac_rsample: bad args");
+    Engine& e = *h->e;
+    REQUIRE(e.algo == RLE_SAC, "sac_rsample: SAC engines only");
+    HIPCHK(hipSetDevice(e.cfg.device));
+    const int A = e.A;
+    const std::string key = "rsample|" + std::to_string(n);
+    auto it = e.eval_graphs.find(key);
+    if (it == e.eval_graphs.end()) {
+      rle::Prog pg;
+      const int M = rle::r16(n);
+      Engine::EvalGraph eg;
+      eg.in0 = e.buf(M, 2 * A);              // raw head output: mean | log_std (as mlp.4's output)
+      eg.in1 = e.buf(M, A, false, true);     // eps
+      eg.out = e.buf(M, A);                  // tanh action
+      rle::View lp = e.vec(M);
+      eg.out_vec = lp.p;
+      rle::Op op{};
+      op.kind = rle::OP_SAC_ACTOR;
+      rle::SacActorArgs& sa = op.sac;
+      sa.out = eg.in0.m;
+      sa.A = A;
+      sa.rows = n;
+      sa.eps = eg.in1.m;
+      sa.eps2 = eg.in1.m;
+      sa.eps_row_split = 0;  // every row draws from eps
+      sa.act = eg.out.m;
+      sa.logpi = lp.p;
+      sa.min_log_std = e.cfg.min_log_std;
+      sa.max_log_std = e.cfg.max_log_std;
+      sa.mean_off = 0;
+      sa.ls_off = A;
+      op.wg_count = rle::cdiv(n, rle::kThreads);
+      pg.add(op, {eg.in0.id, eg.in1.id}, {eg.out.id, lp.id});
+      eg.width = A;
+      eg.G = e.capture(pg);
+      it = e.eval_graphs.emplace(key, eg).first;
+    }
+    Engine::EvalGraph& eg = it->second;
+    std::vector<float> raw((size_t)n * 2 * A);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < A; ++j) {
+        raw[(size_t)i * 2 * A + j] = mean[(size_t)i * A + j];
+        raw[(size_t)i * 2 * A + A + j] = log_std[(size_t)i * A + j];
+      }
+    e.upload(eg.in0, raw.data(), n, 2 * A);
+    e.upload(eg.in1, eps, n, A);
+    HIPCHK(hipGraphLaunch(eg.G.x, e.stream));
+    e.download(eg.out, action, n, A);
+    HIPCHK(hipMemcpy(log_pi, eg.out_vec, (size_t)n * 4, hipMemcpyDeviceToHost));
+  });
+}
+
+int rle_get_info(rle_engine* h, int n, float* out) {
+  return guard([&] {
+    Engine& e = *h->e;
+    REQUIRE(out && n >= 0 && n <= e.info_cap, "get_info: 0 <= n <= info capacity (4096)");
+    HIPCHK(hipStreamSynchronize(e.stream));
+    HIPCHK(hipMemcpy(out, e.info, (size_t)n * rle::kInfoMax * sizeof(float), hipMemcpyDeviceToHost));
   });
 }
 

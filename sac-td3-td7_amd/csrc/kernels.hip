@@ -970,7 +970,7 @@ __device__ __forceinline__ void op_normbwd(const CAS NormBwdArgs& a, int t) {
   if (in1) dot += (g1.x * x1.x + g1.y * x1.y) + (g1.z * x1.z + g1.w * x1.w);
   dot = wave_sum(dot);
   // y = x / m: dy/dx path g/m ; dm path -(sum g x)/m^2 * sign(x)/n (unless clamped)
-  const float gm = clamped ? 0.f : (-dot * inv * inv) / (float)a.width;
+  const float gm = (clamped || a.fwd) ? 0.f : (-dot * inv * inv) / (float)a.width;
   auto sgn = [](float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); };
   auto f = [&](float4 gv, float4 xv) {
     return make_float4(gv.x * inv + sgn(xv.x) * gm, gv.y * inv + sgn(xv.y) * gm, gv.z * inv + sgn(xv.z) * gm,

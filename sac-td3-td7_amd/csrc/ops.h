@@ -187,10 +187,12 @@ struct GemmArgs {
 
 // AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise);
 // 4 rows per workgroup (1 per wave), N images in, N + T images out.
+// fwd = 1: the forward itself, dx = x / m (g = x; diagnostics: rle_eval's zs output).
 struct NormBwdArgs {
   Mat g, x, dx;
   int rows, width;
   NormRef norm;  // partials for m (x rows)
+  int fwd, pad_;
 };
 
 enum HeadMode : int {

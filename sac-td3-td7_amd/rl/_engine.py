@@ -13,6 +13,7 @@ import os
 import numpy as np
 
 RLE_TD7, RLE_TD3, RLE_SAC = 0, 1, 2
+RLE_EVAL_Q, RLE_EVAL_ZS, RLE_EVAL_ZSA = 0, 1, 2
 INFO_MAX = 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -79,6 +80,9 @@ SIGNATURES = {
     "rle_graph_describe": (_int, [_vp, _int, ctypes.c_char_p, _int]),
     "rle_graph_trace": (_int, [_vp, _int, ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)]),
     "rle_trace_stride": (_int, []),
+    "rle_eval": (_int, [_vp, _int, _cs, _cs, _f32p, _f32p, _int, _f32p]),
+    "rle_sac_rsample": (_int, [_vp, _f32p, _f32p, _f32p, _int, _f32p, _f32p]),
+    "rle_get_info": (_int, [_vp, _int, _f32p]),
     "rle_copy_state": (_int, [_vp, _vp]),
     "rle_synchronize": (_int, [_vp]),
 }
@@ -295,6 +299,49 @@ class Engine:
         out = np.empty((n, width), np.float32)
         _check(lib().rle_act(self.h, _fp(obs), n, _fp(out)))
         return out
+
+    def eval_q(self, net, s, a, enc="fixed_encoder"):
+        """estimate_q_value of critic `net` on (s, a) -> [n] (TD7: embeddings of encoder `enc`)."""
+        s = _f32(s)
+        n = s.shape[0]
+        a = _f32(a, (n, self.cfg.action_dim))
+        out = np.empty(n, np.float32)
+        enc_b = enc.encode() if (enc and self.cfg.algo == RLE_TD7) else None
+        _check(lib().rle_eval(self.h, RLE_EVAL_Q, net.encode(), enc_b, _fp(s), _fp(a), n, _fp(out)))
+        return out
+
+    def eval_zs(self, enc, s):
+        """encode_state of encoder `enc` (TD7) -> [n][hidden]."""
+        s = _f32(s)
+        n = s.shape[0]
+        out = np.empty((n, self.cfg.hidden), np.float32)
+        _check(lib().rle_eval(self.h, RLE_EVAL_ZS, enc.encode(), None, _fp(s), None, n, _fp(out)))
+        return out
+
+    def eval_zsa(self, enc, s, a):
+        """encode_state_action(encode_state(s), a) of encoder `enc` (TD7) -> [n][hidden]."""
+        s = _f32(s)
+        n = s.shape[0]
+        a = _f32(a, (n, self.cfg.action_dim))
+        out = np.empty((n, self.cfg.hidden), np.float32)
+        _check(lib().rle_eval(self.h, RLE_EVAL_ZSA, enc.encode(), None, _fp(s), _fp(a), n, _fp(out)))
+        return out
+
+    def sac_rsample(self, mean, log_std, eps):
+        """SAC._rsample through the device op: (tanh action [n][A], log_pi [n])."""
+        mean = _f32(mean)
+        n, A = mean.shape
+        log_std, eps = _f32(log_std, (n, A)), _f32(eps, (n, A))
+        act = np.empty((n, A), np.float32)
+        lp = np.empty(n, np.float32)
+        _check(lib().rle_sac_rsample(self.h, _fp(mean), _fp(log_std), _fp(eps), n, _fp(act), _fp(lp)))
+        return act, lp
+
+    def get_info(self, n):
+        """Info rows of the last step / step_async call."""
+        out = np.empty((max(n, 1), INFO_MAX), np.float32)
+        _check(lib().rle_get_info(self.h, n, _fp(out)))
+        return out[:n]
 
     def launch_count(self):
         n = ctypes.c_longlong()

@@ -134,6 +134,30 @@ def digest(arr, rng_seed=7, k=64):
     return np.array([a.astype(np.float64).sum(), np.abs(a.astype(np.float64)).sum()]), pos, a[pos]
 
 
+def optimizer_moments(agent, nets):
+    """Adam first / second moments (exp_avg, exp_avg_sq) of every trained parameter, keyed
+    "{net}.{param}" as in the engine's rle_get_adam (td7.py:127-133, td3.py:102-107,
+    sac.py:109-123: optim_policy / optim_q_fns / optim_encoder / optim_tmp)."""
+    owner = {}
+    for net in nets:
+        for name, p in getattr(agent, net).named_parameters():
+            owner.setdefault(id(p), f"{net}.{name}")
+    if getattr(agent, "tmp", None) is not None:
+        owner[id(agent.tmp)] = "tmp.log_alpha"
+    out = {}
+    for attr in ("optim_policy", "optim_q_fns", "optim_encoder", "optim_tmp"):
+        opt = getattr(agent, attr, None)
+        if opt is None:
+            continue
+        for p, st in opt.state.items():
+            if "exp_avg" not in st:
+                continue
+            key = owner[id(p)]
+            out[key + ":m"] = st["exp_avg"].detach().numpy().copy()
+            out[key + ":v"] = st["exp_avg_sq"].detach().numpy().copy()
+    return out
+
+
 def forward_outputs(agent, alg, batch):
     """Forward-only outputs of the nets on a fixed batch (before training)."""
     out = {}
@@ -170,8 +194,13 @@ INFO_KEYS = {
 }
 
 
+ONLY = set(sys.argv[1:])  # optional fixture names to (re)generate; default: all
+
+
 def run_config(name, alg, env_id, H, B, N, n_fill, n_steps, use_lap, seed, extra=None,
-               full=True):
+               full=True, sparse_prio=False, adam_steps=2):
+    if ONLY and name not in ONLY:
+        return
     extra = dict(extra or {})
     S, A, hi = spec.TASKS[env_id]
     nets = spec.agent_params(alg, S, A, H, seed)
@@ -218,8 +247,20 @@ def run_config(name, alg, env_id, H, B, N, n_fill, n_steps, use_lap, seed, extra
         inds.append(ind)
         infos.append([np.nan if info.get(k) is None else float(info[k]) for k in INFO_KEYS[alg]])
         if lap:
-            res[f"prio_{t}"] = replay.priority.numpy().copy()
+            if sparse_prio:  # only rows ind_t change at step t (lap.py:66-69): their new values
+                res[f"prioi_{t}"] = replay.priority.numpy()[ind].copy()
+            else:
+                res[f"prio_{t}"] = replay.priority.numpy().copy()
             res[f"maxprio_{t}"] = np.array(replay.max_priority, dtype=np.float64)
+        if t < adam_steps:  # optimizer moments after steps 1 and 2 (m = 0.1 g after an optimizer's 1st step)
+            for key, arr in optimizer_moments(agent, nets).items():
+                if full:
+                    res[f"adam{t}_{key}"] = arr
+                else:
+                    d, pos, vals = digest(arr, k=512)
+                    res[f"adam{t}_{key}:digest"] = d
+                    res[f"adam{t}_{key}:pos"] = pos.astype(np.int32)
+                    res[f"adam{t}_{key}:vals"] = vals
         if alg == "td7":
             res[f"vbounds_{t}"] = np.array([float(agent.value_max), float(agent.value_min),
                                             float(agent.value_target_max), float(agent.value_target_min)])
@@ -306,9 +347,10 @@ def sac_rsample_fixture():
 
 
 def main():
-    lap_sampler_fixture()
-    uniform_sampler_fixture()
-    sac_rsample_fixture()
+    if not ONLY:
+        lap_sampler_fixture()
+        uniform_sampler_fixture()
+        sac_rsample_fixture()
     # Tiny full dumps (H=32): multi-step trajectories incl. hard updates.
     run_config("td7_tiny", "td7", "Tiny-v0", 32, 16, 64, 50, 10, True, 5,
                extra={"target_update_rate": 4})
@@ -325,6 +367,10 @@ def main():
                full=False)
     run_config("sac_humanoid", "sac", "Humanoid-v4", 256, 256, 2048, 2048, 2, False, 44,
                full=False)
+    # Many-block LAP trajectory at full width: 65,536 rows (16 block sums of 4,096), 12 steps,
+    # hard updates at steps 5 and 10 (td7.py:278-285, 325-331), a 4-step graph at steps 6-9.
+    run_config("td7_humanoid_64k", "td7", "Humanoid-v4", 256, 256, 65536, 65536, 12, True, 45,
+               extra={"target_update_rate": 5}, full=False, sparse_prio=True)
 
 
 if __name__ == "__main__":

@@ -1,9 +1,12 @@
 """Parity of the HIP engine (through the C ABI) against reference goldens + the oracle.
 
 Tolerances (SURVEY.md §4 evidence: fp32 reference vs fp64 of the same math):
-forward outputs |d| <= 1e-5 + 1e-5 |ref|; per-step losses rel 1e-3 over <= 10 steps on identical
-batches; parameters after k Adam steps within 2*lr*k + 1e-5 (Adam's first steps are ~lr*sign(g),
-so near-zero gradients may flip sign between summation orders).
+forward outputs |d| <= 1e-5 + 1e-5 |ref|; per-step losses rel 2e-3 over <= 18 steps on identical
+batches; parameters after k Adam steps: >= 99.9% of the elements (full size; 99% of each H=32
+tensor) within 1e-5 of the reference, and every element within 2*lr*k + 1e-4 (Adam's first steps
+are ~lr*sign(g): a gradient that rounds to the other sign in another summation order moves its
+parameter 2*lr away, so the bulk criterion is what catches a wrong gradient).  Gradients
+themselves are pinned through the Adam moments in test_parity_gpu.py.
 """
 
 import numpy as np
@@ -16,6 +19,16 @@ pytestmark = pytest.mark.gpu
 E = pytest.importorskip("rl._engine")
 from harness import engine_from_golden, parse, run_with_tapes  # noqa: E402
 from oracle import spec  # noqa: E402
+from test_oracle import expected_priorities  # noqa: E402
+
+BULK = 0.999  # fraction of parameter elements within 1e-5 of the reference (full size)
+
+
+def assert_params_close(got, ref, tol, what, bulk=BULK):
+    d = np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64))
+    assert d.max() <= tol, (what, float(d.max()))
+    assert (d <= 1e-5).mean() >= bulk, (what, float((d <= 1e-5).mean()))
+    return int((d <= 1e-5).sum()), d.size
 
 
 def test_lap_sampler_device():
@@ -101,7 +114,7 @@ def test_forward_matches_reference(name):
 
 
 TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny"]
-FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid"]
+FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k"]
 
 
 @pytest.mark.parametrize("burst", [False, True], ids=["per_step", "burst"])
@@ -117,7 +130,8 @@ def test_step_trajectory_matches_reference(name, burst):
     def check(t):
         np.testing.assert_array_equal(eng.last_indices(), g["ind"][t])
         if use_lap:
-            np.testing.assert_allclose(rep.get_priority(Ncap), g[f"prio_{t}"], rtol=1e-4, atol=1e-5)
+            exp = g[f"prio_{t}"] if f"prio_{t}" in g else expected_priorities(g, Ncap, t)
+            np.testing.assert_allclose(rep.get_priority(Ncap), exp, rtol=1e-4, atol=1e-5)
         if f"vbounds_{t}" in g:
             np.testing.assert_allclose(eng.value_bounds(), g[f"vbounds_{t}"].astype(np.float32),
                                        rtol=1e-4, atol=1e-4)
@@ -135,22 +149,25 @@ def test_step_trajectory_matches_reference(name, burst):
     np.testing.assert_array_equal(np.isnan(infos[:, :k]), np.isnan(ref))
     np.testing.assert_allclose(infos[:, :k], ref, rtol=2e-3, atol=1e-4, equal_nan=True)
     # parameters after the trajectory
-    n_upd = n_steps
-    tol = 2 * 3e-4 * n_upd + 1e-4
+    tol = 2 * 3e-4 * n_steps + 1e-4
+    within = total = 0
     for key in g:
         if not key.startswith("out_") or key == "out_log_alpha":
             continue
         net, rest = key[4:].split(".", 1)
-        if rest.endswith(":digest"):
+        if rest.endswith(":digest"):  # full size: 64 sampled elements per tensor, pooled
             pname = rest[: -len(":digest")]
             v = eng.get_param(net, pname)
             base = key[: -len(":digest")]
-            np.testing.assert_allclose(v[g[base + ":pos"]], g[base + ":vals"], rtol=0, atol=tol)
+            w, n = assert_params_close(v[g[base + ":pos"]], g[base + ":vals"], tol, key, bulk=0.0)
+            within, total = within + w, total + n
         elif ":" not in rest:
-            v = eng.get_param(net, rest, g[key].shape)
-            d = np.abs(v - g[key])
-            assert d.max() <= tol, (key, d.max())
-            assert (d <= 1e-5).mean() >= 0.99, (key, (d <= 1e-5).mean())
+            assert_params_close(eng.get_param(net, rest, g[key].shape), g[key], tol, key, bulk=0.99)
+    if total:
+        assert within / total >= BULK, (name, within / total)
+    if "out_log_alpha" in g:  # SAC temperature (sac.py:55-60, 271-284)
+        np.testing.assert_allclose(eng.get_param("tmp", "log_alpha"), g["out_log_alpha"].reshape(-1),
+                                   rtol=1e-5, atol=1e-7)
 
 
 def _synthetic_golden(alg, env, H, B, ncap, n_fill, n_steps, use_lap, seed):
@@ -191,8 +208,7 @@ def test_td7_humanoid_b1024_matches_oracle():
     tol = 2 * 3e-4 * n_steps + 1e-4
     for net, d in orc.nets().items():
         for name, v in d.items():
-            got = eng.get_param(net, name, tuple(v.shape))
-            assert np.abs(got - v.detach().numpy()).max() <= tol, (net, name)
+            assert_params_close(eng.get_param(net, name, tuple(v.shape)), v.detach().numpy(), tol, (net, name))
 
 
 @pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny"])
@@ -302,5 +318,4 @@ def test_multistep_burst_matches_oracle(alg, env, n):
     tol = 2 * 3e-4 * n_steps + 1e-4
     for net, d in orc.nets().items():
         for name, v in d.items():
-            got = eng.get_param(net, name, tuple(v.shape))
-            assert np.abs(got - v.detach().numpy()).max() <= tol, (net, name)
+            assert_params_close(eng.get_param(net, name, tuple(v.shape)), v.detach().numpy(), tol, (net, name))

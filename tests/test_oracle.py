@@ -77,7 +77,41 @@ def build_from_golden(g):
 
 
 TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny"]
-FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid"]
+FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k"]
+
+
+def golden_moments(g, t):
+    """{key: (positions or None, values)} of the reference's Adam moments after step t."""
+    out = {}
+    pre = f"adam{t}_"
+    for k in g:
+        if not k.startswith(pre) or k.endswith(":digest") or k.endswith(":pos"):
+            continue
+        if k.endswith(":vals"):
+            key = k[len(pre):-len(":vals")]
+            out[key] = (g[pre + key + ":pos"], g[k])
+        else:
+            out[k[len(pre):]] = (None, g[k])
+    return out
+
+
+def expected_priorities(g, ncap, t_last):
+    """Full priority vector after step t_last from a golden that stores only the rows each step
+    wrote (prioi_t = priority[ind_t] after step t; other rows keep their values, lap.py:66-69)."""
+    H, B, Ncap, n_fill, n_steps, use_lap, seed = (int(x) for x in g["meta"])
+    p = spec.init_priorities(Ncap, seed + 2)
+    p[n_fill:] = 0.0
+    for t in range(t_last + 1):
+        p[g["ind"][t]] = g[f"prioi_{t}"]
+    return p[:ncap]
+
+
+def assert_moments_close(got, ref, what, rtol=1e-4):
+    """|d| <= rtol |ref| + rtol * max|ref| of the tensor (m, v of one parameter)."""
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    scale = max(np.abs(ref).max(), 1e-30)
+    d = np.abs(got - ref)
+    assert (d <= rtol * np.abs(ref) + rtol * scale).all(), (what, d.max(), scale)
 
 
 @pytest.mark.parametrize("name", TINY + FULL)
@@ -95,6 +129,16 @@ def test_oracle_matches_reference(name):
         _close(got, g["info"][t], rtol=1e-5, atol=1e-6)
         if f"prio_{t}" in g:
             _close(rep.priority, g[f"prio_{t}"], rtol=1e-6, atol=0)
+        if f"prioi_{t}" in g:
+            _close(rep.priority, expected_priorities(g, rep.priority.size, t), rtol=1e-6, atol=0)
+            assert rep.max_priority == pytest.approx(float(g[f"maxprio_{t}"]), rel=1e-6)
+        ref_m = golden_moments(g, t)
+        if ref_m:
+            mom = agents.moments(orc)
+            assert set(ref_m) == set(mom), sorted(set(ref_m) ^ set(mom))
+            for key, (pos, vals) in ref_m.items():
+                got = mom[key].ravel() if pos is None else mom[key].ravel()[pos]
+                assert_moments_close(got, np.ravel(vals), (t, key), rtol=1e-5)
         if f"vbounds_{t}" in g:
             _close([orc.value_max, orc.value_min, orc.vt_max, orc.vt_min], g[f"vbounds_{t}"])
     nets = orc.nets()
