@@ -7,9 +7,11 @@ every 250 steps.  Synthetic replay: s, s' ~ N(0,1), a ~ U(-1,1)
 r ~ N(0,1), notdone ~ Bernoulli(0.99), priorities 1.0; random-init weights of the
 reference architecture (nn.Linear default init family).
 
-Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`` runs one
-independent seed per GPU (replicas; no collective on the data path); a gloo
-group is used only for the start barrier and the max-over-ranks timing.
+Multi-GPU: ``python bench.py --gpus N`` starts N fresh rank processes itself (one per GPU,
+before the parent touches any GPU); ``python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N`` does the same through the launcher.  Each rank runs one independent seed
+(replicas; no collective on the data path); a gloo group is used only for the
+start barrier and the max-over-ranks timing.
 
 Prints ONE JSON line on rank 0.
 """
@@ -128,9 +130,36 @@ def cpu_baseline(seconds=12.0, algo="td7", env="Humanoid-v4", batch=B, lap=True)
         one()
         n += 1
     dt = time.perf_counter() - t0
+    hc = host_cpu()
     return {"value": round(n / dt, 3), "unit": "gradient-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n} {algo.upper()} {env} B={batch} steps ({'LAP' if lap else 'uniform'} over a 1M replay) "
-                      f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads}"}
+                      f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads}",
+            "host": hc}
+
+
+def host_cpu():
+    """CPU model, sockets and logical CPUs of this host (/proc/cpuinfo), and the CPUs this
+    process may run on."""
+    model, sockets, logical = "unknown", set(), 0
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model == "unknown":
+                    model = v
+                elif k == "physical id":
+                    sockets.add(v)
+                elif k == "processor":
+                    logical += 1
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = os.cpu_count() or 0
+    return {"cpu_model": model, "sockets": max(1, len(sockets)), "logical_cpus": logical,
+            "cpus_allowed": allowed}
 
 
 def max_over_ranks(vals, dist=None):
@@ -278,6 +307,51 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, chunk=25):
         dist.barrier()
 
 
+def launch_ranks(n, argv, device_count):
+    """``--gpus N`` without a launcher (WORLD_SIZE unset): start N fresh rank processes of this
+    script, one per GPU, each with RANK / LOCAL_RANK / WORLD_SIZE and a local rendezvous.  The
+    parent has not initialised any GPU (it only counted devices); ranks inherit stdout, so rank
+    0's JSON line is the output.  Returns the first failing rank's exit code, else 0."""
+    import socket
+    import subprocess
+
+    visible = device_count()
+    if n > visible:
+        raise SystemExit(f"bench.py: --gpus {n} but only {visible} GPU(s) visible")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:  # the others would wait at the barrier forever
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def _stub_engine_module(path):
+    """Test hook (tests/test_host.py): RLE_BENCH_STUB=<file> replaces the engine module by a
+    CPU stub so the rank launcher and the JSON line can be tested without a GPU."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("rle_bench_stub", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -294,8 +368,19 @@ def main():
     if (args.algo, args.env, args.batch) not in WORK:
         ap.error(f"no SURVEY §8(d) work figures for {args.algo} {args.env} B={args.batch}")
     lap = args.algo == "td7"  # TD7 runs LAP (td7_exp.sh); SAC / TD3 the uniform replay
+    stub = _stub_engine_module(os.environ["RLE_BENCH_STUB"]) if os.environ.get("RLE_BENCH_STUB") else None
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if stub:
+            count = stub.device_count
+        else:
+            import torch
+
+            count = torch.cuda.device_count  # counts devices without initialising them
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], count))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -303,10 +388,15 @@ def main():
         import torch.distributed as dist  # gloo: start barrier + timing reduction only
         dist.init_process_group("gloo")
 
-    import torch
+    if stub:
+        E, init_agent, cuda_sync = stub, stub.init_agent, stub.synchronize
+    else:
+        import torch
 
-    from rl import _engine as E
-    from rl.nn.layout import init_agent
+        from rl import _engine as E
+        from rl.nn.layout import init_agent
+
+        cuda_sync = torch.cuda.synchronize
 
     # --- engine: one independent seed per GPU (seed 111, 222, ... as scripts/td7_exp.sh)
     s_dim, a_dim, _ = TASKS[args.env]
@@ -327,11 +417,11 @@ def main():
     eng.step_timed(args.warmup)
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(local)
+    cuda_sync(local)
     n_l0 = eng.launch_count()
     t0 = time.perf_counter()
     gpu_ms = eng.step_timed(args.steps)
-    torch.cuda.synchronize(local)
+    cuda_sync(local)
     t1 = time.perf_counter()
     launches = (eng.launch_count() - n_l0) / args.steps
     wall = t1 - t0

@@ -129,6 +129,32 @@ def test_bench_max_over_ranks_gloo_world2(tmp_path):
     assert value == 2 * 100 / 2.0
 
 
+def test_bench_gpus_n_launches_its_own_ranks():
+    """``bench.py --gpus 2`` with no launcher (how the driver runs ``--gpus 1``): the script
+    starts two rank processes itself (gloo rendezvous on 127.0.0.1) and rank 0 prints one
+    JSON line with n_gpus 2.  The engine is a CPU stub (tests/bench_stub.py)."""
+    env = dict(os.environ, RLE_BENCH_STUB=os.path.join(REPO, "tests", "bench_stub.py"))
+    env.pop("WORLD_SIZE", None)
+    res = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "40",
+                          "--warmup", "2", "--no-cpu-baseline"], capture_output=True, text=True, timeout=240,
+                         env=env)
+    assert res.returncode == 0, res.stderr[-2000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 40 and out["scaling"] == "weak"
+    assert out["value"] > 0
+
+
+def test_bench_gpus_more_than_visible_fails():
+    env = dict(os.environ, RLE_BENCH_STUB=os.path.join(REPO, "tests", "bench_stub.py"))
+    env.pop("WORLD_SIZE", None)
+    res = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "9", "--steps", "4",
+                          "--warmup", "1", "--no-cpu-baseline"], capture_output=True, text=True, timeout=120,
+                         env=env)
+    assert res.returncode != 0 and "only 8 GPU(s) visible" in res.stderr
+
+
 def test_sac_lap_fails_like_the_reference():
     # sac.py:202 calls an undefined _lap_huber (SURVEY Q13): train_ops raises before any engine call
     sac = SAC.__new__(SAC)

@@ -18,7 +18,7 @@ from oracle import agents as OA
 from oracle import replay as OR
 from rl.agent import SAC, TD3, TD7
 from rl.replay_memory import LAPReplayMemory, SimpleReplayMemory
-from rl.runner import run_train_ops
+from rl.runner.run import run_train_ops
 from rl.utils import register_env
 
 pytestmark = pytest.mark.gpu
