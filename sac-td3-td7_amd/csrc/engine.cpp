@@ -203,6 +203,8 @@ static void check_gemm(const GemmArgs& g) {
   REQUIRE(g.R <= 16 * 1024, "gemm: reduction too long");
 }
 
+static void xcd_plan(GemmArgs& g);
+
 // Device-side dispatch fields of a GEMM op: compiled variant, split count, tile-row
 // reciprocal (kernels.hip gemm_v).
 static void gemm_finalize(GemmArgs& g) {
@@ -246,6 +248,50 @@ static void gemm_finalize(GemmArgs& g) {
   h.a0p = g.A.seg[0].p;
   h.b0p = g.B.seg[0].p;
   h.bias = g.epi == EPI_ADAM ? nullptr : g.bias;
+  h.tiles = g.tiles_m * g.tiles_n;
+  xcd_plan(g);
+}
+
+// XCD-aware tile order of a GEMM (GemmHot::xb): each of the 8 XCDs takes ~tiles/8 tiles as
+// a band-ordered run.  Band width b (in tiles) minimises the operand blocks one XCD reads:
+// ceil(share / b) A row-blocks of 16 rows plus b B column-blocks of tn columns (both x R).
+// RLE_XCD=0 keeps the plain row-major tile order.
+static void xcd_plan(GemmArgs& g) {
+  GemmHot& h = g.hot;
+  h.xb = 0;
+  const char* e = std::getenv("RLE_XCD");
+  if (e && e[0] == '0') return;
+  const int T = g.tiles_m * g.tiles_n;
+  if (T < 16 || g.tiles_n < 2) return;
+  const int share = (T + 7) / 8;
+  int best = g.tiles_n;
+  long long bc = -1;
+  for (int b = 1; b <= g.tiles_n; ++b) {
+    const long long rows = std::min<long long>(g.tiles_m, (share + b - 1) / b + 1);  // a run may straddle a row
+    const long long cost = rows * 16 + (long long)std::min(b, share) * g.tn;
+    if (bc < 0 || cost < bc) {
+      bc = cost;
+      best = b;
+    }
+  }
+  h.xb = best;
+  h.tmb = g.tiles_m * best;
+  h.nfull = g.tiles_n / best;
+  h.inv_tmb = 1.f / (float)h.tmb;
+  h.inv_xb = 1.f / (float)best;
+  const int blast = g.tiles_n - h.nfull * best;
+  h.inv_blast = blast ? 1.f / (float)blast : 0.f;
+  std::vector<char> seen((size_t)T, 0);  // the order must be a permutation of the tiles
+  for (int t = 0; t < T; ++t) {
+    int it, jt;
+    xcd_tile(t, T, g.tiles_n, h.xb, h.tmb, h.nfull, h.inv_tmb, h.inv_xb, h.inv_blast, it, jt);
+    const bool ok = it >= 0 && it < g.tiles_m && jt >= 0 && jt < g.tiles_n && !seen[(size_t)it * g.tiles_n + jt];
+    if (!ok) {
+      h.xb = 0;
+      return;
+    }
+    seen[(size_t)it * g.tiles_n + jt] = 1;
+  }
 }
 
 struct Prog {

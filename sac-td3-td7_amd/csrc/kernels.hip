@@ -596,11 +596,10 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   // ---- every descriptor field the prologue and the first operand segment need (GemmHot)
   // in ONE batch of scalar loads.  Left to the compiler, each load is issued next to its
   // use, behind branches: one dependent round trip each, ~6 before the first operand load.
-  u32x16 h0;
-  u32x4 h1;
+  u32x16 h0, h1;
   asm volatile(
       "s_load_dwordx16 %0, %2, 0x0\n\t"
-      "s_load_dwordx4 %1, %2, 0x40\n\t"
+      "s_load_dwordx16 %1, %2, 0x40\n\t"
       "s_waitcnt lgkmcnt(0)"
       : "=s"(h0), "=s"(h1)
       : "s"(&g.hot));
@@ -613,8 +612,14 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   const float* b0p = ptr(h1[0], h1[1]);
   const float* biasp = ptr(h1[2], h1[3]);
   const int cg = wave >> ksl, kp = wave & ((1 << ksl) - 1);
-  const int it = (int)(((float)t + 0.5f) * inv_tn);
-  const int jt = t - it * tiles_n;
+  int it, jt;
+  if (h1[4]) {  // XCD-aware order (GemmHot::xb): residue class t % 8 -> a contiguous run p
+    xcd_tile(t, (int)h0[13], tiles_n, (int)h1[4], (int)h1[5], (int)h1[9], __uint_as_float(h1[6]),
+             __uint_as_float(h1[7]), __uint_as_float(h1[8]), it, jt);
+  } else {
+    it = (int)(((float)t + 0.5f) * inv_tn);
+    jt = t - it * tiles_n;
+  }
   const int i0 = it << 4, j0 = jt * tn + (cg << 4);
   const bool bias_tile = EPI == EPI_ADAM && jt * tn >= bias_col;
   const bool lead = kp == 0;

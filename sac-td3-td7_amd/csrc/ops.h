@@ -127,12 +127,35 @@ struct GemmHot {
   int ks_log, tiles_n, tn, N, R;
   float inv_tiles_n;
   int bias_col, nseg_a, nseg_b;
-  int a0xs, a0r0, a0r1, b0xs, pad_;
+  int a0xs, a0r0, a0r1, b0xs, tiles;  // tiles = tiles_m * tiles_n
   const float* a0p;
   const float* b0p;
   const float* bias;
+  // XCD-aware tile order (xb > 0): workgroups t with equal t % 8 run on one XCD (round-robin
+  // dispatch); each such residue class takes a contiguous run of tiles in a banded order
+  // (bands of xb tile columns, rows inside a band, columns inside a row), i.e. a compact
+  // rectangle, so an XCD reads few distinct A row-blocks and B column-blocks.
+  int xb, tmb;                    // band width in tiles, tiles per full band (tiles_m * xb)
+  float inv_tmb, inv_xb, inv_blast;
+  int nfull;                      // full bands; the last band is tiles_n - nfull * xb wide
+  int pad_[6];
 };
-static_assert(sizeof(GemmHot) == 80, "GemmHot is loaded as 16 + 4 dwords");
+static_assert(sizeof(GemmHot) == 128, "GemmHot is loaded as 2 x 16 dwords");
+
+// Tile (it, jt) of workgroup t of a GEMM under the XCD-aware order (GemmHot::xb > 0); the same
+// code runs in the kernel (scalar registers) and in the host planner, which checks that it
+// is a bijection before enabling it.
+__host__ __device__ inline void xcd_tile(int t, int T, int tiles_n, int xb, int tmb, int nfull, float inv_tmb,
+                                         float inv_xb, float inv_blast, int& it, int& jt) {
+  const int q = T >> 3, m = T & 7, r0 = t & 7;
+  const int p = r0 * q + (r0 < m ? r0 : m) + (t >> 3);
+  const int band = (int)(((float)p + 0.5f) * inv_tmb);
+  const int rem = p - band * tmb;
+  const bool full = band < nfull;
+  const int bw = full ? xb : tiles_n - nfull * xb;
+  it = (int)(((float)rem + 0.5f) * (full ? inv_xb : inv_blast));
+  jt = band * xb + rem - it * bw;
+}
 
 // The actor's output layer (rl/nn/sale.py:77-83 / mlp.py:55-68, N = act_dim <= 32) recomputed
 // by a consuming GEMM for its own 16 rows into an LDS fragment block, so the consumer does not
@@ -152,7 +175,7 @@ struct PreArgs {
 };
 
 struct GemmArgs {
-  GemmHot hot;           // (first: one s_load_dwordx16 + one s_load_dwordx4)
+  GemmHot hot;           // (first: two s_load_dwordx16)
   int mode;              // GemmMode (operand layouts; every segment of an operand shares it)
   int M, N, R;           // output rows, output cols (x-extent of B), reduction length
   int tn;                // tile width: 16 x tn output tile; the 4 waves are tn/16 column groups
