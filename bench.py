@@ -173,17 +173,66 @@ def max_over_ranks(vals, dist=None):
     return [float(v) for v in t]
 
 
-def pmc_traffic():
-    """HBM bytes per rle_level launch from the committed PMC summary of the same command
-    (tools/pmc.sh + tools/pmc_summary.py --json): 2 x FETCH_SIZE (gfx950 reports half of
-    wide coalesced reads, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, both in KB.  None when
-    no summary is committed."""
-    path = os.path.join(REPO, "profiles", "r01_pmc.json")
-    if not os.path.exists(path):
-        return None
+def _latest_profile(name):
+    """Newest committed profiles/rNN_<name> (the round's own evidence), or None."""
+    import glob
+
+    c = sorted(glob.glob(os.path.join(REPO, "profiles", f"r[0-9][0-9]_{name}")))
+    return c[-1] if c else None
+
+
+def pmc_evidence():
+    """Counters of the dominant kernel from the committed PMC summary of the same command
+    (tools/pmc.sh + tools/pmc_summary.py --json; mean per rle_level dispatch of a
+    `bench.py --steps 200` run), NOT measured in this process:
+    * traffic: HBM bytes per launch = 2 x FETCH_SIZE (gfx950 reports half of wide coalesced
+      reads, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, both in KB;
+    * mfma_busy: SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x shader cycles), shader cycles =
+      GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs; it reads high on dispatches this short,
+      MI355X_MICROARCH.md 'DVFS', so this fraction is a lower bound; summarize() adds the same
+      cycles over the measured launch time)."""
+    path = _latest_profile("pmc.json")
+    if path is None:
+        return {"traffic": None}
     with open(path) as f:
         pmc = json.load(f)
-    return round((2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0)
+    out = {"traffic": round((2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0),
+           "traffic_source": f"profiles/{os.path.basename(path)} (rocprofv3 --pmc, mean per rle_level dispatch)"}
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in pmc and "GRBM_GUI_ACTIVE" in pmc:
+        cycles = pmc["GRBM_GUI_ACTIVE"] / 8.0
+        out["mfma_busy"] = round(pmc["SQ_VALU_MFMA_BUSY_CYCLES"] / (cycles * 256 * 4), 5)
+        out["mfma_busy_source"] = out["traffic_source"]
+    return out
+
+
+def _pmc_value(key):
+    path = _latest_profile("pmc.json")
+    if path is None:
+        return None
+    with open(path) as f:
+        return json.load(f).get(key)
+
+
+def gather_evidence(s_dim, a_dim, batch, n_replay, lap):
+    """Achieved GB/s of the replay sampler op (OP_SAMPLE_GATHER: index search + row gather)
+    from the committed level trace (tools/trace_levels.py --json: mean op span from in-kernel
+    s_memrealtime stamps).  Bytes per launch: the rows read and written into the batch images,
+    B x [(2 S + A + 2) x 4 x 2 + 8 index], plus the LAP search reads, B x (4096 x 4 block +
+    8 x block sums)."""
+    path = _latest_profile("level_trace.json")
+    if path is None:
+        return {}
+    with open(path) as f:
+        tr = json.load(f)
+    if "sgather_all" not in tr:
+        return {}
+    sp = (s_dim + 15) // 16 * 16
+    ap = (a_dim + 15) // 16 * 16
+    rows = batch * ((2 * sp + ap + 2) * 4 * 2 + 8)
+    search = batch * (4096 * 4 + 8 * math.ceil(n_replay / 4096)) if lap else 0
+    us = tr["sgather_all"]["mean_us"]
+    return {"gather_GBs": round((rows + search) / (us * 1e-6) / 1e9, 2), "gather_bytes": rows + search,
+            "gather_us": round(us, 3), "gather_source": f"profiles/{os.path.basename(path)}"}
 
 
 def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7", env="Humanoid-v4",
@@ -211,7 +260,7 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
         "peak": PEAK_FP32_TFLOPS,
         "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_FP32_TFLOPS, 5),
-        "traffic": pmc_traffic() if headline else None,
+        **(pmc_evidence() if headline else {"traffic": None}),
         "traffic_algorithmic": round(bytes_step / launches),
         "kernel": "rle_level (one launch per dependency level of the step graph)",
         "flop_per_step": flop_step,
@@ -220,6 +269,11 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
         "hbm_bytes_per_step_algorithmic": round(bytes_step),
         "hbm_achieved_GBs": round(bytes_step * steps / gpu_s / 1e9, 2),
     }
+    if headline:
+        roofline.update(gather_evidence(s_dim, a_dim, batch, N_REPLAY, lap))
+        busy = _pmc_value("SQ_VALU_MFMA_BUSY_CYCLES")
+        if busy is not None:  # the same counter over this run's measured launch duration, 2.4 GHz
+            roofline["mfma_busy_vs_launch_time"] = round(busy / (1024 * 2.4e9 * per_launch_s), 5)
     metric = METRIC if headline else (f"gradient-steps/sec, {algo.upper()} {env} batch={batch}"
                                       f"{' LAP' if lap else ''} (secondary config)")
     return {

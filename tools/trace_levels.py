@@ -29,6 +29,8 @@ eng.bind(rep)
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 eng.step_timed(steps)
 graphs = [int(w) for w in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 3]
+JSON = sys.argv[3] if len(sys.argv) > 3 else None  # per-op-kind spans (bench.py reads the sampler's)
+opspans = {}
 for which in graphs:
     tr = eng.trace(which).astype(np.int64)
     if tr.size == 0:
@@ -55,6 +57,12 @@ for which in graphs:
         tot = (t[:, 3] - t[:, 0]) * 10 / 1000
         print(f"gap {gap:5.2f} span {span:6.2f} | disp max {disp.max():5.2f} | wg med {np.median(tot):5.2f} max {tot.max():5.2f}"
               f" | pro {np.median(pro):5.2f} loop {np.median(loop):5.2f} epi {np.median(epi):5.2f} | {line[:90]}")
+        if JSON:  # every op's span (first entry -> last exit), all levels
+            o = 0
+            for name, w in re.findall(r"([a-z]+(?:\[[^\]]*\])?)/(\d+)", line.split(":", 1)[1]):
+                tt = t[o:o + int(w)]
+                o += int(w)
+                opspans.setdefault(name.split("[")[0] + "_all", []).append(float((tt[:, 3].max() - tt[:, 0].min()) * 10 / 1000))
         if os.environ.get("RLE_DESC_WG") and span > 6.0:  # per-op longest workgroup
             o = 0
             parts = []
@@ -77,3 +85,9 @@ for which in graphs:
                 print(f"      gemm: decode {med(0, 11):5.2f} desc {med(11, 12):5.2f} prefetch {med(12, 1):5.2f}"
                       f" | loop {med(1, 2):5.2f} | splitK {med(2, 13):5.2f} epi {med(13, 3):5.2f}")
     print(f"total (gaps + spans) {tot_t:7.2f} us over {len(desc)} levels")
+if JSON:
+    import json
+
+    out = {k: {"n": len(v), "mean_us": float(np.mean(v)), "max_us": float(np.max(v))} for k, v in sorted(opspans.items())}
+    out["_note"] = "op spans (first workgroup entry -> last exit, us) from RLE_TRACE in-kernel stamps, graphs " + str(graphs)
+    json.dump(out, open(JSON, "w"), indent=1)
