@@ -70,12 +70,19 @@ static float host_unkey(int k) {
   return f;
 }
 
+// Live device allocations (address -> bytes) for the RLE_AUDIT=1 operand-range check.
+static std::map<uintptr_t, size_t>& live_allocs() {
+  static std::map<uintptr_t, size_t> m;
+  return m;
+}
+
 struct DevMem {
   std::vector<void*> ptrs;
   void* alloc(size_t bytes) {
     void* p = nullptr;
     if (bytes == 0) bytes = 16;
     HIPCHK(hipMalloc(&p, bytes));
+    live_allocs()[(uintptr_t)p] = bytes;
     HIPCHK(hipMemset(p, 0, bytes));
     // hipMemset runs on the null stream, which does not order against our
     // non-blocking streams: finish it before any stream touches the buffer.
@@ -88,7 +95,10 @@ struct DevMem {
     return reinterpret_cast<T*>(alloc(n * sizeof(T)));
   }
   ~DevMem() {
-    for (void* p : ptrs) (void)hipFree(p);
+    for (void* p : ptrs) {
+      live_allocs().erase((uintptr_t)p);
+      (void)hipFree(p);
+    }
   }
 };
 
@@ -294,6 +304,181 @@ static void xcd_plan(GemmArgs& g) {
   }
 }
 
+
+// ---- RLE_AUDIT=1: every byte range a GEMM op's workgroups can touch (the address arithmetic of
+// kernels.hip gemm_v / pre_issue / pre_finish, replayed on the host) must lie inside one live
+// device allocation.  A debugging aid for new tile layouts; off in production.
+static void audit_range(const void* base, long long lo, long long bytes, const char* what, const GemmArgs& g) {
+  if (bytes <= 0) return;
+  const uintptr_t a = (uintptr_t)base + (uintptr_t)lo, b = a + (uintptr_t)bytes;
+  auto& m = live_allocs();
+  auto it = m.upper_bound(a);
+  bool ok = base != nullptr && lo >= 0 && it != m.begin();
+  if (ok) {
+    --it;
+    ok = a >= it->first && b <= it->first + it->second;
+  }
+  if (!ok) {
+    char msg[256];
+    snprintf(msg, sizeof msg, "audit: %s [%lld, +%lld) outside its allocation (gemm mode %d epi %d M %d N %d R %d tn %d)",
+             what, lo, bytes, g.mode, g.epi, g.M, g.N, g.R, g.tn);
+    throw Error{RLE_EINVAL, msg};
+  }
+}
+
+static long long h_nblk(int cbn, int r, int c) { return ((long long)(r >> 4) * cbn + (c >> 4)) * 1024; }  // bytes
+static long long h_tblk(int rbs, int r, int c) { return ((long long)(c >> 4) * rbs + (r >> 4)) * 1024; }
+
+static void audit_mat(const Mat& m, int r, int c, const char* what, const GemmArgs& g, bool need_n = false,
+                      bool need_t = false) {
+  if (m.n) audit_range(m.n, h_nblk(m.cbn, r, c), 1024, what, g);
+  if (m.t) audit_range(m.t, h_tblk(m.rbs, r, c), 1024, what, g);
+  if (need_n && !m.n) throw Error{RLE_EINVAL, std::string("audit: no N image for ") + what};
+  if (need_t && !m.t) throw Error{RLE_EINVAL, std::string("audit: no T image for ") + what};
+}
+
+static void audit_norm(const NormRef& nr, int row, int nrows, const GemmArgs& g) {
+  if (!nr.part) return;
+  for (int p = 0; p < nr.nparts; ++p)
+    audit_range(nr.part, ((long long)p * nr.ld + nr.row0 + row) * 4, (long long)nrows * 4, "norm partials", g);
+}
+
+static void audit_gemm(const GemmArgs& g) {
+  const GemmHot& h = g.hot;
+  // wave w of a 16 x tn tile: column group w >> ks_log, reduction split w & (2^ks_log - 1)
+  const int NB = g.tn / 16, T = g.tiles_m * g.tiles_n, ks = 1 << g.ks_log;
+  const int nch = g.R / 16, per = (nch + ks - 1) / ks;
+  for (int t = 0; t < T; ++t) {
+    int it, jt;
+    if (h.xb) xcd_tile(t, h.tiles, h.tiles_n, h.xb, h.tmb, h.nfull, h.inv_tmb, h.inv_xb, h.inv_blast, it, jt);
+    else {
+      it = (int)(((float)t + 0.5f) * g.inv_tiles_n);
+      jt = t - it * g.tiles_n;
+    }
+    const int i0 = it * 16, jt0 = jt * g.tn;
+    const int bias_col = g.epi == EPI_ADAM ? g.adam.bias_col : 0;
+    const bool bias_tile = g.epi == EPI_ADAM && jt0 >= bias_col;
+    bool on[4];
+    for (int cb = 0; cb < NB; ++cb) on[cb] = bias_tile ? cb == 0 : jt0 + cb * 16 < g.N;
+    for (int w = 0; w < 4; ++w) {
+      const int cgw = w >> g.ks_log;
+      const int c0 = (w & (ks - 1)) * per, c1 = std::min(nch, c0 + per);
+      bool mine[4] = {false, false, false, false};  // the wave's column block
+      if (cgw < NB) mine[cgw] = on[cgw];
+      if (g.mode != GEMM_DW) {
+        const bool wabs = g.mode == GEMM_FWD && g.B.nseg == 1;
+        for (int q = 0; q < g.A.nseg; ++q) {
+          const Seg& sa = g.A.seg[q];
+          const Seg& sb = g.B.seg[wabs ? 0 : q];
+          const int s0 = sa.r0 / 16, k0 = std::max(c0, s0), k1 = std::min(c1, (sa.r1 + 15) / 16);
+          if (k0 >= k1) continue;
+          const int kb = wabs ? k0 : k0 - s0;
+          if (!mine[0] && !mine[1] && !mine[2] && !mine[3]) continue;  // inactive wave: no loads
+          if (!(g.has_pre && q == g.prea.seg)) {
+            audit_range(sa.p, ((long long)(i0 / 16) * sa.xs + (k0 - s0)) * 1024, (long long)(k1 - k0) * 1024, "A", g);
+            if (sa.norm.part) audit_norm(sa.norm, i0, 16, g);
+          }
+          for (int cb = 0; cb < NB; ++cb)
+            if (mine[cb])
+              audit_range(sb.p, ((long long)(jt0 / 16 + cb) * sb.xs + kb) * 1024, (long long)(k1 - k0) * 1024, "B", g);
+        }
+        if (g.has_pre) {  // pre-GEMM operands (pre_issue / pre_finish): 16 rows at i0, both column blocks
+          const PreArgs& p = g.prea;
+          const int nchp = p.R / 16, perp = (nchp + 3) / 4;
+          const int c0p = w * perp, c1p = std::min(nchp, c0p + perp);
+          const bool wp = p.mode == GEMM_FWD && p.B.nseg == 1;
+          for (int q = 0; q < p.A.nseg; ++q) {
+            const Seg& sa = p.A.seg[q];
+            const Seg& sb = p.B.seg[wp ? 0 : q];
+            const int s0 = sa.r0 / 16, k0 = std::max(c0p, s0), k1 = std::min(c1p, (sa.r1 + 15) / 16);
+            if (k0 >= k1) continue;
+            const int kb = wp ? k0 : k0 - s0;
+            audit_range(sa.p, ((long long)(i0 / 16) * sa.xs + (k0 - s0)) * 1024, (long long)(k1 - k0) * 1024, "pre A", g);
+            audit_range(sb.p, (long long)kb * 1024, (long long)(k1 - k0) * 1024, "pre B", g);
+            if (p.N > 16) audit_range(sb.p, ((long long)sb.xs + kb) * 1024, (long long)(k1 - k0) * 1024, "pre B1", g);
+          }
+          if (w == 0) {
+            for (int cb = 0; cb < 2 && cb * 16 < p.N; ++cb) {
+              if (p.mode == GEMM_FWD) {
+                if (p.bias) audit_range(p.bias, cb * 64, (long long)std::min(16, p.N - cb * 16) * 4, "pre bias", g);
+                if (p.noise.t) audit_range(p.noise.t, h_tblk(p.noise.rbs, i0, cb * 16), 1024, "pre noise", g);
+              } else {
+                audit_range(p.dsrc.t, h_tblk(p.dsrc.rbs, i0, cb * 16), 1024, "pre dsrc", g);
+              }
+            }
+          }
+        }
+      } else {
+        const int nrun = c1 > c0 ? c1 - c0 : 0;
+        if (!nrun || !(mine[0] || mine[1] || mine[2] || mine[3])) continue;
+        audit_range(h.a0p, ((long long)(i0 / 16) * h.a0xs + c0) * 1024, (long long)nrun * 1024, "DW A", g);
+        if (g.act == kDwNb || (g.nbx.t && g.nbm.part))
+          audit_range(g.nbx.t, ((long long)(i0 / 16) * g.nbx_xs + c0) * 1024, (long long)nrun * 1024, "DW x", g);
+        if (bias_tile) continue;
+        for (int cb = 0; cb < NB; ++cb) {
+          if (!mine[cb]) continue;
+          const int xq = jt0 + cb * 16;
+          int qb = 0;
+          for (int q = 1; q < g.B.nseg; ++q)
+            if (xq >= g.B.seg[q].x0) qb = q;
+          const Seg& sb = g.B.seg[qb];
+          audit_range(sb.p, ((long long)((xq - sb.x0) / 16) * sb.xs + c0) * 1024, (long long)nrun * 1024, "DW B", g);
+        }
+      }
+    }
+    if (g.mode == GEMM_DW)
+      for (int q = 0; q < g.B.nseg; ++q)
+        if (g.B.seg[q].norm.part) audit_norm(g.B.seg[q].norm, 0, g.B.seg[q].r1 - g.B.seg[q].r0, g);
+    // epilogue: column block w of the tile, rows i0..i0+15
+    for (int w = 0; w < NB; ++w) {
+      const int j0 = jt0 + w * 16;
+      const bool active = bias_tile ? w == 0 : j0 < g.N;
+      if (!active) continue;
+      const int ncol = bias_tile ? 1 : std::min(16, g.N - j0);
+      switch (g.epi) {
+        case EPI_ADAM: {
+          const AdamArgs& ad = g.adam;
+          if (bias_tile) {
+            for (long long o : {0LL, ad.mo, ad.vo}) audit_range(ad.b, (o + i0) * 4, 64, "adam bias", g);
+          } else {
+            for (long long o : {0LL, ad.mo, ad.vo})
+              audit_range(ad.w.t, o * 4 + h_tblk(ad.w.rbs, i0, j0), 1024, "adam w.t", g);
+            audit_range(ad.w.n, h_nblk(ad.w.cbn, i0, j0), 1024, "adam w.n", g);
+          }
+          if (ad.gsq) {
+            if (bias_tile) audit_range(ad.gsq_b, (long long)it * 4, 4, "gsq_b", g);
+            else audit_range(ad.gsq, ((long long)it * (g.tiles_n - 1) + jt) * 4, 4, "gsq", g);
+          }
+          break;
+        }
+        default: {
+          audit_mat(g.out, i0, j0, "out", g);
+          if (g.bias) audit_range(g.bias, (long long)j0 * 4, (long long)ncol * 4, "bias", g);
+          if (g.mode == GEMM_FWD && g.pre.t) audit_mat(g.pre, i0, j0, "pre-act", g);
+          if (g.mode == GEMM_DX && g.dact != ACT_NONE) audit_mat(g.dsrc, i0, j0, "dsrc", g, false, true);
+          if (g.noise.t && i0 + 15 >= g.noise_row0) {
+            const int r0 = std::max(i0, g.noise_row0) - g.noise_row0;
+            audit_range(g.noise.t, h_tblk(g.noise.rbs, r0, j0), 1024, "noise", g);
+            audit_range(g.noise.t, h_tblk(g.noise.rbs, i0 + 15 - g.noise_row0, j0), 1024, "noise", g);
+          }
+          if (g.epi == EPI_NBDOT) audit_mat(g.nbx, i0, j0, "nbx", g, false, true);
+          if (g.epi == EPI_MSE) {
+            audit_mat(g.tgt, i0, j0, "tgt", g, false, true);
+            audit_norm(g.tgt_norm, i0, 16, g);
+          }
+          if (g.epi == EPI_QHEAD) audit_range(g.qw, h_nblk(g.qw_cbn, 0, j0), 1024, "qw", g);
+          if (g.norm_out) audit_range(g.norm_out, ((long long)jt * g.norm_ld + i0) * 4, 64, "norm_out", g);
+          if (g.epi == EPI_MSE || g.epi == EPI_QHEAD) audit_range(g.loss_part, (long long)t * 4, 4, "loss_part", g);
+        }
+      }
+    }
+  }
+  if (g.mode == GEMM_DW && g.act == kDwNb) {
+    audit_norm(g.nbm, 0, g.R, g);
+    for (int p = 0; p < g.nbdot_n; ++p) audit_range(g.nbdot, (long long)p * g.nbdot_ld * 4, (long long)g.R * 4, "nbdot", g);
+  }
+}
+
 struct Prog {
   struct Item {
     std::vector<Op> ops;  // one op, or a group writing disjoint parts of the same buffers
@@ -307,6 +492,8 @@ struct Prog {
       if (op.kind == OP_GEMM) {
         gemm_finalize(op.gemm);
         check_gemm(op.gemm);
+        static const bool audit = std::getenv("RLE_AUDIT") != nullptr;
+        if (audit) audit_gemm(op.gemm);
       }
     Item it;
     it.ops = std::move(ops);
