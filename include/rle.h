@@ -130,9 +130,22 @@ int rle_set_tapes(rle_engine* e, int n_steps, const float* u, const float* eps, 
 int rle_last_indices(rle_engine* e, long long* ind_out);
 /* Agent.sample / _inference_action forward (td7.py:158-162, td3.py:131-135, sac.py:154-159):
  * obs [n][S] (n <= 1024) -> out [n][W]: TD7 tanh actor output (W = A); TD3 actor MLP output
- * before tanh (W = A); SAC raw (mean | log_std) head (W = 2A).  Exploration noise, clipping and
- * scale/bias stay on the host as in the reference. */
+ * before tanh (W = A); SAC raw (mean | log_std) head (W = 2A).  Raw network outputs (evaluation and
+ * diagnostics); rle_act_sample returns the environment action. */
 int rle_act(rle_engine* e, const float* obs, int n, float* out);
+/* Agent.sample (td7.py:141-156, td3.py:114-129, sac.py:132-152) as ONE device program: the B = n
+ * actor (TD7: + fixed encoder) forward, exploration noise, clip and the action map, written by the
+ * last kernel straight into pinned host memory.  obs [n][S] -> out [n][A] environment actions:
+ *   TD7 / TD3: clip(tanh(pi(s)) + exploration_noise * eps, -1, 1) * scale + bias
+ *   SAC:       tanh(mean + exp(clamp(log_std)) * eps) * scale + bias
+ * mode 0: deterministic (eps = 0); 1: eps from the engine's own Philox stream (counter advanced
+ * per call; the reference draws torch.randn_like from torch's global generator instead);
+ * 2: eps given as eps [n][A] (parity tape).  Syncs. */
+int rle_act_sample(rle_engine* e, const float* obs, int n, int mode, const float* eps, float* out);
+/* The environment action map of rle_act_sample: scale [A], bias [A] (get_action_bias_scale,
+ * rl/utils/miscellaneous.py:59-66) and TD7 / TD3 exploration_noise (td7.py:41, td3.py:40).
+ * Default: identity, 0.1. */
+int rle_set_action_map(rle_engine* e, const float* scale, const float* bias, float exploration_noise);
 /* Forward diagnostics on a given batch (host rows s [n][S], a [n][A], n <= 1024), for parity
  * checks of the nets the step trains:
  *   RLE_EVAL_Q:   critic `net`'s estimate_q_value -> out [n].  TD7 (SALECritic, sale.py:106-121)

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
@@ -33,6 +35,7 @@ hipError_t launch_append(float* state, float* next_state, float* action, float* 
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count,
                          int Sp, int Ap, const float* max_priority, int lap, double* bsum,
                          long long size_before, hipStream_t st);
+hipError_t launch_act_chain(const ActChainArgs& a, hipStream_t st);
 hipError_t launch_fill(float* state, float* next_state, float* action, float* reward, float* notdone,
                        float* priority, long long n, int S, int Sp, int A, int Ap, unsigned long long seed,
                        hipStream_t st);
@@ -98,6 +101,26 @@ struct DevMem {
     for (void* p : ptrs) {
       live_allocs().erase((uintptr_t)p);
       (void)hipFree(p);
+    }
+  }
+};
+
+// Pinned host allocations (coherent, mapped into the device's address space): act-call
+// staging and the zero-copy action output.
+struct PinMem {
+  std::vector<void*> ptrs;
+  void* alloc(size_t bytes) {
+    void* p = nullptr;
+    HIPCHK(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(p, 0, bytes);
+    ptrs.push_back(p);
+    live_allocs()[(uintptr_t)p] = bytes;
+    return p;
+  }
+  ~PinMem() {
+    for (void* p : ptrs) {
+      live_allocs().erase((uintptr_t)p);
+      (void)hipHostFree(p);
     }
   }
 };
@@ -740,6 +763,90 @@ struct Engine {
   // act programs (cached per n)
   std::map<int, std::pair<Graph, View>> act_graphs;  // n -> graph, output view
   std::map<int, View> act_inputs;
+  // act-sample programs (rle_act_sample): environment action straight into pinned memory
+  struct ActSample {
+    Graph G;
+    View in;
+    float* img = nullptr;  // pinned staging of the input image (N image, M rows)
+    int* ctl = nullptr;    // pinned: mode, Philox counter lo / hi
+    float* eps = nullptr;  // pinned [n][A] noise tape
+    float* out = nullptr;  // pinned [n][A] actions
+  };
+  std::map<int, ActSample> act_samplers;
+  // B = 1 act chain (one launch, in-kernel hand-offs): built on first use when it fits
+  bool chain_tried = false, chain_ok = false;
+  ActChainArgs chain{};
+  unsigned chain_tag = 0;
+  volatile unsigned* done_host = nullptr;  // pinned [64]: head workgroups' completion tags
+  PinMem pin;
+  float* act_map = nullptr;  // [scale A | bias A | exploration_noise] (rle_set_action_map)
+  unsigned long long act_counter = 0;  // Philox counter of the exploration draws
+  // The rle_act_chain program of this engine's actor (ops.h ActChainArgs), or false when it does
+  // not fit (observation wider than 384, hidden wider than 256, LDS).
+  bool build_chain(const ActArgs& ao) {
+    ActChainArgs& c = chain;
+    c = ActChainArgs{};
+    if (Sp > 384) return false;
+    auto layer = [&](const Layer& L, int act, int in0, int in1, int norm, int dst, int sync) {
+      ActLayer& x = c.L[c.nl++];
+      x.wn = P + L.wn_off;
+      x.bias = P + L.b_off;
+      x.cbn = L.cb;
+      x.rbs = L.rb;
+      x.out = L.out;
+      x.act = act;
+      x.in0 = in0;
+      x.in1 = in1;
+      x.k0 = L.seg_p.empty() ? 0 : L.seg_p[0];
+      x.norm = norm;
+      x.dst = dst;
+      x.sync = sync;
+      return L.K <= kActVec || in1 >= 0;
+    };
+    bool ok = true;
+    if (algo == RLE_TD7) {  // td7.py:158-162: zs = fixed_encoder(s); policy(s, zs)
+      Net& fe = net("fixed_encoder");
+      Net& pi = net("policy");
+      ok &= layer(fe.layers[0], ACT_ELU, 0, -1, 0, 1, 0);
+      ok &= layer(pi.layers[0], ACT_NONE, 0, -1, 1, 2, 1);
+      ok &= layer(fe.layers[1], ACT_ELU, 1, -1, 0, 3, 1);
+      ok &= layer(fe.layers[2], ACT_NONE, 3, -1, 1, 4, 1);
+      ok &= layer(pi.layers[1], ACT_RELU, 2, 4, 0, 5, 1);
+      ok &= layer(pi.layers[2], ACT_RELU, 5, -1, 0, 6, 1);
+      ok &= layer(pi.layers[3], ACT_TANH, 6, -1, 0, 7, 0);
+    } else {  // mlp.py:55-68
+      Net& pi = net("policy");
+      ok &= layer(pi.layers[0], ACT_RELU, 0, -1, 0, 1, 1);
+      ok &= layer(pi.layers[1], ACT_RELU, 1, -1, 0, 2, 1);
+      ok &= layer(pi.layers[2], algo == RLE_SAC ? ACT_NONE : ACT_TANH, 2, -1, 0, 7, 0);
+      c.sac = algo == RLE_SAC;
+    }
+    c.nwg = 1;
+    for (int l = 0; l < c.nl; ++l) {
+      ok &= c.L[l].out <= kActVec && c.L[l].cbn <= 32;  // (kernels.hip act_load: <= 8 blocks per lane)
+      if (l < c.nl - 1) c.nwg = std::max(c.nwg, c.L[l].rbs);
+    }
+    c.heads = c.sac ? 1 : c.L[c.nl - 1].rbs;
+    ok &= c.heads <= c.nwg;
+    if (!ok) return false;
+    c.Sp = Sp;
+    c.xbuf = mem.make<unsigned long long>((size_t)kActMaxL * kActVec);
+    c.err = const_cast<int*>(ao.ctl) + 8;  // pinned (ActSample::ctl[8], [9]): read by the host directly
+    done_host = (volatile unsigned*)pin.alloc(64 * sizeof(unsigned));
+    HIPCHK(hipHostGetDevicePointer((void**)&c.done, (void*)done_host, 0));
+    c.ao = ao;
+    c.min_log_std = cfg.min_log_std;
+    c.max_log_std = cfg.max_log_std;
+    return true;
+  }
+  void ensure_action_map() {  // default: identity map, exploration_noise 0.1 (td7.py:41, td3.py:40)
+    if (act_map) return;
+    std::vector<float> m((size_t)2 * A + 1, 0.f);
+    for (int j = 0; j < A; ++j) m[j] = 1.f;
+    m[2 * A] = 0.1f;
+    act_map = mem.make<float>(m.size());
+    HIPCHK(hipMemcpy(act_map, m.data(), m.size() * 4, hipMemcpyHostToDevice));
+  }
 
   // ---------------------------------------------------------------- params
   Net& net(const std::string& name) {
@@ -3246,6 +3353,197 @@ int rle_act(rle_engine* h, const float* obs, int n, float* out) {
     HIPCHK(hipStreamSynchronize(e.stream));
     for (int i = 0; i < n; ++i)
       for (int c = 0; c < W; ++c) out[(size_t)i * W + c] = res[Engine::h_tidx(o.m.rbs, i, c)];
+  });
+}
+
+int rle_set_action_map(rle_engine* h, const float* scale, const float* bias, float exploration_noise) {
+  return guard([&] {
+    Engine& e = *h->e;
+    REQUIRE(scale && bias, "set_action_map: null scale / bias");
+    HIPCHK(hipSetDevice(e.cfg.device));
+    e.ensure_action_map();
+    std::vector<float> m((size_t)2 * e.A + 1);
+    std::copy(scale, scale + e.A, m.begin());
+    std::copy(bias, bias + e.A, m.begin() + e.A);
+    m[2 * e.A] = exploration_noise;
+    HIPCHK(hipStreamSynchronize(e.stream));
+    HIPCHK(hipMemcpy(e.act_map, m.data(), m.size() * 4, hipMemcpyHostToDevice));
+  });
+}
+
+int rle_act_sample(rle_engine* h, const float* obs, int n, int mode, const float* eps, float* out) {
+  return guard([&] {
+    Engine& e = *h->e;
+    REQUIRE(n > 0 && n <= 1024 && obs && out, "act_sample: 0 < n <= 1024, obs and out");
+    REQUIRE(mode >= 0 && mode <= 2 && (mode != 2 || eps), "act_sample: mode 0 / 1 / 2 (2 needs eps)");
+    HIPCHK(hipSetDevice(e.cfg.device));
+    e.ensure_action_map();
+    auto it = e.act_samplers.find(n);
+    if (it == e.act_samplers.end()) {
+      Engine::ActSample as;
+      const int M = rle::r16(n);
+      as.in = e.buf(M, e.S, true, false);
+      as.img = (float*)e.pin.alloc((size_t)M * as.in.cols * 4);
+      as.ctl = (int*)e.pin.alloc(64);
+      as.eps = (float*)e.pin.alloc((size_t)n * e.A * 4);
+      as.out = (float*)e.pin.alloc((size_t)n * e.A * 4);
+      rle::ActArgs ao{};
+      HIPCHK(hipHostGetDevicePointer((void**)&ao.out, as.out, 0));
+      HIPCHK(hipHostGetDevicePointer((void**)&ao.ctl, as.ctl, 0));
+      HIPCHK(hipHostGetDevicePointer((void**)&ao.eps, as.eps, 0));
+      ao.scale = e.act_map;
+      ao.bias = e.act_map + e.A;
+      ao.sigma = e.act_map + 2 * e.A;
+      ao.n = n;
+      ao.A = e.A;
+      ao.seed = e.cfg.seed * 0x9E3779B97F4A7C15ull + 0x5851F42D4C957F2Dull;  // own stream, not the step's
+      rle::Prog pg;
+      rle::View in = as.in;
+      auto tanh_act = [&](rle::Prog& p) {  // the last GEMM becomes the act epilogue (EPI_ACT)
+        rle::Op& op = p.items.back().ops[0];
+        op.gemm.epi = rle::EPI_ACT;
+        op.gemm.ao = ao;
+        rle::gemm_finalize(op.gemm);
+      };
+      if (e.algo == RLE_TD7) {  // td7.py:141-162
+        rle::Net& fe = e.net("fixed_encoder");
+        rle::Net& pi = e.net("policy");
+        rle::View h1 = e.fwd(pg, fe.layers[0], {{in}}, M, rle::ACT_ELU, nullptr, false);
+        rle::View h2 = e.fwd(pg, fe.layers[1], {{h1}}, M, rle::ACT_ELU, nullptr, false);
+        rle::View zs = e.fwd(pg, fe.layers[2], {{h2}}, M, rle::ACT_NONE, nullptr, true);
+        rle::View p0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_NONE, nullptr, true);
+        rle::View p1 = e.fwd(pg, pi.layers[1], {{p0}, {zs}}, M, rle::ACT_RELU, nullptr, false);
+        rle::View p2 = e.fwd(pg, pi.layers[2], {{p1}}, M, rle::ACT_RELU, nullptr, false);
+        e.fwd(pg, pi.layers[3], {{p2}}, M, rle::ACT_TANH, nullptr, false);
+        tanh_act(pg);
+      } else if (e.algo == RLE_TD3) {  // td3.py:114-135
+        rle::Net& pi = e.net("policy");
+        rle::View h0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_RELU, nullptr, false);
+        rle::View h1 = e.fwd(pg, pi.layers[1], {{h0}}, M, rle::ACT_RELU, nullptr, false);
+        e.fwd(pg, pi.layers[2], {{h1}}, M, rle::ACT_TANH, nullptr, false);
+        tanh_act(pg);
+      } else {  // sac.py:132-159
+        rle::Net& pi = e.net("policy");
+        rle::View h0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_RELU, nullptr, false);
+        rle::View h1 = e.fwd(pg, pi.layers[1], {{h0}}, M, rle::ACT_RELU, nullptr, false);
+        rle::View raw = e.fwd(pg, pi.layers[2], {{h1}}, M, rle::ACT_NONE, nullptr, false);
+        rle::Op op{};
+        op.kind = rle::OP_SAC_ACTOR;
+        rle::SacActorArgs& sa = op.sac;
+        sa.ao = ao;
+        sa.out = raw.m;
+        sa.A = e.A;
+        sa.rows = n;
+        sa.min_log_std = e.cfg.min_log_std;
+        sa.max_log_std = e.cfg.max_log_std;
+        sa.mean_off = 0;
+        sa.ls_off = e.A;
+        op.wg_count = rle::cdiv(n, rle::kThreads);
+        pg.add(op, {raw.id}, {});
+      }
+      as.G = e.capture(pg);
+      it = e.act_samplers.emplace(n, as).first;
+    }
+    Engine::ActSample& as = it->second;
+    if (n == 1 && !e.chain_tried) {
+      e.chain_tried = true;
+      static const bool no_chain = std::getenv("RLE_NO_ACT_CHAIN") != nullptr;  // A/B
+      rle::ActArgs ao{};
+      HIPCHK(hipHostGetDevicePointer((void**)&ao.out, as.out, 0));
+      HIPCHK(hipHostGetDevicePointer((void**)&ao.ctl, as.ctl, 0));
+      HIPCHK(hipHostGetDevicePointer((void**)&ao.eps, as.eps, 0));
+      ao.scale = e.act_map;
+      ao.bias = e.act_map + e.A;
+      ao.sigma = e.act_map + 2 * e.A;
+      ao.n = 1;
+      ao.A = e.A;
+      ao.seed = e.cfg.seed * 0x9E3779B97F4A7C15ull + 0x5851F42D4C957F2Dull;
+      e.chain_ok = !no_chain && e.build_chain(ao);
+    }
+    if (n == 1 && e.chain_ok) {  // one launch, in-kernel hand-offs (kernels.hip rle_act_chain)
+      rle::ActChainArgs& c = e.chain;
+      std::memset(c.obs, 0, sizeof c.obs);
+      std::memcpy(c.obs, obs, (size_t)e.S * 4);
+      if (++e.chain_tag == 0) e.chain_tag = 1;
+      c.tag = e.chain_tag;
+      as.ctl[0] = mode;
+      as.ctl[1] = (int)(unsigned)e.act_counter;
+      as.ctl[2] = (int)(unsigned)(e.act_counter >> 32);
+      if (mode == 1) ++e.act_counter;
+      if (mode == 2) std::memcpy(as.eps, eps, (size_t)e.A * 4);
+      static const bool cprof = std::getenv("RLE_ACT_PROF") != nullptr;
+      static double cp[3] = {0, 0, 0};
+      static long long ccalls = 0;
+      static hipEvent_t ce0 = nullptr, ce1 = nullptr;
+      if (cprof && !ce0) {
+        HIPCHK(hipEventCreate(&ce0));
+        HIPCHK(hipEventCreate(&ce1));
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      if (cprof) HIPCHK(hipEventRecord(ce0, e.stream));
+      HIPCHK(rle::launch_act_chain(c, e.stream));
+      if (cprof) HIPCHK(hipEventRecord(ce1, e.stream));
+      const auto t1 = std::chrono::steady_clock::now();
+      // the head workgroups' completion tags (system-scope release after their action stores):
+      // poll pinned memory instead of waiting for the stream; a failed launch ends the poll
+      for (int hw = 0; hw < c.heads; ++hw) {
+        for (long long k = 1; e.done_host[hw] != c.tag; ++k) {
+          if ((k & 4095) == 0 && hipStreamQuery(e.stream) != hipErrorNotReady) {
+            HIPCHK(hipStreamSynchronize(e.stream));
+            REQUIRE(e.done_host[hw] == c.tag, "act chain: the kernel ended without its completion tag");
+            break;
+          }
+        }
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+      const auto t2 = std::chrono::steady_clock::now();
+      if (cprof) HIPCHK(hipStreamSynchronize(e.stream));
+      REQUIRE(as.ctl[8] == 0, "act chain: a workgroup hand-off timed out");
+      std::memcpy(out, as.out, (size_t)e.A * 4);
+      if (cprof) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, ce0, ce1));
+        cp[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+        cp[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
+        cp[2] += ms * 1e3;
+        if (++ccalls % 2000 == 0) {
+          fprintf(stderr, "act chain (us/call): launch %.2f  sync %.2f  kernel (events) %.2f\n", cp[0] / 2000,
+                  cp[1] / 2000, cp[2] / 2000);
+          cp[0] = cp[1] = cp[2] = 0;
+        }
+      }
+      return;
+    }
+    const int M = rle::r16(n);
+    static const bool prof = std::getenv("RLE_ACT_PROF") != nullptr;  // phase times, tools/act_bench.py
+    static double tp[4] = {0, 0, 0, 0};
+    static long long calls = 0;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = now();
+    for (int i = 0; i < n; ++i)
+      for (int c = 0; c < e.S; ++c) as.img[Engine::h_nidx(as.in.m.cbn, i, c)] = obs[(size_t)i * e.S + c];
+    as.ctl[0] = mode;
+    as.ctl[1] = (int)(unsigned)e.act_counter;
+    as.ctl[2] = (int)(unsigned)(e.act_counter >> 32);
+    if (mode == 1) ++e.act_counter;
+    if (mode == 2) std::memcpy(as.eps, eps, (size_t)n * e.A * 4);
+    HIPCHK(hipMemcpyAsync(as.in.m.n, as.img, (size_t)M * as.in.cols * 4, hipMemcpyHostToDevice, e.stream));
+    const auto t1 = now();
+    e.launch_graph(as.G);
+    const auto t2 = now();
+    HIPCHK(hipStreamSynchronize(e.stream));
+    const auto t3 = now();
+    std::memcpy(out, as.out, (size_t)n * e.A * 4);
+    if (prof) {
+      tp[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+      tp[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
+      tp[2] += std::chrono::duration<double, std::micro>(t3 - t2).count();
+      if (++calls % 2000 == 0) {
+        fprintf(stderr, "act_sample phases (us/call): stage+H2D %.2f  graph launch %.2f  sync %.2f\n", tp[0] / 2000,
+                tp[1] / 2000, tp[2] / 2000);
+        tp[0] = tp[1] = tp[2] = 0;
+      }
+    }
   });
 }
 

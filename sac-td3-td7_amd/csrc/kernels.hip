@@ -277,6 +277,21 @@ constexpr int kTraceStride = 4;
   } while (0)
 #endif
 
+// ---------------------------------------------------------------- act graph output
+// Exploration draw e (row-major index row * A + j) of an act call (ActArgs::ctl).
+template <class AO>  // (ActArgs in the constant address space, or a kernel argument)
+__device__ __forceinline__ float act_eps(const AO& ao, int mode, int e) {
+  if (mode == 2) return G(ao.eps)[e];
+  const uint2 key = make_uint2((unsigned)ao.seed, (unsigned)(ao.seed >> 32));
+  const uint4 r = philox(key, make_uint4((unsigned)e, 7u, (unsigned)G(ao.ctl)[1], (unsigned)G(ao.ctl)[2]));
+  return normal_from(r.x, r.y);
+}
+// out = a * scale + bias (numpy float32: two rounded ops)
+template <class AO>
+__device__ __forceinline__ void act_store(const AO& ao, int row, int j, float a) {
+  GW(ao.out)[(size_t)row * ao.A + j] = __fadd_rn(__fmul_rn(a, G(ao.scale)[j]), G(ao.bias)[j]);
+}
+
 // ---------------------------------------------------------------- GEMM
 //
 // One workgroup = one 16 x tn output tile (tn in {16, 32, 64}); its 4 waves are
@@ -857,6 +872,24 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     __syncthreads();
     if (tid < 16)
       GW(g.norm_out)[(size_t)jt * g.norm_ld + i0 + tid] = (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
+  } else if constexpr (EPI == EPI_ACT) {  // td7.py:141-156 / td3.py:114-129: env action of the act graph
+    if (jok) {
+      const CAS ActArgs& ao = g.ao;
+      const int mode = G(ao.ctl)[0];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = ib + q;
+        if (row >= ao.n) continue;
+        float a = act_f<ACT>(acc[q] + pre_b);
+        if (mode) {  // action += randn * exploration_noise; clip(-1, 1)
+          const float nz = __fmul_rn(act_eps(ao, mode, row * ao.A + j), sload(ao.sigma));
+          a = fminf(fmaxf(__fadd_rn(a, nz), -1.f), 1.f);
+        } else {
+          a = fminf(fmaxf(a, -1.f), 1.f);
+        }
+        act_store(ao, row, j, a);
+      }
+    }
   } else if constexpr (EPI == EPI_MSE) {  // td7.py:256 encoder loss, grad wrt zsa
     float d2 = 0.f;
     if (jok) {
@@ -937,6 +970,7 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_V(GEMM_FWD, EPI_QHEAD, ACT_ELU, false)
     RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, false)
     RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, true)
+    RLE_V(GEMM_FWD, EPI_ACT, ACT_TANH, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_NONE, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_RELU, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_ELU, false)
@@ -1470,6 +1504,21 @@ __device__ __forceinline__ void op_priority(const CAS PriorityArgs& a, float* sm
 
 __device__ __forceinline__ void op_sac_actor(const CAS SacActorArgs& s, int t) {
   const int b = t * kThreads + threadIdx.x;
+  if (s.ao.out) {  // act graph (sac.py:132-152): tanh(mean) or tanh(rsample), env map
+    const CAS ActArgs& ao = s.ao;
+    if (b >= ao.n) return;
+    const int mode = G(ao.ctl)[0];
+    for (int j = 0; j < ao.A; ++j) {
+      const float mu = mat_ld(s.out, b, s.mean_off + j);
+      float u = mu;
+      if (mode) {
+        const float ls = fminf(fmaxf(mat_ld(s.out, b, s.ls_off + j), s.min_log_std), s.max_log_std);
+        u = __fadd_rn(mu, __fmul_rn(act_eps(ao, mode, b * ao.A + j), expf(ls)));  // Normal.rsample
+      }
+      act_store(ao, b, j, tanhf(u));
+    }
+    return;
+  }
   if (b >= s.rows) return;
   const bool pol = b < s.eps_row_split;  // rows < split use eps2 (policy), else eps (target)
   const int eb = pol ? b : b - s.eps_row_split;
@@ -1771,6 +1820,145 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(const LevelArgs
   trace_mark(tr, 3);
 }
 
+
+// ---------------------------------------------------------------- B = 1 act chain (ops.h ActChainArgs)
+// Row block rb of layer L in registers: column block cb = wave + 4 i of the [16][K] strip, lane l
+// holding row l % 16, columns 4 (l / 16) .. +3 of each 1 KB block (K <= 512: at most 8 per lane).
+constexpr int kActPre = 8;
+struct ActW {
+  float4 v[kActPre];
+};
+__device__ __forceinline__ void act_load(const ActLayer& L, int rb, ActW& W) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < kActPre; ++i) {
+    const int cb = wave + 4 * i;
+    W.v[i] = cb < L.cbn ? ld4g(G(L.wn) + ((size_t)rb * L.cbn + cb) * 256 + lane * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+// The 16 rows against the LDS vectors; the 4 lane groups and the 4 waves summed in fixed order.
+// Result (bias, activation) for row r in red[64 + r].
+__device__ __forceinline__ void act_rows(const ActLayer& L, int rb, const ActW& W, const float* vec, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < kActPre; ++i) {
+    const int cb = wave + 4 * i;
+    if (cb >= L.cbn) break;
+    const int c = cb * 16 + (lane >> 4) * 4;  // reduction column of v[i].x
+    const float* x = (L.in1 >= 0 && c >= L.k0) ? vec + L.in1 * kActVec + (c - L.k0) : vec + L.in0 * kActVec + c;
+    acc += W.v[i].x * x[0] + W.v[i].y * x[1] + W.v[i].z * x[2] + W.v[i].w * x[3];
+  }
+  acc += __shfl_xor(acc, 16);
+  acc += __shfl_xor(acc, 32);
+  if (lane < 16) red[wave * 16 + lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int r = threadIdx.x, row = rb * 16 + r;
+    float y = (red[r] + red[16 + r]) + (red[32 + r] + red[48 + r]);
+    y += row < L.out ? G(L.bias)[row] : 0.f;
+    red[64 + r] = act_fwd(L.act, y);
+  }
+  __syncthreads();
+}
+
+// Reads the granules of layer q (this call's tag) into vector slot Q.dst, then AvgL1Norm.
+__device__ __forceinline__ void act_receive(const ActChainArgs& a, int q, float* vec, float* red) {
+  const ActLayer& Q = a.L[q];
+  for (int i = threadIdx.x; i < Q.out; i += kThreads) {
+    unsigned long long g = 0;
+    int spins = 0;
+    while (true) {
+      g = __hip_atomic_load(a.xbuf + (size_t)q * kActVec + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((g >> 32) == (unsigned long long)a.tag) break;
+      if (++spins > (1 << 20)) {  // ~0.1 s: a workgroup never arrived (fail, do not hang)
+        __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // (plain store: host memory)
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    vec[Q.dst * kActVec + i] = __uint_as_float((unsigned)g);
+  }
+  __syncthreads();
+  if (Q.norm) {  // AvgL1Norm: x / max(mean |x|, 1e-8), the same fixed-order sum in every workgroup
+    float sabs = 0.f;
+    for (int i = threadIdx.x; i < Q.out; i += kThreads) sabs += fabsf(vec[Q.dst * kActVec + i]);
+    sabs = wg_sum(sabs, red);
+    const float m = fmaxf(sabs / (float)Q.out, 1e-8f);
+    for (int i = threadIdx.x; i < Q.out; i += kThreads) vec[Q.dst * kActVec + i] /= m;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kThreads, 1) void rle_act_chain(const ActChainArgs a) {
+  __shared__ __attribute__((aligned(16))) float vec[8 * kActVec];  // vector slots (0: observation, 7: head)
+  __shared__ float red[128];
+  const int tid = threadIdx.x, w = blockIdx.x;
+  const unsigned long long tag = (unsigned long long)a.tag << 32;
+  const int last = a.nl - 1;
+  ActW W;
+  int next = 0;  // first layer whose row block w exists
+  while (next < last && w >= a.L[next].rbs) ++next;
+  if (next < last) act_load(a.L[next], w, W);
+  for (int i = tid; i < 8 * kActVec; i += kThreads) vec[i] = i < a.Sp ? a.obs[i] : 0.f;
+  __syncthreads();
+  for (int l = 0; l < last; ++l) {
+    const ActLayer& L = a.L[l];
+    if (w < L.rbs) {  // produce row block w: one 8-byte {value, tag} sc1 store per row
+      act_rows(L, w, W, vec, red);
+      if (tid < 16 && w * 16 + tid < L.out)
+        __hip_atomic_store(a.xbuf + (size_t)l * kActVec + w * 16 + tid,
+                           tag | (unsigned long long)__float_as_uint(red[64 + tid]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      next = l + 1;
+      while (next < last && w >= a.L[next].rbs) ++next;
+      // the next layer's weights (or the head's) load while this layer is handed off
+      if (next < last) act_load(a.L[next], w, W);
+      else if (w < a.L[last].rbs && !a.sac) act_load(a.L[last], w, W);
+      else if (w == 0 && a.sac) act_load(a.L[last], 0, W);
+    }
+    if (!L.sync) continue;
+    for (int q = l; q >= 0 && (q == l || !a.L[q].sync); --q) act_receive(a, q, vec, red);
+  }
+  // ---- the head: env action (td7.py:141-156, td3.py:114-129, sac.py:132-152).  TD7 / TD3: row
+  // block w of the tanh layer in workgroup w, actions written directly; SAC: workgroup 0, whole.
+  const ActLayer& L = a.L[last];
+  const ActArgs& ao = a.ao;
+  const int nrb = a.sac ? (w == 0 ? L.rbs : 0) : (w < L.rbs ? 1 : 0);
+  if (!nrb) return;
+  const int mode = G(ao.ctl)[0];
+  for (int k = 0; k < nrb; ++k) {
+    const int rb = a.sac ? k : w;
+    if (k) act_load(L, rb, W);
+    act_rows(L, rb, W, vec, red);
+    if (tid < 16) vec[7 * kActVec + rb * 16 + tid] = red[64 + tid];
+    __syncthreads();
+  }
+  const float* h = vec + 7 * kActVec;
+  const int j0 = a.sac ? 0 : w * 16, j1 = a.sac ? ao.A : min(ao.A, w * 16 + 16);
+  for (int j = j0 + tid; j < j1; j += kThreads) {
+    float act;
+    if (a.sac) {
+      const float mu = h[j];
+      float u = mu;
+      if (mode) {
+        const float ls = fminf(fmaxf(h[ao.A + j], a.min_log_std), a.max_log_std);
+        u = __fadd_rn(mu, __fmul_rn(act_eps(ao, mode, j), expf(ls)));
+      }
+      act = tanhf(u);
+    } else {
+      act = h[j];  // tanh applied by act_rows (L.act)
+      if (mode) act = __fadd_rn(act, __fmul_rn(act_eps(ao, mode, j), sload(ao.sigma)));
+      act = fminf(fmaxf(act, -1.f), 1.f);
+    }
+    act_store(ao, 0, j, act);
+  }
+  // completion for the host's poll: this workgroup's action stores, then its slot := tag with a
+  // system-scope release (a plain store, no PCIe atomic)
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(a.done + w, a.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------- standalone kernels
 
 // Scatter `count` staged transitions into the ring at ptr (wrapping).
@@ -1874,6 +2062,10 @@ hipError_t launch_append(float* state, float* next_state, float* action, float* 
   hipLaunchKernelGGL(rle_append_kernel, dim3(count), dim3(256), 0, st, state, next_state, action, reward, notdone,
                      priority, st_s, st_ns, st_a, st_r, st_d, ptr, cap, count, Sp, Ap, max_priority, lap, bsum,
                      size_before);
+  return hipGetLastError();
+}
+hipError_t launch_act_chain(const ActChainArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(rle_act_chain, dim3(a.nwg), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_fill(float* state, float* next_state, float* action, float* reward, float* notdone,

@@ -88,6 +88,25 @@ enum Epi : int {
                    // out = qscale * w3 * act'(z) (= dZ), loss partial sum of act(z) * w3 (+ M b3)
   EPI_NBDOT = 4,   // DX whose output g feeds an AvgL1Norm backward deferred into its consumer:
                    // out = g, per-tile row partials of sum_j g x (x: nbx) into norm_out
+  EPI_ACT = 5,     // act graph (TD7 / TD3 actor's tanh layer): environment action, ActArgs
+};
+
+// Environment action of an act graph (td7.py:141-156, td3.py:114-129, sac.py:132-152), written
+// as compact [n][A] rows straight into host-mapped memory:
+//   TD7 / TD3 (EPI_ACT):     a = clip(tanh(z) + sigma * eps, -1, 1)   (eps = 0: deterministic)
+//   SAC (OP_SAC_ACTOR):      a = tanh(mean + exp(clamp(log_std)) * eps)
+//   out = a * scale + bias   (fp32, unfused, as numpy's float32 ops)
+// eps: ctl[0] = 0 none (deterministic), 1 Philox normal at counter (ctl[1], ctl[2]) keyed by seed,
+// 2 the host tape eps[n][A] (parity).
+struct ActArgs {
+  float* out;
+  const int* ctl;
+  const float* eps;
+  const float* scale;     // [A]   (rle_set_action_map)
+  const float* bias;      // [A]
+  const float* sigma;     // [1]   TD7 / TD3 exploration_noise
+  int n, A;
+  unsigned long long seed;
 };
 // GEMM_DW variant whose A operand (dZ) is an AvgL1Norm backward applied on load:
 // a = g / m + sign(x) * gm, gm = -(sum_j g x) / (n m^2) (0 when m is clamped), rows by LDS table
@@ -206,6 +225,7 @@ struct GemmArgs {
   PreArgs prea;
   int pad_;
   AdamArgs adam;
+  ActArgs ao;                      // EPI_ACT
 };
 
 // AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise);
@@ -294,6 +314,7 @@ struct PriorityArgs {
 };
 
 struct SacActorArgs {
+  ActArgs ao;                        // act graph: ao.out != nullptr -> environment actions only
   Mat out;                           // raw head output [rows][2A(p)]: mean | log_std (T)
   int A, rows;                       // rows = 2B
   Mat eps; int eps_row_split; Mat eps2;  // rows < split use eps2 (policy), else eps (target) (T)
@@ -373,6 +394,43 @@ struct Op {
     CtrlArgs ctrl;
     FoldBiasArgs fb;
   };
+};
+
+// ---- B = 1 act chain (rle_act_sample, one observation): ONE launch of nwg workgroups
+// (kernels.hip rle_act_chain).  Workgroup w owns row block w of every hidden layer, its next
+// layer's weights loaded into registers while the current one is handed off; after each layer
+// the workgroups exchange the layer output as 8-byte {value, call tag} granules (sc1 stores /
+// loads: a stale granule is re-read until its tag is this call's), so a layer costs one
+// hand-off instead of one kernel launch.  The head runs with the act epilogue (ActArgs):
+// TD7 / TD3 row block w in workgroup w, SAC whole in workgroup 0; each head workgroup then
+// stores the call tag into its pinned `done` slot with a system-scope release; the host polls.
+constexpr int kActMaxL = 7;
+constexpr int kActVec = 512;   // floats per LDS vector slot
+struct ActLayer {
+  const float* wn;     // weights, N image [out][K] (fragment blocks)
+  const float* bias;   // [16 * row blocks]
+  int cbn, rbs, out;   // column blocks (K / 16), row blocks, rows
+  int act;             // ACT_*
+  int in0, in1;        // input vector slots (in1 < 0: one segment); in1 starts at column k0
+  int k0;              // padded width of segment 0
+  int norm;            // output AvgL1Norm'd (sale.py:11-13) before its consumers read it
+  int dst;             // output vector slot
+  int sync;            // exchange after this layer (0: the next layer does not read it)
+  int pad_[2];
+};
+struct ActChainArgs {
+  ActLayer L[kActMaxL];
+  int nl, nwg;
+  int sac;             // last layer: SAC raw head (mean | log_std) + rsample law, else tanh + EPI_ACT law
+  int Sp;              // observation slot width
+  unsigned long long* xbuf;  // [nl][kActVec] granules {float bits, tag}
+  unsigned tag;        // this call's tag (never 0)
+  int heads;           // head workgroups (0 .. heads-1) that set their `done` slot per call
+  int* err;            // 1: a hand-off timed out (pinned)
+  unsigned* done;      // [64] per head workgroup: tag of the last call it finished (pinned)
+  ActArgs ao;
+  float min_log_std, max_log_std;
+  float obs[384];      // the observation (padded, zeros)
 };
 
 // Kernel argument of one level launch: the workgroup -> op table travels in the

@@ -75,6 +75,9 @@ SIGNATURES = {
     "rle_set_tapes": (_int, [_vp, _int, _f32p, _f32p, _f32p, _i64p]),
     "rle_last_indices": (_int, [_vp, _i64p]),
     "rle_act": (_int, [_vp, _f32p, _int, _f32p]),
+    # (raw addresses: the per-env-step path skips ctypes pointer conversions)
+    "rle_act_sample": (_int, [_vp, _vp, _int, _int, _vp, _vp]),
+    "rle_set_action_map": (_int, [_vp, _f32p, _f32p, ctypes.c_float]),
     "rle_launch_count": (_int, [_vp, ctypes.POINTER(ctypes.c_longlong)]),
     "rle_graph_stats": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "rle_graph_describe": (_int, [_vp, _int, ctypes.c_char_p, _int]),
@@ -202,6 +205,7 @@ class Engine:
         self.h = _vp()
         _check(lib().rle_create(ctypes.byref(cfg), ctypes.byref(self.h)))
         self.replay = None
+        self._act_out = {}
 
     def close(self):
         if self.h:
@@ -298,6 +302,30 @@ class Engine:
         n = obs.shape[0]
         out = np.empty((n, width), np.float32)
         _check(lib().rle_act(self.h, _fp(obs), n, _fp(out)))
+        return out
+
+    def set_action_map(self, scale, bias, exploration_noise=0.1):
+        """Environment action map of act_sample: a * scale + bias, and the TD7 / TD3
+        exploration noise std (rle_set_action_map)."""
+        scale = _f32(np.broadcast_to(np.asarray(scale, np.float32), (self.cfg.action_dim,)))
+        bias = _f32(np.broadcast_to(np.asarray(bias, np.float32), (self.cfg.action_dim,)))
+        _check(lib().rle_set_action_map(self.h, _fp(scale), _fp(bias), float(exploration_noise)))
+
+    def act_sample(self, obs, mode, eps=None):
+        """Agent.sample on the device (rle_act_sample): obs [S] or [n][S] -> environment
+        actions [n][A].  mode 0 deterministic, 1 Philox exploration noise, 2 noise tape eps."""
+        x = obs if (type(obs) is np.ndarray and obs.dtype == np.float32 and obs.flags.c_contiguous) else _f32(obs)
+        n = 1 if x.ndim == 1 else x.shape[0]
+        out = self._act_out.get(n)
+        if out is None:
+            out = self._act_out[n] = np.empty((n, self.cfg.action_dim), np.float32)
+        e = 0
+        if mode == 2:
+            eps = _f32(eps).reshape(n, self.cfg.action_dim)
+            e = eps.ctypes.data
+        rc = lib().rle_act_sample(self.h, x.ctypes.data, n, mode, e, out.ctypes.data)
+        if rc:
+            _check(rc)
         return out
 
     def eval_q(self, net, s, a, enc="fixed_encoder"):

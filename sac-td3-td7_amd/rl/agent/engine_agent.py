@@ -227,6 +227,20 @@ class EngineAgent(Agent, Sampler):
         return [self._info(r) for r in rows]
 
     # ---- acting --------------------------------------------------------------
+    def _act(self, state, deterministic, eps=None):
+        """Agent.sample as one device program (rle_act_sample): forward, exploration noise
+        (the engine's Philox stream, or the tape `eps` [A]), clip and the action map, written
+        into pinned memory by the last kernel.  Returns the first row as the reference does."""
+        eng = self.engine
+        if not getattr(eng, "_act_map_set", False):
+            eng.set_action_map(self.action_scale, self.action_bias, getattr(self, "exploration_noise", 0.1))
+            eng._act_map_set = True
+        if hasattr(state, "detach"):
+            state = state.detach().cpu().numpy()
+        if eps is not None:
+            return eng.act_sample(state, 2, eps)[0].copy()
+        return eng.act_sample(state, 0 if deterministic else 1)[0].copy()
+
     def _forward(self, state, width):
         if hasattr(state, "detach"):
             state = state.detach().cpu().numpy()

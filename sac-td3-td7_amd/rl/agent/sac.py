@@ -69,12 +69,9 @@ class SAC(EngineAgent):
         return torch.distributions.Normal(mean, log_std.exp())
 
     def sample(self, state, deterministic: bool = False, **kwargs):
-        """sac.py:132-152."""
-        import torch
-
-        dist = self._inference(state)
-        action = torch.tanh(dist.mean) if deterministic else torch.tanh(dist.rsample())
-        return action.numpy()[0] * self.action_scale + self.action_bias
+        """sac.py:132-152: tanh(mean) or tanh(mean + std * randn) (rsample), * scale + bias, one
+        device program (rle_act_sample; engine Philox stream, or kwargs eps=[A] for parity)."""
+        return self._act(state, deterministic, kwargs.get("eps"))
 
     def __repr__(self) -> str:
         return "SAC"

@@ -41,14 +41,10 @@ class TD3(EngineAgent):
         return ("train/q_fn", "train/policy", "norm/policy")  # td3.py:226-235
 
     def sample(self, state, deterministic: bool = False, **kwargs):
-        """td3.py:114-135: tanh(policy(s)) + exploration noise, clip, affine map."""
-        import torch
-
-        action = torch.tanh(torch.from_numpy(self._forward(state, self.action_dim)))
-        if not deterministic:
-            action += torch.randn_like(action) * self.exploration_noise
-        action = np.clip(action.numpy()[0], -1.0, 1.0)
-        return action * self.action_scale + self.action_bias
+        """td3.py:114-135: clip(tanh(policy(s)) + exploration_noise * randn, -1, 1) * scale + bias, one
+        device program (rle_act_sample).  The noise comes from the engine's Philox stream (the
+        reference uses torch's global generator); kwargs eps=[A] supplies it instead (parity)."""
+        return self._act(state, deterministic, kwargs.get("eps"))
 
     def __repr__(self) -> str:
         return "TD3"

@@ -59,15 +59,10 @@ class TD7(EngineAgent):
         return float(self.engine.value_bounds()[3])
 
     def sample(self, state, deterministic: bool = False, **kwargs):
-        """td7.py:141-156: policy(s, fixed_encoder.zs(s)) on the device; exploration noise,
-        clip and affine map on the host (torch's global RNG, like the reference)."""
-        import torch
-
-        action = torch.from_numpy(self._forward(state, self.action_dim))
-        if not deterministic:
-            action += torch.randn_like(action) * self.exploration_noise
-        action = np.clip(action.numpy()[0], -1.0, 1.0)
-        return action * self.action_scale + self.action_bias
+        """td7.py:141-156: clip(tanh(policy(s)) + exploration_noise * randn, -1, 1) * scale + bias, one
+        device program (rle_act_sample).  The noise comes from the engine's Philox stream (the
+        reference uses torch's global generator); kwargs eps=[A] supplies it instead (parity)."""
+        return self._act(state, deterministic, kwargs.get("eps"))
 
     def __repr__(self) -> str:
         return "TD7"

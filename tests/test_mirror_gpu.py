@@ -166,6 +166,81 @@ def test_sample_actions_match_oracle_forward():
         assert stoch.shape == (A,) and np.all(np.abs(stoch) <= HI + 1e-6)
 
 
+def _oracle_env_action(Agent, ag, obs, eps):
+    """The reference's sample() (td7.py:141-156, td3.py:114-129, sac.py:132-152) on the oracle
+    nets with the exploration draw eps in place of torch.randn_like: float32 throughout."""
+    from oracle import nets as N
+
+    sd = {k: {n: torch.from_numpy(v) for n, v in d.items()} for k, d in ag.state_dict().items()}
+    x = torch.from_numpy(np.asarray(obs, np.float32))[None]
+    e = torch.from_numpy(np.asarray(eps, np.float32))[None]
+    with torch.no_grad():
+        if Agent is SAC:
+            mean, log_std = N.mlp(sd["policy"], x).chunk(2, -1)
+            log_std = torch.clamp(log_std, ag.min_log_std, ag.max_log_std)
+            a = torch.tanh(mean + e * log_std.exp()).numpy()[0]
+        else:
+            if Agent is TD7:
+                a = N.sale_actor(sd["policy"], x, N.sale_zs(sd["fixed_encoder"], x))
+            else:
+                a = torch.tanh(N.mlp(sd["policy"], x))
+            a = a + e * ag.exploration_noise
+            a = np.clip(a.numpy()[0], -1.0, 1.0)
+    return a * ag.action_scale + ag.action_bias
+
+
+@pytest.mark.parametrize("Agent", [TD7, TD3, SAC])
+def test_fused_act_sample_matches_oracle_with_noise_tape(Agent):
+    """agent.sample as one device program (forward + exploration noise +
+    clip + action map, rle_act_sample) equals the reference's sample() on the same draw:
+    |d| <= 2e-6 + 1e-5 |ref| (fp32 tanh / exp ulps)."""
+    ag = Agent("Tiny-v0", hidden=32, batch_size=32, seed=7)
+    rng = np.random.default_rng(3)
+    for k in range(4):
+        obs = rng.standard_normal(S).astype(np.float32) * (1 + 2 * k)  # k = 3: saturated outputs
+        eps = rng.standard_normal(A).astype(np.float32) * (1 + 4 * (k == 2))  # k = 2: clipping
+        ref = _oracle_env_action(Agent, ag, obs, eps)
+        got = ag.sample(obs, eps=eps)
+        assert got.dtype == np.float32 and got.shape == (A,)
+        assert (np.abs(got - ref) <= 2e-6 + 1e-5 * np.abs(ref)).all(), (k, got, ref)
+        det = ag.sample(obs, deterministic=True)
+        ref0 = _oracle_env_action(Agent, ag, obs, np.zeros(A, np.float32))
+        assert (np.abs(det - ref0) <= 2e-6 + 1e-5 * np.abs(ref0)).all(), (k, det, ref0)
+
+
+def test_fused_act_sample_humanoid_and_batches():
+    """Full-size TD7 Humanoid (S 376, A 17, scale 0.4): the taped draw against the oracle, and a
+    batch of n = 5 observations (the act graph) agrees with five single calls (n = 1: the
+    one-launch act chain, its own summation order) to fp32 rounding."""
+    ag = TD7("Humanoid-v4", batch_size=256, seed=11)
+    rng = np.random.default_rng(5)
+    obs = rng.standard_normal(376).astype(np.float32)
+    eps = rng.standard_normal(17).astype(np.float32)
+    ref = _oracle_env_action(TD7, ag, obs, eps)
+    got = ag.sample(obs, eps=eps)
+    assert (np.abs(got - ref) <= 2e-6 + 1e-5 * np.abs(ref)).all(), np.abs(got - ref).max()
+    xs = rng.standard_normal((5, 376)).astype(np.float32)
+    es = rng.standard_normal((5, 17)).astype(np.float32)
+    batch = ag.engine.act_sample(xs, 2, es).copy()
+    for i in range(5):
+        one = ag.sample(xs[i], eps=es[i])
+        assert (np.abs(batch[i] - one) <= 2e-6 + 1e-5 * np.abs(one)).all(), (i, np.abs(batch[i] - one).max())
+        ref = _oracle_env_action(TD7, ag, xs[i], es[i])
+        assert (np.abs(one - ref) <= 2e-6 + 1e-5 * np.abs(ref)).all(), (i, np.abs(one - ref).max())
+
+
+def test_fused_act_sample_philox_noise_statistics():
+    """Device exploration draws (mode 1): (stochastic - deterministic) / (scale * sigma) is
+    N(0, 1) per action dimension where unclipped, and consecutive calls draw fresh noise."""
+    ag = TD3("Tiny-v0", hidden=32, batch_size=32, seed=2)
+    obs = np.zeros(S, np.float32)
+    det = ag.sample(obs, deterministic=True)
+    z = np.stack([ag.sample(obs) for _ in range(3000)])
+    z = (z - det) / (HI * ag.exploration_noise)
+    assert len({tuple(r) for r in z[:50]}) == 50
+    assert np.abs(z.mean(0)).max() < 0.08 and np.abs(z.std(0) - 1).max() < 0.06, (z.mean(0), z.std(0))
+
+
 def test_batch_size_change_rebuilds_engine():
     ag = TD3("Tiny-v0", hidden=32, batch_size=32, seed=1)
     rep = SimpleReplayMemory(256, "Tiny-v0")

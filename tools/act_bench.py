@@ -1,5 +1,6 @@
 """Per-env-step costs around the gradient step (GPU box):
-agent.sample latency (B=1 device actor/encoder forward + host exploration noise), and
+agent.sample latency (one device program: B=1 fixed-encoder + actor forward, Philox exploration
+noise, clip and action map into pinned memory, rle_act_sample), the bare ABI call, and
 replay append throughput (staged host rows -> one batched H2D append kernel).
 python tools/act_bench.py  -> one JSON line."""
 import json
@@ -28,6 +29,15 @@ for det in (False, True):
     for _ in range(n):
         agent.sample(obs, deterministic=det)
     out[f"sample_us_{'det' if det else 'explore'}"] = round((time.perf_counter() - t0) / n * 1e6, 2)
+x = obs[None].copy()
+for mode in (0, 1):
+    for _ in range(20):
+        agent.engine.act_sample(x, mode)
+    n = 2000
+    t0 = time.perf_counter()
+    for _ in range(n):
+        agent.engine.act_sample(x, mode)
+    out[f"engine_act_sample_us_mode{mode}"] = round((time.perf_counter() - t0) / n * 1e6, 2)
 rows = 200_000
 s = rng.standard_normal((rows, 376)).astype(np.float32)
 a = rng.uniform(-0.4, 0.4, (rows, 17)).astype(np.float32)
