@@ -824,10 +824,12 @@ struct Engine {
     c.nwg = 1;
     for (int l = 0; l < c.nl; ++l) {
       ok &= c.L[l].out <= kActVec && c.L[l].cbn <= 32;  // (kernels.hip act_load: <= 8 blocks per lane)
+    ok &= A <= 32;  // ActChainArgs::eps, one output per thread
       if (l < c.nl - 1) c.nwg = std::max(c.nwg, c.L[l].rbs);
     }
     c.heads = c.sac ? 1 : c.L[c.nl - 1].rbs;
     ok &= c.heads <= c.nwg;
+    for (int l = 0; l < c.nl - 1; ++l) ok &= c.L[l].rbs == c.nwg;  // (every workgroup in every hidden layer)
     if (!ok) return false;
     c.Sp = Sp;
     c.xbuf = mem.make<unsigned long long>((size_t)kActMaxL * kActVec);
@@ -3466,18 +3468,21 @@ int rle_act_sample(rle_engine* h, const float* obs, int n, int mode, const float
       std::memcpy(c.obs, obs, (size_t)e.S * 4);
       if (++e.chain_tag == 0) e.chain_tag = 1;
       c.tag = e.chain_tag;
-      as.ctl[0] = mode;
-      as.ctl[1] = (int)(unsigned)e.act_counter;
-      as.ctl[2] = (int)(unsigned)(e.act_counter >> 32);
+      c.mode = mode;
+      c.ctr_lo = (unsigned)e.act_counter;
+      c.ctr_hi = (unsigned)(e.act_counter >> 32);
       if (mode == 1) ++e.act_counter;
-      if (mode == 2) std::memcpy(as.eps, eps, (size_t)e.A * 4);
+      if (mode == 2) std::memcpy(c.eps, eps, (size_t)e.A * 4);
       static const bool cprof = std::getenv("RLE_ACT_PROF") != nullptr;
       static double cp[3] = {0, 0, 0};
       static long long ccalls = 0;
       static hipEvent_t ce0 = nullptr, ce1 = nullptr;
+      static std::vector<double> sacc;
       if (cprof && !ce0) {
         HIPCHK(hipEventCreate(&ce0));
         HIPCHK(hipEventCreate(&ce1));
+        c.stamps = e.mem.make<unsigned long long>((size_t)c.nwg * 16);
+        sacc.assign(16, 0.0);
       }
       const auto t0 = std::chrono::steady_clock::now();
       if (cprof) HIPCHK(hipEventRecord(ce0, e.stream));
@@ -3506,10 +3511,25 @@ int rle_act_sample(rle_engine* h, const float* obs, int n, int mode, const float
         cp[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
         cp[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
         cp[2] += ms * 1e3;
+        std::vector<unsigned long long> sv((size_t)c.nwg * 16);
+        HIPCHK(hipMemcpy(sv.data(), c.stamps, sv.size() * 8, hipMemcpyDeviceToHost));
+        unsigned long long t0s = ~0ull;
+        for (int q = 0; q < c.nwg; ++q) t0s = std::min(t0s, sv[(size_t)q * 16]);
+        for (int k = 1; k < 16; ++k) {  // latest workgroup to reach stamp k, after the first start
+          unsigned long long mx = 0;
+          for (int q = 0; q < c.nwg; ++q) mx = std::max(mx, sv[(size_t)q * 16 + k]);
+          sacc[k] += mx > t0s ? (double)(mx - t0s) * 0.01 : 0.0;  // 100 MHz ticks -> us
+        }
+        HIPCHK(hipMemset(c.stamps, 0, sv.size() * 8));
         if (++ccalls % 2000 == 0) {
           fprintf(stderr, "act chain (us/call): launch %.2f  sync %.2f  kernel (events) %.2f\n", cp[0] / 2000,
                   cp[1] / 2000, cp[2] / 2000);
+          fprintf(stderr, "  stamps (us after first start, latest wg): load %.2f", sacc[1] / 2000);
+          for (int k = 2; k < 15; ++k)
+            if (sacc[k] > 0) fprintf(stderr, " | hand-off %d %.2f", k - 1, sacc[k] / 2000);
+          fprintf(stderr, " | head %.2f\n", sacc[15] / 2000);
           cp[0] = cp[1] = cp[2] = 0;
+          std::fill(sacc.begin(), sacc.end(), 0.0);
         }
       }
       return;

@@ -279,12 +279,15 @@ constexpr int kTraceStride = 4;
 
 // ---------------------------------------------------------------- act graph output
 // Exploration draw e (row-major index row * A + j) of an act call (ActArgs::ctl).
+__device__ __forceinline__ float act_noise(unsigned long long seed, int e, unsigned lo, unsigned hi) {
+  const uint2 key = make_uint2((unsigned)seed, (unsigned)(seed >> 32));
+  const uint4 r = philox(key, make_uint4((unsigned)e, 7u, lo, hi));
+  return normal_from(r.x, r.y);
+}
 template <class AO>  // (ActArgs in the constant address space, or a kernel argument)
 __device__ __forceinline__ float act_eps(const AO& ao, int mode, int e) {
   if (mode == 2) return G(ao.eps)[e];
-  const uint2 key = make_uint2((unsigned)ao.seed, (unsigned)(ao.seed >> 32));
-  const uint4 r = philox(key, make_uint4((unsigned)e, 7u, (unsigned)G(ao.ctl)[1], (unsigned)G(ao.ctl)[2]));
-  return normal_from(r.x, r.y);
+  return act_noise(ao.seed, e, (unsigned)G(ao.ctl)[1], (unsigned)G(ao.ctl)[2]);
 }
 // out = a * scale + bias (numpy float32: two rounded ops)
 template <class AO>
@@ -1823,10 +1826,12 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(const LevelArgs
 
 // ---------------------------------------------------------------- B = 1 act chain (ops.h ActChainArgs)
 // Row block rb of layer L in registers: column block cb = wave + 4 i of the [16][K] strip, lane l
-// holding row l % 16, columns 4 (l / 16) .. +3 of each 1 KB block (K <= 512: at most 8 per lane).
+// holding row l % 16, columns 4 (l / 16) .. +3 of each 1 KB block (K <= 512: at most 8 per lane),
+// and (threads 0..15) the row's bias.
 constexpr int kActPre = 8;
 struct ActW {
   float4 v[kActPre];
+  float b;
 };
 __device__ __forceinline__ void act_load(const ActLayer& L, int rb, ActW& W) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1835,10 +1840,12 @@ __device__ __forceinline__ void act_load(const ActLayer& L, int rb, ActW& W) {
     const int cb = wave + 4 * i;
     W.v[i] = cb < L.cbn ? ld4g(G(L.wn) + ((size_t)rb * L.cbn + cb) * 256 + lane * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  const int row = rb * 16 + (int)threadIdx.x;
+  W.b = threadIdx.x < 16 && row < L.out ? G(L.bias)[row] : 0.f;
 }
 // The 16 rows against the LDS vectors; the 4 lane groups and the 4 waves summed in fixed order.
 // Result (bias, activation) for row r in red[64 + r].
-__device__ __forceinline__ void act_rows(const ActLayer& L, int rb, const ActW& W, const float* vec, float* red) {
+__device__ __forceinline__ void act_rows(const ActLayer& L, const ActW& W, const float* vec, float* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float acc = 0.f;
 #pragma unroll
@@ -1854,9 +1861,8 @@ __device__ __forceinline__ void act_rows(const ActLayer& L, int rb, const ActW& 
   if (lane < 16) red[wave * 16 + lane] = acc;
   __syncthreads();
   if (threadIdx.x < 16) {
-    const int r = threadIdx.x, row = rb * 16 + r;
-    float y = (red[r] + red[16 + r]) + (red[32 + r] + red[48 + r]);
-    y += row < L.out ? G(L.bias)[row] : 0.f;
+    const int r = threadIdx.x;
+    const float y = (red[r] + red[16 + r]) + (red[32 + r] + red[48 + r]) + W.b;
     red[64 + r] = act_fwd(L.act, y);
   }
   __syncthreads();
@@ -1890,72 +1896,124 @@ __device__ __forceinline__ void act_receive(const ActChainArgs& a, int q, float*
   }
 }
 
+// One row block of an exchanged layer: compute from W, publish as {value, tag} granules.
+__device__ __forceinline__ void act_publish(const ActChainArgs& a, int l, int w, const ActW& W, const float* vec,
+                                            float* red) {
+  const ActLayer& L = a.L[l];
+  act_rows(L, W, vec, red);
+  if (threadIdx.x < 16 && w * 16 + (int)threadIdx.x < L.out)  // one 8-byte sc1 store per row
+    __hip_atomic_store(a.xbuf + (size_t)l * kActVec + w * 16 + threadIdx.x,
+                       ((unsigned long long)a.tag << 32) | (unsigned long long)__float_as_uint(red[64 + threadIdx.x]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The act chain as straight-line code (TD7: 6 hidden layers, MLP: 2), so the compiler sees every
+// weight load's place in the in-order load counter: each layer's weights load one hand-off ahead
+// into one of two register sets, and computing a layer waits only for its own set.  Every
+// workgroup owns row block w of every hidden layer (all are H wide: nwg = H / 16).
+template <bool TD7>
 __global__ __launch_bounds__(kThreads, 1) void rle_act_chain(const ActChainArgs a) {
   __shared__ __attribute__((aligned(16))) float vec[8 * kActVec];  // vector slots (0: observation, 7: head)
   __shared__ float red[128];
   const int tid = threadIdx.x, w = blockIdx.x;
-  const unsigned long long tag = (unsigned long long)a.tag << 32;
+  unsigned long long* st = a.stamps ? a.stamps + (size_t)w * 16 : nullptr;
+  auto stamp = [&](int k) {
+    if (st && tid == 0) st[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   const int last = a.nl - 1;
-  ActW W;
-  int next = 0;  // first layer whose row block w exists
-  while (next < last && w >= a.L[next].rbs) ++next;
-  if (next < last) act_load(a.L[next], w, W);
+  const ActLayer& H = a.L[last];
+  const ActArgs& ao = a.ao;
+  // head row blocks of this workgroup: TD7 / TD3 row block w (if any), SAC all in workgroup 0
+  const int hr0 = a.sac ? 0 : w, hr1 = a.sac ? (w == 0 ? H.rbs : 0) : (w < H.rbs ? w + 1 : 0);
+  const bool head = hr1 > hr0;
+  const int j0 = a.sac ? 0 : w * 16;  // head outputs of this workgroup: [j0, j1), one per thread
+  const int j1 = a.sac ? ao.A : min(ao.A, w * 16 + 16);
+  float sc = 0.f, bi = 0.f;           // their action map, prefetched
+  const float sg = sload(ao.sigma);
+  if (j0 + tid < j1) {
+    sc = G(ao.scale)[j0 + tid];
+    bi = G(ao.bias)[j0 + tid];
+  }
+  ActW W, X;
+  act_load(a.L[0], w, W);
+  act_load(a.L[1], w, X);
   for (int i = tid; i < 8 * kActVec; i += kThreads) vec[i] = i < a.Sp ? a.obs[i] : 0.f;
   __syncthreads();
-  for (int l = 0; l < last; ++l) {
-    const ActLayer& L = a.L[l];
-    if (w < L.rbs) {  // produce row block w: one 8-byte {value, tag} sc1 store per row
-      act_rows(L, w, W, vec, red);
-      if (tid < 16 && w * 16 + tid < L.out)
-        __hip_atomic_store(a.xbuf + (size_t)l * kActVec + w * 16 + tid,
-                           tag | (unsigned long long)__float_as_uint(red[64 + tid]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      next = l + 1;
-      while (next < last && w >= a.L[next].rbs) ++next;
-      // the next layer's weights (or the head's) load while this layer is handed off
-      if (next < last) act_load(a.L[next], w, W);
-      else if (w < a.L[last].rbs && !a.sac) act_load(a.L[last], w, W);
-      else if (w == 0 && a.sac) act_load(a.L[last], 0, W);
-    }
-    if (!L.sync) continue;
-    for (int q = l; q >= 0 && (q == l || !a.L[q].sync); --q) act_receive(a, q, vec, red);
+  stamp(1);
+  if constexpr (TD7) {  // 0 fe0 | 1 pi0 (norm) || 2 fe1 || 3 fe2 (norm) || 4 pi1 || 5 pi2 || 6 head
+    act_publish(a, 0, w, W, vec, red);
+    act_load(a.L[2], w, W);
+    act_publish(a, 1, w, X, vec, red);
+    act_load(a.L[3], w, X);
+    stamp(2);
+    act_receive(a, 0, vec, red);
+    act_receive(a, 1, vec, red);
+    stamp(3);
+    act_publish(a, 2, w, W, vec, red);
+    act_load(a.L[4], w, W);
+    act_receive(a, 2, vec, red);
+    stamp(4);
+    act_publish(a, 3, w, X, vec, red);
+    act_load(a.L[5], w, X);
+    act_receive(a, 3, vec, red);
+    stamp(5);
+    act_publish(a, 4, w, W, vec, red);
+    if (head) act_load(H, hr0, W);
+    act_receive(a, 4, vec, red);
+    stamp(6);
+    act_publish(a, 5, w, X, vec, red);
+    if (!head) return;
+    if (hr0 + 1 < hr1) act_load(H, hr0 + 1, X);
+    act_receive(a, 5, vec, red);
+    stamp(7);
+  } else {  // 0 h0 || 1 h1 || 2 head
+    act_publish(a, 0, w, W, vec, red);
+    if (head) act_load(H, hr0, W);
+    act_receive(a, 0, vec, red);
+    stamp(2);
+    act_publish(a, 1, w, X, vec, red);
+    if (!head) return;
+    if (hr0 + 1 < hr1) act_load(H, hr0 + 1, X);
+    act_receive(a, 1, vec, red);
+    stamp(3);
   }
-  // ---- the head: env action (td7.py:141-156, td3.py:114-129, sac.py:132-152).  TD7 / TD3: row
-  // block w of the tanh layer in workgroup w, actions written directly; SAC: workgroup 0, whole.
-  const ActLayer& L = a.L[last];
-  const ActArgs& ao = a.ao;
-  const int nrb = a.sac ? (w == 0 ? L.rbs : 0) : (w < L.rbs ? 1 : 0);
-  if (!nrb) return;
-  const int mode = G(ao.ctl)[0];
-  for (int k = 0; k < nrb; ++k) {
-    const int rb = a.sac ? k : w;
-    if (k) act_load(L, rb, W);
-    act_rows(L, rb, W, vec, red);
+  // ---- the head: env action (td7.py:141-156, td3.py:114-129, sac.py:132-152)
+  for (int rb = hr0; rb < hr1; ++rb) {
+    if (rb == hr0) act_rows(H, W, vec, red);
+    else if (rb == hr0 + 1) act_rows(H, X, vec, red);
+    else {  // (SAC, a third row block: 2A > 32)
+      act_load(H, rb, W);
+      act_rows(H, W, vec, red);
+    }
     if (tid < 16) vec[7 * kActVec + rb * 16 + tid] = red[64 + tid];
     __syncthreads();
   }
   const float* h = vec + 7 * kActVec;
-  const int j0 = a.sac ? 0 : w * 16, j1 = a.sac ? ao.A : min(ao.A, w * 16 + 16);
-  for (int j = j0 + tid; j < j1; j += kThreads) {
+  const int mode = a.mode;
+  const int j = j0 + tid;
+  if (j < j1) {
+    const float e = mode == 2 ? a.eps[j] : (mode ? act_noise(ao.seed, j, a.ctr_lo, a.ctr_hi) : 0.f);
     float act;
     if (a.sac) {
       const float mu = h[j];
       float u = mu;
       if (mode) {
         const float ls = fminf(fmaxf(h[ao.A + j], a.min_log_std), a.max_log_std);
-        u = __fadd_rn(mu, __fmul_rn(act_eps(ao, mode, j), expf(ls)));
+        u = __fadd_rn(mu, __fmul_rn(e, expf(ls)));  // Normal.rsample: loc + eps * scale
       }
       act = tanhf(u);
     } else {
-      act = h[j];  // tanh applied by act_rows (L.act)
-      if (mode) act = __fadd_rn(act, __fmul_rn(act_eps(ao, mode, j), sload(ao.sigma)));
+      act = h[j];  // tanh applied by act_rows (L.act); + exploration_noise * eps, clip
+      if (mode) act = __fadd_rn(act, __fmul_rn(e, sg));
       act = fminf(fmaxf(act, -1.f), 1.f);
     }
-    act_store(ao, 0, j, act);
+    GW(ao.out)[j] = __fadd_rn(__fmul_rn(act, sc), bi);
   }
   // completion for the host's poll: this workgroup's action stores, then its slot := tag with a
   // system-scope release (a plain store, no PCIe atomic)
   __syncthreads();
+  stamp(15);
   if (tid == 0) __hip_atomic_store(a.done + w, a.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -2065,7 +2123,8 @@ hipError_t launch_append(float* state, float* next_state, float* action, float* 
   return hipGetLastError();
 }
 hipError_t launch_act_chain(const ActChainArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(rle_act_chain, dim3(a.nwg), dim3(kThreads), 0, st, a);
+  if (a.nl == 7) hipLaunchKernelGGL(rle_act_chain<true>, dim3(a.nwg), dim3(kThreads), 0, st, a);
+  else hipLaunchKernelGGL(rle_act_chain<false>, dim3(a.nwg), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_fill(float* state, float* next_state, float* action, float* reward, float* notdone,

@@ -428,6 +428,10 @@ struct ActChainArgs {
   int heads;           // head workgroups (0 .. heads-1) that set their `done` slot per call
   int* err;            // 1: a hand-off timed out (pinned)
   unsigned* done;      // [64] per head workgroup: tag of the last call it finished (pinned)
+  unsigned long long* stamps;  // optional [nwg][16] s_memrealtime phase stamps (RLE_ACT_PROF)
+  int mode;            // ActArgs::ctl[0] semantics, carried here (no host-memory read in the kernel)
+  unsigned ctr_lo, ctr_hi;  // Philox counter of this call
+  float eps[32];       // mode 2: the draw [A] (A <= 32)
   ActArgs ao;
   float min_log_std, max_log_std;
   float obs[384];      // the observation (padded, zeros)
