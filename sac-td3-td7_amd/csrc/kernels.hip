@@ -614,13 +614,57 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   // ---- every descriptor field the prologue and the first operand segment need (GemmHot)
   // in ONE batch of scalar loads.  Left to the compiler, each load is issued next to its
   // use, behind branches: one dependent round trip each, ~6 before the first operand load.
+  // The same batch also touches (one dword each) every other 64-byte line of the descriptor
+  // this variant reads later (segments, epilogue, Adam, pre-GEMM fields), so those loads hit
+  // the scalar cache instead of each paying a dependent L2/MALL round trip (+2% steps/s).
+  // Early-clobber outputs: the base must not share SGPRs with a load still being issued.
   u32x16 h0, h1;
-  asm volatile(
-      "s_load_dwordx16 %0, %2, 0x0\n\t"
-      "s_load_dwordx16 %1, %2, 0x40\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=s"(h0), "=s"(h1)
-      : "s"(&g.hot));
+  unsigned dsink;
+#define RLE_HOT_ASM(TOUCH)                                  \
+  asm volatile("s_load_dwordx16 %0, %3, 0x0\n\t"            \
+               "s_load_dwordx16 %1, %3, 0x40\n\t" TOUCH     \
+               "s_waitcnt lgkmcnt(0)"                       \
+               : "=&s"(h0), "=&s"(h1), "=&s"(dsink)         \
+               : "s"(&g.hot))
+#define TL(off) "s_load_dword %2, %3, " #off "\n\t"
+#define TL_A TL(0xb0) TL(0xf0) TL(0x130) TL(0x170)
+#define TL_B TL(0x1b0) TL(0x1f0) TL(0x230) TL(0x270)
+#define TL_S TL(0x2b0)
+#define TL_N TL(0x2f0) TL(0x330)
+#define TL_X TL(0x370)
+#define TL_P TL(0x3b0) TL(0x3f0) TL(0x430) TL(0x470) TL(0x4b0) TL(0x4f0) TL(0x530) TL(0x570) TL(0x5b0) TL(0x5f0)
+#define TL_D TL(0x5f0) TL(0x630)
+#define TL_O TL(0x670)
+#ifdef RLE_NO_TOUCH
+  RLE_HOT_ASM("");
+#else
+  if constexpr (MODE == GEMM_DW) {
+    if constexpr (ACT == kDwNb) RLE_HOT_ASM(TL_B TL_D TL_X);
+    else RLE_HOT_ASM(TL_B TL_D);
+  } else if constexpr (PRE) {
+    if constexpr (MODE == GEMM_FWD && ACT == ACT_TANH) RLE_HOT_ASM(TL_A TL_B TL_S TL_N TL_P);
+    else RLE_HOT_ASM(TL_A TL_B TL_S TL_P);
+  } else if constexpr (EPI == EPI_NBDOT) {
+    RLE_HOT_ASM(TL_A TL_B TL_S TL_X);
+  } else if constexpr (EPI == EPI_ACT) {
+    RLE_HOT_ASM(TL_A TL_B TL_S TL_O);
+  } else if constexpr (EPI == EPI_MSE || EPI == EPI_QHEAD || (MODE == GEMM_FWD && ACT == ACT_TANH)) {
+    RLE_HOT_ASM(TL_A TL_B TL_S TL_N);
+  } else {
+    RLE_HOT_ASM(TL_A TL_B TL_S);
+  }
+#endif
+#undef RLE_HOT_ASM
+#undef TL
+#undef TL_A
+#undef TL_B
+#undef TL_S
+#undef TL_N
+#undef TL_X
+#undef TL_P
+#undef TL_D
+#undef TL_O
+  (void)dsink;
   auto ptr = [](unsigned lo, unsigned hi) { return (const float*)(((unsigned long long)hi << 32) | lo); };
   const int ksl = (int)h0[0], tiles_n = (int)h0[1], tn = (int)h0[2], gN = (int)h0[3], gR = (int)h0[4];
   const float inv_tn = __uint_as_float(h0[5]);

@@ -395,6 +395,14 @@ struct Op {
     FoldBiasArgs fb;
   };
 };
+// kernels.hip gemm_v touches the descriptor's 64-byte lines by fixed offsets from &gemm (its
+// TL_* lists): ops are 64-byte aligned in their tables and the GEMM fields sit at these offsets.
+static_assert(sizeof(Op) % 64 == 0 && offsetof(Op, gemm) == 16, "Op layout (descriptor line touches)");
+static_assert(offsetof(GemmArgs, A) == 0xb0 && offsetof(GemmArgs, B) == 0x1a0 && offsetof(GemmArgs, out) == 0x290 &&
+                  offsetof(GemmArgs, noise) == 0x2f0 && offsetof(GemmArgs, nbx) == 0x370 &&
+                  offsetof(GemmArgs, prea) == 0x3c0 && offsetof(GemmArgs, adam) == 0x600 &&
+                  offsetof(GemmArgs, ao) == 0x670,
+              "GemmArgs layout (descriptor line touches)");
 
 // ---- B = 1 act chain (rle_act_sample, one observation): ONE launch of nwg workgroups
 // (kernels.hip rle_act_chain).  Workgroup w owns row block w of every hidden layer, its next
