@@ -1832,6 +1832,25 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(const LevelArgs
   // (stamp 0 is taken on entry, before the kernel-argument loads)
   unsigned long long* tr = TRACE ? la.trace + (size_t)wg * kTraceStride : nullptr;
   if (TRACE && threadIdx.x == 0) tr[0] = t_in;
+  // Non-GEMM ops (head, sampler, norm backward, priority, step end, ...): their descriptors
+  // are at most 7 lines; touching them all in one batch makes every later descriptor load a
+  // scalar-cache hit instead of a chain of dependent misses.  (GEMM variants touch their own
+  // line sets together with the hot header: gemm_v.)
+  if (kind != OP_GEMM) {
+    unsigned dsink;
+    asm volatile(
+        "s_load_dword %0, %1, 0x0\n\t"
+        "s_load_dword %0, %1, 0x40\n\t"
+        "s_load_dword %0, %1, 0x80\n\t"
+        "s_load_dword %0, %1, 0xc0\n\t"
+        "s_load_dword %0, %1, 0x100\n\t"
+        "s_load_dword %0, %1, 0x140\n\t"
+        "s_load_dword %0, %1, 0x180\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(dsink)
+        : "s"(&op));
+    (void)dsink;
+  }
   FINE_MARK(7);
   switch (kind) {
 #define RLE_OP(K, call)                       \

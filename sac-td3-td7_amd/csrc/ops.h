@@ -398,6 +398,8 @@ struct Op {
 // kernels.hip gemm_v touches the descriptor's 64-byte lines by fixed offsets from &gemm (its
 // TL_* lists): ops are 64-byte aligned in their tables and the GEMM fields sit at these offsets.
 static_assert(sizeof(Op) % 64 == 0 && offsetof(Op, gemm) == 16, "Op layout (descriptor line touches)");
+static_assert(16 + sizeof(HeadArgs) <= 7 * 64 && 16 + sizeof(StepEndArgs) <= 7 * 64 && 16 + sizeof(SampleArgs) <= 7 * 64,
+              "rle_level touches 7 descriptor lines of a non-GEMM op");
 static_assert(offsetof(GemmArgs, A) == 0xb0 && offsetof(GemmArgs, B) == 0x1a0 && offsetof(GemmArgs, out) == 0x290 &&
                   offsetof(GemmArgs, noise) == 0x2f0 && offsetof(GemmArgs, nbx) == 0x370 &&
                   offsetof(GemmArgs, prea) == 0x3c0 && offsetof(GemmArgs, adam) == 0x600 &&
