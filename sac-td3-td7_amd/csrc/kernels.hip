@@ -1805,32 +1805,39 @@ __device__ __forceinline__ void op_foldbias(const CAS FoldBiasArgs& f) {
 
 // TRACE: compiled with the phase stamps (RLE_TRACE=1 runs); the production instance has
 // none, so nothing but the op table is read before the op body starts.
+// The op table entries and the op array pointer are the first 14 dwords of the kernel
+// arguments, scalar arguments that the command processor preloads into SGPRs
+// (-mllvm -amdgpu-kernarg-preload-count=14, Makefile): a workgroup knows its op without
+// a kernel-argument load; its first memory access is its op's descriptor.
+static_assert(kLevelOps == 12, "rle_level takes the op table as 12 scalar arguments");
 template <bool TRACE>
 #ifndef RLE_WAVES
 #define RLE_WAVES 4  // waves per SIMD the register allocation must allow (4 workgroups per CU)
 #endif
-__global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(const LevelArgs la) {
+__global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, unsigned e1, unsigned e2, unsigned e3,
+                                                                  unsigned e4, unsigned e5, unsigned e6, unsigned e7,
+                                                                  unsigned e8, unsigned e9, unsigned e10, unsigned e11,
+                                                                  const Op* ops_arg, unsigned long long* trace_arg) {
   __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
-  // op of this workgroup from the kernel-argument table: straight-line selects over
-  // SGPRs, so all kernel-argument loads go out in one batch (one round trip) and no
-  // descriptor is read before the op is known
+  // op of this workgroup from the (preloaded) entry table: straight-line selects over SGPRs
   const unsigned long long t_in = TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;  // before any load
+  const unsigned entry[kLevelOps] = {e0, e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11};
   const int wg = blockIdx.x;
   int k = 0;
-  unsigned e = la.entry[0];
+  unsigned e = entry[0];
 #pragma unroll
   for (int q = 1; q < kLevelOps; ++q) {
-    const unsigned x = la.entry[q];
+    const unsigned x = entry[q];
     const bool in = (int)(x & 0xffffu) <= wg;
     e = in ? x : e;
     k = in ? q : k;
   }
   const int kind = (e >> 16) & 0xf, vid = e >> 20;
-  const CAS Op* ops = (const CAS Op*)la.ops;
+  const CAS Op* ops = (const CAS Op*)ops_arg;
   const CAS Op& op = ops[k];
   const int t = wg - (int)(e & 0xffffu);
   // (stamp 0 is taken on entry, before the kernel-argument loads)
-  unsigned long long* tr = TRACE ? la.trace + (size_t)wg * kTraceStride : nullptr;
+  unsigned long long* tr = TRACE ? trace_arg + (size_t)wg * kTraceStride : nullptr;
   if (TRACE && threadIdx.x == 0) tr[0] = t_in;
   // Non-GEMM ops (head, sampler, norm backward, priority, step end, ...): their descriptors
   // are at most 7 lines; touching them all in one batch makes every later descriptor load a
@@ -2168,8 +2175,12 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
         la.entry[q] = 0xffffu;
       }
     }
-    if (trace) hipLaunchKernelGGL(rle_level<true>, dim3(w1 - w0), dim3(kThreads), 0, st, la);
-    else hipLaunchKernelGGL(rle_level<false>, dim3(w1 - w0), dim3(kThreads), 0, st, la);
+#define RLE_LEVEL_ARGS                                                                                         \
+  la.entry[0], la.entry[1], la.entry[2], la.entry[3], la.entry[4], la.entry[5], la.entry[6], la.entry[7], \
+      la.entry[8], la.entry[9], la.entry[10], la.entry[11], la.ops, la.trace
+    if (trace) hipLaunchKernelGGL(rle_level<true>, dim3(w1 - w0), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    else hipLaunchKernelGGL(rle_level<false>, dim3(w1 - w0), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+#undef RLE_LEVEL_ARGS
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -449,7 +449,7 @@ struct ActChainArgs {
 
 // Kernel argument of one level launch: the workgroup -> op table travels in the
 // kernarg segment (one scalar load burst) instead of being searched in memory.
-constexpr int kLevelOps = 16;
+constexpr int kLevelOps = 12;  // ops per launch: the op table is 12 preloaded kernel arguments
 struct LevelArgs {
   const Op* ops;
   unsigned long long* trace;  // optional phase timestamps [wg][4] (s_memrealtime, 100 MHz)
