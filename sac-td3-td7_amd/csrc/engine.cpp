@@ -658,6 +658,7 @@ struct Graph {
   std::vector<int> nops, nwg, off;
   std::string desc;
   int nlaunch = 0;  // rle_level dispatches per replay (a level of > kLevelOps ops takes several)
+  std::vector<std::vector<Op>> host_levels;  // the launches' host op tables (RLE_EAGER replays)
   int levels() const { return (int)nops.size(); }
 };
 
@@ -2442,6 +2443,7 @@ struct Engine {
     }
     HIPCHK(hipStreamEndCapture(stream, &G.g));
     HIPCHK(hipGraphInstantiate(&G.x, G.g, nullptr, nullptr, 0));
+    G.host_levels = std::move(levels);
     return G;
   }
 
@@ -2613,7 +2615,16 @@ struct Engine {
   // ---------------------------------------------------------------- run
   long long launches = 0;  // rle_level dispatches enqueued by step graphs (rle_launch_count)
   void launch_graph(const Graph& G) {
-    HIPCHK(hipGraphLaunch(G.x, stream));
+    static const bool eager = [] {
+      const char* e = std::getenv("RLE_EAGER");  // A/B: level launches on the stream, no graph
+      return e && e[0] == '1';
+    }();
+    if (eager && !G.trace) {
+      for (size_t l = 0; l < G.host_levels.size(); ++l)
+        HIPCHK(launch_level(G.d_ops + G.off[l], G.host_levels[l].data(), G.nops[l], G.nwg[l], stream));
+    } else {
+      HIPCHK(hipGraphLaunch(G.x, stream));
+    }
     launches += G.nlaunch;
   }
   void step(int n, float* info_out, float* gpu_ms = nullptr, bool async = false) {

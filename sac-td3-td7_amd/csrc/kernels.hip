@@ -1068,8 +1068,27 @@ __device__ __forceinline__ void op_normbwd(const CAS NormBwdArgs& a, int t) {
 
 // ---------------------------------------------------------------- critic heads
 
-// max(|td|, 1)^0.4 rounded from double (torch's float pow is correctly rounded).
-__device__ __attribute__((noinline)) float lap_priority(float d) { return (float)pow((double)fmaxf(d, 1.f), 0.4); }
+// max(|td|, 1)^0.4 rounded from double (torch's float pow is correctly rounded).  The double pow
+// is ~1.3 us of dependent FP64 work on the loss head's critical path, so: a float seed, two
+// Newton steps on y^5 = x^2 in double (relative error ~1e-15), rounded to float; the exact
+// pow runs only when that double lies within 1e-13 (relative) of a float rounding boundary,
+// where the two could round differently -- otherwise both round to the same float.
+__device__ __attribute__((noinline)) float lap_priority_pow(float x) { return (float)pow((double)x, 0.4); }
+__device__ __forceinline__ float lap_priority(float d) {
+  const float x = fmaxf(d, 1.f);
+  const double x2 = (double)x * (double)x;
+  double y = (double)exp2f(0.4f * log2f(x));
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double y2 = y * y;
+    y = 0.2 * (4.0 * y + x2 / (y2 * y2));
+  }
+  const float f = (float)y;
+  const float nb = __int_as_float(__float_as_int(f) + (y > (double)f ? 1 : -1));  // (f >= 1)
+  const double mid = 0.5 * ((double)f + (double)nb);  // the rounding boundary on y's side of f
+  if (!(fabs(y - mid) > 1e-13 * y)) return lap_priority_pow(x);
+  return f;
+}
 
 // Last critic layer (H -> 1) as a dot product fused with the TD target / loss /
 // priority / policy objective and the gradient into the last hidden layer.  One
