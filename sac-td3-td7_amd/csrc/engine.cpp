@@ -79,18 +79,40 @@ static std::map<uintptr_t, size_t>& live_allocs() {
   return m;
 }
 
+// Zero-filled device buffers.  Small ones (< 1 MB: step scratch, vectors, op tables, ...) are
+// carved out of 32 MB slabs that are zeroed once, each rounded up to a whole page plus a guard
+// page (as a hipMalloc of its own would be padded), so an engine's thousands of buffers cost a
+// few hipMalloc / hipMemset calls instead of one synchronised pair each.
 struct DevMem {
-  std::vector<void*> ptrs;
-  void* alloc(size_t bytes) {
+  static constexpr size_t kSlab = 32u << 20, kSmall = 1u << 20, kPage = 4096;
+  std::vector<std::pair<void*, size_t>> ptrs;  // hipMalloc'd blocks (slabs and large buffers)
+  char* slab = nullptr;
+  size_t slab_used = 0;
+  void* fresh(size_t bytes) {
     void* p = nullptr;
-    if (bytes == 0) bytes = 16;
     HIPCHK(hipMalloc(&p, bytes));
-    live_allocs()[(uintptr_t)p] = bytes;
     HIPCHK(hipMemset(p, 0, bytes));
     // hipMemset runs on the null stream, which does not order against our
     // non-blocking streams: finish it before any stream touches the buffer.
     HIPCHK(hipDeviceSynchronize());
-    ptrs.push_back(p);
+    ptrs.emplace_back(p, bytes);
+    return p;
+  }
+  void* alloc(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    void* p;
+    if (bytes >= kSmall) {
+      p = fresh(bytes);
+    } else {
+      const size_t need = (bytes + kPage - 1) / kPage * kPage + kPage;
+      if (!slab || slab_used + need > kSlab) {
+        slab = static_cast<char*>(fresh(kSlab));
+        slab_used = 0;
+      }
+      p = slab + slab_used;
+      slab_used += need;
+    }
+    live_allocs()[(uintptr_t)p] = bytes;
     return p;
   }
   template <class T>
@@ -98,8 +120,10 @@ struct DevMem {
     return reinterpret_cast<T*>(alloc(n * sizeof(T)));
   }
   ~DevMem() {
-    for (void* p : ptrs) {
-      live_allocs().erase((uintptr_t)p);
+    for (auto& [p, bytes] : ptrs) {
+      auto& m = live_allocs();  // the block's buffers (a large buffer, or a slab's carved ones)
+      const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
+      for (auto it = m.lower_bound(lo); it != m.end() && it->first < hi;) it = m.erase(it);
       (void)hipFree(p);
     }
   }

@@ -73,6 +73,20 @@ for which in graphs:
                 parts.append(f"{name.replace(' ', '_')}:{(tt[:, 3] - tt[:, 0]).max() * 10 / 1000:.1f}"
                              f"@{(tt[:, 0].min() - t0) * 10 / 1000:.1f}")
             print("      ops: " + " ".join(parts))
+            if os.environ.get("RLE_TRACE_OPS"):  # per-op phase medians / maxima (us)
+                o = 0
+                for name, w in re.findall(r"([a-z]+(?:\[[^\]]*\])?)/(\d+)", line.split(":", 1)[1]):
+                    w = int(w)
+                    tt = t[o:o + w]
+                    o += w
+                    ph = lambda a, b: (tt[:, b] - tt[:, a]) * 10 / 1000
+                    f = lambda x: f"{np.median(x):4.1f}/{x.max():4.1f}"
+                    extra = ""
+                    if tr.shape[1] == 16 and "gemm" in name and (tt[:, 11] > 0).all() and (tt[:, 12] > 0).all():
+                        extra = (f" [dec {f(ph(0, 11))} desc {f(ph(11, 12))} pf {f(ph(12, 1))}"
+                                 f" splitK {f(ph(2, 13))} epi {f(ph(13, 3))}]")
+                    print(f"        {name.replace(' ', '_'):32s} start {f((tt[:, 0] - t0) * 10 / 1000)} pro {f(ph(0, 1))}"
+                          f" loop {f(ph(1, 2))} epi {f(ph(2, 3))}{extra}")
         if tr.shape[1] == 16 and line.rstrip().endswith("head/64"):  # fine build: loss head phases
             med = lambda a, b: np.median((t[:, b] - t[:, a]) * 10 / 1000)
             print(f"      head: issue {med(0, 4):5.2f} loads+q {med(4, 5):5.2f} target {med(5, 1):5.2f}"
