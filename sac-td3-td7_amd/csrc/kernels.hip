@@ -704,6 +704,16 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   if constexpr (EPI == EPI_QHEAD) {
     if (jok) qwj = G(g.qw)[nidx(g.qw_cbn, 0, j)];
   }
+  // EPI_MSE: the target tile and the |zs'| partials of its 16 rows (thread t: part t / 16, row
+  // t % 16), so the epilogue does not wait on 4 dependent norm fetches after the loop
+  float4 tgv = make_float4(0.f, 0.f, 0.f, 0.f);
+  float tnv = 0.f;
+  if constexpr (EPI == EPI_MSE) {
+    if (jok) tgv = mat_ld4(g.tgt, ib, j);
+    const CAS NormRef& nr = g.tgt_norm;
+    if (nr.part && (tid >> 4) < nr.nparts && nr.nparts <= 16)
+      tnv = G(nr.part)[(size_t)(tid >> 4) * nr.ld + nr.row0 + i0 + (tid & 15)];
+  }
   float4 nbxv = make_float4(0.f, 0.f, 0.f, 0.f);
   if constexpr (EPI == EPI_NBDOT) {
     if (jok) nbxv = mat_ld4(g.nbx, ib, j);
@@ -939,13 +949,27 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     }
   } else if constexpr (EPI == EPI_MSE) {  // td7.py:256 encoder loss, grad wrt zsa
     float d2 = 0.f;
+    const CAS NormRef& nr = g.tgt_norm;
+    const bool tab = nr.part && nr.nparts <= 16;  // row norms from the prefetched partials
+    if (tab) {
+      tabs[tid] = tnv;
+      __syncthreads();
+    }
     if (jok) {
-      const float4 tv = mat_ld4(g.tgt, ib, j);
-      const float tq[4] = {tv.x, tv.y, tv.z, tv.w};
+      const float tq[4] = {tgv.x, tgv.y, tgv.z, tgv.w};
       float gr[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float d = (acc[q] + pre_b) - tq[q] * norm_inv(g.tgt_norm, ib + q);
+        float inv;
+        if (tab) {  // the sum order, clamp and reciprocal of norm_inv
+          float sm = 0.f;
+          for (int p = 0; p < nr.nparts; ++p) sm += tabs[p * 16 + (ib - i0) + q];
+          const float m = sm / (float)nr.width;
+          inv = 1.f / (m < 1e-8f ? 1e-8f : m);
+        } else {
+          inv = norm_inv(nr, ib + q);
+        }
+        const float d = (acc[q] + pre_b) - tq[q] * inv;
         gr[q] = (2.f * d) * g.mse_scale;  // mse_scale = 1/n
         d2 += d * d;
       }
