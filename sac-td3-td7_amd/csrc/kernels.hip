@@ -1377,13 +1377,17 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
     if (tape & kTapeU) u = G(s.tape_u)[(size_t)pos * s.B + b];
     else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
   }
-  // LAP block sums: thread tid owns blocks [tid*per, tid*per + per), per <= 8 (capacity <= 8M)
+  // LAP block sums: thread tid owns blocks [tid*per, tid*per + per) of the CAPACITY's blocks,
+  // per <= 8 (capacity <= 8M), so the loads go out with the control loads above instead of
+  // after them; blocks past the replay size are zeroed below (exact fp64 sums: the prefix
+  // does not depend on how the blocks are split over threads)
   const int nb = (int)((size + kBlk - 1) / kBlk);
-  const int per = (nb + kThreads - 1) / kThreads;
+  const int nbc = (int)((s.cap + kBlk - 1) / kBlk);
+  const int per = (nbc + kThreads - 1) / kThreads;
   double bs[8];
-  if (!tind && s.lap) {
+  if (s.lap) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) bs[q] = G(s.bsum)[min(tid * per + q, nb - 1)];
+    for (int q = 0; q < 8; ++q) bs[q] = G(s.bsum)[min(tid * per + q, nbc - 1)];
   }
   FINE_MARK(1);
   long long ind;
