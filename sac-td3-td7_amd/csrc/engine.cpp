@@ -197,6 +197,9 @@ struct View {
   // into the consuming DW, kDwNb): row partials of sum_j g x
   const float* nbdot = nullptr;
   int nbdot_ld = 0, nbdot_n = 0, nbdot_id = -1;
+  // EPI_QDOT output: row partials [qd_n][qd_ld] of sum_j y_j w_j (a critic's q before its bias)
+  const float* qd = nullptr;
+  int qd_ld = 0, qd_n = 0, qd_id = -1;
   View sub(int r0, int n) const {
     View v = *this;
     if (m.n || m.t) {
@@ -278,11 +281,17 @@ static void gemm_finalize(GemmArgs& g) {
           "gemm: EPI_NBDOT is a plain DX with x and partials");
   REQUIRE(g.epi != EPI_MSE || act == ACT_NONE, "gemm: MSE epilogue takes no activation");
   REQUIRE((g.dact == ACT_NONE) == (g.dsrc.t == nullptr) || g.mode != GEMM_DX, "gemm: DX derivative source");
-  REQUIRE(!g.has_pre || ((g.mode == GEMM_FWD || g.mode == GEMM_DX) && g.prea.N <= 32 && g.prea.seg < g.A.nseg &&
-                          g.A.seg[g.prea.seg].r1 - g.A.seg[g.prea.seg].r0 <= 32 && g.prea.mode == g.mode &&
-                          g.prea.R % 16 == 0),
+  REQUIRE(g.has_pre != 1 || ((g.mode == GEMM_FWD || g.mode == GEMM_DX) && g.prea.N <= 32 && g.prea.seg < g.A.nseg &&
+                               g.A.seg[g.prea.seg].r1 - g.A.seg[g.prea.seg].r0 <= 32 && g.prea.mode == g.mode &&
+                               g.prea.R % 16 == 0),
           "gemm: pre-GEMM layout");
-  g.vid = gemm_vid(g.mode, g.epi, act, norm, g.has_pre ? 1 : 0);
+  REQUIRE(g.has_pre != 2 || (g.mode == GEMM_DX && g.epi == EPI_STORE && act == ACT_ELU && !norm && g.A.nseg == 1 &&
+                             g.hd.mode == HEAD_TD7_LOSS && g.hd.tgt_mode == HEAD_TD7_TARGET && g.hd.dact == ACT_ELU &&
+                             g.hd.H <= 256 && g.hd.H % 4 == 0 && g.R == r16(g.hd.H) && g.M % 16 == 0 &&
+                             g.hd.rows == g.M && (g.head_n == 0 || g.head_n == 1)),
+          "gemm: fused loss head layout");
+  REQUIRE(g.has_pre >= 0 && g.has_pre <= 2, "gemm: pre kind");
+  g.vid = gemm_vid(g.mode, g.epi, act, norm, g.has_pre);
   REQUIRE(g.tn == 16 || g.tn == 32 || g.tn == 64, "gemm: tile width");
   g.ks_log = g.tn == 16 ? 2 : (g.tn == 32 ? 1 : 0);
   REQUIRE(g.R % 16 == 0, "gemm: reduction length must be a multiple of 16");
@@ -1130,6 +1139,12 @@ struct Engine {
     PreArgs a;
     std::vector<int> rd;
   };
+  // The critic loss head fused into the DX of critic n's last hidden layer (GemmArgs::has_pre 2)
+  struct HeadUse {
+    HeadArgs h;
+    int n;
+    std::vector<int> rd, wr;  // the head's resources (beyond the DX's own)
+  };
   // The actor's tanh output layer L over rows x (+ target smoothing noise) as a pre-GEMM
   // (sale.py:77-83 / mlp.py:55-62, td7.py:188-194, td3.py:154-158).
   PreUse pre_actor_fwd(const Layer& L, const View& x, const View* noise, int seg) {
@@ -1193,7 +1208,7 @@ struct Engine {
 
   View fwd(Prog& pg, const Layer& L, const std::vector<std::vector<View>>& ins, int M, int act, View* pre_out,
            bool normed, const View* noise = nullptr, int noise_row0 = 0, const std::vector<WSeg>* wsegs = nullptr,
-           const View* bias_ovr = nullptr, const PreUse* pre = nullptr) {
+           const View* bias_ovr = nullptr, const PreUse* pre = nullptr, const Layer* qdot = nullptr) {
     REQUIRE(ins.size() == L.seg_p.size(), "fwd: input segment count mismatch for " + L.wname);
     REQUIRE(M % kTileM == 0, "fwd: rows must be a multiple of 16");
     REQUIRE(!wsegs || wsegs->size() == ins.size(), "fwd: one weight block per input segment");
@@ -1240,6 +1255,17 @@ struct Engine {
       out.width = L.out;
       out.norm_id = next_id++;
       wr.push_back(out.norm_id);
+    }
+    float* qpart = nullptr;
+    if (qdot) {  // EPI_QDOT: row partials of the H -> 1 layer qdot applied to this output
+      REQUIRE(!normed && qdot->out == 1 && qdot->K == L.out && act == ACT_ELU, "fwd: q-dot partial layout");
+      qpart = mem.make<float>((size_t)tiles_n * M);
+      out.qd = qpart;
+      out.qd_ld = M;
+      out.qd_n = tiles_n;
+      out.qd_id = next_id++;
+      wr.push_back(out.qd_id);
+      rd.push_back(qdot->res);
     }
     if (noise) rd.push_back(noise->id);
     std::vector<Op> ops;
@@ -1301,6 +1327,13 @@ struct Engine {
         g.norm_out = part + ra;
         g.norm_ld = M;
       }
+      if (qdot) {
+        g.epi = EPI_QDOT;
+        g.qw = P + qdot->wn_off;
+        g.qw_cbn = qdot->cb;
+        g.norm_out = qpart + ra;
+        g.norm_ld = M;
+      }
       if (noise && rb > noise_row0) {
         const int first = std::max(ra, noise_row0);  // first noised row (global)
         g.noise = noise->sub(first - noise_row0, rb - first).m;
@@ -1323,7 +1356,8 @@ struct Engine {
 
   // dX[:, 0:ncols] = sum_t dZ_t W_t[:, col0_t : col0_t + ncols]  (* act'(saved))
   View dx(Prog& pg, const std::vector<DxTerm>& terms, int ncols, int M, int dact, const View* saved,
-          const View* into = nullptr, const View* nb_x = nullptr, const PreUse* pre = nullptr) {
+          const View* into = nullptr, const View* nb_x = nullptr, const PreUse* pre = nullptr,
+          const HeadUse* head = nullptr) {
     Op op{};
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
@@ -1393,6 +1427,13 @@ struct Engine {
       g.has_pre = 1;
       g.prea = pre->a;
       rd.insert(rd.end(), pre->rd.begin(), pre->rd.end());
+    }
+    if (head) {  // A segment 0 is z of critic head->n's last hidden layer, not dZ
+      g.has_pre = 2;
+      g.hd = head->h;
+      g.head_n = head->n;
+      rd.insert(rd.end(), head->rd.begin(), head->rd.end());
+      wr.insert(wr.end(), head->wr.begin(), head->wr.end());
     }
     op.wg_count = g.tiles_m * g.tiles_n;
     pg.add(op, rd, wr);
@@ -1737,6 +1778,7 @@ struct Engine {
     Net* tq[2] = {&net("target_q1"), &net("target_q2")};
     const bool lap = cfg.use_lap;
     const bool nbd = td7_nb_defer();
+    const bool qpart = td7_qdot();  // the loss head's q from EPI_QDOT partials
     use_set(set);
     asc_set = set;
     add_adam_scalars(pg);
@@ -1851,19 +1893,23 @@ struct Engine {
       } else {
         t1 = fwd(pg, tq[n]->layers[1], {{t01}, {tzsa}, {tzs}}, B, ACT_ELU, nullptr, false);
       }
-      th[n] = fwd(pg, tq[n]->layers[2], {{t1}}, B, ACT_ELU, nullptr, false);
+      th[n] = fwd(pg, tq[n]->layers[2], {{t1}}, B, ACT_ELU, nullptr, false, nullptr, 0, nullptr, nullptr, nullptr,
+                  qpart ? &tq[n]->layers[3] : nullptr);
     }
     // ---- online critics on (s, a, zsa_f, zs_f)
     View c01[2], c1[2], c2[2], c1z[2], c2z[2];
     for (int n = 0; n < 2; ++n) {
       c01[n] = fwd(pg, q[n]->layers[0], {{s}, {act_in}}, B, ACT_NONE, nullptr, true);
       c1[n] = fwd(pg, q[n]->layers[1], {{c01[n]}, {fzsa}, {fzs}}, B, ACT_ELU, &c1z[n], false);
-      c2[n] = fwd(pg, q[n]->layers[2], {{c1[n]}}, B, ACT_ELU, &c2z[n], false);
+      c2[n] = fwd(pg, q[n]->layers[2], {{c1[n]}}, B, ACT_ELU, &c2z[n], false, nullptr, 0, nullptr, nullptr, nullptr,
+                  qpart ? &q[n]->layers[3] : nullptr);
     }
     View dz2[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
     View prio = vec(B);
     const int hw = cdiv(B, 4);
     qloss_part = mem.make<float>((size_t)hw * 4);
+    const bool hdx = td7_headdx() && qpart;  // (the fused head reads q partials only)
+    View d1f[2];  // (hdx) dZ of each critic's first hidden layer from the fused head + DX
     {
       // target head (td7.py:211-218) fused: y per row from the target twins, then the loss
       Op op = head_op(HEAD_TD7_LOSS, B);
@@ -1885,10 +1931,41 @@ struct Engine {
       h.dq[1] = dq[1].m;
       h.loss_part = qloss_part;
       h.prio = prio.p;
-      pg.add(op,
-             {c2[0].id, c2[1].id, c2z[0].id, c2z[1].id, q[0]->layers[3].res, q[1]->layers[3].res, th[0].id, th[1].id,
-              tq[0]->layers[3].res, tq[1]->layers[3].res, rw.id, nd.id, R_VT},
-             {dz2[0].id, dz2[1].id, dq[0].id, dq[1].id, prio.id, qloss_id = next_id++, R_VKEYS});
+      std::vector<int> qrd;
+      if (qpart) {
+        for (int n = 0; n < 2; ++n) {
+          h.qp[n] = c2[n].qd;
+          h.tp[n] = th[n].qd;
+          h.qp_n[n] = c2[n].qd_n;
+          h.tp_n[n] = th[n].qd_n;
+          qrd.push_back(c2[n].qd_id);
+          qrd.push_back(th[n].qd_id);
+        }
+        h.qp_ld = c2[0].qd_ld;
+        h.tp_ld = th[0].qd_ld;
+        REQUIRE(c2[1].qd_ld == h.qp_ld && th[1].qd_ld == h.tp_ld && h.qp_n[0] <= 64 && h.qp_n[1] <= 64 &&
+                    h.tp_n[0] <= 64 && h.tp_n[1] <= 64,
+                "head: q partial layout");
+      }
+      qloss_id = next_id++;
+      if (!hdx) {
+        std::vector<int> rd{c2[0].id, c2[1].id, c2z[0].id, c2z[1].id, q[0]->layers[3].res, q[1]->layers[3].res,
+                            th[0].id, th[1].id, tq[0]->layers[3].res, tq[1]->layers[3].res, rw.id, nd.id, R_VT};
+        rd.insert(rd.end(), qrd.begin(), qrd.end());
+        pg.add(op, rd, {dz2[0].id, dz2[1].id, dq[0].id, dq[1].id, prio.id, qloss_id, R_VKEYS});
+      } else {
+        // the head runs inside the DX of each critic's second hidden layer (one level fewer on
+        // the critic chain); critic 0's op stores the priorities, loss partials and value bounds
+        for (int n = 0; n < 2; ++n) {
+          HeadUse hu{h, n,
+                     {c2[0].id, c2[1].id, q[0]->layers[3].res, q[1]->layers[3].res, th[0].id, th[1].id,
+                      tq[0]->layers[3].res, tq[1]->layers[3].res, rw.id, nd.id, R_VT},
+                     {dz2[n].id, dq[n].id}};
+          if (n == 0) hu.wr.insert(hu.wr.end(), {prio.id, qloss_id, R_VKEYS});
+          hu.rd.insert(hu.rd.end(), qrd.begin(), qrd.end());
+          d1f[n] = dx(pg, {{c2z[n], &q[n]->layers[2], 0}}, H, B, ACT_ELU, &c1z[n], nullptr, nullptr, nullptr, &hu);
+        }
+      }
     }
     if (lap) {
       Op op{};
@@ -1906,7 +1983,7 @@ struct Engine {
     for (int n = 0; n < 2; ++n) {  // critic backward + Adam (optim_q_fns spans q1 + q2)
       Net& Q = *q[n];
       dw(pg, Q.layers[3], dq[n], {c2[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
-      View d1 = dx(pg, {{dz2[n], &Q.layers[2], 0}}, H, B, ACT_ELU, &c1z[n]);
+      View d1 = hdx ? d1f[n] : dx(pg, {{dz2[n], &Q.layers[2], 0}}, H, B, ACT_ELU, &c1z[n]);
       dw(pg, Q.layers[2], dz2[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
       View g01 = dx(pg, {{d1, &Q.layers[1], 0}}, H, B, ACT_NONE, nullptr, nullptr, nbd ? &c01[n] : nullptr);
       dw(pg, Q.layers[1], d1, {c01[n], fzsa, fzs}, B, CNT_ADAM_Q, cfg.critic_lr);
@@ -2057,6 +2134,18 @@ struct Engine {
   bool actor_pre() const {
     const char* e = std::getenv("RLE_NO_PRE");
     return A <= 32 && !(e && e[0] == '1');
+  }
+  // The critics' and target critics' last hidden layers emit EPI_QDOT row partials of q, so the
+  // loss head reads 2 x 16 floats per row instead of 4 rows of H.  RLE_NO_QDOT=1: row loads (A/B).
+  bool td7_qdot() const {
+    const char* e = std::getenv("RLE_NO_QDOT");
+    return !(e && e[0] == '1');
+  }
+  // The critic loss head fused into the DX of the critics' second hidden layers (HeadUse):
+  // H <= 256, B a multiple of 16.  RLE_NO_HEADDX=1: the standalone head (tests, A/B).
+  bool td7_headdx() const {
+    const char* e = std::getenv("RLE_NO_HEADDX");
+    return algo == RLE_TD7 && H <= 256 && H % 16 == 0 && B % 16 == 0 && !(e && e[0] == '1');
   }
   // AvgL1Norm backwards that feed only a weight-gradient GEMM are applied inside it
   // (EPI_NBDOT producer + kDwNb consumer: one level fewer).  RLE_NO_NBDEFER=1: separate
@@ -2433,8 +2522,11 @@ struct Engine {
       for (auto& op : levels[l]) {
         G.desc += std::string(" ") + kname[op.kind];
         if (op.kind == OP_GEMM) {
-          static const char* kepi[] = {"st", "adam", "mse", "qhead", "nbdot"};
-          const char* ep = op.gemm.mode == GEMM_DW && op.gemm.act == kDwNb ? "adam+nb" : kepi[op.gemm.epi];
+          static const char* kepi[] = {"st", "adam", "mse", "qhead", "nbdot", "act", "qdot"};
+          static_assert(sizeof(kepi) / sizeof(kepi[0]) == EPI_QDOT + 1, "every epilogue has a name");
+          const char* ep = op.gemm.mode == GEMM_DW && op.gemm.act == kDwNb ? "adam+nb"
+                           : op.gemm.has_pre == 2                         ? "head+dx"
+                                                                           : kepi[op.gemm.epi];
           G.desc += "[" + std::to_string(op.gemm.M) + "x" + std::to_string(op.gemm.N) + "x" +
                     std::to_string(op.gemm.R) + " " + ep + "]";
         }

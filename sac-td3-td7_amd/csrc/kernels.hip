@@ -607,7 +607,153 @@ __device__ __forceinline__ void pre_finish(const CAS PreArgs& p, int i0, PreRing
   __syncthreads();
 }
 
-template <int MODE, int EPI, int ACT, bool NORM, bool PRE = false>
+// max(|td|, 1)^0.4 rounded from double (torch's float pow is correctly rounded).  The double pow
+// is ~1.3 us of dependent FP64 work on the loss head's critical path, so: a float seed, two
+// Newton steps on y^5 = x^2 in double (relative error ~1e-15), rounded to float; the exact
+// pow runs only when that double lies within 1e-13 (relative) of a float rounding boundary,
+// where the two could round differently -- otherwise both round to the same float.
+__device__ __attribute__((noinline)) float lap_priority_pow(float x) { return (float)pow((double)x, 0.4); }
+__device__ __forceinline__ float lap_priority(float d) {
+  const float x = fmaxf(d, 1.f);
+  const double x2 = (double)x * (double)x;
+  double y = (double)exp2f(0.4f * log2f(x));
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double y2 = y * y;
+    y = 0.2 * (4.0 * y + x2 / (y2 * y2));
+  }
+  const float f = (float)y;
+  const float nb = __int_as_float(__float_as_int(f) + (y > (double)f ? 1 : -1));  // (f >= 1)
+  const double mid = 0.5 * ((double)f + (double)nb);  // the rounding boundary on y's side of f
+  if (!(fabs(y - mid) > 1e-13 * y)) return lap_priority_pow(x);
+  return f;
+}
+
+// ---- fused loss head (GemmArgs::has_pre 2): the TD7 critic head (op_head_t, HEAD_TD7_LOSS with
+// the target twins fused, q from EPI_QDOT partials) for the tile's 16 rows, one per lane, then the
+// DX reduction of critic head_n whose A operand dZ = (dq * w3) * act'(z) is formed from z
+// (segment 0) as op_head_t formed dz.  own_wg: this workgroup stores the head's outputs of its
+// rows (tile column 0); own_dz: this wave also stores its dZ chunks (column group 0).
+__device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, int j0, bool active, bool own_wg,
+                                               bool own_dz, int c0, int c1, int nch, const float* a0p, int a0xs,
+                                               const float* b0p, int b0xs, float* smem, f32x4 acc) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const CAS HeadArgs& h = g.hd;
+  const int hn = g.head_n;
+  float* dqs = smem + 64 + 1024;  // [16] dq of critic hn per tile row (the tabs region)
+  float* w3s = dqs + 16;          // [H] critic hn's last-layer weights
+  for (int c = 4 * tid; c < h.H; c += 4 * kThreads) *(float4*)(w3s + c) = ld4g(G(h.w[hn]) + nidx(h.w_cbn, 0, c));
+  // q of the twins and of the target twins for the tile's 16 rows from their EPI_QDOT row
+  // partials: wave w sums quantity w (0 / 1: q of critic 0 / 1, 2 / 3: the target critics' q),
+  // lane l adds partials 16 (l / 16) .. +15 of row l % 16 in order, then the 4 lane groups
+  float* qv = w3s + 256;        // [4][16] the quantities (+ bias)
+  float* acs = qv + 64;         // [2][16] loss terms
+  int* kq = (int*)(acs + 32);   // [16] value keys
+  const int row = lane & 15, grp = lane >> 4;
+  const float* src = wave == 0 ? h.qp[0] : (wave == 1 ? h.qp[1] : (wave == 2 ? h.tp[0] : h.tp[1]));
+  const int np = wave == 0 ? h.qp_n[0] : (wave == 1 ? h.qp_n[1] : (wave == 2 ? h.tp_n[0] : h.tp_n[1]));
+  const int ld = wave < 2 ? h.qp_ld : h.tp_ld;
+  float pv[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int p = grp * 16 + k;
+    pv[k] = p < np ? G(src)[(size_t)p * ld + i0 + row] : 0.f;
+  }
+  float rw = 0.f, ndn = 0.f;
+  if (wave == 0 && lane < 16) {
+    if (h.reward) rw = G(h.reward)[i0 + lane];
+    if (h.notdone) ndn = G(h.notdone)[i0 + lane];
+  }
+  const float bq = sload(wave == 0 ? h.b[0] : (wave == 1 ? h.b[1] : (wave == 2 ? h.tb[0] : h.tb[1])));
+  const float vtmax = h.vt ? sload(h.vt) : 0.f, vtmin = h.vt ? sload(h.vt + 1) : 0.f;
+  float sm = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sm += pv[k];
+  sm += __shfl_xor(sm, 16);
+  sm += __shfl_xor(sm, 32);
+  if (lane < 16) qv[wave * 16 + lane] = sm + bq;
+  __syncthreads();
+  if (wave == 0 && lane < 16) {  // one row per lane (op_head_t HEAD_TD7_LOSS, target fused)
+    const int b = i0 + lane;
+    const float q[2] = {qv[lane], qv[16 + lane]};
+    float v = fminf(qv[32 + lane], qv[48 + lane]);
+    v = fminf(fmaxf(v, vtmin), vtmax);
+    const float yv = rw + (h.gamma * v) * ndn;
+    float dq[2], ac[2], dmax = 0.f;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {  // td7.py:231-244
+      const float diff = q[n] - yv;
+      if (h.lap) {
+        const float d = fabsf(diff);
+        ac[n] = d < 1.f ? 0.5f * (d * d) : d;
+        const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+        dq[n] = (d < 1.f ? d : 1.f) * sg * h.inv_b;
+        dmax = fmaxf(dmax, d);
+      } else {
+        const float e = yv - q[n];
+        ac[n] = e * e;
+        dq[n] = -e * h.inv_b;
+      }
+    }
+    if (own_wg && hn == 0 && h.lap) GW(h.prio)[b] = lap_priority(dmax);
+    const float dqn = hn ? dq[1] : dq[0];
+    if (own_wg && h.dq[hn].t) GW(h.dq[hn].t)[tidx(h.dq[hn].rbs, b, 0)] = dqn;
+    dqs[lane] = dqn;
+    acs[lane] = ac[0];
+    acs[16 + lane] = ac[1];
+    kq[lane] = fkey(yv);
+  }
+  __syncthreads();
+  if (own_wg && hn == 0 && wave == 0) {
+    if (lane < 4 && h.loss_part) {  // op_head_t's partials: its workgroups of 4 rows
+      GAS float* lp = GW(h.loss_part) + (size_t)((i0 >> 2) + lane) * 4;
+      const int r4 = 4 * lane;
+      lp[0] = (acs[r4] + acs[r4 + 1]) + (acs[r4 + 2] + acs[r4 + 3]);
+      lp[1] = (acs[16 + r4] + acs[16 + r4 + 1]) + (acs[16 + r4 + 2] + acs[16 + r4 + 3]);
+      lp[2] = 0.f;
+      lp[3] = 0.f;
+    }
+    if (lane == 0) {  // value_max / value_min (td7.py:217-218)
+      int kmax = kq[0], kmin = kq[0];
+      for (int r = 1; r < 16; ++r) {
+        kmax = max(kmax, kq[r]);
+        kmin = min(kmin, kq[r]);
+      }
+      atomicMax(h.vmax_key, kmax);
+      atomicMin(h.vmin_key, kmin);
+    }
+  }
+  __syncthreads();
+  // ---- the DX reduction over this wave's chunks [c0, c1) of the single A segment
+  if (!active || c0 >= c1) return acc;
+  const float dqr = dqs[lane & 15];
+  const int lb = lane * 16, n = c1 - c0, cq = 4 * (lane >> 4);
+  const int va = ((i0 >> 4) * a0xs + c0) * 1024 + lb;
+  const int vb = ((j0 >> 4) * b0xs + c0) * 1024 + lb;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(a0p), rb = rsrc(b0p);
+  float4 xa[kRing], xb[kRing];
+  ring_issue(xa, xb, ra, va, rb, vb, n, false);
+  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int c = 0; c < n; c += kRing) {
+#pragma unroll
+    for (int r = 0; r < kRing; ++r) {
+      const int k = c0 + c + r;  // absolute chunk
+      const float4 z = xa[r], w = *(const float4*)(w3s + min(k, nch - 1) * 16 + cq);
+      const float4 y = make_float4((dqr * w.x) * act_b<ACT_ELU>(z.x), (dqr * w.y) * act_b<ACT_ELU>(z.y),
+                                   (dqr * w.z) * act_b<ACT_ELU>(z.z), (dqr * w.w) * act_b<ACT_ELU>(z.w));
+      if (own_dz && c + r < n) mat_str4(h.dz[hn], i0 + (lane & 15), k * 16 + cq, y);
+      if (r & 1) acc1 = mfma4(y, xb[r], acc1);
+      else acc = mfma4(y, xb[r], acc);
+      const int nx = c + r + kRing;
+      xa[r] = bload(ra, nx < n ? va + nx * 1024 : kOOB);
+      xb[r] = bload(rb, nx < n ? vb + nx * 1024 : kOOB);
+    }
+  }
+  return acc + acc1;
+}
+
+template <int MODE, int EPI, int ACT, bool NORM, int PK = 0>  // PK: 1 pre-GEMM, 2 fused loss head
 __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -641,14 +787,14 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   if constexpr (MODE == GEMM_DW) {
     if constexpr (ACT == kDwNb) RLE_HOT_ASM(TL_B TL_D TL_X);
     else RLE_HOT_ASM(TL_B TL_D);
-  } else if constexpr (PRE) {
+  } else if constexpr (PK != 0) {
     if constexpr (MODE == GEMM_FWD && ACT == ACT_TANH) RLE_HOT_ASM(TL_A TL_B TL_S TL_N TL_P);
     else RLE_HOT_ASM(TL_A TL_B TL_S TL_P);
   } else if constexpr (EPI == EPI_NBDOT) {
     RLE_HOT_ASM(TL_A TL_B TL_S TL_X);
   } else if constexpr (EPI == EPI_ACT) {
     RLE_HOT_ASM(TL_A TL_B TL_S TL_O);
-  } else if constexpr (EPI == EPI_MSE || EPI == EPI_QHEAD || (MODE == GEMM_FWD && ACT == ACT_TANH)) {
+  } else if constexpr (EPI == EPI_MSE || EPI == EPI_QHEAD || EPI == EPI_QDOT || (MODE == GEMM_FWD && ACT == ACT_TANH)) {
     RLE_HOT_ASM(TL_A TL_B TL_S TL_N);
   } else {
     RLE_HOT_ASM(TL_A TL_B TL_S);
@@ -701,7 +847,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   float4 ds = make_float4(1.f, 1.f, 1.f, 1.f), pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
   size_t wt = 0;
   float qwj = 0.f;
-  if constexpr (EPI == EPI_QHEAD) {
+  if constexpr (EPI == EPI_QHEAD || EPI == EPI_QDOT) {
     if (jok) qwj = G(g.qw)[nidx(g.qw_cbn, 0, j)];
   }
   // EPI_MSE: the target tile and the |zs'| partials of its 16 rows (thread t: part t / 16, row
@@ -770,7 +916,10 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       const float inva = inv_of(q);
       acc = ring_run<NORM ? 1 : 0, 0>(ra, rb, rsrc(sap), va, rsrc(sbp), vb, k1 - k0, acc, inva, nullptr, nullptr, false);
     };
-    if constexpr (PRE) {  // segment g.prea.seg comes from the pre-GEMM in LDS
+    if constexpr (PK == 2) {  // fused loss head: one A segment, dZ of the critic's last hidden layer
+      acc = headdx_reduce(g, i0, j0, active, jt == 0, jt == 0 && cg == 0, c0, c1, nch, a0p, a0xs, b0p, b0xs, smem,
+                          acc);
+    } else if constexpr (PK == 1) {  // segment g.prea.seg comes from the pre-GEMM in LDS
       float* pimg = smem + 64 + 2048;
       PreRing pr;
       pre_issue<MODE>(g.prea, i0, pr);
@@ -859,7 +1008,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   FINE_MARK(9);
 
   // ---- epilogue
-  if constexpr (EPI == EPI_STORE) {
+  if constexpr (EPI == EPI_STORE || EPI == EPI_QDOT) {
     float rowabs[4] = {0.f, 0.f, 0.f, 0.f};
     if (jok) {
       float y[4];
@@ -886,11 +1035,11 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         for (int q = 0; q < 4; ++q) y[q] *= act_b<ACT>(dv[q]);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rowabs[q] = fabsf(y[q]);
+      for (int q = 0; q < 4; ++q) rowabs[q] = EPI == EPI_QDOT ? y[q] * qwj : fabsf(y[q]);
       mat_st4(g.out, ib, j, make_float4(y[0], y[1], y[2], y[3]));
     }
     if constexpr (MODE == GEMM_FWD) {
-      if (g.norm_out) {  // |y| summed over the tile's tn columns, per row
+      if (EPI == EPI_QDOT || g.norm_out) {  // |y| (EPI_QDOT: y w) summed over the tile's tn columns, per row
 #pragma unroll
         for (int q = 0; q < 4; ++q) rowabs[q] = row16_sum(rowabs[q]);
         if ((lane & 15) == 0) *(float4*)(red + wave * 16 + ((lane >> 4) << 2)) =
@@ -1027,7 +1176,12 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
 #define RLE_VP(mode, epi, act, norm)                                  \
   case gemm_vid(mode, epi, act, norm, 1):                            \
     asm volatile("; gemm variant pre " #mode #epi #act #norm ::);    \
-    gemm_v<mode, epi, act, norm, true>(g, t, smem, tr);              \
+    gemm_v<mode, epi, act, norm, 1>(g, t, smem, tr);                 \
+    break;
+#define RLE_VH(mode, epi, act, norm)                                  \
+  case gemm_vid(mode, epi, act, norm, 2):                            \
+    asm volatile("; gemm variant head " #mode #epi #act #norm ::);   \
+    gemm_v<mode, epi, act, norm, 2>(g, t, smem, tr);                 \
     break;
   switch (vid) {
     RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, false)
@@ -1042,6 +1196,7 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, false)
     RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, true)
     RLE_V(GEMM_FWD, EPI_ACT, ACT_TANH, false)
+    RLE_V(GEMM_FWD, EPI_QDOT, ACT_ELU, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_NONE, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_RELU, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_ELU, false)
@@ -1054,10 +1209,12 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_VP(GEMM_FWD, EPI_STORE, ACT_RELU, false)
     RLE_VP(GEMM_FWD, EPI_STORE, ACT_ELU, true)
     RLE_VP(GEMM_DX, EPI_STORE, ACT_RELU, false)
+    RLE_VH(GEMM_DX, EPI_STORE, ACT_ELU, false)
     default: break;
   }
 #undef RLE_V
 #undef RLE_VP
+#undef RLE_VH
 }
 
 // ---------------------------------------------------------------- AvgL1Norm backward
@@ -1092,27 +1249,6 @@ __device__ __forceinline__ void op_normbwd(const CAS NormBwdArgs& a, int t) {
 
 // ---------------------------------------------------------------- critic heads
 
-// max(|td|, 1)^0.4 rounded from double (torch's float pow is correctly rounded).  The double pow
-// is ~1.3 us of dependent FP64 work on the loss head's critical path, so: a float seed, two
-// Newton steps on y^5 = x^2 in double (relative error ~1e-15), rounded to float; the exact
-// pow runs only when that double lies within 1e-13 (relative) of a float rounding boundary,
-// where the two could round differently -- otherwise both round to the same float.
-__device__ __attribute__((noinline)) float lap_priority_pow(float x) { return (float)pow((double)x, 0.4); }
-__device__ __forceinline__ float lap_priority(float d) {
-  const float x = fmaxf(d, 1.f);
-  const double x2 = (double)x * (double)x;
-  double y = (double)exp2f(0.4f * log2f(x));
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const double y2 = y * y;
-    y = 0.2 * (4.0 * y + x2 / (y2 * y2));
-  }
-  const float f = (float)y;
-  const float nb = __int_as_float(__float_as_int(f) + (y > (double)f ? 1 : -1));  // (f >= 1)
-  const double mid = 0.5 * ((double)f + (double)nb);  // the rounding boundary on y's side of f
-  if (!(fabs(y - mid) > 1e-13 * y)) return lap_priority_pow(x);
-  return f;
-}
 
 // Last critic layer (H -> 1) as a dot product fused with the TD target / loss /
 // priority / policy objective and the gradient into the last hidden layer.  One
@@ -1131,18 +1267,26 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
     const int k0 = in0 ? c0 : 0, k1 = in1 ? c1 : 0;
     const bool dz = h.mode != HEAD_TD7_TARGET && h.mode != HEAD_MLP_TARGET;
     const bool fused = h.tgt_mode >= 0;  // target twins in this op too (wave-uniform)
+    const bool qpart = h.qp[0] != nullptr, tpart = fused && h.tp[0] != nullptr;  // EPI_QDOT partials
     float4 hv[2][2], wv[2][2], dv[2][2], tv[2][2], twv[2][2];
+    float qpv[2] = {0.f, 0.f}, tpv[2] = {0.f, 0.f};
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-      hv[n][0] = mat_ldr4(h.h[n], b, k0);
-      hv[n][1] = mat_ldr4(h.h[n], b, k1);
+      if (qpart) {
+        if (lane < h.qp_n[n]) qpv[n] = G(h.qp[n])[(size_t)lane * h.qp_ld + b];
+      } else {
+        hv[n][0] = mat_ldr4(h.h[n], b, k0);
+        hv[n][1] = mat_ldr4(h.h[n], b, k1);
+      }
       wv[n][0] = ld4g(G(h.w[n]) + nidx(h.w_cbn, 0, k0));
       wv[n][1] = ld4g(G(h.w[n]) + nidx(h.w_cbn, 0, k1));
       if (dz) {
         dv[n][0] = mat_ldr4(h.dsrc[n], b, k0);
         dv[n][1] = mat_ldr4(h.dsrc[n], b, k1);
       }
-      if (fused) {
+      if (tpart) {
+        if (lane < h.tp_n[n]) tpv[n] = G(h.tp[n])[(size_t)lane * h.tp_ld + b];
+      } else if (fused) {
         tv[n][0] = mat_ldr4(h.th[n], b, k0);
         tv[n][1] = mat_ldr4(h.th[n], b, k1);
         twv[n][0] = ld4g(G(h.tw[n]) + nidx(h.w_cbn, 0, k0));
@@ -1164,10 +1308,11 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
     };
     float q[2];
 #pragma unroll
-    for (int n = 0; n < 2; ++n) q[n] = dot2(hv[n], wv[n]) + (n ? bias1 : bias0);
+    for (int n = 0; n < 2; ++n) q[n] = (qpart ? wave_sum(qpv[n]) : dot2(hv[n], wv[n])) + (n ? bias1 : bias0);
     FINE_MARK(1);
     if (fused) {  // the TD target of this row (as HEAD_TD7_TARGET / HEAD_MLP_TARGET below)
-      const float qt0 = dot2(tv[0], twv[0]) + sload(h.tb[0]), qt1 = dot2(tv[1], twv[1]) + sload(h.tb[1]);
+      const float qt0 = (tpart ? wave_sum(tpv[0]) : dot2(tv[0], twv[0])) + sload(h.tb[0]);
+      const float qt1 = (tpart ? wave_sum(tpv[1]) : dot2(tv[1], twv[1])) + sload(h.tb[1]);
       float v = fminf(qt0, qt1);
       if (h.tgt_mode == HEAD_TD7_TARGET) v = fminf(fmaxf(v, vtmin), vtmax);
       else if (h.sac) v = v - alpha * lp;
@@ -1887,7 +2032,7 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
   unsigned long long* tr = TRACE ? trace_arg + (size_t)wg * kTraceStride : nullptr;
   if (TRACE && threadIdx.x == 0) tr[0] = t_in;
   // Non-GEMM ops (head, sampler, norm backward, priority, step end, ...): their descriptors
-  // are at most 7 lines; touching them all in one batch makes every later descriptor load a
+  // are at most 8 lines; touching them all in one batch makes every later descriptor load a
   // scalar-cache hit instead of a chain of dependent misses.  (GEMM variants touch their own
   // line sets together with the hot header: gemm_v.)
   if (kind != OP_GEMM) {
@@ -1900,6 +2045,7 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
         "s_load_dword %0, %1, 0x100\n\t"
         "s_load_dword %0, %1, 0x140\n\t"
         "s_load_dword %0, %1, 0x180\n\t"
+        "s_load_dword %0, %1, 0x1c0\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&s"(dsink)
         : "s"(&op));

@@ -89,6 +89,8 @@ enum Epi : int {
   EPI_NBDOT = 4,   // DX whose output g feeds an AvgL1Norm backward deferred into its consumer:
                    // out = g, per-tile row partials of sum_j g x (x: nbx) into norm_out
   EPI_ACT = 5,     // act graph (TD7 / TD3 actor's tanh layer): environment action, ActArgs
+  EPI_QDOT = 6,    // EPI_STORE (forward) + per-tile row partials of sum_j act(z)_j w_j (w: qw, a
+                   // critic's H -> 1 head row) into norm_out: the loss head's q without a row load
 };
 
 // Environment action of an act graph (td7.py:141-156, td3.py:114-129, sac.py:132-152), written
@@ -193,51 +195,6 @@ struct PreArgs {
   Mat dsrc;            // DX: saved tanh output (T image, consumer rows)
 };
 
-struct GemmArgs {
-  GemmHot hot;           // (first: two s_load_dwordx16)
-  int mode;              // GemmMode (operand layouts; every segment of an operand shares it)
-  int M, N, R;           // output rows, output cols (x-extent of B), reduction length
-  int tn;                // tile width: 16 x tn output tile; the 4 waves are tn/16 column groups
-                         // x 64/tn reduction splits (partials summed through LDS, fixed order)
-  int tiles_m, tiles_n;  // tiles_n = cdiv(N, tn), + 1 bias tile column for EPI_ADAM
-  int vid;               // compiled variant (host: gemm_variant): mode, epilogue, activation, norm
-  int ks_log;            // log2(64 / tn): reduction splits per tile
-  float inv_tiles_n;     // 1 / tiles_n (tile row = floor((t + 0.5) * inv_tiles_n))
-  int epi;
-  int act;               // forward activation (EPI_STORE)
-  Operand A, B;
-  Mat out;                         // output images (EPI_STORE, EPI_MSE)
-  const float* bias;
-  Mat pre;                         // pre-activation store, T image (optional)
-  float* norm_out; int norm_ld;    // |y| partials: norm_out[jt * norm_ld + i] (optional)
-  int dact;                        // derivative mask: out *= act'(dsrc(i, j))
-  Mat dsrc;                        // T image
-  Mat noise; int noise_row0; float noise_sigma, noise_clip;  // tanh-noise (T image)
-  Mat tgt; NormRef tgt_norm;       // EPI_MSE target (T image of a normed view)
-  float* loss_part;                // EPI_MSE / EPI_QHEAD per-tile partial sums
-  float mse_scale;                 // 1/n
-  const float* qw; const float* qb; int qw_cbn;  // EPI_QHEAD: head weight row (N image of [1][N]), bias
-  float qscale;                    // EPI_QHEAD: dL/dq
-  Mat nbx; int nbx_xs;             // EPI_NBDOT / kDwNb: x of the AvgL1Norm (T image; DW: its x-block step)
-  NormRef nbm;                     // kDwNb: m of x's rows (producer |x| partials)
-  const float* nbdot; int nbdot_ld, nbdot_n;  // kDwNb: the EPI_NBDOT producer's row partials of sum g x
-  int has_pre;                     // pre-GEMM (PreArgs) in use
-  PreArgs prea;
-  int pad_;
-  AdamArgs adam;
-  ActArgs ao;                      // EPI_ACT
-};
-
-// AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise);
-// 4 rows per workgroup (1 per wave), N images in, N + T images out.
-// fwd = 1: the forward itself, dx = x / m (g = x; diagnostics: rle_eval's zs output).
-struct NormBwdArgs {
-  Mat g, x, dx;
-  int rows, width;
-  NormRef norm;  // partials for m (x rows)
-  int fwd, pad_;
-};
-
 enum HeadMode : int {
   HEAD_TD7_TARGET = 0,   // tq_i, y = r + g*clamp(min, vt_min, vt_max)*nd, vmax/vmin
   HEAD_TD7_LOSS = 1,     // q_i, LAP huber (or MSE), priority, dq, dZ
@@ -276,7 +233,67 @@ struct HeadArgs {                   // 4 rows per workgroup (1 per wave)
   Mat th[2];
   const float* tw[2];
   const float* tb[2];
+  // EPI_QDOT partials of the twins' q (qp) and of the target twins' q (tp): [n][ld], summed over
+  // the n column tiles (null: q is the dot product of the h / th row with w / tw)
+  const float* qp[2];
+  const float* tp[2];
+  int qp_n[2], tp_n[2];  // column tiles of each twin's producer (their tile plans may differ)
+  int qp_ld, tp_ld;
 };
+
+struct GemmArgs {
+  GemmHot hot;           // (first: two s_load_dwordx16)
+  int mode;              // GemmMode (operand layouts; every segment of an operand shares it)
+  int M, N, R;           // output rows, output cols (x-extent of B), reduction length
+  int tn;                // tile width: 16 x tn output tile; the 4 waves are tn/16 column groups
+                         // x 64/tn reduction splits (partials summed through LDS, fixed order)
+  int tiles_m, tiles_n;  // tiles_n = cdiv(N, tn), + 1 bias tile column for EPI_ADAM
+  int vid;               // compiled variant (host: gemm_variant): mode, epilogue, activation, norm
+  int ks_log;            // log2(64 / tn): reduction splits per tile
+  float inv_tiles_n;     // 1 / tiles_n (tile row = floor((t + 0.5) * inv_tiles_n))
+  int epi;
+  int act;               // forward activation (EPI_STORE)
+  Operand A, B;
+  Mat out;                         // output images (EPI_STORE, EPI_MSE)
+  const float* bias;
+  Mat pre;                         // pre-activation store, T image (optional)
+  float* norm_out; int norm_ld;    // |y| partials: norm_out[jt * norm_ld + i] (optional)
+  int dact;                        // derivative mask: out *= act'(dsrc(i, j))
+  Mat dsrc;                        // T image
+  Mat noise; int noise_row0; float noise_sigma, noise_clip;  // tanh-noise (T image)
+  Mat tgt; NormRef tgt_norm;       // EPI_MSE target (T image of a normed view)
+  float* loss_part;                // EPI_MSE / EPI_QHEAD per-tile partial sums
+  float mse_scale;                 // 1/n
+  const float* qw; const float* qb; int qw_cbn;  // EPI_QHEAD: head weight row (N image of [1][N]), bias
+  float qscale;                    // EPI_QHEAD: dL/dq
+  Mat nbx; int nbx_xs;             // EPI_NBDOT / kDwNb: x of the AvgL1Norm (T image; DW: its x-block step)
+  NormRef nbm;                     // kDwNb: m of x's rows (producer |x| partials)
+  const float* nbdot; int nbdot_ld, nbdot_n;  // kDwNb: the EPI_NBDOT producer's row partials of sum g x
+  int has_pre;                     // 1: pre-GEMM (prea) in use; 2: loss head fused into this DX (hd)
+  union {
+    PreArgs prea;
+    // has_pre 2 (TD7 critic backward, engine.cpp build_td7): the HEAD_TD7_LOSS head (target
+    // twins fused) of this tile's rows runs in the workgroup, and the DX's A operand dZ of critic
+    // head_n's last hidden layer = dq * w3 * act'(z) is formed on load from z (segment 0); the
+    // tile-column-0 workgroups store what the standalone head stored (dz / dq of critic head_n;
+    // head_n 0 also the priorities, loss partials and value bounds)
+    HeadArgs hd;
+  };
+  int head_n;
+  AdamArgs adam;
+  ActArgs ao;                      // EPI_ACT
+};
+
+// AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise);
+// 4 rows per workgroup (1 per wave), N images in, N + T images out.
+// fwd = 1: the forward itself, dx = x / m (g = x; diagnostics: rle_eval's zs output).
+struct NormBwdArgs {
+  Mat g, x, dx;
+  int rows, width;
+  NormRef norm;  // partials for m (x rows)
+  int fwd, pad_;
+};
+
 
 enum { kTapeU = 1, kTapeInd = 2, kTapeEps = 4 };
 
@@ -397,9 +414,10 @@ struct Op {
 };
 // kernels.hip gemm_v touches the descriptor's 64-byte lines by fixed offsets from &gemm (its
 // TL_* lists): ops are 64-byte aligned in their tables and the GEMM fields sit at these offsets.
+static_assert(sizeof(HeadArgs) <= sizeof(PreArgs), "GemmArgs: the fused head shares the pre-GEMM's fields");
 static_assert(sizeof(Op) % 64 == 0 && offsetof(Op, gemm) == 16, "Op layout (descriptor line touches)");
-static_assert(16 + sizeof(HeadArgs) <= 7 * 64 && 16 + sizeof(StepEndArgs) <= 7 * 64 && 16 + sizeof(SampleArgs) <= 7 * 64,
-              "rle_level touches 7 descriptor lines of a non-GEMM op");
+static_assert(16 + sizeof(HeadArgs) <= 8 * 64 && 16 + sizeof(StepEndArgs) <= 8 * 64 && 16 + sizeof(SampleArgs) <= 8 * 64,
+              "rle_level touches 8 descriptor lines of a non-GEMM op");
 static_assert(offsetof(GemmArgs, A) == 0xb0 && offsetof(GemmArgs, B) == 0x1a0 && offsetof(GemmArgs, out) == 0x290 &&
                   offsetof(GemmArgs, noise) == 0x2f0 && offsetof(GemmArgs, nbx) == 0x370 &&
                   offsetof(GemmArgs, prea) == 0x3c0 && offsetof(GemmArgs, adam) == 0x600 &&
