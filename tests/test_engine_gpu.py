@@ -123,6 +123,20 @@ def test_step_trajectory_matches_reference(name, burst):
     """per_step: one rle_step(1) per step (single-step graphs), checked after every step.
     burst: the whole taped trajectory in one rle_step(n) (two-step graphs g_pair wherever a
     policy step is followed by a plain step, or any two SAC steps), checked at the end."""
+    _trajectory(name, burst)
+
+
+@pytest.mark.parametrize("variant", ["RLE_NO_HEADDX", "RLE_NO_QDOT"])
+@pytest.mark.parametrize("name", ["td7_tiny", "td7_tiny_nolap", "td7_humanoid"])
+def test_td7_head_variants_match_reference(name, variant, monkeypatch):
+    """The TD7 critic loss head's alternative schedules, read at engine build: RLE_NO_HEADDX
+    runs the head as its own op (q from the EPI_QDOT row partials), RLE_NO_QDOT (implies no
+    fusion) runs it from the critics' last hidden activations with row dot products."""
+    monkeypatch.setenv(variant, "1")
+    _trajectory(name, False)
+
+
+def _trajectory(name, burst):
     g = load_golden(name)
     alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
     eng, rep, tp = engine_from_golden(g)
