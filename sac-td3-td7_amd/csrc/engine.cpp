@@ -26,8 +26,10 @@
 #include "rle.h"
 
 namespace rle {
+// next_ops / next_nops: descriptors of the level launched after this one (prefetched into
+// every XCD's L2 during this level; 0: none)
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
-                        unsigned long long* trace = nullptr);
+                        unsigned long long* trace = nullptr, const Op* next_ops = nullptr, int next_nops = 0);
 int level_capacity();
 int trace_stride();
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
@@ -2547,9 +2549,16 @@ struct Engine {
     }
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     long long tr_off = 0;
+    static const bool dpf = [] {
+      const char* e = std::getenv("RLE_NO_DPF");  // A/B: no next-level descriptor prefetch
+      return !(e && e[0] == '1');
+    }();
     for (size_t l = 0; l < levels.size(); ++l) {
+      // (after the last level: this graph's first, as the next replay is usually of the same graph)
+      const size_t ln = l + 1 < levels.size() ? l + 1 : 0;
       hipError_t e = launch_level(G.d_ops + G.off[l], levels[l].data(), G.nops[l], G.nwg[l], stream,
-                                  G.trace ? G.trace + tr_off * trace_stride() : nullptr);
+                                  G.trace ? G.trace + tr_off * trace_stride() : nullptr, G.d_ops + G.off[ln],
+                                  dpf ? G.nops[ln] : 0);
       tr_off += G.nwg[l];
       if (e != hipSuccess) {
         hipGraph_t tmp;

@@ -923,6 +923,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       float* pimg = smem + 64 + 2048;
       PreRing pr;
       pre_issue<MODE>(g.prea, i0, pr);
+      FINE_MARK(0);
       const int pseg = g.prea.seg;
       for (int q = 0; q < nseg_a; ++q) {
         if (q == pseg) continue;
@@ -930,7 +931,9 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
         seg(sa.p, sa.xs, sa.r0, sa.r1, sb.p, sb.xs, q);
       }
+      FINE_MARK(1);
       pre_finish<MODE>(g.prea, i0, pr, part, smem + 64 + 1024, pimg);
+      FINE_MARK(2);
       const CAS Seg& sa = g.A.seg[pseg];
       const CAS Seg& sb = g.B.seg[wabs ? 0 : pseg];
       const int s0 = sa.r0 >> 4;
@@ -2009,12 +2012,28 @@ template <bool TRACE>
 __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, unsigned e1, unsigned e2, unsigned e3,
                                                                   unsigned e4, unsigned e5, unsigned e6, unsigned e7,
                                                                   unsigned e8, unsigned e9, unsigned e10, unsigned e11,
-                                                                  const Op* ops_arg, unsigned long long* trace_arg) {
+                                                                  const Op* ops_arg, unsigned long long* trace_arg,
+                                                                  const Op* next_arg, unsigned next_lines) {
   __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
   // op of this workgroup from the (preloaded) entry table: straight-line selects over SGPRs
   const unsigned long long t_in = TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;  // before any load
-  const unsigned entry[kLevelOps] = {e0, e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11};
-  const int wg = blockIdx.x;
+  // Entry 0 bit 31: the launch leads with 8 workgroups that only load the next launch's
+  // descriptors into L2, one per XCD (round-robin dispatch).  Between two uses of a descriptor
+  // (one graph replay) tens of MB pass through every L2, so without them the next launch's
+  // first scalar batch goes to the memory-side cache.  They are dispatched first and finish
+  // well within the level; only they read the two (not preloaded) kernel arguments.
+  if ((e0 >> 31) && blockIdx.x < 8) {
+    const unsigned nl = next_lines;
+    const char* nb = (const char*)next_arg;
+    unsigned v0 = 0, v1 = 0;
+    const unsigned l0 = threadIdx.x, l1 = threadIdx.x + kThreads;
+    if (l0 < nl) asm volatile("global_load_dword %0, %1, off" : "=v"(v0) : "v"(nb + l0 * 64) : "memory");
+    if (l1 < nl) asm volatile("global_load_dword %0, %1, off" : "=v"(v1) : "v"(nb + l1 * 64) : "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(v0), "v"(v1) : "memory");
+    return;
+  }
+  const unsigned entry[kLevelOps] = {e0 & 0x7fffffffu, e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11};
+  const int wg = (int)blockIdx.x - (int)(e0 >> 31) * 8;
   int k = 0;
   unsigned e = entry[0];
 #pragma unroll
@@ -2348,17 +2367,24 @@ int level_capacity() {
 }
 
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
-                        unsigned long long* trace) {
+                        unsigned long long* trace, const Op* next_ops, int next_nops) {
   // a level of more than kLevelOps ops runs as consecutive launches of kLevelOps (its
   // ops are independent, so any split is correct)
   for (int q0 = 0; q0 < nops; q0 += kLevelOps) {
     const int n = nops - q0 < kLevelOps ? nops - q0 : kLevelOps;
     const int w0 = h_ops[q0].wg_begin;
     const int w1 = q0 + n < nops ? h_ops[q0 + n].wg_begin : nwg;
-    if (w1 - w0 > kMaxLevelWG) return hipErrorInvalidValue;
+    if (w1 - w0 + 8 > kMaxLevelWG) return hipErrorInvalidValue;
     LevelArgs la{};
     la.ops = d_ops + q0;
     la.trace = trace ? trace + (size_t)w0 * kTraceStride : nullptr;
+    // the following launch's ops: the rest of this level, then the next level's
+    const bool last = q0 + n >= nops;
+    const int nn = !last ? (nops - q0 - n < kLevelOps ? nops - q0 - n : kLevelOps)
+                         : (next_nops < kLevelOps ? next_nops : kLevelOps);
+    const Op* next = !last ? d_ops + q0 + n : next_ops;
+    const unsigned next_lines = (unsigned)(nn * (int)(sizeof(Op) / 64));
+    const int npf = next_lines ? 8 : 0;  // leading prefetch workgroups (entry 0 bit 31)
     for (int q = 0; q < kLevelOps; ++q) {
       if (q < n) {
         const Op& o = h_ops[q0 + q];
@@ -2368,11 +2394,12 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
         la.entry[q] = 0xffffu;
       }
     }
+    if (npf) la.entry[0] |= 0x80000000u;
 #define RLE_LEVEL_ARGS                                                                                         \
   la.entry[0], la.entry[1], la.entry[2], la.entry[3], la.entry[4], la.entry[5], la.entry[6], la.entry[7], \
-      la.entry[8], la.entry[9], la.entry[10], la.entry[11], la.ops, la.trace
-    if (trace) hipLaunchKernelGGL(rle_level<true>, dim3(w1 - w0), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
-    else hipLaunchKernelGGL(rle_level<false>, dim3(w1 - w0), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+      la.entry[8], la.entry[9], la.entry[10], la.entry[11], la.ops, la.trace, next, next_lines
+    if (trace) hipLaunchKernelGGL(rle_level<true>, dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    else hipLaunchKernelGGL(rle_level<false>, dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
 #undef RLE_LEVEL_ARGS
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -85,6 +85,9 @@ for which in graphs:
                     if tr.shape[1] == 16 and "gemm" in name and (tt[:, 11] > 0).all() and (tt[:, 12] > 0).all():
                         extra = (f" [dec {f(ph(0, 11))} desc {f(ph(11, 12))} pf {f(ph(12, 1))}"
                                  f" splitK {f(ph(2, 13))} epi {f(ph(13, 3))}]")
+                        if (tt[:, 4] > 0).all() and (tt[:, 6] > 0).all():  # pre-GEMM consumer phases
+                            extra += (f" [pre issue {f(ph(1, 4))} segs {f(ph(4, 5))} finish {f(ph(5, 6))}"
+                                      f" lds {f(ph(6, 2))}]")
                     print(f"        {name.replace(' ', '_'):32s} start {f((tt[:, 0] - t0) * 10 / 1000)} pro {f(ph(0, 1))}"
                           f" loop {f(ph(1, 2))} epi {f(ph(2, 3))}{extra}")
         if tr.shape[1] == 16 and line.rstrip().endswith("head/64"):  # fine build: loss head phases
