@@ -527,18 +527,19 @@ __device__ __forceinline__ void pre_issue(const CAS PreArgs& p, int i0, PreRing&
     R.b0[r] = bload(rsrc(sb.p), ok ? kb * 1024 + lb : kOOB);
     R.b1[r] = bload(rsrc(sb.p), ok && p.N > 16 ? (sb.xs + kb) * 1024 + lb : kOOB);
   }
+  // (buffer loads at an out-of-range offset return 0: no branch, so no register merge that would
+  // wait for every load in flight)
   const int rb = (lane >> 4) << 2;
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb) {
     const int j = cb * 16 + (lane & 15);
     const bool jok = wave == 0 && j < p.N;
-    R.e[cb] = make_float4(0.f, 0.f, 0.f, 0.f);
-    R.bj[cb] = 0.f;
     if constexpr (MODE == GEMM_FWD) {
-      if (jok && p.bias) R.bj[cb] = G(p.bias)[j];
-      if (jok && p.noise.t) R.e[cb] = mat_ld4(p.noise, i0 + rb, j);
+      R.bj[cb] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(p.bias), jok && p.bias ? j * 4 : kOOB, 0, 0));
+      R.e[cb] = bload(rsrc(p.noise.t), jok && p.noise.t ? (int)tidx(p.noise.rbs, i0 + rb, j) * 4 : kOOB);
     } else {
-      if (jok) R.e[cb] = mat_ld4(p.dsrc, i0 + rb, j);
+      R.bj[cb] = 0.f;
+      R.e[cb] = bload(rsrc(p.dsrc.t), jok ? (int)tidx(p.dsrc.rbs, i0 + rb, j) * 4 : kOOB);
     }
   }
 }
@@ -755,6 +756,7 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
 
 template <int MODE, int EPI, int ACT, bool NORM, int PK = 0>  // PK: 1 pre-GEMM, 2 fused loss head
 __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
+  FINE_MARK(10);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // ---- every descriptor field the prologue and the first operand segment need (GemmHot)
@@ -925,7 +927,10 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       pre_issue<MODE>(g.prea, i0, pr);
       FINE_MARK(0);
       const int pseg = g.prea.seg;
-      for (int q = 0; q < nseg_a; ++q) {
+      // segment 0 from the hot header, outside the loop: a loop header would wait for every
+      // load in flight (the pre-GEMM's included) before the segment's first load is issued
+      if (pseg != 0) seg(a0p, a0xs, a0r0, a0r1, b0p, b0xs, 0);
+      for (int q = 1; q < nseg_a; ++q) {
         if (q == pseg) continue;
         const CAS Seg& sa = g.A.seg[q];
         const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
@@ -2077,7 +2082,11 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     asm volatile("; op case " #K ::);         \
     call;                                     \
     break;
+#ifdef RLE_EXP_TWICE_GEMM  // diagnostics: the stamps of a second, cache-warm pass overwrite the first
+    RLE_OP(OP_GEMM, op_gemm(op.gemm, vid, t, smem, tr); __syncthreads(); op_gemm(op.gemm, vid, t, smem, tr))
+#else
     RLE_OP(OP_GEMM, op_gemm(op.gemm, vid, t, smem, tr))
+#endif
 #ifndef RLE_EXP_GEMM_ONLY
     RLE_OP(OP_NORMBWD, op_normbwd(op.nb, t))
     RLE_OP(OP_SAMPLE_REDUCE, op_sample_reduce(op.sample, t, smem))

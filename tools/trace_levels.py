@@ -99,6 +99,8 @@ for which in graphs:
             gm = g & (t[:, 11] > 0) & (t[:, 12] > 0)
             if gm.any():
                 med = lambda a, b: np.median((t[gm, b] - t[gm, a]) * 10 / 1000)
+                if (t[gm, 14] > 0).all():  # gemm_v entry stamp: switch -> variant, variant entry -> hot batch done
+                    print(f"      gemm: to-variant {med(11, 14):5.2f} hot {med(14, 12):5.2f}")
                 print(f"      gemm: decode {med(0, 11):5.2f} desc {med(11, 12):5.2f} prefetch {med(12, 1):5.2f}"
                       f" | loop {med(1, 2):5.2f} | splitK {med(2, 13):5.2f} epi {med(13, 3):5.2f}")
     print(f"total (gaps + spans) {tot_t:7.2f} us over {len(desc)} levels")
