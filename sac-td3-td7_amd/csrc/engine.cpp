@@ -432,7 +432,7 @@ static void audit_gemm(const GemmArgs& g) {
           if (k0 >= k1) continue;
           const int kb = wabs ? k0 : k0 - s0;
           if (!mine[0] && !mine[1] && !mine[2] && !mine[3]) continue;  // inactive wave: no loads
-          if (!(g.has_pre && q == g.prea.seg)) {
+          if (!(g.has_pre == 1 && q == g.prea.seg)) {
             audit_range(sa.p, ((long long)(i0 / 16) * sa.xs + (k0 - s0)) * 1024, (long long)(k1 - k0) * 1024, "A", g);
             if (sa.norm.part) audit_norm(sa.norm, i0, 16, g);
           }
@@ -440,7 +440,9 @@ static void audit_gemm(const GemmArgs& g) {
             if (mine[cb])
               audit_range(sb.p, ((long long)(jt0 / 16 + cb) * sb.xs + kb) * 1024, (long long)(k1 - k0) * 1024, "B", g);
         }
-        if (g.has_pre) {  // pre-GEMM operands (pre_issue / pre_finish): 16 rows at i0, both column blocks
+        // pre-GEMM operands (pre_issue / pre_finish): 16 rows at i0, both column blocks (has_pre 2,
+        // the fused loss head, keeps HeadArgs in the same union: its reads are not audited here)
+        if (g.has_pre == 1) {
           const PreArgs& p = g.prea;
           const int nchp = p.R / 16, perp = (nchp + 3) / 4;
           const int c0p = w * perp, c1p = std::min(nchp, c0p + perp);
@@ -550,8 +552,7 @@ struct Prog {
       if (op.kind == OP_GEMM) {
         gemm_finalize(op.gemm);
         check_gemm(op.gemm);
-        static const bool audit = std::getenv("RLE_AUDIT") != nullptr;
-        if (audit) audit_gemm(op.gemm);
+        if (std::getenv("RLE_AUDIT")) audit_gemm(op.gemm);  // (read per op: tests set it per engine)
       }
     Item it;
     it.ops = std::move(ops);

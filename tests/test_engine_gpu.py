@@ -136,6 +136,17 @@ def test_td7_head_variants_match_reference(name, variant, monkeypatch):
     _trajectory(name, False)
 
 
+@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid"])
+def test_gemm_address_audit(name, monkeypatch):
+    """RLE_AUDIT=1: every byte range each GEMM op's workgroups can load or store (the kernel's
+    address arithmetic replayed on the host, engine.cpp audit_gemm) lies inside one live device
+    allocation, for every program the engine builds; then one step runs."""
+    monkeypatch.setenv("RLE_AUDIT", "1")
+    g = load_golden(name)
+    eng, rep, tp = engine_from_golden(g)
+    run_with_tapes(eng, tp, 1, lambda t: None)
+
+
 def _trajectory(name, burst):
     g = load_golden(name)
     alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
