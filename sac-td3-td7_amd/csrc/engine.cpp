@@ -2503,8 +2503,10 @@ struct Engine {
   Graph capture(Prog& pg) {
     const char* eb = std::getenv("RLE_BALANCE");  // A/B
     // measured on MI355X (tools/abk.sh, RLE_BALANCE 0/1/2/3): TD3 HalfCheetah 15481/16050/15911/
-    // 15637, SAC Humanoid 7674/8025/7997/7801, TD7 Humanoid 6532/6478/6498/6517 steps/s
-    pg.balance = eb ? std::atoi(eb) : (algo == RLE_TD7 ? 0 : 1);
+    // 15637, SAC Humanoid 7674/8025/7997/7801, TD7 Humanoid 6532/6478/6498/6517 steps/s (round 1);
+    // TD7 after the guarded operand rings: 7744/7774/7720/7754 (4-step graphs), and 6-step
+    // graphs with mode 1: 7822 (tools/abenv.sh)
+    pg.balance = eb ? std::atoi(eb) : 1;
     auto levels = pg.schedule(sched_cap());
     Graph G;
     size_t total = 0;
@@ -2651,9 +2653,10 @@ struct Engine {
   int pair_k() const {
     const char* e = std::getenv("RLE_PAIR");  // A/B experiments
     // measured on MI355X (tools/abk.sh): TD7 Humanoid K=2/4/6/8 -> 6370/6513/6440/6290
-    // steps/s; TD3 HalfCheetah K=2/4/8/12/16 -> 14072/14885/16066/16203/16348 and SAC
-    // Humanoid K=2/4/8 -> 7874/7977/8052 (with the rebalance pass)
-    int k = e ? std::atoi(e) : (algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 4);
+    // steps/s (round 1), K=4/6/8 -> 7744/7785/7789 after the guarded operand rings (with the
+    // rebalance pass: K=6/8 -> 7822/7825); TD3 HalfCheetah K=2/4/8/12/16 -> 14072/14885/16066/
+    // 16203/16348 and SAC Humanoid K=2/4/8 -> 7874/7977/8052 (with the rebalance pass)
+    int k = e ? std::atoi(e) : (algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 6);
     if (algo != RLE_SAC && cfg.policy_freq != 2) k = 0;  // the pattern assumes policy_freq 2
     return k >= 2 ? k & ~1 : 0;
   }

@@ -541,10 +541,11 @@ __device__ __forceinline__ void pre_issue(const CAS PreArgs& p, int i0, PreRing&
   // (buffer loads at an out-of-range offset return 0: no branch, so no register merge that would
   // wait for every load in flight)
   const int rb = (lane >> 4) << 2;
+  if (wave != 0) return;  // (wave 0 runs the epilogue: no loads for the others)
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb) {
     const int j = cb * 16 + (lane & 15);
-    const bool jok = wave == 0 && j < p.N;
+    const bool jok = j < p.N;
     if constexpr (MODE == GEMM_FWD) {
       R.bj[cb] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(p.bias), jok && p.bias ? j * 4 : kOOB, 0, 0));
       R.e[cb] = bload(rsrc(p.noise.t), jok && p.noise.t ? (int)tidx(p.noise.rbs, i0 + rb, j) * 4 : kOOB);

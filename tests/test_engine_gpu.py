@@ -287,10 +287,10 @@ def test_step_async_equals_step_and_seeds_overlap():
 
 
 # (td7_tiny hard-updates every 4 steps, so its bursts run single-step graphs around the hard
-# updates; with target_update_rate 250 it replays the 4-step graph, LAP included)
+# updates; with target_update_rate 250 it replays the 6-step graph, LAP included)
 @pytest.mark.parametrize("name", ["td7_tiny", "td7_tiny@tur250", "td7_tiny_nolap", "td3_tiny", "sac_tiny"])
 def test_multistep_graphs_equal_single_steps(name):
-    """rle_step(20) replays the K-step graphs (TD7 K=4, SAC K=8, TD3 K=16, plus single-step
+    """rle_step(20) replays the K-step graphs (TD7 K=6, SAC K=8, TD3 K=16, plus single-step
     graphs around them); twenty rle_step(1) calls replay single-step graphs only.  Same ops on
     the same data, only grouped into other levels: bit-identical end state."""
     g = dict(load_golden(name.split("@")[0]))
@@ -312,10 +312,10 @@ def test_multistep_graphs_equal_single_steps(name):
 
 
 @pytest.mark.parametrize("alg,env,n", [("td3", "HalfCheetah-v4", 18), ("sac", "Humanoid-v4", 9),
-                                       ("td7", "Ant-v4", 6)])
+                                       ("td7", "Ant-v4", 8)])
 def test_multistep_burst_matches_oracle(alg, env, n):
     """Full-size burst through the multi-step graphs (TD3: one 16-step graph + 2 single steps;
-    SAC: one 8-step graph + 1; TD7: 1 single + one 4-step graph + 1) against the oracle
+    SAC: one 8-step graph + 1; TD7: 1 single + one 6-step graph + 1) against the oracle
     stepped one taped step at a time on the same draws."""
     from oracle import agents
     from test_oracle import build_from_golden
