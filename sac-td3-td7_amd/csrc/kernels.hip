@@ -1556,7 +1556,7 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
   double bs[8];
   if (s.lap) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) bs[q] = G(s.bsum)[min(tid * per + q, nbc - 1)];
+    for (int q = 0; q < 8; ++q) bs[q] = q < per ? G(s.bsum)[min(tid * per + q, nbc - 1)] : 0.0;  // (per: uniform)
   }
   FINE_MARK(1);
   long long ind;
