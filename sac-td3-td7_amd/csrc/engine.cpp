@@ -1204,6 +1204,7 @@ struct Engine {
     p.N = ncols;
     p.R = roff;
     p.seg = seg;
+    REQUIRE(a.m.t, "pre: the saved tanh output needs a T image");
     p.dsrc = a.m;
     u.rd.push_back(a.id);
     return u;
@@ -1211,7 +1212,8 @@ struct Engine {
 
   View fwd(Prog& pg, const Layer& L, const std::vector<std::vector<View>>& ins, int M, int act, View* pre_out,
            bool normed, const View* noise = nullptr, int noise_row0 = 0, const std::vector<WSeg>* wsegs = nullptr,
-           const View* bias_ovr = nullptr, const PreUse* pre = nullptr, const Layer* qdot = nullptr) {
+           const View* bias_ovr = nullptr, const PreUse* pre = nullptr, const Layer* qdot = nullptr,
+           bool pre_n = false) {
     REQUIRE(ins.size() == L.seg_p.size(), "fwd: input segment count mismatch for " + L.wname);
     REQUIRE(M % kTileM == 0, "fwd: rows must be a multiple of 16");
     REQUIRE(!wsegs || wsegs->size() == ins.size(), "fwd: one weight block per input segment");
@@ -1242,10 +1244,12 @@ struct Engine {
     const auto tq = choose_tn(M, L.out);
     const int tn = tq.first;
     const int tiles_n = cdiv(L.out, tn);
-    View out = buf(M, L.out);
+    View out = buf(M, L.out, true, out_t);
     wr.push_back(out.id);
     if (pre_out) {
-      *pre_out = buf(M, L.out);  // T: DX epilogue masks; N: head rows
+      // T: DX epilogue masks; N (pre_n) only where the loss head reads the rows: 4 scattered
+      // stores per lane saved everywhere else
+      *pre_out = buf(M, L.out, pre_n, true);
       wr.push_back(pre_out->id);
     }
     float* part = nullptr;
@@ -1852,14 +1856,18 @@ struct Engine {
       dw(pg, enc.layers[0], dh1, {s}, B, CNT_ADAM_ENC, cfg.policy_lr);
     }
     // ---- fixed encoder on s, fixed target encoder on s'
+    out_t = false;  // forward-only outputs (no weight gradient reads them)
     View fh1 = fwd(pg, fe.layers[0], {{s}}, B, ACT_ELU, nullptr, false);
     View fh2 = fwd(pg, fe.layers[1], {{fh1}}, B, ACT_ELU, nullptr, false);
+    out_t = true;
     View fzs = fwd(pg, fe.layers[2], {{fh2}}, B, ACT_NONE, nullptr, true);
+    out_t = false;
     View th1 = fwd(pg, fet.layers[0], {{s2}}, B, ACT_ELU, nullptr, false);
     View th2 = fwd(pg, fet.layers[1], {{th1}}, B, ACT_ELU, nullptr, false);
     View tzs = fwd(pg, fet.layers[2], {{th2}}, B, ACT_NONE, nullptr, true);
     View fa1 = fwd(pg, fe.layers[3], {{fzs}, {act_in}}, B, ACT_ELU, nullptr, false);
     View fa2 = fwd(pg, fe.layers[4], {{fa1}}, B, ACT_ELU, nullptr, false);
+    out_t = true;
     View fzsa = fwd(pg, fe.layers[5], {{fa2}}, B, ACT_NONE, nullptr, false);
     // ---- actor on [s; s'] (target policy aliases the policy, Q1)
     View ap0 = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_NONE, nullptr, true);
@@ -1874,7 +1882,8 @@ struct Engine {
     const View ap2n = ap2.sub(B, B);
     const PreUse pn1 = prea ? pre_actor_fwd(pi.layers[3], ap2n, &eps, 1) : PreUse{};
     const PreUse* pnext = prea ? &pn1 : nullptr;
-    // ---- target: zsa' and target critics
+    // ---- target: zsa' and target critics (forward only)
+    out_t = false;
     View ta1 = fwd(pg, fet.layers[3], {{tzs}, {a_next}}, B, ACT_ELU, nullptr, false, nullptr, 0, nullptr, nullptr, pnext);
     View ta2 = fwd(pg, fet.layers[4], {{ta1}}, B, ACT_ELU, nullptr, false);
     // zsa' = zsa3(ta2) only feeds the target critics' first hidden layer, a linear map:
@@ -1899,13 +1908,14 @@ struct Engine {
       th[n] = fwd(pg, tq[n]->layers[2], {{t1}}, B, ACT_ELU, nullptr, false, nullptr, 0, nullptr, nullptr, nullptr,
                   qpart ? &tq[n]->layers[3] : nullptr);
     }
+    out_t = true;
     // ---- online critics on (s, a, zsa_f, zs_f)
     View c01[2], c1[2], c2[2], c1z[2], c2z[2];
     for (int n = 0; n < 2; ++n) {
       c01[n] = fwd(pg, q[n]->layers[0], {{s}, {act_in}}, B, ACT_NONE, nullptr, true);
       c1[n] = fwd(pg, q[n]->layers[1], {{c01[n]}, {fzsa}, {fzs}}, B, ACT_ELU, &c1z[n], false);
       c2[n] = fwd(pg, q[n]->layers[2], {{c1[n]}}, B, ACT_ELU, &c2z[n], false, nullptr, 0, nullptr, nullptr, nullptr,
-                  qpart ? &q[n]->layers[3] : nullptr);
+                  qpart ? &q[n]->layers[3] : nullptr, true);
     }
     View dz2[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
     View prio = vec(B);
@@ -1998,8 +2008,9 @@ struct Engine {
       }
     }
     ploss_part = nullptr;
-    if (policy) {  // td7.py:259-276 with the updated critics
+    if (policy) {  // td7.py:259-276 with the updated critics (no weight gradient of these layers)
       View pa1z, pa2z;
+      out_t = false;
       View pa1 = fwd(pg, fe.layers[3], {{fzs}, {a_pi}}, B, ACT_ELU, &pa1z, false);
       View pa2 = fwd(pg, fe.layers[4], {{pa1}}, B, ACT_ELU, &pa2z, false);
       View pzsa = fwd(pg, fe.layers[5], {{pa2}}, B, ACT_NONE, nullptr, false);
@@ -2008,6 +2019,7 @@ struct Engine {
         p01[n] = fwd(pg, q[n]->layers[0], {{s}, {a_pi}}, B, ACT_NONE, nullptr, true);
         p1[n] = fwd(pg, q[n]->layers[1], {{p01[n]}, {pzsa}, {fzs}}, B, ACT_ELU, &p1z[n], false);
       }
+      out_t = true;
       // q2 + q3 + dL/dQ = -1/(2B) fused (EPI_QHEAD): dZ of q2 straight from the GEMM
       ploss_id = next_id++;  // one loss resource per critic: the two heads share a level
       ploss_id2 = next_id++;
@@ -2125,6 +2137,10 @@ struct Engine {
   }
   float* qloss_part = nullptr;
   float* ploss_part = nullptr;
+  // fwd outputs get a T image (weight-gradient B operand) unless out_t is cleared around the
+  // forward-only layers (fixed and target networks, the policy pass through the critics): one
+  // store per lane and the written-back bytes of each such layer saved
+  bool out_t = true;
 
   // Algebraic folds of TD7's linear zsa3 layer into its consumers (build_td7): on when
   // every block is 16-aligned.  RLE_NO_FOLD=1 keeps the unfolded programs (tests).
@@ -2281,7 +2297,9 @@ struct Engine {
     View a_pi = actv.sub(0, B), a_next = prea ? a_pi : actv.sub(B, B);  // (pre: layout only)
     // target critics + y
     View th0[2], th1[2];
+    out_t = false;  // (forward only)
     for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n], prea ? &pn1 : nullptr);
+    out_t = true;
     // online critics
     View c0[2], c1[2];
     for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c0[n], c1[n]);
