@@ -1405,7 +1405,7 @@ struct Engine {
     g.tiles_n = cdiv(ncols, g.tn);
     g.epi = EPI_STORE;
     g.act = ACT_NONE;
-    View out = into ? *into : buf(M, ncols);
+    View out = into ? *into : buf(M, ncols, out_n, out_t);
     if (nb_x) {  // out = g of AvgL1Norm(x): row partials of sum_j g x for the consuming DW (kDwNb)
       REQUIRE(!saved && nb_x->norm && nb_x->m.t && nb_x->rows == M && nb_x->cols == r16(ncols),
               "dx: deferred AvgL1Norm backward operands");
@@ -1532,7 +1532,7 @@ struct Engine {
     Op op{};
     op.kind = OP_NORMBWD;
     NormBwdArgs& a = op.nb;
-    View out = buf(gv.rows, x.width);
+    View out = buf(gv.rows, x.width, out_n, out_t);
     a.g = gv.m;
     a.x = x.m;
     a.dx = out.m;
@@ -1845,7 +1845,9 @@ struct Engine {
       dw(pg, enc.layers[5], ed3, {ea2}, B, CNT_ADAM_ENC, cfg.policy_lr);
       View d1 = dx(pg, {{d2, &enc.layers[4], 0}}, H, B, ACT_ELU, &ea1z);
       dw(pg, enc.layers[4], d2, {ea1}, B, CNT_ADAM_ENC, cfg.policy_lr);
+      out_t = false;  // (read by the norm backward only)
       View gzs = dx(pg, {{d1, &enc.layers[3], 0}}, H, B, ACT_NONE, nullptr);
+      out_t = true;
       dw(pg, enc.layers[3], d1, {ezs, act_in}, B, CNT_ADAM_ENC, cfg.policy_lr);
       View dx3 = normbwd(pg, gzs, ex3.sub(0, B));
       View ez2s = ez2.sub(0, B), ez1s = ez1.sub(0, B);
@@ -1998,7 +2000,9 @@ struct Engine {
       dw(pg, Q.layers[3], dq[n], {c2[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
       View d1 = hdx ? d1f[n] : dx(pg, {{dz2[n], &Q.layers[2], 0}}, H, B, ACT_ELU, &c1z[n]);
       dw(pg, Q.layers[2], dz2[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
+      (nbd ? out_n : out_t) = false;  // (read by the weight gradient / the norm backward only)
       View g01 = dx(pg, {{d1, &Q.layers[1], 0}}, H, B, ACT_NONE, nullptr, nullptr, nbd ? &c01[n] : nullptr);
+      out_n = out_t = true;
       dw(pg, Q.layers[1], d1, {c01[n], fzsa, fzs}, B, CNT_ADAM_Q, cfg.critic_lr);
       if (nbd) {  // AvgL1Norm backward deferred into the weight-gradient GEMM (kDwNb)
         dw(pg, Q.layers[0], g01, {s, act_in}, B, CNT_ADAM_Q, cfg.critic_lr, nullptr, nullptr, &c01[n]);
@@ -2032,24 +2036,30 @@ struct Engine {
         ploss_n += nt;
       }
       View dzp1[2], dxp01[2];
+      out_t = false;  // (no weight gradient of the critics or the fixed encoder in the policy pass)
       for (int n = 0; n < 2; ++n) {
         dzp1[n] = dx(pg, {{dzp2[n], &q[n]->layers[2], 0}}, H, B, ACT_ELU, &p1z[n]);
         View g = dx(pg, {{dzp1[n], &q[n]->layers[1], 0}}, H, B, ACT_NONE, nullptr);
         dxp01[n] = normbwd(pg, g, p01[n]);
       }
+      out_t = true;
       // grad wrt zsa from both critics (q1 input columns [H, 2H))
       View dpa2;
       if (fold) {  // d zsa -> d pa2 through zsa3 folded: G_n = q_n.q1[:, zsa block] x fe.zsa3 (updated critics)
         View G[2];
         for (int n = 0; n < 2; ++n)
           G[n] = dx(pg, {{wview_n(q[n]->layers[1], Hp, H), &fe.layers[5], 0}}, H, H, ACT_NONE, nullptr);
+        out_t = false;
         dpa2 = dx(pg, {{dzp1[0], nullptr, 0, &G[0]}, {dzp1[1], nullptr, 0, &G[1]}}, H, B, ACT_ELU, &pa2z);
+        out_t = true;
       } else {
         View gzsa = dx(pg, {{dzp1[0], &q[0]->layers[1], Hp}, {dzp1[1], &q[1]->layers[1], Hp}}, H, B, ACT_NONE,
                        nullptr);
         dpa2 = dx(pg, {{gzsa, &fe.layers[5], 0}}, H, B, ACT_ELU, &pa2z);
       }
+      out_t = false;
       View dpa1 = dx(pg, {{dpa2, &fe.layers[4], 0}}, H, B, ACT_ELU, &pa1z);
+      out_t = true;
       // d action = sum of three paths, then tanh' (actor output)
       const std::vector<DxTerm> t3{
           {dxp01[0], &q[0]->layers[0], Sp}, {dxp01[1], &q[1]->layers[0], Sp}, {dpa1, &fe.layers[3], Hp}};
@@ -2063,7 +2073,9 @@ struct Engine {
       View dl1 = dx(pg, {{dl2, &pi.layers[2], 0}}, H, B, ACT_RELU, &ap1s);
       dw(pg, pi.layers[2], dl2, {ap1s}, B, CNT_ADAM_PI, cfg.policy_lr);
       const View ap0s = ap0.sub(0, B);
+      (nbd ? out_n : out_t) = false;
       View gl0 = dx(pg, {{dl1, &pi.layers[1], 0}}, H, B, ACT_NONE, nullptr, nullptr, nbd ? &ap0s : nullptr);
+      out_n = out_t = true;
       dw(pg, pi.layers[1], dl1, {ap0s, fzs}, B, CNT_ADAM_PI, cfg.policy_lr);
       if (nbd) {
         dw(pg, pi.layers[0], gl0, {s}, B, CNT_ADAM_PI, cfg.policy_lr, nullptr, nullptr, &ap0s);
@@ -2141,6 +2153,7 @@ struct Engine {
   // forward-only layers (fixed and target networks, the policy pass through the critics): one
   // store per lane and the written-back bytes of each such layer saved
   bool out_t = true;
+  bool out_n = true;  // (the same for the N image: dx / normbwd outputs only a DW reads)
 
   // Algebraic folds of TD7's linear zsa3 layer into its consumers (build_td7): on when
   // every block is 16-aligned.  RLE_NO_FOLD=1 keeps the unfolded programs (tests).
