@@ -1919,11 +1919,14 @@ struct Engine {
       c2[n] = fwd(pg, q[n]->layers[2], {{c1[n]}}, B, ACT_ELU, &c2z[n], false, nullptr, 0, nullptr, nullptr, nullptr,
                   qpart ? &q[n]->layers[3] : nullptr, true);
     }
-    View dz2[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
+    const bool hdx = td7_headdx() && qpart;  // (the fused head reads q partials only)
+    // (dZ of the critics' last hidden layers: with the fused head only their weight gradients
+    // read it, in the T image)
+    View dz2[2] = {buf(B, H, !hdx, true), buf(B, H, !hdx, true)},
+         dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
     View prio = vec(B);
     const int hw = cdiv(B, 4);
     qloss_part = mem.make<float>((size_t)hw * 4);
-    const bool hdx = td7_headdx() && qpart;  // (the fused head reads q partials only)
     View d1f[2];  // (hdx) dZ of each critic's first hidden layer from the fused head + DX
     {
       // target head (td7.py:211-218) fused: y per row from the target twins, then the loss
@@ -2136,7 +2139,7 @@ struct Engine {
     g.epi = EPI_QHEAD;
     g.act = ACT_ELU;
     g.bias = bias(L);
-    View dz = buf(M, L.out);
+    View dz = buf(M, L.out, true, false);  // (read by the input-gradient GEMM only: no weight update here)
     g.out = dz.m;
     g.loss_part = part;
     g.qw = P + Lq.wn_off;
@@ -2257,9 +2260,12 @@ struct Engine {
 
   // MLP critic stack forward: returns (h0, h1)
   void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, View& h0, View& h1,
-                      const PreUse* pre = nullptr) {
+                      const PreUse* pre = nullptr, bool h1_t = true) {
     h0 = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pre);
+    const bool keep = out_t;
+    out_t = keep && h1_t;  // (h1_t = false: only the head reads h1, in the N image)
     h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false);
+    out_t = keep;
   }
 
   // TD3 (td3.py:206-242) and SAC (sac.py:251-295)
@@ -2374,8 +2380,9 @@ struct Engine {
     int ngsq = 0;
     if (policy) {
       View p0[2], p1[2];
-      for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, a_pi, p0[n], p1[n]);
-      View dzp1[2] = {buf(B, H), buf(B, H)};
+      for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, a_pi, p0[n], p1[n], nullptr, false);
+      // (no weight gradient of the critics in the policy pass: the gradients keep N images only)
+      View dzp1[2] = {buf(B, H, true, false), buf(B, H, true, false)};
       ploss_part = mem.make<float>((size_t)hw * 4);
       {
         Op op = head_op(HEAD_MLP_POLICY, B);
@@ -2398,7 +2405,9 @@ struct Engine {
         pg.add(op, rd, {dzp1[0].id, dzp1[1].id, ploss_id = next_id++});
       }
       View dzp0[2];
+      out_t = false;
       for (int n = 0; n < 2; ++n) dzp0[n] = dx(pg, {{dzp1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &p0[n]);
+      out_t = true;
       View dout;
       PreUse pdout{};  // TD3: d1 recomputes dout in-tile
       if (!sac) {
