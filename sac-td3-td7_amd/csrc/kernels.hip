@@ -846,6 +846,12 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     jt = t - it * tiles_n;
   }
   const int i0 = it << 4, j0 = jt * tn + (cg << 4);
+  // the 16 x 64 weight-gradient + Adam tiles are the longest ops of their levels: their waves win
+  // instruction arbitration over the shorter ops sharing a CU (A/B: +0.2-0.3%; also raising the
+  // pre-GEMM and fused-head consumers: no further gain)
+  if constexpr (MODE == GEMM_DW) {
+    if (tn == 64) __builtin_amdgcn_s_setprio(3);
+  }
   const bool bias_tile = EPI == EPI_ADAM && jt * tn >= bias_col;
   const bool lead = kp == 0;
   const bool active = bias_tile ? cg == 0 : j0 < gN;  // wave-uniform
