@@ -102,6 +102,11 @@ int rle_set_adam(rle_engine* e, const char* net, const char* name, int which, co
  * [4] rng step, [5] SAC temperature Adam t. */
 int rle_get_counters(rle_engine* e, long long* out6);
 int rle_set_counters(rle_engine* e, const long long* in6);
+// Philox counter of the act path's exploration draws (rle_act_sample mode 1): carried across
+// engine rebuilds and pickling so a rebuilt agent does not repeat earlier draws (the reference's
+// torch.randn stream, td7.py:153, never restarts either).
+int rle_get_act_counter(rle_engine* e, unsigned long long* out);
+int rle_set_act_counter(rle_engine* e, unsigned long long v);
 /* TD7 value clipping state [value_max, value_min, value_target_max, value_target_min]. */
 int rle_get_value_bounds(rle_engine* e, float* out4);
 int rle_set_value_bounds(rle_engine* e, const float* in4);

@@ -217,7 +217,7 @@ class TD3Oracle:
 
 class SACOracle:
     def __init__(self, nets, A, discount=0.99, policy_lr=3e-4, critic_lr=3e-4, tau=0.005,
-                 min_log_std=-20.0, max_log_std=2.0):
+                 min_log_std=-20.0, max_log_std=2.0, tmp=-1.0):
         self.pi = _params(nets["policy"])
         self.q1 = _params(nets["q1"])
         self.q2 = _params(nets["q2"])
@@ -231,6 +231,10 @@ class SACOracle:
         self.opt_pi = Adam(self.pi.values(), lr=policy_lr)
         self.opt_q = Adam(list(self.q1.values()) + list(self.q2.values()), lr=critic_lr)
         self.opt_t = Adam([self.log_alpha], lr=policy_lr)
+        # sac.py:55-60: tmp >= 0 is a fixed temperature, a plain Python float (no optimizer,
+        # no temperature loss); multiplying an fp32 tensor by it rounds it to fp32 (Q of torch)
+        self.auto = tmp < 0.0
+        self.tmp = None if self.auto else float(tmp)
         self.n_runs = 0
 
     def _dist(self, s, eps):
@@ -246,7 +250,7 @@ class SACOracle:
         with torch.no_grad():
             a2, lp2 = self._dist(s2, eps)
             nq = torch.min(N.mlp_critic(self.tq1, s2, a2), N.mlp_critic(self.tq2, s2, a2))
-            alpha = self.log_alpha.exp()
+            alpha = self.log_alpha.exp() if self.auto else self.tmp  # sac.py:189
             y = r + self.gamma * (nq - alpha * lp2) * nd
         q1, q2 = N.mlp_critic(self.q1, s, a), N.mlp_critic(self.q2, s, a)
         loss_q = torch.mean((y - q1) ** 2.0) * 0.5 + torch.mean((y - q2) ** 2.0) * 0.5
@@ -256,10 +260,19 @@ class SACOracle:
         info["train/q_fn"] = float(loss_q.detach())
         act, lp = self._dist(s, eps_pi)
         qv = torch.min(N.mlp_critic(self.q1, s, act), N.mlp_critic(self.q2, s, act))
-        alpha_d = self.log_alpha.exp().detach()
+        alpha_d = self.log_alpha.exp().detach() if self.auto else self.tmp  # sac.py:227-228
         policy_obj = torch.mean(-qv + lp * alpha_d)
-        tmp_obj = torch.mean(self.log_alpha.exp() * (-lp.detach() - self.target_entropy))
         entropy = -(lp.mean().detach())
+        if not self.auto:  # sac.py:228-236, 271-290 without the temperature terms
+            keys = list(self.pi.keys())
+            gs = torch.autograd.grad(policy_obj, [self.pi[k] for k in keys])
+            self.opt_pi.step(gs)
+            info["train/policy"] = float(policy_obj.detach())
+            info["entropy"] = float(entropy)
+            self._polyak()
+            self.n_runs += 1
+            return info
+        tmp_obj = torch.mean(self.log_alpha.exp() * (-lp.detach() - self.target_entropy))
         obj = policy_obj
         obj += tmp_obj  # in place: logged policy loss includes the temperature loss (Q15)
         keys = list(self.pi.keys())
@@ -271,12 +284,15 @@ class SACOracle:
         info["train/policy"] = float(policy_obj.detach())
         info["train/tmp"] = float(tmp_obj.detach())
         info["entropy"] = float(entropy)
+        self._polyak()
+        self.n_runs += 1
+        return info
+
+    def _polyak(self):
         with torch.no_grad():  # sac.py:243-249
             for src, dst in ((self.q1, self.tq1), (self.q2, self.tq2)):
                 for k in src:
                     dst[k].copy_(self.tau * src[k] + dst[k] * (1 - self.tau))
-        self.n_runs += 1
-        return info
 
     def nets(self):
         return {"policy": self.pi, "q1": self.q1, "q2": self.q2,

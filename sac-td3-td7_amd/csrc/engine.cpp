@@ -18,6 +18,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -75,10 +76,16 @@ static float host_unkey(int k) {
   return f;
 }
 
-// Live device allocations (address -> bytes) for the RLE_AUDIT=1 operand-range check.
+// Live device allocations (address -> bytes) for the RLE_AUDIT=1 operand-range check and the
+// RLE_HAZARD=1 level check.  Engines and replays on other host threads allocate concurrently
+// (ctypes drops the GIL), so every access holds live_mu().
 static std::map<uintptr_t, size_t>& live_allocs() {
   static std::map<uintptr_t, size_t> m;
   return m;
+}
+static std::mutex& live_mu() {
+  static std::mutex mu;
+  return mu;
 }
 
 // Zero-filled device buffers.  Small ones (< 1 MB: step scratch, vectors, op tables, ...) are
@@ -114,7 +121,10 @@ struct DevMem {
       p = slab + slab_used;
       slab_used += need;
     }
-    live_allocs()[(uintptr_t)p] = bytes;
+    {
+      std::lock_guard<std::mutex> lk(live_mu());
+      live_allocs()[(uintptr_t)p] = bytes;
+    }
     return p;
   }
   template <class T>
@@ -122,6 +132,7 @@ struct DevMem {
     return reinterpret_cast<T*>(alloc(n * sizeof(T)));
   }
   ~DevMem() {
+    std::lock_guard<std::mutex> lk(live_mu());
     for (auto& [p, bytes] : ptrs) {
       auto& m = live_allocs();  // the block's buffers (a large buffer, or a slab's carved ones)
       const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
@@ -140,14 +151,33 @@ struct PinMem {
     HIPCHK(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(p, 0, bytes);
     ptrs.push_back(p);
+    std::lock_guard<std::mutex> lk(live_mu());
     live_allocs()[(uintptr_t)p] = bytes;
     return p;
   }
   ~PinMem() {
+    std::lock_guard<std::mutex> lk(live_mu());
     for (void* p : ptrs) {
       live_allocs().erase((uintptr_t)p);
       (void)hipHostFree(p);
     }
+  }
+};
+
+// Named device buffers reused across calls (grown on demand, never shrunk): the replay's eager
+// entry points (sample_indices, update_priority, ...) allocate once instead of per call.
+struct Scratch {
+  DevMem mem;
+  std::map<std::string, std::pair<void*, size_t>> bufs;
+  template <class T>
+  T* get(const std::string& name, size_t n) {
+    const size_t bytes = std::max<size_t>(n * sizeof(T), 16);
+    auto& b = bufs[name];
+    if (b.second < bytes) {
+      b.first = mem.alloc(bytes);
+      b.second = bytes;
+    }
+    return static_cast<T*>(b.first);
   }
 };
 
@@ -169,6 +199,7 @@ struct Replay {
   int maxred_nwg = 256;
   hipStream_t stream = nullptr;
   DevMem mem;
+  Scratch scratch;  // eager entry points' temporaries
   // append staging
   float* stage = nullptr;
   long long stage_rows = 0;
@@ -366,9 +397,24 @@ static void xcd_plan(GemmArgs& g) {
 // ---- RLE_AUDIT=1: every byte range a GEMM op's workgroups can touch (the address arithmetic of
 // kernels.hip gemm_v / pre_issue / pre_finish, replayed on the host) must lie inside one live
 // device allocation.  A debugging aid for new tile layouts; off in production.
-static void audit_range(const void* base, long long lo, long long bytes, const char* what, const GemmArgs& g) {
+// RLE_HAZARD=1 reuses the same address replay to collect each op's byte ranges (Access) instead
+// of checking them against the allocations: see level_hazards().
+struct Access {
+  uintptr_t lo, hi;
+  int w;  // 1: the op stores (or atomically updates) these bytes
+  const char* what;
+};
+static thread_local std::vector<Access>* g_sink = nullptr;
+
+static void audit_range(const void* base, long long lo, long long bytes, const char* what, const GemmArgs& g,
+                        int w = 0) {
   if (bytes <= 0) return;
   const uintptr_t a = (uintptr_t)base + (uintptr_t)lo, b = a + (uintptr_t)bytes;
+  if (g_sink) {
+    g_sink->push_back({a, b, w, what});
+    return;
+  }
+  std::lock_guard<std::mutex> lk(live_mu());
   auto& m = live_allocs();
   auto it = m.upper_bound(a);
   bool ok = base != nullptr && lo >= 0 && it != m.begin();
@@ -388,9 +434,9 @@ static long long h_nblk(int cbn, int r, int c) { return ((long long)(r >> 4) * c
 static long long h_tblk(int rbs, int r, int c) { return ((long long)(c >> 4) * rbs + (r >> 4)) * 1024; }
 
 static void audit_mat(const Mat& m, int r, int c, const char* what, const GemmArgs& g, bool need_n = false,
-                      bool need_t = false) {
-  if (m.n) audit_range(m.n, h_nblk(m.cbn, r, c), 1024, what, g);
-  if (m.t) audit_range(m.t, h_tblk(m.rbs, r, c), 1024, what, g);
+                      bool need_t = false, int w = 0) {
+  if (m.n) audit_range(m.n, h_nblk(m.cbn, r, c), 1024, what, g, w);
+  if (m.t) audit_range(m.t, h_tblk(m.rbs, r, c), 1024, what, g, w);
   if (need_n && !m.n) throw Error{RLE_EINVAL, std::string("audit: no N image for ") + what};
   if (need_t && !m.t) throw Error{RLE_EINVAL, std::string("audit: no T image for ") + what};
 }
@@ -499,22 +545,22 @@ static void audit_gemm(const GemmArgs& g) {
         case EPI_ADAM: {
           const AdamArgs& ad = g.adam;
           if (bias_tile) {
-            for (long long o : {0LL, ad.mo, ad.vo}) audit_range(ad.b, (o + i0) * 4, 64, "adam bias", g);
+            for (long long o : {0LL, ad.mo, ad.vo}) audit_range(ad.b, (o + i0) * 4, 64, "adam bias", g, 1);
           } else {
             for (long long o : {0LL, ad.mo, ad.vo})
-              audit_range(ad.w.t, o * 4 + h_tblk(ad.w.rbs, i0, j0), 1024, "adam w.t", g);
-            audit_range(ad.w.n, h_nblk(ad.w.cbn, i0, j0), 1024, "adam w.n", g);
+              audit_range(ad.w.t, o * 4 + h_tblk(ad.w.rbs, i0, j0), 1024, "adam w.t", g, 1);
+            audit_range(ad.w.n, h_nblk(ad.w.cbn, i0, j0), 1024, "adam w.n", g, 1);
           }
           if (ad.gsq) {
-            if (bias_tile) audit_range(ad.gsq_b, (long long)it * 4, 4, "gsq_b", g);
-            else audit_range(ad.gsq, ((long long)it * (g.tiles_n - 1) + jt) * 4, 4, "gsq", g);
+            if (bias_tile) audit_range(ad.gsq_b, (long long)it * 4, 4, "gsq_b", g, 1);
+            else audit_range(ad.gsq, ((long long)it * (g.tiles_n - 1) + jt) * 4, 4, "gsq", g, 1);
           }
           break;
         }
         default: {
-          audit_mat(g.out, i0, j0, "out", g);
+          audit_mat(g.out, i0, j0, "out", g, false, false, 1);
           if (g.bias) audit_range(g.bias, (long long)j0 * 4, (long long)ncol * 4, "bias", g);
-          if (g.mode == GEMM_FWD && g.pre.t) audit_mat(g.pre, i0, j0, "pre-act", g);
+          if (g.mode == GEMM_FWD && g.pre.t) audit_mat(g.pre, i0, j0, "pre-act", g, false, false, 1);
           if (g.mode == GEMM_DX && g.dact != ACT_NONE) audit_mat(g.dsrc, i0, j0, "dsrc", g, false, true);
           if (g.noise.t && i0 + 15 >= g.noise_row0) {
             const int r0 = std::max(i0, g.noise_row0) - g.noise_row0;
@@ -526,16 +572,278 @@ static void audit_gemm(const GemmArgs& g) {
             audit_mat(g.tgt, i0, j0, "tgt", g, false, true);
             audit_norm(g.tgt_norm, i0, 16, g);
           }
-          if (g.epi == EPI_QHEAD) audit_range(g.qw, h_nblk(g.qw_cbn, 0, j0), 1024, "qw", g);
-          if (g.norm_out) audit_range(g.norm_out, ((long long)jt * g.norm_ld + i0) * 4, 64, "norm_out", g);
-          if (g.epi == EPI_MSE || g.epi == EPI_QHEAD) audit_range(g.loss_part, (long long)t * 4, 4, "loss_part", g);
+          if (g.epi == EPI_QHEAD || g.epi == EPI_QDOT) audit_range(g.qw, h_nblk(g.qw_cbn, 0, j0), 1024, "qw", g);
+          if (g.epi == EPI_QHEAD && t == 0) audit_range(g.qb, 0, 4, "qb", g);
+          if (g.norm_out) audit_range(g.norm_out, ((long long)jt * g.norm_ld + i0) * 4, 64, "norm_out", g, 1);
+          if (g.epi == EPI_MSE || g.epi == EPI_QHEAD) audit_range(g.loss_part, (long long)t * 4, 4, "loss_part", g, 1);
         }
+      }
+    }
+  }
+  if (g.epi == EPI_ADAM) {  // this step's bias corrections (Ctrl / adamsc1)
+    audit_range(g.adam.step, 0, 4, "adam step", g);
+    audit_range(g.adam.bc2s, 0, 4, "adam bc2s", g);
+  }
+  if (g.has_pre == 2) {  // the fused loss head (kernels.hip headdx_reduce), tile rows i0 .. i0 + 15
+    const HeadArgs& h = g.hd;
+    const int hn = g.head_n;
+    audit_range(h.w[hn], 0, (long long)h.w_cbn * 1024, "head w3", g);
+    for (int n = 0; n < 2; ++n) {
+      audit_range(h.b[n], 0, 4, "head b3", g);
+      audit_range(h.tb[n], 0, 4, "head tb3", g);
+    }
+    if (h.vt) audit_range(h.vt, 0, 8, "head vt", g);
+    for (int it = 0; it < g.tiles_m; ++it) {
+      const int i0 = it * 16;
+      for (int n = 0; n < 2; ++n) {
+        for (int p = 0; p < h.qp_n[n]; ++p) audit_range(h.qp[n], ((long long)p * h.qp_ld + i0) * 4, 64, "head qp", g);
+        for (int p = 0; p < h.tp_n[n]; ++p) audit_range(h.tp[n], ((long long)p * h.tp_ld + i0) * 4, 64, "head tp", g);
+      }
+      if (h.reward) audit_range(h.reward, (long long)i0 * 4, 64, "head reward", g);
+      if (h.notdone) audit_range(h.notdone, (long long)i0 * 4, 64, "head notdone", g);
+      // tile column 0 stores the head's outputs of its rows
+      if (hn == 0 && h.lap) audit_range(h.prio, (long long)i0 * 4, 64, "head prio", g, 1);
+      if (h.dq[hn].t) audit_range(h.dq[hn].t, h_tblk(h.dq[hn].rbs, i0, 0), 1024, "head dq", g, 1);
+      for (int c = 0; c < g.R; c += 16) audit_mat(h.dz[hn], i0, c, "head dz", g, false, false, 1);
+      if (hn == 0) {
+        if (h.loss_part) audit_range(h.loss_part, (long long)(i0 / 4) * 16, 64, "head loss", g, 1);
+        audit_range(h.vmax_key, 0, 4, "head vmax", g, 1);
+        audit_range(h.vmin_key, 0, 4, "head vmin", g, 1);
       }
     }
   }
   if (g.mode == GEMM_DW && g.act == kDwNb) {
     audit_norm(g.nbm, 0, g.R, g);
     for (int p = 0; p < g.nbdot_n; ++p) audit_range(g.nbdot, (long long)p * g.nbdot_ld * 4, (long long)g.R * 4, "nbdot", g);
+  }
+}
+
+// ---- RLE_HAZARD=1: byte-level check of every level's ops against each other.  The scheduler
+// orders ops by declared resources; this replays what each op's workgroups actually touch
+// (GEMMs: audit_gemm's per-tile address replay; other ops: their descriptor's buffers, a tensor
+// image from its pointer to the end of its allocation) and fails the build if a byte one op of a
+// level stores is read or stored by another op of the same level -- a race whose outcome would
+// depend on workgroup timing.  Ops of one program item (row pieces of one GEMM) are exempt from
+// each other: they write disjoint rows by construction.
+static uintptr_t alloc_end(const void* p) {
+  std::lock_guard<std::mutex> lk(live_mu());
+  auto& m = live_allocs();
+  auto it = m.upper_bound((uintptr_t)p);
+  if (it == m.begin()) return (uintptr_t)p + 4;
+  --it;
+  const uintptr_t e = it->first + it->second;
+  return (uintptr_t)p < e ? e : (uintptr_t)p + 4;
+}
+static void acc_whole(std::vector<Access>& v, const void* p, int w, const char* what) {
+  if (p) v.push_back({(uintptr_t)p, alloc_end(p), w, what});
+}
+static void acc_bytes(std::vector<Access>& v, const void* p, long long bytes, int w, const char* what) {
+  if (p && bytes > 0) v.push_back({(uintptr_t)p, (uintptr_t)p + (uintptr_t)bytes, w, what});
+}
+static void acc_mat(std::vector<Access>& v, const Mat& m, int w, const char* what) {
+  acc_whole(v, m.n, w, what);
+  acc_whole(v, m.t, w, what);
+}
+static void op_accesses(const Op& op, std::vector<Access>& v) {
+  switch (op.kind) {
+    case OP_GEMM: {
+      g_sink = &v;
+      audit_gemm(op.gemm);
+      g_sink = nullptr;
+      break;
+    }
+    case OP_NORMBWD: {
+      const NormBwdArgs& a = op.nb;
+      acc_mat(v, a.g, 0, "nb g");
+      acc_mat(v, a.x, 0, "nb x");
+      acc_whole(v, a.norm.part, 0, "nb norm");
+      acc_mat(v, a.dx, 1, "nb dx");
+      break;
+    }
+    case OP_SAMPLE_REDUCE:
+    case OP_SAMPLE_GATHER:
+    case OP_NOISE: {
+      const SampleArgs& s = op.sample;
+      acc_bytes(v, s.size, 8, 0, "sample size");
+      acc_bytes(v, s.tape_mode, 4, 0, "tape mode");
+      acc_bytes(v, s.tape_pos, 8, 0, "tape pos");
+      acc_bytes(v, s.ctrl_rng, 8, 0, "rng step");
+      if (op.kind == OP_NOISE) {
+        acc_whole(v, s.tape_eps, 0, "tape eps");
+        acc_whole(v, s.tape_eps2, 0, "tape eps2");
+        acc_mat(v, s.eps, 1, "eps");
+        acc_mat(v, s.eps2, 1, "eps2");
+        break;
+      }
+      acc_whole(v, s.priority, 0, "priority");
+      acc_whole(v, s.bsum, op.kind == OP_SAMPLE_REDUCE, "bsum");
+      if (op.kind == OP_SAMPLE_REDUCE) break;
+      for (const void* r : {(const void*)s.state, (const void*)s.next_state, (const void*)s.action,
+                            (const void*)s.reward, (const void*)s.notdone})
+        acc_whole(v, r, 0, "replay");
+      acc_whole(v, s.tape_u, 0, "tape u");
+      acc_whole(v, s.tape_ind, 0, "tape ind");
+      acc_mat(v, s.ss, 1, "batch ss");
+      acc_mat(v, s.a, 1, "batch a");
+      acc_whole(v, s.r, 1, "batch r");
+      acc_whole(v, s.nd, 1, "batch nd");
+      acc_whole(v, s.ind, 1, "batch ind");
+      acc_whole(v, s.u_out, 1, "batch u");
+      break;
+    }
+    case OP_HEAD: {
+      const HeadArgs& h = op.head;
+      for (int n = 0; n < 2; ++n) {
+        acc_mat(v, h.h[n], 0, "head h");
+        acc_mat(v, h.dsrc[n], 0, "head dsrc");
+        acc_bytes(v, h.w[n], (long long)h.w_cbn * 1024, 0, "head w");
+        acc_bytes(v, h.b[n], 4, 0, "head b");
+        if (h.tgt_mode >= 0) {
+          acc_mat(v, h.th[n], 0, "head th");
+          acc_bytes(v, h.tw[n], (long long)h.w_cbn * 1024, 0, "head tw");
+          acc_bytes(v, h.tb[n], 4, 0, "head tb");
+        }
+        acc_whole(v, h.qp[n], 0, "head qp");
+        acc_whole(v, h.tp[n], 0, "head tp");
+        acc_mat(v, h.dz[n], 1, "head dz");
+        acc_mat(v, h.dq[n], 1, "head dq");
+      }
+      acc_whole(v, h.reward, 0, "head reward");
+      acc_whole(v, h.notdone, 0, "head notdone");
+      const bool tgt = h.mode == HEAD_TD7_TARGET || h.mode == HEAD_MLP_TARGET;
+      acc_whole(v, h.y, tgt || h.tgt_mode >= 0, "head y");
+      acc_whole(v, h.logpi, 0, "head logpi");
+      acc_bytes(v, h.log_alpha, 4, 0, "head log_alpha");
+      acc_bytes(v, h.vt, 8, 0, "head vt");
+      acc_whole(v, h.loss_part, 1, "head loss");
+      acc_whole(v, h.prio, 1, "head prio");
+      if (h.mode == HEAD_TD7_TARGET || h.tgt_mode == HEAD_TD7_TARGET) {
+        acc_bytes(v, h.vmax_key, 4, 1, "head vmax");
+        acc_bytes(v, h.vmin_key, 4, 1, "head vmin");
+      }
+      break;
+    }
+    case OP_PRIORITY: {
+      const PriorityArgs& a = op.prio;
+      acc_whole(v, a.p, 0, "prio p");
+      acc_whole(v, a.ind, 0, "prio ind");
+      acc_whole(v, a.priority, 1, "priority");
+      acc_whole(v, a.bsum, 1, "bsum");
+      acc_bytes(v, a.max_priority, 4, 1, "max priority");
+      break;
+    }
+    case OP_SAC_ACTOR:
+    case OP_SAC_ACTOR_BWD: {
+      const SacActorArgs& a = op.sac;
+      acc_mat(v, a.out, 0, "sac out");
+      acc_mat(v, a.eps2, 0, "sac eps2");
+      if (op.kind == OP_SAC_ACTOR) {
+        acc_mat(v, a.eps, 0, "sac eps");
+        acc_mat(v, a.act, 1, "sac act");
+        acc_whole(v, a.logpi, 1, "sac logpi");
+      } else {
+        acc_mat(v, a.da, 0, "sac da");
+        acc_bytes(v, a.log_alpha, 4, 0, "sac log_alpha");
+        acc_mat(v, a.dout, 1, "sac dout");
+      }
+      break;
+    }
+    case OP_STEP_END: {
+      const StepEndArgs& a = op.end;
+      for (int k = 0; k < a.ninfo; ++k)
+        if (a.part[k]) acc_bytes(v, a.part[k], (long long)a.npart[k] * a.stride[k] * 4, 0, "info part");
+      if (a.logpi_part) acc_bytes(v, a.logpi_part, (long long)a.nlogpi * 16, 0, "logpi part");
+      if (a.gsq && a.ngsq_t > 0) acc_bytes(v, a.gsq, (long long)a.gsq_off[a.ngsq_t] * 4, 0, "gsq");
+      acc_bytes(v, a.counters, 16 * 8, 1, "counters");
+      acc_bytes(v, a.info_slot, 4, 1, "info slot");
+      acc_whole(v, a.info, 1, "info ring");
+      if (a.log_alpha) acc_bytes(v, a.log_alpha, 4, a.la_lr > 0.f, "log_alpha");
+      if (a.la_lr > 0.f) {
+        acc_bytes(v, a.la_m, 4, 1, "la_m");
+        acc_bytes(v, a.la_v, 4, 1, "la_v");
+        acc_bytes(v, a.la_t, 8, 1, "la_t");
+      }
+      break;
+    }
+    case OP_POLYAK:
+    case OP_COPY: {
+      const FlatArgs& f = op.flat;
+      acc_bytes(v, f.dst, f.n * 4, 1, "flat dst");
+      if (!f.self_alias) acc_bytes(v, f.src, f.n * 4, 0, "flat src");
+      break;
+    }
+    case OP_MAXRED: {
+      const FlatArgs& f = op.flat;
+      if (f.stage == 0) {
+        acc_bytes(v, f.size, 8, 0, "maxred size");
+        acc_whole(v, f.src, 0, "maxred src");
+        acc_bytes(v, f.partial, (long long)f.nwg * 4, 1, "maxred partial");
+      } else {
+        acc_bytes(v, f.partial, (long long)f.nwg * 4, 0, "maxred partial");
+        acc_bytes(v, f.out, 4, 1, "maxred out");
+      }
+      break;
+    }
+    case OP_CTRL: {
+      const CtrlArgs& c = op.ctrl;
+      if (c.mode == 0) {
+        acc_bytes(v, c.vmax_key, 4, 0, "vmax key");
+        acc_bytes(v, c.vmin_key, 4, 0, "vmin key");
+        acc_bytes(v, c.vt, 8, 1, "vt");
+      } else {
+        acc_bytes(v, c.counters, 3 * 8, 0, "counters");
+        acc_bytes(v, c.adam_step, 3 * 4, 1, "adam step");
+        acc_bytes(v, c.adam_bc2s, 3 * 4, 1, "adam bc2s");
+      }
+      break;
+    }
+    case OP_FOLDBIAS: {
+      const FoldBiasArgs& f = op.fb;
+      acc_bytes(v, f.wn, (long long)((f.H + 15) / 16) * f.cbn * 1024, 0, "fold w");
+      acc_bytes(v, f.bin, (long long)f.H * 4, 0, "fold bin");
+      acc_bytes(v, f.bbase, (long long)f.H * 4, 0, "fold bbase");
+      acc_bytes(v, f.bout, (long long)f.H * 4, 1, "fold bout");
+      break;
+    }
+    default:
+      throw Error{RLE_EINVAL, "hazard check: unknown op kind " + std::to_string(op.kind)};
+  }
+}
+
+// ops: one level's ops; item[i]: the program item op i came from.  Throws on a conflict.
+static void level_hazards(const std::vector<Op>& ops, const std::vector<int>& item, int level) {
+  struct A {
+    uintptr_t lo, hi;
+    int w, op;
+    const char* what;
+  };
+  std::vector<A> all;
+  std::vector<Access> v;
+  for (size_t i = 0; i < ops.size(); ++i) {
+    v.clear();
+    op_accesses(ops[i], v);
+    for (const Access& a : v) all.push_back({a.lo, a.hi, a.w, (int)i, a.what});
+  }
+  std::sort(all.begin(), all.end(), [](const A& x, const A& y) { return x.lo < y.lo; });
+  // sweep: active intervals (those whose hi > current lo); report a pair from different items
+  // where one side writes
+  std::vector<int> act;
+  for (size_t k = 0; k < all.size(); ++k) {
+    const A& c = all[k];
+    size_t keep = 0;
+    for (int j : act)
+      if (all[j].hi > c.lo) act[keep++] = j;
+    act.resize(keep);
+    for (int j : act) {
+      const A& o = all[j];
+      if (o.op == c.op || item[o.op] == item[c.op] || !(o.w || c.w)) continue;
+      char msg[320];
+      snprintf(msg, sizeof msg, "hazard: level %d op %d (%s, kind %d, %s) and op %d (%s, kind %d, %s) overlap at %#lx", level,
+               o.op, o.what, ops[o.op].kind, o.w ? "write" : "read", c.op, c.what, ops[c.op].kind, c.w ? "write" : "read",
+               (unsigned long)c.lo);
+      throw Error{RLE_EINVAL, msg};
+    }
+    act.push_back((int)k);
   }
 }
 
@@ -672,8 +980,14 @@ struct Prog {
     }
     if (balance) rebalance(maxl, nops, nwg, wg_cap);
     std::vector<std::vector<Op>> levels(maxl + 1);
-    for (auto& it : items)
-      for (auto& op : it.ops) levels[it.level].push_back(op);
+    std::vector<std::vector<int>> owner(maxl + 1);
+    for (size_t i = 0; i < items.size(); ++i)
+      for (auto& op : items[i].ops) {
+        levels[items[i].level].push_back(op);
+        owner[items[i].level].push_back((int)i);
+      }
+    if (const char* hz = std::getenv("RLE_HAZARD"); hz && hz[0] == '1')
+      for (size_t l = 0; l < levels.size(); ++l) level_hazards(levels[l], owner[l], (int)l);
     for (auto& lv : levels) {
       int wg = 0;
       for (auto& op : lv) {
@@ -876,6 +1190,8 @@ struct Engine {
     c.ao = ao;
     c.min_log_std = cfg.min_log_std;
     c.max_log_std = cfg.max_log_std;
+    const char* fw = std::getenv("RLE_ACT_FAIL_WG");  // failure-path test, first call only
+    c.fail_wg = fw ? std::atoi(fw) : -1;
     return true;
   }
   void ensure_action_map() {  // default: identity map, exploration_noise 0.1 (td7.py:41, td3.py:40)
@@ -2268,6 +2584,19 @@ struct Engine {
     out_t = keep;
   }
 
+  // SAC temperature operand of the heads and the actor backward: log_alpha (autotune, the
+  // trained parameter), or fp32(tmp) itself for a fixed temperature -- the reference multiplies
+  // by the Python float (sac.py:189, 227), so exp(log(tmp)) would be an ulp off
+  float* alpha_fixed = nullptr;
+  const float* alpha_src() {
+    if (cfg.tmp < 0.f) return P + (nP - 4);
+    if (!alpha_fixed) {
+      alpha_fixed = mem.make<float>(1);
+      HIPCHK(hipMemcpy(alpha_fixed, &cfg.tmp, 4, hipMemcpyHostToDevice));
+    }
+    return alpha_fixed;
+  }
+
   // TD3 (td3.py:206-242) and SAC (sac.py:251-295)
   void build_mlp(Prog& pg, bool policy, int set) {
     const bool sac = algo == RLE_SAC;
@@ -2339,7 +2668,8 @@ struct Engine {
       if (sac) {
         h.sac = 1;
         h.logpi = logpi.p + B;  // next-state rows
-        h.log_alpha = P + (nP - 4);
+        h.log_alpha = alpha_src();
+        h.alpha_lin = cfg.tmp >= 0.f;
         rd.push_back(logpi.id);
         rd.push_back(R_LA);
       }
@@ -2398,7 +2728,8 @@ struct Engine {
         if (sac) {
           h.sac = 1;
           h.logpi = logpi.p;
-          h.log_alpha = P + (nP - 4);
+          h.log_alpha = alpha_src();
+          h.alpha_lin = cfg.tmp >= 0.f;
           rd.push_back(logpi.id);
           rd.push_back(R_LA);
         }
@@ -2430,7 +2761,8 @@ struct Engine {
         a.ls_off = A;
         a.da = da.m;
         a.dout = dout.m;
-        a.log_alpha = P + (nP - 4);
+        a.log_alpha = alpha_src();
+        a.alpha_lin = cfg.tmp >= 0.f;
         a.inv_b = 1.f / (float)B;
         op.wg_count = cdiv(B, kThreads);
         pg.add(op, {raw.id, eps2.id, da.id, R_LA}, {dout.id});
@@ -3069,14 +3401,15 @@ int rle_replay_set_priority(rle_replay* h, const float* p, long long n, float ma
 }
 
 // Runs a small op program eagerly on the replay's stream (test hooks).
-static void run_eager(Replay& r, rle::DevMem& tmp, std::vector<std::vector<rle::Op>> levels) {
-  for (auto& lv : levels) {
+static void run_eager(Replay& r, std::vector<std::vector<rle::Op>> levels) {
+  for (size_t l = 0; l < levels.size(); ++l) {
+    auto& lv = levels[l];
     int wg = 0;
     for (auto& op : lv) {
       op.wg_begin = wg;
       wg += op.wg_count;
     }
-    rle::Op* d = tmp.make<rle::Op>(lv.size());
+    rle::Op* d = r.scratch.get<rle::Op>("ops" + std::to_string(l), lv.size());
     HIPCHK(hipMemcpy(d, lv.data(), lv.size() * sizeof(rle::Op), hipMemcpyHostToDevice));
     HIPCHK(rle::launch_level(d, lv.data(), (int)lv.size(), wg, r.stream));
   }
@@ -3086,14 +3419,13 @@ static void run_eager(Replay& r, rle::DevMem& tmp, std::vector<std::vector<rle::
 // Full recompute of the LAP block sums (after bulk priority writes).  In-step and
 // eager priority scatters and appends keep them exact incrementally.
 static void recompute_bsum(Replay& r) {
-  rle::DevMem tmp;
   rle::Op a{};
   a.kind = rle::OP_SAMPLE_REDUCE;
   a.sample.priority = r.priority;
   a.sample.size = r.size_d;
   a.sample.bsum = r.bsum;
   a.wg_count = r.nblk;
-  run_eager(r, tmp, {{a}});
+  run_eager(r, {{a}});
 }
 
 int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* ind_out) {
@@ -3102,7 +3434,7 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     REQUIRE(n > 0 && r.size > 0, "sample_indices: bad args / empty replay");
     HIPCHK(hipSetDevice(r.device));
     r.wait_users();
-    rle::DevMem tmp;
+    rle::Scratch& tmp = r.scratch;
     rle::SampleArgs s{};
     s.state = r.state;
     s.next_state = r.next_state;
@@ -3120,39 +3452,39 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     s.B = n;
     s.bsum = r.bsum;
     s.nblk = r.nblk;
-    auto timg = [&](int rows, int cols) {  // scratch T image (outputs are not read back)
+    auto timg = [&](const char* name, int rows, int cols) {  // scratch T image (outputs are not read back)
       rle::Mat m{};
       m.rbs = rle::r16(rows) / 16;
       m.cbn = cols / 16;
-      m.t = tmp.make<float>((size_t)rle::r16(rows) * cols);
+      m.t = tmp.get<float>(name, (size_t)rle::r16(rows) * cols);
       return m;
     };
-    s.ss = timg(2 * n, r.Sp);
-    s.a = timg(n, r.Ap);
-    s.r = tmp.make<float>(n);
-    s.nd = tmp.make<float>(n);
-    long long* dind = tmp.make<long long>(n);
+    s.ss = timg("ss", 2 * n, r.Sp);
+    s.a = timg("a", n, r.Ap);
+    s.r = tmp.get<float>("r", n);
+    s.nd = tmp.get<float>("nd", n);
+    long long* dind = tmp.get<long long>("ind", n);
     s.ind = dind;
-    s.u_out = tmp.make<float>(n);
-    s.eps = timg(n, r.Ap);
-    long long* cnt = tmp.make<long long>(2);
-    int* mode = tmp.make<int>(1);
-    const int one = rle::kTapeU;
-    HIPCHK(hipMemcpy(mode, &one, 4, hipMemcpyHostToDevice));
+    s.u_out = tmp.get<float>("u_out", n);
+    s.eps = timg("eps", n, r.Ap);
+    // [0] rng step = 0, [1] tape position = 0 (zero from allocation, only read), [2] tape mode
+    long long* cnt = tmp.get<long long>("ctl", 3);
+    const long long ctl[3] = {0, 0, rle::kTapeU};
+    float* du = tmp.get<float>("u", n);
+    HIPCHK(hipMemcpyAsync(cnt, ctl, sizeof ctl, hipMemcpyHostToDevice, r.stream));
+    HIPCHK(hipMemcpyAsync(du, u, n * 4, hipMemcpyHostToDevice, r.stream));
     s.ctrl_rng = cnt;
-    s.tape_mode = mode;
     s.tape_pos = cnt + 1;
-    float* du = tmp.make<float>(n);
-    HIPCHK(hipMemcpy(du, u, n * 4, hipMemcpyHostToDevice));
+    s.tape_mode = (const int*)(cnt + 2);
     s.tape_u = du;
-    s.tape_eps = tmp.make<float>((size_t)n * r.A);
+    s.tape_eps = tmp.get<float>("tape_eps", (size_t)n * r.A);
     std::vector<std::vector<rle::Op>> lv;
     rle::Op b{};
     b.kind = rle::OP_SAMPLE_GATHER;
     b.sample = s;
     b.wg_count = n;
     lv.push_back({b});
-    run_eager(r, tmp, lv);
+    run_eager(r, lv);
     HIPCHK(hipMemcpy(ind_out, dind, n * sizeof(long long), hipMemcpyDeviceToHost));
   });
 }
@@ -3168,11 +3500,10 @@ int rle_replay_update_priority(rle_replay* h, int n, const long long* ind, const
     // 2^-23 summing below 2^30); any smaller value -> full recompute of the block sums instead.
     bool small = false;
     for (int i = 0; i < n; ++i) small = small || !(p[i] >= 1.f);
-    rle::DevMem tmp;
-    long long* di = tmp.make<long long>(n);
-    float* dp = tmp.make<float>(n);
-    HIPCHK(hipMemcpy(di, ind, n * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(dp, p, n * 4, hipMemcpyHostToDevice));
+    long long* di = r.scratch.get<long long>("prio_ind", n);
+    float* dp = r.scratch.get<float>("prio_p", n);
+    HIPCHK(hipMemcpyAsync(di, ind, n * 8, hipMemcpyHostToDevice, r.stream));
+    HIPCHK(hipMemcpyAsync(dp, p, n * 4, hipMemcpyHostToDevice, r.stream));
     rle::Op op{};
     op.kind = rle::OP_PRIORITY;
     op.prio.priority = r.priority;
@@ -3182,7 +3513,7 @@ int rle_replay_update_priority(rle_replay* h, int n, const long long* ind, const
     op.prio.max_priority = r.maxp_d;
     op.prio.bsum = r.lap && !small ? r.bsum : nullptr;
     op.wg_count = 1;
-    run_eager(r, tmp, {{op}});
+    run_eager(r, {{op}});
     if (r.lap && small) recompute_bsum(r);
     ++r.version;
   });
@@ -3194,7 +3525,6 @@ int rle_replay_reset_max_priority(rle_replay* h) {
     REQUIRE(r.size > 0, "reset_max_priority: empty");
     HIPCHK(hipSetDevice(r.device));
     r.wait_users();
-    rle::DevMem tmp;
     rle::Op a{};
     a.kind = rle::OP_MAXRED;
     a.flat.src = r.priority;
@@ -3207,7 +3537,7 @@ int rle_replay_reset_max_priority(rle_replay* h) {
     b.flat.stage = 1;
     b.flat.out = r.maxp_d;
     b.wg_count = 1;
-    run_eager(r, tmp, {{a}, {b}});
+    run_eager(r, {{a}, {b}});
   });
 }
 
@@ -3375,6 +3705,14 @@ int rle_get_counters(rle_engine* h, long long* out6) {
     out6[3] = e.n_runs;
     out6[5] = c.la_t;
   });
+}
+
+int rle_get_act_counter(rle_engine* h, unsigned long long* out) {
+  return guard([&] { *out = h->e->act_counter; });
+}
+
+int rle_set_act_counter(rle_engine* h, unsigned long long v) {
+  return guard([&] { h->e->act_counter = v; });
 }
 
 int rle_set_counters(rle_engine* h, const long long* in6) {
@@ -3646,8 +3984,9 @@ int rle_act_sample(rle_engine* h, const float* obs, int n, int mode, const float
       rle::ActChainArgs& c = e.chain;
       std::memset(c.obs, 0, sizeof c.obs);
       std::memcpy(c.obs, obs, (size_t)e.S * 4);
-      if (++e.chain_tag == 0) e.chain_tag = 1;
+      if (++e.chain_tag >= 0x80000000u) e.chain_tag = 1;  // (bit 31 marks poisoned granules)
       c.tag = e.chain_tag;
+      as.ctl[8] = 0;  // the error flag of this call (set by a head workgroup whose hand-off failed)
       c.mode = mode;
       c.ctr_lo = (unsigned)e.act_counter;
       c.ctr_hi = (unsigned)(e.act_counter >> 32);
@@ -3667,6 +4006,7 @@ int rle_act_sample(rle_engine* h, const float* obs, int n, int mode, const float
       const auto t0 = std::chrono::steady_clock::now();
       if (cprof) HIPCHK(hipEventRecord(ce0, e.stream));
       HIPCHK(rle::launch_act_chain(c, e.stream));
+      c.fail_wg = -1;
       if (cprof) HIPCHK(hipEventRecord(ce1, e.stream));
       const auto t1 = std::chrono::steady_clock::now();
       // the head workgroups' completion tags (system-scope release after their action stores):
@@ -3683,7 +4023,7 @@ int rle_act_sample(rle_engine* h, const float* obs, int n, int mode, const float
       std::atomic_thread_fence(std::memory_order_acquire);
       const auto t2 = std::chrono::steady_clock::now();
       if (cprof) HIPCHK(hipStreamSynchronize(e.stream));
-      REQUIRE(as.ctl[8] == 0, "act chain: a workgroup hand-off timed out");
+      REQUIRE(((volatile int*)as.ctl)[8] == 0, "act chain: a workgroup hand-off failed");
       std::memcpy(out, as.out, (size_t)e.A * 4);
       if (cprof) {
         float ms = 0.f;

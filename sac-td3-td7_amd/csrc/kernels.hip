@@ -868,6 +868,9 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   // ---- epilogue operands fetched ahead of the main loop
   float pre_b = 0.f;
   float4 ds = make_float4(1.f, 1.f, 1.f, 1.f), pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
+#ifdef RLE_EXP_EARLY_ADAM
+  float early_step = 0.f, early_bc2s = 1.f;
+#endif
   size_t wt = 0;
   float qwj = 0.f;
   if constexpr (EPI == EPI_QHEAD || EPI == EPI_QDOT) {
@@ -893,6 +896,10 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       if (jok) ds = mat_ld4(g.dsrc, ib, j);
     }
   } else {
+#ifdef RLE_EXP_EARLY_ADAM  // diagnostics build (tools/bitcmp.py): Adam scalars read before the main loop
+    early_step = sload(g.adam.step);
+    early_bc2s = sload(g.adam.bc2s);
+#endif
     if (jok) {
       const CAS AdamArgs& ad = g.adam;
       if (bias_tile) {
@@ -1160,7 +1167,11 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     const CAS AdamArgs& ad = g.adam;
     float gg = 0.f;
     if (jok) {
+#ifdef RLE_EXP_EARLY_ADAM
+      const float step_size = early_step, bc2s = early_bc2s;
+#else
       const float step_size = sload(ad.step), bc2s = sload(ad.bc2s);  // this step's (level-0 CTRL op)
+#endif
       const float p4[4] = {pp.x, pp.y, pp.z, pp.w}, m4[4] = {mm.x, mm.y, mm.z, mm.w}, v4[4] = {vv.x, vv.y, vv.z, vv.w};
       float po[4], mo[4], vo[4];
 #pragma unroll
@@ -1327,7 +1338,7 @@ __device__ __forceinline__ void op_head_t(const CAS HeadArgs& h, int t, float* s
     const float rw = h.reward ? sload(h.reward + b) : 0.f, ndn = h.notdone ? sload(h.notdone + b) : 0.f;
     float yv = ((h.mode == HEAD_TD7_LOSS || h.mode == HEAD_MLP_LOSS) && !fused) ? sload(h.y + b) : 0.f;
     const float lp = h.sac ? sload(h.logpi + b) : 0.f;
-    const float alpha = h.sac ? expf(sload(h.log_alpha)) : 0.f;
+    const float alpha = h.sac ? (h.alpha_lin ? sload(h.log_alpha) : expf(sload(h.log_alpha))) : 0.f;
     const float bias0 = sload(h.b[0]), bias1 = sload(h.b[1]);
     const float vtmax = h.vt ? sload(h.vt) : 0.f, vtmin = h.vt ? sload(h.vt + 1) : 0.f;
     auto dot2 = [&](const float4 (&x)[2], const float4 (&w)[2]) {
@@ -1812,7 +1823,7 @@ __device__ __forceinline__ void op_sac_actor(const CAS SacActorArgs& s, int t) {
 __device__ __forceinline__ void op_sac_actor_bwd(const CAS SacActorArgs& s, int t) {
   const int b = t * kThreads + threadIdx.x;
   if (b >= s.rows) return;
-  const float w = expf(G(s.log_alpha)[0]) * s.inv_b;  // d obj / d logpi_b
+  const float w = (s.alpha_lin ? G(s.log_alpha)[0] : expf(G(s.log_alpha)[0])) * s.inv_b;  // d obj / d logpi_b
   for (int j = 0; j < s.A; ++j) {
     const float mu = mat_ld(s.out, b, s.mean_off + j);
     const float lsr = mat_ld(s.out, b, s.ls_off + j);
@@ -2182,23 +2193,30 @@ __device__ __forceinline__ void act_rows(const ActLayer& L, const ActW& W, const
 }
 
 // Reads the granules of layer q (this call's tag) into vector slot Q.dst, then AvgL1Norm.
-__device__ __forceinline__ void act_receive(const ActChainArgs& a, int q, float* vec, float* red) {
+// Returns true (every thread) when the hand-off failed: a granule never arrived (~0.1 s), or it
+// arrived poisoned (kActPoison: its producer had failed before it).  A failed workgroup keeps
+// going, so the grid drains, but publishes poisoned granules from then on: the failure reaches
+// the head workgroups, which report it before their completion tag.
+constexpr unsigned kActPoison = 0x80000000u;  // tag bit 31 (the host's call tags stay below it)
+__device__ __forceinline__ bool act_receive(const ActChainArgs& a, int q, float* vec, float* red) {
   const ActLayer& Q = a.L[q];
+  bool fail = false;
   for (int i = threadIdx.x; i < Q.out; i += kThreads) {
     unsigned long long g = 0;
     int spins = 0;
     while (true) {
       g = __hip_atomic_load(a.xbuf + (size_t)q * kActVec + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((g >> 32) == (unsigned long long)a.tag) break;
-      if (++spins > (1 << 20)) {  // ~0.1 s: a workgroup never arrived (fail, do not hang)
-        __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // (plain store: host memory)
+      const unsigned gt = (unsigned)(g >> 32);
+      if (gt == a.tag) break;
+      if (gt == (a.tag | kActPoison) || ++spins > (1 << 20)) {  // (fail, do not hang)
+        fail = true;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
     vec[Q.dst * kActVec + i] = __uint_as_float((unsigned)g);
   }
-  __syncthreads();
+  fail = __syncthreads_or(fail);
   if (Q.norm) {  // AvgL1Norm: x / max(mean |x|, 1e-8), the same fixed-order sum in every workgroup
     float sabs = 0.f;
     for (int i = threadIdx.x; i < Q.out; i += kThreads) sabs += fabsf(vec[Q.dst * kActVec + i]);
@@ -2207,16 +2225,19 @@ __device__ __forceinline__ void act_receive(const ActChainArgs& a, int q, float*
     for (int i = threadIdx.x; i < Q.out; i += kThreads) vec[Q.dst * kActVec + i] /= m;
     __syncthreads();
   }
+  return fail;
 }
 
 // One row block of an exchanged layer: compute from W, publish as {value, tag} granules.
 __device__ __forceinline__ void act_publish(const ActChainArgs& a, int l, int w, const ActW& W, const float* vec,
-                                            float* red) {
+                                            float* red, bool bad) {
   const ActLayer& L = a.L[l];
   act_rows(L, W, vec, red);
+  const unsigned tag = bad ? (a.tag | kActPoison) : a.tag;
+  if (l == 0 && w == a.fail_wg) return;  // (failure-path test: these granules never arrive)
   if (threadIdx.x < 16 && w * 16 + (int)threadIdx.x < L.out)  // one 8-byte sc1 store per row
     __hip_atomic_store(a.xbuf + (size_t)l * kActVec + w * 16 + threadIdx.x,
-                       ((unsigned long long)a.tag << 32) | (unsigned long long)__float_as_uint(red[64 + threadIdx.x]),
+                       ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(red[64 + threadIdx.x]),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -2254,41 +2275,42 @@ __global__ __launch_bounds__(kThreads, 1) void rle_act_chain(const ActChainArgs 
   for (int i = tid; i < 8 * kActVec; i += kThreads) vec[i] = i < a.Sp ? a.obs[i] : 0.f;
   __syncthreads();
   stamp(1);
+  bool bad = false;  // a hand-off of this call failed (workgroup-uniform)
   if constexpr (TD7) {  // 0 fe0 | 1 pi0 (norm) || 2 fe1 || 3 fe2 (norm) || 4 pi1 || 5 pi2 || 6 head
-    act_publish(a, 0, w, W, vec, red);
+    act_publish(a, 0, w, W, vec, red, bad);
     act_load(a.L[2], w, W);
-    act_publish(a, 1, w, X, vec, red);
+    act_publish(a, 1, w, X, vec, red, bad);
     act_load(a.L[3], w, X);
     stamp(2);
-    act_receive(a, 0, vec, red);
-    act_receive(a, 1, vec, red);
+    bad |= act_receive(a, 0, vec, red);
+    bad |= act_receive(a, 1, vec, red);
     stamp(3);
-    act_publish(a, 2, w, W, vec, red);
+    act_publish(a, 2, w, W, vec, red, bad);
     act_load(a.L[4], w, W);
-    act_receive(a, 2, vec, red);
+    bad |= act_receive(a, 2, vec, red);
     stamp(4);
-    act_publish(a, 3, w, X, vec, red);
+    act_publish(a, 3, w, X, vec, red, bad);
     act_load(a.L[5], w, X);
-    act_receive(a, 3, vec, red);
+    bad |= act_receive(a, 3, vec, red);
     stamp(5);
-    act_publish(a, 4, w, W, vec, red);
+    act_publish(a, 4, w, W, vec, red, bad);
     if (head) act_load(H, hr0, W);
-    act_receive(a, 4, vec, red);
+    bad |= act_receive(a, 4, vec, red);
     stamp(6);
-    act_publish(a, 5, w, X, vec, red);
+    act_publish(a, 5, w, X, vec, red, bad);
     if (!head) return;
     if (hr0 + 1 < hr1) act_load(H, hr0 + 1, X);
-    act_receive(a, 5, vec, red);
+    bad |= act_receive(a, 5, vec, red);
     stamp(7);
   } else {  // 0 h0 || 1 h1 || 2 head
-    act_publish(a, 0, w, W, vec, red);
+    act_publish(a, 0, w, W, vec, red, bad);
     if (head) act_load(H, hr0, W);
-    act_receive(a, 0, vec, red);
+    bad |= act_receive(a, 0, vec, red);
     stamp(2);
-    act_publish(a, 1, w, X, vec, red);
+    act_publish(a, 1, w, X, vec, red, bad);
     if (!head) return;
     if (hr0 + 1 < hr1) act_load(H, hr0 + 1, X);
-    act_receive(a, 1, vec, red);
+    bad |= act_receive(a, 1, vec, red);
     stamp(3);
   }
   // ---- the head: env action (td7.py:141-156, td3.py:114-129, sac.py:132-152)
@@ -2327,7 +2349,11 @@ __global__ __launch_bounds__(kThreads, 1) void rle_act_chain(const ActChainArgs 
   // system-scope release (a plain store, no PCIe atomic)
   __syncthreads();
   stamp(15);
-  if (tid == 0) __hip_atomic_store(a.done + w, a.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // (a failed hand-off is reported by the same thread before the tag: the release orders it)
+  if (tid == 0) {
+    if (bad) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.done + w, a.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ---------------------------------------------------------------- standalone kernels

@@ -220,6 +220,7 @@ struct HeadArgs {                   // 4 rows per workgroup (1 per wave)
   float* prio;                       // LAP priority out [rows]
   float gamma;
   int sac;                           // SAC: alpha term
+  int alpha_lin;                     // SAC fixed temperature: *log_alpha holds alpha itself (sac.py:55-60)
   const float* logpi;                // SAC logpi [rows] (target rows / policy rows)
   const float* log_alpha;            // SAC log alpha scalar
   int* vmax_key; int* vmin_key;      // TD7 value tracking (ordered-int keys)
@@ -343,6 +344,7 @@ struct SacActorArgs {
   Mat da;                            // grad wrt action from critics [B][Ap] (T)
   Mat dout;                          // grad wrt raw output [B][2A(p)] (N + T)
   const float* log_alpha; float inv_b;
+  int alpha_lin;                     // as HeadArgs::alpha_lin
 };
 
 // Step end: info ring row + counter increments + SAC temperature Adam.
@@ -458,6 +460,7 @@ struct ActChainArgs {
   unsigned* done;      // [64] per head workgroup: tag of the last call it finished (pinned)
   unsigned long long* stamps;  // optional [nwg][16] s_memrealtime phase stamps (RLE_ACT_PROF)
   int mode;            // ActArgs::ctl[0] semantics, carried here (no host-memory read in the kernel)
+  int fail_wg;         // tests (RLE_ACT_FAIL_WG, one call): this workgroup withholds its layer-0 granules
   unsigned ctr_lo, ctr_hi;  // Philox counter of this call
   float eps[32];       // mode 2: the draw [A] (A <= 32)
   ActArgs ao;

@@ -67,6 +67,8 @@ SIGNATURES = {
     "rle_set_adam": (_int, [_vp, _cs, _cs, _int, _f32p, _ll]),
     "rle_get_counters": (_int, [_vp, _i64p]),
     "rle_set_counters": (_int, [_vp, _i64p]),
+    "rle_get_act_counter": (_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
+    "rle_set_act_counter": (_int, [_vp, ctypes.c_uint64]),
     "rle_get_value_bounds": (_int, [_vp, _f32p]),
     "rle_set_value_bounds": (_int, [_vp, _f32p]),
     "rle_step": (_int, [_vp, _int, _f32p]),
@@ -252,6 +254,14 @@ class Engine:
         _check(lib().rle_get_counters(self.h, _ip(out)))
         return out
 
+    def act_counter(self):
+        v = ctypes.c_uint64(0)
+        _check(lib().rle_get_act_counter(self.h, ctypes.byref(v)))
+        return int(v.value)
+
+    def set_act_counter(self, v):
+        _check(lib().rle_set_act_counter(self.h, int(v)))
+
     def set_counters(self, c):
         c = np.ascontiguousarray(c, np.int64)
         _check(lib().rle_set_counters(self.h, _ip(c)))
@@ -299,6 +309,8 @@ class Engine:
         obs = _f32(obs)
         if obs.ndim == 1:
             obs = obs[None]
+        if obs.ndim != 2 or obs.shape[1] != self.cfg.state_dim:
+            raise ValueError(f"act: observation shape {obs.shape}, expected (n, {self.cfg.state_dim})")
         n = obs.shape[0]
         out = np.empty((n, width), np.float32)
         _check(lib().rle_act(self.h, _fp(obs), n, _fp(out)))
@@ -315,7 +327,14 @@ class Engine:
         """Agent.sample on the device (rle_act_sample): obs [S] or [n][S] -> environment
         actions [n][A].  mode 0 deterministic, 1 Philox exploration noise, 2 noise tape eps."""
         x = obs if (type(obs) is np.ndarray and obs.dtype == np.float32 and obs.flags.c_contiguous) else _f32(obs)
+        # the kernel reads n rows of state_dim floats from this address: shapes are checked here,
+        # as the reference's first Linear would reject them
+        if x.ndim not in (1, 2) or x.shape[-1] != self.cfg.state_dim:
+            raise ValueError(f"act_sample: observation shape {x.shape}, expected ({self.cfg.state_dim},) "
+                             f"or (n, {self.cfg.state_dim})")
         n = 1 if x.ndim == 1 else x.shape[0]
+        if not 1 <= n <= 1024:
+            raise ValueError(f"act_sample: {n} observations (1..1024)")
         out = self._act_out.get(n)
         if out is None:
             out = self._act_out[n] = np.empty((n, self.cfg.action_dim), np.float32)

@@ -130,7 +130,8 @@ class EngineAgent(Agent, Sampler):
         if self.ALG == "sac":
             params["tmp"] = {"log_alpha": e.get_param("tmp", "log_alpha")}
             adam["tmp"] = {"log_alpha": (e.get_adam("tmp", "log_alpha", 0), e.get_adam("tmp", "log_alpha", 1))}
-        return {"params": params, "adam": adam, "counters": e.counters(), "vbounds": e.value_bounds()}
+        return {"params": params, "adam": adam, "counters": e.counters(), "vbounds": e.value_bounds(),
+                "act_counter": e.act_counter()}
 
     def _import(self, st):
         e = self.engine
@@ -145,6 +146,8 @@ class EngineAgent(Agent, Sampler):
             e.set_counters(st["counters"])
         if "vbounds" in st:
             e.set_value_bounds(st["vbounds"])
+        if "act_counter" in st:
+            e.set_act_counter(st["act_counter"])
 
     def state_dict(self):
         """{net: {param name: ndarray}} in the reference's state_dict naming."""
@@ -232,9 +235,13 @@ class EngineAgent(Agent, Sampler):
         (the engine's Philox stream, or the tape `eps` [A]), clip and the action map, written
         into pinned memory by the last kernel.  Returns the first row as the reference does."""
         eng = self.engine
-        if not getattr(eng, "_act_map_set", False):
-            eng.set_action_map(self.action_scale, self.action_bias, getattr(self, "exploration_noise", 0.1))
-            eng._act_map_set = True
+        # the reference reads action_scale / action_bias / exploration_noise on every call
+        # (td7.py:151-155): re-send the map whenever any of them changed
+        amap = (np.asarray(self.action_scale, np.float32).tobytes(), np.asarray(self.action_bias, np.float32).tobytes(),
+                float(getattr(self, "exploration_noise", 0.1)))
+        if getattr(eng, "_act_map", None) != amap:
+            eng.set_action_map(self.action_scale, self.action_bias, amap[2])
+            eng._act_map = amap
         if hasattr(state, "detach"):
             state = state.detach().cpu().numpy()
         if eps is not None:

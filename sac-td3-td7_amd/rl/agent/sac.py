@@ -56,8 +56,9 @@ class SAC(EngineAgent):
     @property
     def tmp(self):
         """exp-space temperature parameter: log_alpha (auto mode) or the fixed value."""
-        la = float(self.engine.get_param("tmp", "log_alpha")[0])
-        return la if self.auto_tmp_mode else float(np.exp(la))
+        if not self.auto_tmp_mode:  # sac.py:56-60: the fixed float itself
+            return float(self._cfg["tmp"])
+        return float(self.engine.get_param("tmp", "log_alpha")[0])
 
     def _inference(self, state):
         """sac.py:154-159: Normal(mean, exp(clamp(log_std))) from the device actor head."""

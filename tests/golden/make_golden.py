@@ -191,6 +191,7 @@ INFO_KEYS = {
     "td7": ["train/encoder", "train/q_fn", "train/policy"],
     "td3": ["train/q_fn", "train/policy", "norm/policy"],
     "sac": ["train/q_fn", "tmp", "norm/tmp", "train/policy", "train/tmp", "entropy"],
+    "sac_fixed": ["train/q_fn", "train/policy", "entropy"],  # tmp >= 0 (sac.py:268-290)
 }
 
 
@@ -245,7 +246,8 @@ def run_config(name, alg, env_id, H, B, N, n_fill, n_steps, use_lap, seed, extra
             info = agent.train_ops(batch, replay_buffer=replay)
             assert not tape.queue, "tape not fully consumed"
         inds.append(ind)
-        infos.append([np.nan if info.get(k) is None else float(info[k]) for k in INFO_KEYS[alg]])
+        ikeys = INFO_KEYS["sac_fixed" if alg == "sac" and extra.get("tmp", -1.0) >= 0 else alg]
+        infos.append([np.nan if info.get(k) is None else float(info[k]) for k in ikeys])
         if lap:
             if sparse_prio:  # only rows ind_t change at step t (lap.py:66-69): their new values
                 res[f"prioi_{t}"] = replay.priority.numpy()[ind].copy()
@@ -266,7 +268,7 @@ def run_config(name, alg, env_id, H, B, N, n_fill, n_steps, use_lap, seed, extra
                                             float(agent.value_target_max), float(agent.value_target_min)])
     res["ind"] = np.stack(inds)
     res["info"] = np.array(infos)
-    res["info_keys"] = np.array(INFO_KEYS[alg])
+    res["info_keys"] = np.array(ikeys)
     names = list(nets.keys())
     for net in names:
         for k, v in dump_net(getattr(agent, net)).items():
@@ -278,7 +280,7 @@ def run_config(name, alg, env_id, H, B, N, n_fill, n_steps, use_lap, seed, extra
                 res[key + ":digest"] = d
                 res[key + ":pos"] = pos
                 res[key + ":vals"] = vals
-    if alg == "sac":
+    if alg == "sac" and agent.auto_tmp_mode:
         res["out_log_alpha"] = agent.tmp.detach().numpy().copy()
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **res)
@@ -359,6 +361,8 @@ def main():
     run_config("td3_tiny", "td3", "Tiny-v0", 32, 16, 64, 50, 6, False, 7)
     run_config("td3_tiny_lap", "td3", "Tiny-v0", 32, 16, 64, 64, 4, True, 8)
     run_config("sac_tiny", "sac", "Tiny-v0", 32, 16, 64, 50, 6, False, 9)
+    # fixed temperature (sac.py:55-60: tmp >= 0 is a float; no temperature loss or optimizer)
+    run_config("sac_tiny_fixed", "sac", "Tiny-v0", 32, 16, 64, 50, 6, False, 10, extra={"tmp": 0.2})
     # Full-size digests at the BASELINE configs' shapes.
     run_config("td7_humanoid", "td7", "Humanoid-v4", 256, 256, 2048, 2048, 3, True, 41,
                full=False)

@@ -34,6 +34,8 @@ def engine_from_golden(g, device=0):
     kw = {}
     if "target_update_rate" in extra:
         kw["target_update_rate"] = int(extra["target_update_rate"])
+    if "tmp" in extra:  # SAC fixed temperature (sac.py:55-60)
+        kw["tmp"] = float(extra["tmp"])
     cfg = E.make_config(ALGO[alg], S, A, H, B, use_lap=use_lap, seed=seed, device=device, **kw)
     eng = E.Engine(cfg)
     for net, params in spec.agent_params(alg, S, A, H, seed).items():

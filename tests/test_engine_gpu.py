@@ -113,7 +113,7 @@ def test_forward_matches_reference(name):
     _fwd_check(name)
 
 
-TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny"]
+TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed"]
 FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k"]
 
 
@@ -134,6 +134,19 @@ def test_td7_head_variants_match_reference(name, variant, monkeypatch):
     fusion) runs it from the critics' last hidden activations with row dot products."""
     monkeypatch.setenv(variant, "1")
     _trajectory(name, False)
+
+
+@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah",
+                                  "sac_humanoid"])
+def test_level_hazards(name, monkeypatch):
+    """RLE_HAZARD=1: no byte that one op of a level stores is read or stored by another op of the
+    same level (engine.cpp level_hazards: each op's accesses replayed from its descriptor) in any
+    program the engine builds -- single-step, multi-step, hard-update and eval graphs; then one
+    step runs."""
+    monkeypatch.setenv("RLE_HAZARD", "1")
+    g = load_golden(name)
+    eng, rep, tp = engine_from_golden(g)
+    run_with_tapes(eng, tp, 1, lambda t: None)
 
 
 @pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid"])

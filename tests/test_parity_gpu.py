@@ -23,7 +23,7 @@ from harness import engine_from_golden, parse  # noqa: E402
 from oracle import spec  # noqa: E402
 from test_oracle import expected_priorities, golden_moments  # noqa: E402
 
-ALL = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td7_ant",
+ALL = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed", "td7_humanoid", "td7_ant",
        "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k"]
 
 

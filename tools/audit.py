@@ -1,9 +1,14 @@
-"""RLE_AUDIT=1 operand-range audit of every GEMM op of every step graph (GPU box; builds and
-captures the graphs, launches no step).  Usage: python tools/audit.py"""
+"""RLE_AUDIT=1 operand-range audit of every GEMM op of every step graph, and the RLE_HAZARD=1
+same-level byte-conflict check of every level (GPU box; builds and captures the graphs, launches
+no step).  Usage: python tools/audit.py [audit|hazard|both]"""
 import os
 import sys
 
-os.environ["RLE_AUDIT"] = "1"
+MODE = sys.argv[1] if len(sys.argv) > 1 else "both"
+if MODE in ("audit", "both"):
+    os.environ["RLE_AUDIT"] = "1"
+if MODE in ("hazard", "both"):
+    os.environ["RLE_HAZARD"] = "1"
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd")]
 from rl import _engine as E  # noqa: E402
@@ -26,7 +31,7 @@ for algo, env, B, lap in CASES:
             try:
                 eng.describe(w)
             except RuntimeError as e:
-                if "audit" in str(e):
+                if "audit" in str(e) or "hazard" in str(e):
                     raise
         print(f"{algo} {env} B={B} lap={lap}: ok ({lv})", flush=True)
     except RuntimeError as e:
