@@ -87,14 +87,65 @@ def td7_bytes_per_step(S, A, H, B, N, target_update_rate=250, policy_freq=2):
     return gather + B * 8 + 4 * N + adam + hard
 
 
-def cpu_baseline(seconds=12.0, algo="td7", env="Humanoid-v4", batch=B, lap=True):
+def socket_cores():
+    """(socket, CPUs, physical cores of that socket): one logical CPU per physical core of the
+    socket holding this process's first allowed CPU, among the allowed CPUs (/proc/cpuinfo)."""
+    entries, cur = [], {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if not k:
+                    if cur:
+                        entries.append(cur)
+                    cur = {}
+                elif k in ("processor", "physical id", "core id"):
+                    cur[k] = int(v)
+            if cur:
+                entries.append(cur)
+    except OSError:
+        entries = []
+    allowed = sorted(os.sched_getaffinity(0))
+    by_cpu = {e["processor"]: e for e in entries if "processor" in e}
+    if not allowed or allowed[0] not in by_cpu or "core id" not in by_cpu[allowed[0]]:
+        return 0, allowed, len(allowed)
+    sock = by_cpu[allowed[0]].get("physical id", 0)
+    cores = {e.get("core id") for e in entries if e.get("physical id", 0) == sock}
+    seen, cpus = set(), []
+    for c in allowed:
+        e = by_cpu.get(c)
+        if e is None or e.get("physical id", 0) != sock or e.get("core id") in seen:
+            continue
+        seen.add(e.get("core id"))
+        cpus.append(c)
+    return sock, cpus, len(cores)
+
+
+def cpu_baseline(seconds=12.0, algo="td7", env="Humanoid-v4", batch=B, lap=True, pin=True):
     """Oracle (torch-CPU restatement of train_ops + replay sample) on host cores, same
-    synthetic workload as the GPU run (full 1M replay)."""
+    synthetic workload as the GPU run (full 1M replay).  SURVEY §8(d): torch threads = the
+    physical cores of one socket, the process pinned to one logical CPU of each (restored after)."""
     import torch
 
     from oracle import agents, replay, spec
 
     s_dim, a_dim, hi = TASKS[env]
+    old_aff, old_threads = os.sched_getaffinity(0), torch.get_num_threads()
+    sock, cpus, ncore = socket_cores()
+    if pin and cpus:
+        os.sched_setaffinity(0, cpus)
+        torch.set_num_threads(len(cpus))
+    try:
+        return _cpu_run(seconds, algo, env, batch, lap, s_dim, a_dim, hi, agents, replay, spec, torch,
+                        {"socket": sock, "physical_cores_socket": ncore, "pinned_cpus": len(cpus) if pin else 0})
+    finally:
+        if pin and cpus:
+            os.sched_setaffinity(0, old_aff)
+            torch.set_num_threads(old_threads)
+
+
+def _cpu_run(seconds, algo, env, batch, lap, s_dim, a_dim, hi, agents, replay, spec, torch, pinning):
     threads = torch.get_num_threads()
     rng = np.random.default_rng(0)
     nets = spec.agent_params(algo, s_dim, a_dim, H, 123)
@@ -131,9 +182,12 @@ def cpu_baseline(seconds=12.0, algo="td7", env="Humanoid-v4", batch=B, lap=True)
         n += 1
     dt = time.perf_counter() - t0
     hc = host_cpu()
-    return {"value": round(n / dt, 3), "unit": "gradient-steps/s", "cores": threads, "kind": "port",
+    hc.update(pinning)
+    return {"value": round(n / dt, 3), "unit": "gradient-steps/s", "cores": threads, "threads": threads,
+            "kind": "port",
             "sample": f"{n} {algo.upper()} {env} B={batch} steps ({'LAP' if lap else 'uniform'} over a 1M replay) "
-                      f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads}",
+                      f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads} pinned one per physical core "
+                      f"of socket {pinning['socket']} ({pinning['physical_cores_socket']} physical cores)",
             "host": hc}
 
 

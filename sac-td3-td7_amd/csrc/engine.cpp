@@ -8,6 +8,9 @@
 // respects RAW, WAR and WAW hazards; each level becomes one launch of the
 // device dispatch kernel, and the whole step is captured into a hipGraph.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <hsa/hsa_ven_amd_loader.h>
 
 #include <algorithm>
 #include <atomic>
@@ -33,10 +36,12 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
                         unsigned long long* trace = nullptr, const Op* next_ops = nullptr, int next_nops = 0);
 int level_capacity();
 int trace_stride();
+extern std::vector<LevelLaunch>* g_level_rec;
+const char* level_kernel_symbol();
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count,
-                         int Sp, int Ap, const float* max_priority, int lap, double* bsum,
+                         int Sp, int Ap, const float* max_priority, int lap, double* bsum, double* ssum,
                          long long size_before, hipStream_t st);
 hipError_t launch_act_chain(const ActChainArgs& a, hipStream_t st);
 hipError_t launch_fill(float* state, float* next_state, float* action, float* reward, float* notdone,
@@ -194,6 +199,7 @@ struct Replay {
   long long* size_d;
   float* maxp_d;
   double* bsum;
+  double* ssum;  // LAP sub-block sums (64 priorities each), nblk * 64
   int nblk;
   float* maxred_part;
   int maxred_nwg = 256;
@@ -677,6 +683,7 @@ static void op_accesses(const Op& op, std::vector<Access>& v) {
       }
       acc_whole(v, s.priority, 0, "priority");
       acc_whole(v, s.bsum, op.kind == OP_SAMPLE_REDUCE, "bsum");
+      acc_whole(v, s.ssum, op.kind == OP_SAMPLE_REDUCE, "ssum");
       if (op.kind == OP_SAMPLE_REDUCE) break;
       for (const void* r : {(const void*)s.state, (const void*)s.next_state, (const void*)s.action,
                             (const void*)s.reward, (const void*)s.notdone})
@@ -729,6 +736,7 @@ static void op_accesses(const Op& op, std::vector<Access>& v) {
       acc_whole(v, a.ind, 0, "prio ind");
       acc_whole(v, a.priority, 1, "priority");
       acc_whole(v, a.bsum, 1, "bsum");
+      acc_whole(v, a.ssum, 1, "ssum");
       acc_bytes(v, a.max_priority, 4, 1, "max priority");
       break;
     }
@@ -999,6 +1007,143 @@ struct Prog {
   }
 };
 
+// ---- Direct AQL dispatch (RLE_AQL=1, an A/B of the launch path): the step graphs' level
+// launches written as kernel-dispatch packets into the engine's own HSA queue instead of
+// hipGraph replays, with chosen fence scopes (RLE_AQL_ACQ / RLE_AQL_REL: 0 none, 1 agent,
+// 2 system; default agent / agent, as HIP's own).  The first packet of a flush acquires and its
+// last releases at system scope (host-written inputs, host-read results).  tools/mbaql.cpp
+// measured the same packets at 3.83 us per level against hipGraph's 4.08.
+struct AqlQueue {
+  hsa_agent_t agent{};
+  hsa_queue_t* q = nullptr;
+  hsa_signal_t sig{};
+  uint64_t kobj = 0;
+  uint32_t gseg = 0, pseg = 0;
+  int acq = HSA_FENCE_SCOPE_AGENT, rel = HSA_FENCE_SCOPE_AGENT;
+  struct Pending {
+    const void* ka;
+    unsigned grid;
+  };
+  std::vector<Pending> pending;
+  ~AqlQueue() {
+    if (q) (void)hsa_queue_destroy(q);
+    if (sig.handle) (void)hsa_signal_destroy(sig);
+  }
+};
+#define HSACHK(x)                                                                              \
+  do {                                                                                         \
+    hsa_status_t s_ = (x);                                                                     \
+    if (s_ != HSA_STATUS_SUCCESS) throw Error{RLE_EHIP, std::string(#x) + ": hsa status " + std::to_string((int)s_)}; \
+  } while (0)
+
+static hsa_status_t aql_find_gpu(hsa_agent_t a, void* data) {
+  auto* want = static_cast<std::pair<uint32_t, hsa_agent_t>*>(data);
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0;
+  if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (bdf == want->first) {
+    want->second = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+struct AqlFind {
+  hsa_agent_t agent;
+  uint64_t kobj;
+  uint32_t gseg, pseg;
+};
+static hsa_status_t aql_find_kernel(hsa_executable_t exe, void* data) {
+  auto* f = static_cast<AqlFind*>(data);
+  hsa_executable_symbol_t sym;
+  if (hsa_executable_get_symbol_by_name(exe, level_kernel_symbol(), &f->agent, &sym) == HSA_STATUS_SUCCESS) {
+    hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &f->kobj);
+    hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &f->gseg);
+    hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &f->pseg);
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// The queue of device `dev`, after HIP has loaded librle's code object (any rle_level launch).
+static std::unique_ptr<AqlQueue> aql_open(int dev) {
+  auto A = std::make_unique<AqlQueue>();
+  HSACHK(hsa_init());
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, dev));
+  std::pair<uint32_t, hsa_agent_t> want{(uint32_t)((prop.pciBusID << 8) | (prop.pciDeviceID << 3)), {}};
+  hsa_iterate_agents(aql_find_gpu, &want);
+  REQUIRE(want.second.handle, "aql: no HSA agent for the HIP device");
+  A->agent = want.second;
+  hsa_ven_amd_loader_1_03_pfn_t tbl;
+  HSACHK(hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof(tbl), &tbl));
+  AqlFind f{A->agent, 0, 0, 0};
+  tbl.hsa_ven_amd_loader_iterate_executables(aql_find_kernel, &f);
+  REQUIRE(f.kobj, "aql: rle_level's kernel object is not loaded");
+  A->kobj = f.kobj;
+  A->gseg = f.gseg;
+  A->pseg = f.pseg;
+  uint32_t qmax = 0;
+  HSACHK(hsa_agent_get_info(A->agent, HSA_AGENT_INFO_QUEUE_MAX_SIZE, &qmax));
+  HSACHK(hsa_queue_create(A->agent, std::min<uint32_t>(qmax, 16384), HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
+                          UINT32_MAX, UINT32_MAX, &A->q));
+  HSACHK(hsa_signal_create(1, 0, nullptr, &A->sig));
+  auto scope = [](const char* v, int d) { return v ? std::max(0, std::min(2, std::atoi(v))) : d; };
+  A->acq = scope(std::getenv("RLE_AQL_ACQ"), HSA_FENCE_SCOPE_AGENT);
+  A->rel = scope(std::getenv("RLE_AQL_REL"), HSA_FENCE_SCOPE_AGENT);
+  return A;
+}
+
+// Writes every pending packet, rings the doorbell and waits for the last (host-side wall time
+// from the first doorbell to completion into *ms when given).
+static void aql_flush(AqlQueue& A, double* ms) {
+  const size_t n = A.pending.size();
+  if (!n) return;
+  hsa_signal_store_relaxed(A.sig, 1);
+  hsa_queue_t* q = A.q;
+  const uint64_t mask = q->size - 1;
+  std::chrono::steady_clock::time_point t0{};
+  bool rung = false;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
+    while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+    }
+    auto* pk = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx & mask);
+    pk->workgroup_size_x = kThreads;
+    pk->workgroup_size_y = 1;
+    pk->workgroup_size_z = 1;
+    pk->reserved0 = 0;
+    pk->grid_size_x = A.pending[i].grid * kThreads;
+    pk->grid_size_y = 1;
+    pk->grid_size_z = 1;
+    pk->private_segment_size = A.pseg;
+    pk->group_segment_size = A.gseg;
+    pk->kernel_object = A.kobj;
+    pk->kernarg_address = const_cast<void*>(A.pending[i].ka);
+    pk->reserved2 = 0;
+    const bool last = i + 1 == n;
+    pk->completion_signal = last ? A.sig : hsa_signal_t{0};
+    const int a = i == 0 ? HSA_FENCE_SCOPE_SYSTEM : A.acq, r = last ? HSA_FENCE_SCOPE_SYSTEM : A.rel;
+    const uint16_t hdr = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+                         (a << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) | (r << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+    __atomic_store_n((uint32_t*)pk, (uint32_t)hdr | (1u << 16), __ATOMIC_RELEASE);  // header | setup (1 dim)
+    if (last || (i & 63) == 63) {
+      hsa_signal_store_screlease(q->doorbell_signal, idx);
+      if (!rung) {
+        t0 = std::chrono::steady_clock::now();
+        rung = true;
+      }
+    }
+  }
+  A.pending.clear();
+  while (hsa_signal_wait_scacquire(A.sig, HSA_SIGNAL_CONDITION_LT, 1, 1000000000ull, HSA_WAIT_STATE_ACTIVE) >= 1) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 60)
+      throw Error{RLE_EHIP, "aql: dispatch did not complete within 60 s"};
+  }
+  if (ms) *ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 struct Graph {
   hipGraph_t g = nullptr;
   hipGraphExec_t x = nullptr;
@@ -1009,6 +1154,8 @@ struct Graph {
   std::string desc;
   int nlaunch = 0;  // rle_level dispatches per replay (a level of > kLevelOps ops takes several)
   std::vector<std::vector<Op>> host_levels;  // the launches' host op tables (RLE_EAGER replays)
+  std::vector<LevelLaunch> aql;               // (RLE_AQL) the dispatches' kernel arguments ...
+  unsigned char* aql_ka = nullptr;            // ... in device memory, 128 B apart
   int levels() const { return (int)nops.size(); }
 };
 
@@ -1960,7 +2107,7 @@ struct Engine {
     op.kind = OP_SAMPLE_GATHER;
     fill_sample_args(op.sample, sac);
     op.sample.ahead = ahead;
-    op.wg_count = B;
+    op.wg_count = cdiv(B, 4);  // one wave per query
     // reads the RNG step / tape position counters -> ordered before STEP_END (WAR)
     pg.add(op, {bsum_id, R_PRIO, R_REPLAY, R_CNT}, {ss.id, act_in.id, rw.id, nd.id, ind_id});
     Op nz{};
@@ -1989,6 +2136,7 @@ struct Engine {
     s.lap = rp.lap;
     s.B = B;
     s.bsum = rp.bsum;
+    s.ssum = rp.ssum;
     s.nblk = rp.nblk;
     s.ss = ss.m;
     s.a = act_in.m;
@@ -2310,6 +2458,7 @@ struct Engine {
       op.prio.B = B;
       op.prio.max_priority = replay->maxp_d;
       op.prio.bsum = replay->lap ? replay->bsum : nullptr;
+      op.prio.ssum = replay->ssum;
       op.wg_count = 1;
       pg.add(op, {prio.id, ind_id}, {R_PRIO, R_MAXP, bsum_id});
     }
@@ -2694,6 +2843,7 @@ struct Engine {
       op.prio.B = B;
       op.prio.max_priority = replay->maxp_d;
       op.prio.bsum = replay->lap ? replay->bsum : nullptr;
+      op.prio.ssum = replay->ssum;
       op.wg_count = 1;
       pg.add(op, {prio.id, ind_id}, {R_PRIO, R_MAXP, bsum_id});
     }
@@ -2922,6 +3072,7 @@ struct Engine {
       for (int w : G.nwg) G.trace_n += w;
       G.trace = mem.make<unsigned long long>((size_t)G.trace_n * trace_stride());
     }
+    if (aql_mode() && !G.trace) g_level_rec = &G.aql;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     long long tr_off = 0;
     static const bool dpf = [] {
@@ -2936,12 +3087,20 @@ struct Engine {
                                   dpf ? G.nops[ln] : 0);
       tr_off += G.nwg[l];
       if (e != hipSuccess) {
+        g_level_rec = nullptr;
         hipGraph_t tmp;
         (void)hipStreamEndCapture(stream, &tmp);
         throw Error{RLE_EHIP, std::string("launch during capture: ") + hipGetErrorString(e)};
       }
     }
+    g_level_rec = nullptr;
     HIPCHK(hipStreamEndCapture(stream, &G.g));
+    if (!G.aql.empty()) {
+      std::vector<unsigned char> ka(G.aql.size() * 128, 0);
+      for (size_t i = 0; i < G.aql.size(); ++i) std::memcpy(ka.data() + i * 128, G.aql[i].ka, sizeof G.aql[i].ka);
+      G.aql_ka = mem.make<unsigned char>(ka.size());
+      HIPCHK(hipMemcpy(G.aql_ka, ka.data(), ka.size(), hipMemcpyHostToDevice));
+    }
     HIPCHK(hipGraphInstantiate(&G.x, G.g, nullptr, nullptr, 0));
     G.host_levels = std::move(levels);
     return G;
@@ -3115,11 +3274,25 @@ struct Engine {
 
   // ---------------------------------------------------------------- run
   long long launches = 0;  // rle_level dispatches enqueued by step graphs (rle_launch_count)
+  std::unique_ptr<AqlQueue> aql;  // (RLE_AQL=1) direct dispatch of the step graphs
+  bool aql_active = false;        // inside step(): graphs go to the AQL queue
+  static bool aql_mode() {
+    static const bool on = [] {
+      const char* e = std::getenv("RLE_AQL");
+      return e && e[0] == '1';
+    }();
+    return on;
+  }
   void launch_graph(const Graph& G) {
     static const bool eager = [] {
       const char* e = std::getenv("RLE_EAGER");  // A/B: level launches on the stream, no graph
       return e && e[0] == '1';
     }();
+    if (aql_active && !G.aql.empty()) {
+      for (size_t i = 0; i < G.aql.size(); ++i) aql->pending.push_back({G.aql_ka + i * 128, G.aql[i].grid});
+      launches += G.nlaunch;
+      return;
+    }
     if (eager && !G.trace) {
       for (size_t l = 0; l < G.host_levels.size(); ++l)
         HIPCHK(launch_level(G.d_ops + G.off[l], G.host_levels[l].data(), G.nops[l], G.nwg[l], stream));
@@ -3142,10 +3315,19 @@ struct Engine {
       HIPCHK(hipEventCreate(&ev1));
       HIPCHK(hipEventRecord(ev0, stream));
     }
+    // direct dispatch (RLE_AQL=1): the graphs' levels go to the engine's own queue; the HIP
+    // stream is drained first and the queue after each chunk (host-side ordering between them)
+    const bool use_aql = aql_mode() && !async && !g_pol[0].aql.empty();
+    if (use_aql && !aql) aql = aql_open(cfg.device);
+    double aql_ms = 0.0;
     while (done < n) {
       const int chunk = std::min(n - done, info_cap);
       int zero = 0;
       HIPCHK(hipMemcpyAsync(&ctrl->info_slot, &zero, sizeof(int), hipMemcpyHostToDevice, stream));
+      if (use_aql) {
+        HIPCHK(hipStreamSynchronize(stream));
+        aql_active = true;
+      }
       for (int i = 0; i < chunk; ++i) {
         if (ctrl_tape_mode_host) {
           REQUIRE(tape_left > 0, "tape exhausted");
@@ -3199,6 +3381,10 @@ struct Engine {
         primed = true;
         primed_ver = replay->version;
       }
+      if (use_aql) {
+        aql_active = false;
+        aql_flush(*aql, &aql_ms);
+      }
       if (info_out) {
         HIPCHK(hipMemcpyAsync(info_out + (size_t)done * kInfoMax, info, (size_t)chunk * kInfoMax * sizeof(float),
                               hipMemcpyDeviceToHost, stream));
@@ -3211,6 +3397,7 @@ struct Engine {
       HIPCHK(hipEventRecord(ev1, stream));
       HIPCHK(hipEventSynchronize(ev1));
       HIPCHK(hipEventElapsedTime(gpu_ms, ev0, ev1));
+      if (use_aql) *gpu_ms = (float)aql_ms;  // (the levels ran outside the stream: host wall time)
       (void)hipEventDestroy(ev0);
       (void)hipEventDestroy(ev1);
     }
@@ -3279,7 +3466,9 @@ int rle_replay_create(int device, long long capacity, int state_dim, int action_
       const float one = 1.f;  // lap.py:29 max_priority = 1
       HIPCHK(hipMemcpy(r.maxp_d, &one, 4, hipMemcpyHostToDevice));
       r.nblk = rle::cdiv(capacity, 4096);
+      REQUIRE(!lap || capacity <= 64LL * 16 * 4096, "LAP replay capacity above 4M rows");  // (sampler: 16 blocks per lane)
       r.bsum = r.mem.make<double>(r.nblk);
+      r.ssum = r.mem.make<double>((size_t)r.nblk * 64);
       r.maxred_part = r.mem.make<float>(r.maxred_nwg);
     } catch (...) {
       delete h;
@@ -3338,7 +3527,7 @@ int rle_replay_append(rle_replay* h, const float* state, const float* action, co
       HIPCHK(rle::launch_append(r.state, r.next_state, r.action, r.reward, r.notdone, r.priority, ds,
                                 ds + (size_t)c * r.Sp, ds + 2 * (size_t)c * r.Sp, ds + 2 * (size_t)c * r.Sp + c * r.Ap,
                                 ds + 2 * (size_t)c * r.Sp + c * r.Ap + c, r.ptr, r.cap, (int)c, r.Sp, r.Ap, r.maxp_d,
-                                r.lap, r.bsum, r.size, r.stream));
+                                r.lap, r.bsum, r.ssum, r.size, r.stream));
       r.ptr = (r.ptr + c) % r.cap;
       r.size = std::min(r.size + c, r.cap);
       ++r.version;
@@ -3424,6 +3613,7 @@ static void recompute_bsum(Replay& r) {
   a.sample.priority = r.priority;
   a.sample.size = r.size_d;
   a.sample.bsum = r.bsum;
+  a.sample.ssum = r.ssum;
   a.wg_count = r.nblk;
   run_eager(r, {{a}});
 }
@@ -3451,6 +3641,7 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     s.lap = r.lap;
     s.B = n;
     s.bsum = r.bsum;
+    s.ssum = r.ssum;
     s.nblk = r.nblk;
     auto timg = [&](const char* name, int rows, int cols) {  // scratch T image (outputs are not read back)
       rle::Mat m{};
@@ -3482,7 +3673,7 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     rle::Op b{};
     b.kind = rle::OP_SAMPLE_GATHER;
     b.sample = s;
-    b.wg_count = n;
+    b.wg_count = rle::cdiv(n, 4);
     lv.push_back({b});
     run_eager(r, lv);
     HIPCHK(hipMemcpy(ind_out, dind, n * sizeof(long long), hipMemcpyDeviceToHost));
@@ -3512,6 +3703,7 @@ int rle_replay_update_priority(rle_replay* h, int n, const long long* ind, const
     op.prio.B = n;
     op.prio.max_priority = r.maxp_d;
     op.prio.bsum = r.lap && !small ? r.bsum : nullptr;
+    op.prio.ssum = r.ssum;
     op.wg_count = 1;
     run_eager(r, {{op}});
     if (r.lap && small) recompute_bsum(r);

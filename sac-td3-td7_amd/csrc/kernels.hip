@@ -28,6 +28,9 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <cstring>
+#include <vector>
+
 #include "ops.h"
 
 #define CAS __attribute__((address_space(4)))
@@ -996,7 +999,11 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     const int va = ((i0 >> 4) * a0xs + c0) * 1024 + lb;
     const int vb = (((j0 - sb.x0) >> 4) * sb.xs + c0) * 1024 + lb;
     const int vx = ACT == kDwNb ? ((i0 >> 4) * g.nbx_xs + c0) * 1024 + lb : 0;
+#ifdef RLE_EXP_DW_NOLOOP  // timing experiment only: no DW main loop
+    const int nrun = 0;
+#else
     const int nrun = run ? c1 - c0 : 0;
+#endif
     float4 ra[kRing], rb[kRing], rx[kRing];
     ring_issue(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, bias_tile);
     if constexpr (ACT == kDwNb) {
@@ -1190,7 +1197,11 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       st4g(pw, make_float4(po[0], po[1], po[2], po[3]));
       st4g(pw + ad.mo, make_float4(mo[0], mo[1], mo[2], mo[3]));
       st4g(pw + ad.vo, make_float4(vo[0], vo[1], vo[2], vo[3]));
+#ifdef RLE_EXP_NO_NSTORE  // timing experiment only: no N-image weight store
+      if (false) {
+#else
       if (!bias_tile) {
+#endif
         GAS float* qn = GW(ad.w.n) + nidx(ad.w.cbn, ib, j);
         qn[0] = po[0];
         qn[4] = po[1];
@@ -1477,22 +1488,20 @@ __device__ __forceinline__ void op_head(const CAS HeadArgs& h, int t, float* sme
 
 constexpr int kBlk = 4096;  // priorities per block-sum
 
-// Exact fp64 block sums of the priorities (lap.py:47; Q8: any-order fp64 is exact).
+// Exact fp64 block sums of the priorities (lap.py:47; Q8: any-order fp64 is exact), and the
+// 64-priority sub-block sums of the same block.  Thread tid sums 16 consecutive priorities (rows
+// past the replay size count as 0); 4 threads make a sub-block.
+constexpr int kSub = 64;  // priorities per sub-block sum
 __device__ __forceinline__ void op_sample_reduce(const CAS SampleArgs& s, int t, float* smem) {
   const long long size = sload(s.size);
-  const long long base = (long long)t * kBlk;
+  const long long e0 = (long long)t * kBlk + (long long)threadIdx.x * 16;
   double acc = 0.0;
 #pragma unroll
-  for (int u = 0; u < kBlk / (4 * kThreads); ++u) {
-    const long long k = base + (long long)(u * kThreads + threadIdx.x) * 4;
-    if (k + 3 < size) {
-      const float4 v = ld4g(G(s.priority) + k);
-      acc += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
-    } else {
-      for (int e = 0; e < 4; ++e)
-        if (k + e < size) acc += (double)G(s.priority)[k + e];
-    }
-  }
+  for (int q = 0; q < 16; ++q)
+    if (e0 + q < size) acc += (double)G(s.priority)[e0 + q];
+  double sub = acc + dpp_d<0xb1>(acc);  // quad_perm [1,0,3,2]
+  sub += dpp_d<0x4e>(sub);              // quad_perm [2,3,0,1]: the quad's 64 priorities
+  if ((threadIdx.x & 3) == 0 && s.ssum) GW(s.ssum)[(size_t)t * (kBlk / kSub) + (threadIdx.x >> 2)] = sub;
   acc = wave_sum_d(acc);
   double* dred = reinterpret_cast<double*>(smem);
   if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = acc;
@@ -1547,10 +1556,24 @@ __device__ __forceinline__ void op_noise(const CAS SampleArgs& s, int t) {
   if (s.eps2.t) mat_st(s.eps2, b, j, v2);
 }
 
-// One workgroup per query: uniform / LAP index search (searchsorted left over the
-// fp32-rounded exact prefix), noise for this row, then the coalesced row gather.
-__device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b, float* smem, unsigned long long* tr) {
-  const int tid = threadIdx.x;
+// One WAVE per query (4 per workgroup): uniform / LAP index search (searchsorted left over the
+// fp32-rounded exact prefix), then the coalesced row gather.  The LAP search descends three
+// levels of exact fp64 sums: the 4096-priority block sums (each lane owns a run of blocks), the
+// 64 sub-block sums of the chosen block (one per lane), the 64 priorities of the chosen sub-block
+// (one per lane) -- about 0.8 KB read per query instead of a whole 16 KB block.  At each level the
+// answer lies in the first unit whose rounded inclusive prefix is >= v: prefixes are monotone, so
+// an element qualifying in an earlier unit would make that unit qualify (the last unit if none).
+__device__ __forceinline__ int first_lane(bool p) {
+  const unsigned long long bal = __ballot(p);
+  return bal ? __builtin_ffsll((long long)bal) - 1 : -1;
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t, float* smem, unsigned long long* tr) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = t * 4 + wave;  // query (wave-uniform)
+  if (b >= s.B) return;
   const long long size = sload(s.size);
   const int tape = sload(s.tape_mode);
   const long long pos = sload(s.tape_pos) + s.ahead;
@@ -1558,62 +1581,53 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
   const unsigned long long step = (unsigned long long)sload(s.ctrl_rng) + s.ahead;
   FINE_MARK(0);
   const bool tind = tape & kTapeInd;
-  float u = 0.f;
-  if (!tind) {
-    if (tape & kTapeU) u = G(s.tape_u)[(size_t)pos * s.B + b];
-    else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
-  }
-  // LAP block sums: thread tid owns blocks [tid*per, tid*per + per) of the CAPACITY's blocks,
-  // per <= 8 (capacity <= 8M), so the loads go out with the control loads above instead of
-  // after them; blocks past the replay size are zeroed below (exact fp64 sums: the prefix
-  // does not depend on how the blocks are split over threads)
+  // LAP block sums: lane l owns blocks [l * per, l * per + per) of the CAPACITY's blocks (per <= 16,
+  // capacity <= 4M), loaded with the control values; blocks past the replay size are zeroed below
   const int nb = (int)((size + kBlk - 1) / kBlk);
   const int nbc = (int)((s.cap + kBlk - 1) / kBlk);
-  const int per = (nbc + kThreads - 1) / kThreads;
-  double bs[8];
-  if (s.lap) {
+  const int per = (nbc + 63) >> 6;
+  double bs[16];
+  if (s.lap && !tind) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) bs[q] = q < per ? G(s.bsum)[min(tid * per + q, nbc - 1)] : 0.0;  // (per: uniform)
+    for (int q = 0; q < 16; ++q) bs[q] = q < per ? G(s.bsum)[min(lane * per + q, nbc - 1)] : 0.0;  // (per: uniform)
+  }
+  float u = 0.f;
+  if (!tind) {
+    if (tape & kTapeU) u = sload(s.tape_u + (size_t)pos * s.B + b);
+    else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
   }
   FINE_MARK(1);
   long long ind;
   if (tind) {
-    // (host-checked in range; the clamp only guards a prefetch past a tape's end,
-    // whose batch the host discards)
-    ind = G(s.tape_ind)[(size_t)pos * s.B + b];
+    // (host-checked in range; the clamp only guards a prefetch past a tape's end, whose batch
+    // the host discards)
+    ind = sload(s.tape_ind + (size_t)pos * s.B + b);
     ind = ind < 0 ? 0 : (ind > size - 1 ? size - 1 : ind);
   } else {
-    if (tid == 0) GW(s.u_out)[b] = u;
+    if (lane == 0) GW(s.u_out)[b] = u;
     if (!s.lap) {
       // searchsorted(cumsum(ones(size)), u*size): first j in 1..size with j >= v
       const float v = u * (float)size;
       const long long k = (long long)ceilf(v) - 1;
       ind = k < 0 ? 0 : (k > size - 1 ? size - 1 : k);
     } else {
-      // exact fp64 prefix over block sums, rounded to fp32 per element (Q8)
-      const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-      double* wtot = reinterpret_cast<double*>(smem) + 2;  // [8]: two scans
-      int* wm = reinterpret_cast<int*>(smem + 32);          // [4] per-wave first block
-      double* wb = reinterpret_cast<double*>(smem) + 18;    // [4] its prefix base
-      int* wh = reinterpret_cast<int*>(smem + 48);          // [4] per-wave first hit
+      // level 1: the blocks (exact fp64 prefix, rounded to fp32 per unit: Q8)
       double loc = 0.0;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (q >= per || tid * per + q >= nb) bs[q] = 0.0;
+      for (int q = 0; q < 16; ++q) {
+        if (q >= per || lane * per + q >= nb) bs[q] = 0.0;
         loc += bs[q];
       }
-      FINE_MARK(2);
-      double total;
-      double run = wg_scan_excl_d(loc, wtot, total);
-      FINE_MARK(3);
+      double inc = wave_scan_incl_d(loc);
+      const double total = readlane_d(inc, 63);
       const float v = u * (float)total;
-      // first block whose rounded inclusive prefix >= v (the last block if none)
-      int mine = 0x7FFFFFFF;
+      double run = inc - loc;
+      int mine = -1;
       double mbase = 0.0;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int k = tid * per + q;
-        if (q < per && k < nb && mine == 0x7FFFFFFF) {
+      for (int q = 0; q < 16; ++q) {
+        const int k = lane * per + q;
+        if (q < per && k < nb && mine < 0) {
           if ((float)(run + bs[q]) >= v || k == nb - 1) {
             mine = k;
             mbase = run;
@@ -1621,101 +1635,58 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int b,
           run += bs[q];
         }
       }
-      // the qualifying blocks form a suffix in thread order (monotone prefix), so the
-      // answer is the first qualifying lane of the first wave that has one: ballot +
-      // readlane per wave, no atomics (whose per-lane loops cost microseconds here)
-      {
-        const unsigned long long bal = __ballot(mine != 0x7FFFFFFF);
-        int m = 0x7FFFFFFF;
-        double mb = 0.0;
-        if (bal) {
-          const int fl = __builtin_ffsll((long long)bal) - 1;
-          m = __builtin_amdgcn_readlane(mine, fl);
-          mb = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(mbase), fl),
-                                __builtin_amdgcn_readlane(__double2loint(mbase), fl));
-        }
-        if (lane == 0) {
-          wm[wave] = m;
-          wb[wave] = mb;
-        }
-      }
-      __syncthreads();
-      int lo = 0x7FFFFFFF;
-      double base = 0.0;
-#pragma unroll
-      for (int w = 3; w >= 0; --w) {
-        if (wm[w] != 0x7FFFFFFF) {
-          lo = wm[w];
-          base = wb[w];
-        }
-      }
-      trace_mark(tr, 1);
-      const long long e0 = (long long)lo * kBlk + (long long)tid * 16;
-      // 16 priorities per thread: four 16-byte buffer loads (past the capacity read 0)
-      const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(s.priority + (size_t)lo * kBlk), 0, (int)(min((long long)kBlk, s.cap - (long long)lo * kBlk) * 4),
-          0x00020000);
-      float pv[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 x = bload(pr, (tid * 16 + 4 * q) * 4);
-        pv[4 * q] = x.x;
-        pv[4 * q + 1] = x.y;
-        pv[4 * q + 2] = x.z;
-        pv[4 * q + 3] = x.w;
-      }
-      double tl = 0.0;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        if (e0 + q >= size) pv[q] = 0.f;
-        tl += (double)pv[q];
-      }
-      FINE_MARK(4);
-      double btot;
-      run = base + wg_scan_excl_d(tl, wtot + 4, btot);
-      FINE_MARK(5);
-      int hit = 0x7FFFFFFF;  // offset in the block
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        run += (double)pv[q];
-        if (hit == 0x7FFFFFFF && e0 + q < size && (float)run >= v) hit = tid * 16 + q;
-      }
-      {
-        const unsigned long long bal = __ballot(hit != 0x7FFFFFFF);
-        const int h = bal ? __builtin_amdgcn_readlane(hit, __builtin_ffsll((long long)bal) - 1) : 0x7FFFFFFF;
-        if (lane == 0) wh[wave] = h;
-      }
-      __syncthreads();
-      int off = 0x7FFFFFFF;
-#pragma unroll
-      for (int w = 3; w >= 0; --w)
-        if (wh[w] != 0x7FFFFFFF) off = wh[w];
-      ind = off == 0x7FFFFFFF ? size - 1 : (long long)lo * kBlk + off;
+      const int l1 = first_lane(mine >= 0);  // (nb >= 1: some lane holds the last block)
+      const int blk = __builtin_amdgcn_readlane(mine, l1);
+      double base = readlane_d(mbase, l1);
+      FINE_MARK(2);
+      // level 2: the block's 64 sub-blocks, one per lane
+      const int nsub = (int)min((long long)(kBlk / kSub), (size - (long long)blk * kBlk + kSub - 1) / kSub);
+      const double sv = lane < nsub ? G(s.ssum)[(size_t)blk * (kBlk / kSub) + lane] : 0.0;
+      inc = wave_scan_incl_d(sv);
+      const int l2 = first_lane(lane < nsub && ((float)(base + inc) >= v || lane == nsub - 1));
+      const int sub = max(l2, 0);
+      base += readlane_d(inc - sv, sub);
+      FINE_MARK(3);
+      // level 3: the sub-block's 64 priorities, one per lane
+      const long long e = (long long)blk * kBlk + (long long)sub * kSub + lane;
+      const float pv = e < size ? G(s.priority)[e] : 0.f;
+      inc = wave_scan_incl_d((double)pv);
+      const int l3 = first_lane(e < size && (float)(base + inc) >= v);
+      ind = l3 < 0 ? size - 1 : (long long)blk * kBlk + (long long)sub * kSub + l3;
       if (ind >= size) ind = size - 1;
     }
   }
   trace_mark(tr, 2);
-  // gather the transition into the batch images (rows b and B + b of ss): thread
-  // tid moves columns 4 tid .. 4 tid + 3 (rows are 16-float aligned); every load is
-  // issued before any store (one memory round trip)
-  const int c = 4 * tid;
-  float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0, va = v0;
-  float rv = 0.f, dv = 0.f;
-  if (c < s.Sp) {
-    v0 = ld4g(G(s.state) + (size_t)ind * s.Sp + c);
-    v1 = ld4g(G(s.next_state) + (size_t)ind * s.Sp + c);
+  // gather the transition into the batch images (rows b and B + b of ss): lane l moves columns
+  // 4 l .. 4 l + 3 (+ 256 per pass; rows are 16-float aligned); every load is issued before any
+  // store (one memory round trip)
+  float4 v0[2], v1[2];
+  float4 va = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = 4 * lane + 256 * p;
+    v0[p] = v1[p] = va;
+    if (c < s.Sp) {
+      v0[p] = ld4g(G(s.state) + (size_t)ind * s.Sp + c);
+      v1[p] = ld4g(G(s.next_state) + (size_t)ind * s.Sp + c);
+    }
   }
-  if (c < s.Ap) va = ld4g(G(s.action) + (size_t)ind * s.Ap + c);
-  if (tid == 0) {
+  if (4 * lane < s.Ap) va = ld4g(G(s.action) + (size_t)ind * s.Ap + 4 * lane);
+  float rv = 0.f, dv = 0.f;
+  if (lane == 0) {
     rv = G(s.reward)[ind];
     dv = G(s.notdone)[ind];
   }
-  if (c < s.Sp) {
-    mat_str4(s.ss, b, c, v0);
-    mat_str4(s.ss, s.B + b, c, v1);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = 4 * lane + 256 * p;
+    if (c < s.Sp) {
+      mat_str4(s.ss, b, c, v0[p]);
+      mat_str4(s.ss, s.B + b, c, v1[p]);
+    }
   }
-  if (c < s.Ap) mat_str4(s.a, b, c, va);
-  if (tid == 0) {
+  if (4 * lane < s.Ap) mat_str4(s.a, b, 4 * lane, va);
+  if (lane == 0) {
     GW(s.r)[b] = rv;
     GW(s.nd)[b] = dv;
     GW(s.ind)[b] = ind;
@@ -1765,7 +1736,11 @@ __device__ __forceinline__ void op_priority(const CAS PriorityArgs& a, float* sm
       // priorities (>= 1, lap.py) and their sums are exact, so any order gives the sums
       // a full recompute would (op_sample_reduce)
       const int key = mine[u & 3];
-      if (a.bsum) atomicAdd(&a.bsum[key / kBlk], (double)pv - (double)G(a.priority)[key]);
+      if (a.bsum) {
+        const double d = (double)pv - (double)G(a.priority)[key];
+        atomicAdd(&a.bsum[key / kBlk], d);
+        atomicAdd(&a.ssum[key / kSub], d);
+      }
       GW(a.priority)[key] = pv;
     }
     mx = fmaxf(mx, pv);
@@ -2362,7 +2337,7 @@ __global__ __launch_bounds__(kThreads, 1) void rle_act_chain(const ActChainArgs 
 __global__ void rle_append_kernel(float* state, float* next_state, float* action, float* reward, float* notdone,
                                   float* priority, const float* st_s, const float* st_ns, const float* st_a,
                                   const float* st_r, const float* st_d, long long ptr, long long cap, int count,
-                                  int Sp, int Ap, const float* max_priority, int lap, double* bsum,
+                                  int Sp, int Ap, const float* max_priority, int lap, double* bsum, double* ssum,
                                   long long size_before) {
   const int i = blockIdx.x;
   if (i >= count) return;
@@ -2380,6 +2355,7 @@ __global__ void rle_append_kernel(float* state, float* next_state, float* action
       const float old = row < size_before ? priority[row] : 0.f;
       priority[row] = nv;
       atomicAdd(&bsum[row / kBlk], (double)nv - (double)old);
+      atomicAdd(&ssum[row / kSub], (double)nv - (double)old);
     }
   }
 }
@@ -2423,6 +2399,12 @@ int level_capacity() {
   return per_cu * cus;
 }
 
+// (host) when set, launch_level also appends each dispatch's kernel arguments here (capture of the
+// AQL launch lists; traced launches are never recorded)
+std::vector<LevelLaunch>* g_level_rec = nullptr;
+// the production kernel's HSA symbol name (AQL dispatch)
+const char* level_kernel_symbol() { return "_ZN3rle9rle_levelILb0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"; }
+
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
                         unsigned long long* trace, const Op* next_ops, int next_nops) {
   // a level of more than kLevelOps ops runs as consecutive launches of kLevelOps (its
@@ -2452,6 +2434,16 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
       }
     }
     if (npf) la.entry[0] |= 0x80000000u;
+    if (g_level_rec && !trace) {
+      LevelLaunch L{};
+      std::memcpy(L.ka, la.entry, sizeof la.entry);
+      std::memcpy(L.ka + 48, &la.ops, 8);
+      std::memcpy(L.ka + 56, &la.trace, 8);
+      std::memcpy(L.ka + 64, &next, 8);
+      std::memcpy(L.ka + 72, &next_lines, 4);
+      L.grid = (unsigned)(w1 - w0 + npf);
+      g_level_rec->push_back(L);
+    }
 #define RLE_LEVEL_ARGS                                                                                         \
   la.entry[0], la.entry[1], la.entry[2], la.entry[3], la.entry[4], la.entry[5], la.entry[6], la.entry[7], \
       la.entry[8], la.entry[9], la.entry[10], la.entry[11], la.ops, la.trace, next, next_lines
@@ -2466,10 +2458,10 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count, int Sp,
-                         int Ap, const float* max_priority, int lap, double* bsum, long long size_before,
+                         int Ap, const float* max_priority, int lap, double* bsum, double* ssum, long long size_before,
                          hipStream_t st) {
   hipLaunchKernelGGL(rle_append_kernel, dim3(count), dim3(256), 0, st, state, next_state, action, reward, notdone,
-                     priority, st_s, st_ns, st_a, st_r, st_d, ptr, cap, count, Sp, Ap, max_priority, lap, bsum,
+                     priority, st_s, st_ns, st_a, st_r, st_d, ptr, cap, count, Sp, Ap, max_priority, lap, bsum, ssum,
                      size_before);
   return hipGetLastError();
 }

@@ -308,6 +308,7 @@ struct SampleArgs {
   long long cap;                     // replay capacity (priority array length)
   int lap, B;
   double* bsum; int nblk;            // LAP block sums (fp64), 4096 priorities per block
+  double* ssum;                      // LAP sub-block sums (fp64), 64 priorities each (64 per block)
   // outputs
   Mat ss;                            // [2B][Sp] rows 0..B-1 state, B..2B-1 next_state (N + T)
   Mat a;                             // [B][Ap] (N + T)
@@ -329,6 +330,7 @@ struct PriorityArgs {
   float* priority; const long long* ind; const float* p; int B;
   float* max_priority;
   double* bsum;          // LAP block sums kept in step with the scatter (nullptr: none)
+  double* ssum;          // ... and the sub-block sums
 };
 
 struct SacActorArgs {
@@ -479,6 +481,14 @@ struct LevelArgs {
   unsigned entry[kLevelOps];
 };
 constexpr int kMaxLevelWG = 0xfffe;  // workgroups per launch (16-bit entry field)
+
+// One rle_level dispatch as an AQL packet needs it (engine.cpp direct dispatch, RLE_AQL): the
+// kernel-argument bytes (rle_level<false>'s 76-byte segment: no hidden arguments) and the
+// workgroup count.  launch_level appends one per dispatch while g_level_rec is set.
+struct LevelLaunch {
+  unsigned char ka[80];
+  unsigned grid;  // workgroups
+};
 
 // Device control block.
 struct Ctrl {

@@ -27,7 +27,7 @@ def child(idx, threads, seconds, cpus):
     torch.set_num_threads(threads)
     import bench
 
-    r = bench.cpu_baseline(seconds)
+    r = bench.cpu_baseline(seconds, pin=False)  # (pinned here: this process's own CPU set)
     r["proc"] = idx
     r["cpus"] = sorted(cpus)
     print(json.dumps(r), flush=True)
