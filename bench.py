@@ -133,6 +133,9 @@ def cpu_baseline(seconds=12.0, algo="td7", env="Humanoid-v4", batch=B, lap=True,
     s_dim, a_dim, hi = TASKS[env]
     old_aff, old_threads = os.sched_getaffinity(0), torch.get_num_threads()
     sock, cpus, ncore = socket_cores()
+    # the GPU box is a one-GPU share of an 8-GPU host: 16 of its CPUs are this box's (more threads
+    # contend with other tenants and measure less); RLE_CPU_THREADS overrides
+    cpus = cpus[:int(os.environ.get("RLE_CPU_THREADS", "16"))]
     if pin and cpus:
         os.sched_setaffinity(0, cpus)
         torch.set_num_threads(len(cpus))
@@ -187,7 +190,8 @@ def _cpu_run(seconds, algo, env, batch, lap, s_dim, a_dim, hi, agents, replay, s
             "kind": "port",
             "sample": f"{n} {algo.upper()} {env} B={batch} steps ({'LAP' if lap else 'uniform'} over a 1M replay) "
                       f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads} pinned one per physical core "
-                      f"of socket {pinning['socket']} ({pinning['physical_cores_socket']} physical cores)",
+                      f"of socket {pinning['socket']} ({pinning['physical_cores_socket']} physical cores; the box's "
+                      f"share is 16 CPUs)",
             "host": hc}
 
 
@@ -415,6 +419,26 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, chunk=25):
         dist.barrier()
 
 
+def kfd_gpu_count(root="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs visible to this process without any HIP / HSA call: the KFD topology nodes that have
+    SIMDs (/sys/class/kfd/kfd/topology/nodes/*/properties), narrowed by HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set."""
+    import glob
+
+    n = 0
+    for f in glob.glob(os.path.join(root, "*", "properties")):
+        try:
+            props = dict(line.split() for line in open(f) if len(line.split()) == 2)
+        except OSError:
+            continue
+        n += int(props.get("simd_count", "0")) > 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(n, argv, device_count):
     """``--gpus N`` without a launcher (WORLD_SIZE unset): start N fresh rank processes of this
     script, one per GPU, each with RANK / LOCAL_RANK / WORLD_SIZE and a local rendezvous.  The
@@ -484,7 +508,7 @@ def main():
         else:
             import torch
 
-            count = torch.cuda.device_count  # counts devices without initialising them
+            count = kfd_gpu_count  # (no HIP call in the parent before the ranks start)
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], count))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:

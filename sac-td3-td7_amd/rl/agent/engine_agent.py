@@ -44,8 +44,13 @@ class EngineAgent(Agent, Sampler):
     NULLABLE: tuple = ()  # info keys the reference sets to None on non-policy steps
 
     def _setup(self, env_id, *, hidden, batch_size, seed, device, make_nn, make_nn_kwargs, cfg):
-        if make_nn is not None:
-            raise NotImplementedError("engine agents build the reference's default nets; pass hidden= for width")
+        custom = None
+        if make_nn is not None:  # td7.py:56-61 / td3.py:53-56 / sac.py:47-50 (rl.nn.modules nets only)
+            from rl.nn.modules import nets_from_make_nn
+
+            S, A = get_state_action_dims(env_id)
+            hidden, custom = nets_from_make_nn(self.ALG, make_nn, S, A, make_nn_kwargs)
+            make_nn_kwargs = {}
         hdim = make_nn_kwargs.pop("hdim", None) or make_nn_kwargs.pop("zs_dim", None)
         hs = make_nn_kwargs.pop("hidden_sizes", None)
         if make_nn_kwargs:
@@ -70,7 +75,12 @@ class EngineAgent(Agent, Sampler):
         self.device = device if device is not None else "cuda:0"
         self._replay = None
         self.engine = self._new_engine(int(batch_size))
-        nets = init_agent(self.ALG, self.state_dim, self.action_dim, self.hidden, self.seed)
+        if custom is not None:  # the hook's nets, and their construction-time copies (td7.py:62-66)
+            nets = dict(custom)
+            for name, src in AGENT_COPIES[self.ALG].items():
+                nets[name] = {k: v.copy() for k, v in custom[src].items()}
+        else:
+            nets = init_agent(self.ALG, self.state_dim, self.action_dim, self.hidden, self.seed)
         self._import({"params": nets})
 
     # ---- engine lifecycle ----------------------------------------------------
@@ -208,7 +218,7 @@ class EngineAgent(Agent, Sampler):
         reads rows ``batch.ind`` in HBM (the host tensors in the dict are not re-uploaded).
         Target-policy / rsample noise comes from the engine's Philox stream."""
         if not isinstance(batch, DeviceBatch):
-            raise ValueError("engine train_ops needs the DeviceBatch returned by a device replay's sample()")
+            return self._train_host_batch(batch, replay_buffer)
         rep = replay_buffer if replay_buffer is not None else batch.replay
         if batch.replay is not rep:
             raise ValueError("batch was drawn from a different replay than replay_buffer")
@@ -219,6 +229,53 @@ class EngineAgent(Agent, Sampler):
             row = self.engine.step(1)[0]
         finally:
             self.engine.set_tapes()
+        return self._info(row)
+
+    def _train_host_batch(self, batch, replay_buffer):
+        """train_ops on any BATCH dict (annotation.py:23-30: state, action, reward, next_state,
+        done as arrays or tensors; action in the replay's stored form, done the not-done mask):
+        the rows go into a B-row device ring bound to the engine, the step runs on rows 0..B-1,
+        and a LAP replay_buffer gets the new priorities through its own update_priority (and its
+        reset_max_priority at TD7 hard updates), as td7.py:236-240, 325-331 would call them."""
+
+        missing = [k for k in ("state", "action", "reward", "next_state", "done") if k not in batch]
+        if missing:
+            raise ValueError(f"BATCH (annotation.py:23-30) without {missing}")
+
+        def arr(k, shape):
+            v = batch[k]
+            if hasattr(v, "detach"):
+                v = v.detach().cpu().numpy()
+            return np.ascontiguousarray(np.asarray(v, np.float32).reshape(shape))
+
+        B = int(np.asarray(batch["reward"].shape[0] if hasattr(batch["reward"], "shape") else len(batch["reward"])))
+        s, a = arr("state", (B, self.state_dim)), arr("action", (B, self.action_dim))
+        r, s2, d = arr("reward", (B,)), arr("next_state", (B, self.state_dim)), arr("done", (B,))
+        lap = bool(self._cfg.get("use_lap")) and self.ALG != "sac"
+        ring = getattr(self, "_host_ring", None)
+        if ring is None or ring.capacity != B or getattr(ring, "device", None) != self._device:
+            ring = self._host_ring = E.Replay(B, self.state_dim, self.action_dim, lap, self._device)
+            ring.device = self._device
+        ring.append(s, a, r, s2, d)  # (capacity B: the write pointer returns to row 0)
+        # (graphs capture the bound replay: another replay or batch size means a fresh engine)
+        if B != self.batch_size or (self._replay is not None and self._replay is not ring):
+            self._rebuild(B)
+        if self._replay is not ring:
+            self.engine.bind(ring)
+            self._replay = ring
+        hard_before = self.engine.counters()[3]
+        self.engine.set_tapes(ind=np.arange(B, dtype=np.int64)[None])
+        try:
+            row = self.engine.step(1)[0]
+        finally:
+            self.engine.set_tapes()
+        if lap and replay_buffer is not None and hasattr(replay_buffer, "update_priority"):
+            import torch
+
+            replay_buffer.update_priority(torch.from_numpy(ring.get_priority(B).copy()))
+            tur = int(self._cfg.get("target_update_rate", 250))
+            if self.ALG == "td7" and (hard_before + 1) % tur == 0 and hasattr(replay_buffer, "reset_max_priority"):
+                replay_buffer.reset_max_priority()
         return self._info(row)
 
     def train_n(self, replay_buffer: BaseReplayMemory, batch_size: int, n_ops: int):

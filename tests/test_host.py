@@ -77,8 +77,14 @@ def test_train_ops_rejects_batches_not_drawn_from_a_device_replay():
 
 
 def test_engine_agents_reject_custom_nets():
-    with pytest.raises(NotImplementedError):
+    """make_nn hooks must return the reference's default net types (rl.nn.*), checked before any
+    engine exists."""
+    with pytest.raises(TypeError):
         TD3("HalfCheetah-v4", make_nn=lambda **k: None)
+    import torch
+
+    with pytest.raises(NotImplementedError):
+        TD3("HalfCheetah-v4", make_nn=lambda state_dim, action_dim, **k: (torch.nn.Linear(1, 1),) * 3)
 
 
 def test_missing_library_fails_loudly(tmp_path, monkeypatch):
@@ -161,3 +167,19 @@ def test_sac_lap_fails_like_the_reference():
     sac.use_lap = True
     with pytest.raises(AttributeError, match="_lap_huber"):
         sac.train_ops(DeviceBatch({}, np.zeros(4, np.int64), None), None)
+
+
+def test_kfd_gpu_count_reads_topology_without_hip(tmp_path, monkeypatch):
+    """bench.launch_ranks counts GPUs from the KFD topology (nodes with SIMDs; the CPU node has
+    none), narrowed by the *_VISIBLE_DEVICES variables -- no HIP call in the parent."""
+    import bench
+
+    for i, simd in enumerate((0, 1024, 1024, 1024)):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count {64 if simd == 0 else 0}\nsimd_count {simd}\n")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert bench.kfd_gpu_count(str(tmp_path)) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1,2")
+    assert bench.kfd_gpu_count(str(tmp_path)) == 2

@@ -300,3 +300,87 @@ def test_act_chain_failed_hand_off_is_reported(monkeypatch):
     monkeypatch.delenv("RLE_ACT_FAIL_WG")
     ref = TD3("Tiny-v0", hidden=32, batch_size=32, seed=2).sample(obs, deterministic=True)
     assert np.array_equal(ag.sample(obs, deterministic=True), ref)
+
+
+def test_make_nn_hook_with_reference_net_types():
+    """td7.py:56-61 / td3.py:53-56 / sac.py:47-50: a make_nn callable returning the reference's
+    default net types (rl.nn.SALEActor / SALECritic / SALEEncoder, MLPActor / MLPCritic) at one
+    width builds the engine at that width with the hook's initial weights (targets and fixed
+    encoders copies of them); other types or mixed widths are rejected."""
+    from rl.nn import MLPActor, MLPCritic, SALEActor, SALECritic, SALEEncoder
+
+    torch.manual_seed(0)
+    made = {}
+
+    def mk7(state_dim, action_dim, **kw):
+        made["td7"] = (SALEActor(state_dim, action_dim, 32, 32), SALECritic(state_dim, action_dim, 32, 32),
+                       SALECritic(state_dim, action_dim, 32, 32), SALEEncoder(state_dim, action_dim, 32, 32))
+        return made["td7"]
+
+    ag = TD7("Tiny-v0", make_nn=mk7, batch_size=16, seed=1)
+    assert ag.hidden == 32
+    sd = ag.state_dict()
+    for name, m in zip(("policy", "q1", "q2", "encoder"), made["td7"]):
+        for k, v in m.state_dict().items():
+            np.testing.assert_array_equal(sd[name][k], v.numpy())
+    for k, v in made["td7"][3].state_dict().items():
+        np.testing.assert_array_equal(sd["fixed_encoder_target"][k], v.numpy())
+    # forward parity with the hook's own torch modules (the device act path)
+    obs = np.linspace(-1, 1, S).astype(np.float32)
+    pol, enc = made["td7"][0], made["td7"][3]
+    with torch.no_grad():
+        x = torch.from_numpy(obs)[None]
+        ref = pol.inference_mean(x, enc.encode_state(x)).numpy()[0] * ag.action_scale + ag.action_bias
+    got = ag.sample(obs, deterministic=True)
+    assert np.abs(got - ref).max() <= 2e-6 + 1e-5 * np.abs(ref).max()
+
+    def mk3(state_dim, action_dim, **kw):
+        return MLPActor(state_dim, action_dim, 64), MLPCritic(state_dim, action_dim, 64), MLPCritic(state_dim, action_dim, 64)
+
+    assert TD3("Tiny-v0", make_nn=mk3, batch_size=16, seed=1).hidden == 64
+
+    def mks(state_dim, action_dim, **kw):
+        return (MLPActor(state_dim, 2 * action_dim, [48, 48]), MLPCritic(state_dim, action_dim, 48),
+                MLPCritic(state_dim, action_dim, 48))
+
+    assert SAC("Tiny-v0", make_nn=mks, batch_size=16, seed=1).hidden == 48
+
+    def mixed(state_dim, action_dim, **kw):
+        return MLPActor(state_dim, action_dim, 64), MLPCritic(state_dim, action_dim, 32), MLPCritic(state_dim, action_dim, 32)
+
+    with pytest.raises(NotImplementedError):
+        TD3("Tiny-v0", make_nn=mixed, batch_size=16, seed=1)
+
+    def other(state_dim, action_dim, **kw):
+        return torch.nn.Linear(state_dim, action_dim), MLPCritic(state_dim, action_dim), MLPCritic(state_dim, action_dim)
+
+    with pytest.raises(NotImplementedError):
+        TD3("Tiny-v0", make_nn=other, batch_size=16, seed=1)
+
+
+def test_train_ops_on_a_host_batch_dict():
+    """abc.py:23-28: train_ops on a plain BATCH dict (here the oracle replay's gather, as a host
+    replay would hand it over) trains exactly as on the same rows drawn from a device replay, and
+    a LAP host replay receives the step's priorities through its own update_priority."""
+    cap, B, H, steps = 512, 32, 32, 3
+    trans = _transitions(300, 11)
+    for lap in (True, False):
+        dev = TD7("Tiny-v0", use_lap=lap, target_policy_noise=0.0, hidden=H, batch_size=B, seed=21)
+        host = TD7("Tiny-v0", use_lap=lap, target_policy_noise=0.0, hidden=H, batch_size=B, seed=21)
+        rep = (LAPReplayMemory if lap else SimpleReplayMemory)(cap, "Tiny-v0")
+        _fill(rep, trans)
+        orep = _oracle_replay(cap, lap, trans)
+        for t in range(steps):
+            torch.manual_seed(500 + t)
+            batch = rep.sample(B)
+            orep.ind = np.asarray(batch.ind)
+            hb = {k: torch.from_numpy(v) for k, v in orep.gather(batch.ind).items()}
+            i_dev = dev.train_ops(batch, rep)
+            i_host = host.train_ops(hb, orep)
+            for k in i_dev:
+                _close(i_host[k], i_dev[k], 1e-6)
+            if lap:
+                np.testing.assert_allclose(orep.priority[batch.ind], rep.priority.numpy()[batch.ind], rtol=1e-6)
+        for net, d in dev.state_dict().items():
+            for name, v in d.items():
+                np.testing.assert_array_equal(host.state_dict()[net][name], v)

@@ -26,18 +26,57 @@ passes = defaultdict(list)
 for (p, i), d in sorted(disp.items()):
     passes[p].append(d)
 # find the two graphs: the sequence after the first (prime) dispatch repeats with period P
+def find_period(grids, reps=6):
+    """(offset, period) of the first window of `reps` identical grid-size sequences (the multi-step
+    graph replays, after the warm-up's single-step graphs)."""
+    for off in range(0, 400):
+        for P in range(10, 200):
+            w = grids[off:off + P * reps]
+            if len(w) == P * reps and all(w[i] == w[i % P] for i in range(len(w))):
+                return off, P
+    raise SystemExit("no periodic window")
+
+
+merged = {}  # level -> {column: mean}
 for p, seq in sorted(passes.items()):
-    grids = [d["_grid"] for d in seq[1:]]
-    period = next(P for P in range(2, 200) if grids[P:P * 20] == grids[:P * 19][:len(grids[P:P * 20])])
+    grids = [d["_grid"] for d in seq]
+    off, period = find_period(grids)
     agg = defaultdict(lambda: defaultdict(list))
-    for k, d in enumerate(seq[1:]):
-        for c, v in d.items():
-            agg[k % period][c].append(v)
-    names = sorted(c for c in agg[0] if not c.startswith("_"))
-    print(f"== pass {p}: period {period} levels")
-    print("lvl  grid   us   " + "  ".join(f"{n[:14]:>14s}" for n in names))
-    for k in range(period):
-        a = agg[k]
-        mean = lambda c: sum(a[c]) / len(a[c])
-        print(f"{k:3d} {int(mean('_grid')):5d} {mean('_ns') / 1000:5.1f}  " +
-              "  ".join(f"{mean(n):14.1f}" for n in names))
+    k = 0
+    while off + (k + 1) * period <= len(seq) and grids[off + k * period:off + (k + 1) * period] == grids[off:off + period]:
+        for q in range(period):
+            for c, v in seq[off + k * period + q].items():
+                agg[q][c].append(v)
+        k += 1
+    for q in range(period):
+        row = merged.setdefault(q, {})
+        for c, vs in agg[q].items():
+            if c == "_ns":
+                row.setdefault("us", []).append(sum(vs) / len(vs) / 1000)
+            elif c == "_grid":
+                row["grid"] = vs[0]
+            else:
+                row[c] = sum(vs) / len(vs)
+DESC = {}
+if len(sys.argv) > 2:  # level descriptions (engine describe of the multi-step graph, one "L<k> ..." line each)
+    for line in open(sys.argv[2]):
+        if line.startswith("L"):
+            k, _, rest = line.partition(" ")
+            DESC[int(k[1:])] = rest.strip()
+cols = [c for c in ("FETCH_SIZE", "WRITE_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY",
+                    "SQ_WAVE_CYCLES", "TCC_HIT_sum", "TCC_MISS_sum") if any(c in r for r in merged.values())]
+print("per level of the multi-step graph (means over its replays); traffic KB = 2 x FETCH_SIZE + WRITE_SIZE "
+      "(gfx950: FETCH_SIZE counts half of a 16-B/lane streaming read)")
+print(f"{'lvl':>3} {'grid':>5} {'us':>6} {'trafficKB':>9} " + " ".join(f"{c[:12]:>12}" for c in cols) + "  ops")
+tot = defaultdict(float)
+for q in sorted(merged):
+    r = merged[q]
+    us = sum(r.get("us", [0])) / max(1, len(r.get("us", [0])))
+    tr = 2 * r.get("FETCH_SIZE", 0) + r.get("WRITE_SIZE", 0)
+    tot["us"] += us
+    tot["traffic"] += tr
+    for c in cols:
+        tot[c] += r.get(c, 0)
+    print(f"{q:3d} {r.get('grid', 0):5d} {us:6.1f} {tr:9.0f} " + " ".join(f"{r.get(c, 0):12.0f}" for c in cols) +
+          "  " + DESC.get(q, "")[:160])
+print(f"sum     {tot['us']:6.1f} {tot['traffic']:9.0f} " + " ".join(f"{tot[c]:12.0f}" for c in cols))
