@@ -378,7 +378,12 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, chunk=25):
         eng.bind(rep)
         engs.append((eng, rep))
 
+    group = E.EngineGroup([e for e, _ in engs]) if args.packed else None
+
     def run(n):
+        if group is not None:  # one packed level schedule for all K seeds (rle_group_step)
+            group.step(n)
+            return
         done = 0
         while done < n:
             c = min(chunk, n - done)
@@ -392,29 +397,41 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, chunk=25):
     if dist:
         dist.barrier()
     torch.cuda.synchronize(local)
+    st0 = group.stats() if group is not None else None
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize(local)
     wall = max_over_ranks([time.perf_counter() - t0], dist)[0]
+    packed = None
+    if group is not None:
+        st1 = group.stats()
+        packed = {"launches_per_step": round((st1[0] - st0[0]) / args.steps, 3),
+                  "packed_fraction": round((st1[1] - st0[1]) / (K * args.steps), 4),
+                  "levels_per_program": st1[2]}
     if rank == 0:
         gflop, mb = (SURVEY_MACS_PER_SAMPLE * 2.0 * B / 1e9, None) if (args.algo, args.env, args.batch) == (
             "td7", "Humanoid-v4", B) else WORK[(args.algo, args.env, args.batch)]
         value = world * K * args.steps / wall
         out = {
-            "metric": f"gradient-steps/sec, {K} independent seeds per GPU, {args.algo.upper()} {args.env} "
+            "metric": f"gradient-steps/sec, {K} independent seeds per GPU{' (packed)' if group else ''}, "
+                      f"{args.algo.upper()} {args.env} "
                       f"batch={args.batch} (secondary: SURVEY §8(f) rank 4)",
             "value": round(value, 2), "unit": "gradient-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": f"{K} x {args.algo.upper()} {args.env} gradient step per GPU",
                        "seeds_per_gpu": K, "batch": args.batch, "replay": N_REPLAY, "lap": lap,
-                       "parallelism": f"replicas x{world * K} ({K} seeds per GPU, one HIP stream each)"},
+                       "parallelism": f"replicas x{world * K} ({K} seeds per GPU, " + (
+                           "one packed level schedule)" if group is not None else "one HIP stream each)"),
+                       "packed": packed},
             "roofline": {"bound": "mfma", "achieved": round(gflop * 1e9 * value / world / 1e12, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(gflop * 1e9 * value / world / 1e12 / PEAK_FP32_TFLOPS, 5),
                          "traffic": None, "note": "device aggregate over the K seeds (wall clock)"},
         }
         print(json.dumps(out), flush=True)
+    if group is not None:
+        group.close()
     if dist:
         dist.barrier()
 
@@ -496,6 +513,8 @@ def main():
     ap.add_argument("--batch", type=int, default=B)
     ap.add_argument("--seeds-per-gpu", type=int, default=1,
                     help="independent seeds (engines, one stream each) sharing each GPU (SURVEY §8(f) rank 4)")
+    ap.add_argument("--packed", action="store_true",
+                    help="with --seeds-per-gpu K: step the K seeds as one packed level schedule (rle_group)")
     args = ap.parse_args()
     if (args.algo, args.env, args.batch) not in WORK:
         ap.error(f"no SURVEY §8(d) work figures for {args.algo} {args.env} B={args.batch}")

@@ -855,6 +855,79 @@ static void level_hazards(const std::vector<Op>& ops, const std::vector<int>& it
   }
 }
 
+// ---- RLE_TRAFFIC=1: the bytes each level must move (the union of its ops' byte ranges, so a range
+// several tiles read counts once), by kind: activations read / written, weights read, Adam state
+// (p, m, v read and written, N image written).  Graph descriptions carry it (tools/pmc_levels.py
+// sets it against the PMC counters: traffic above these bytes is re-reads, e.g. one copy per XCD).
+struct LevelTraffic {
+  double act_r = 0, act_w = 0, w_r = 0, adam = 0, other = 0;
+};
+static double union_bytes(std::vector<std::pair<uintptr_t, uintptr_t>>& v) {
+  std::sort(v.begin(), v.end());
+  double tot = 0;
+  uintptr_t lo = 0, hi = 0;
+  bool open = false;
+  for (auto& r : v) {
+    if (!open || r.first > hi) {
+      if (open) tot += (double)(hi - lo);
+      lo = r.first;
+      hi = r.second;
+      open = true;
+    } else {
+      hi = std::max(hi, r.second);
+    }
+  }
+  if (open) tot += (double)(hi - lo);
+  return tot;
+}
+static LevelTraffic level_traffic(const std::vector<Op>& ops, const float* P, size_t nP) {
+  LevelTraffic t;
+  std::vector<std::pair<uintptr_t, uintptr_t>> ar, aw, wr, ad;
+  const uintptr_t p0 = (uintptr_t)P, p1 = p0 + 3 * nP * 4;
+  std::vector<Access> v;
+  for (const Op& op : ops) {
+    v.clear();
+    if (op.kind == OP_SAMPLE_GATHER) {  // rows of the batch + one path down the LAP sum tree per query
+      const SampleArgs& s = op.sample;
+      t.other += (double)s.B * (2.0 * s.Sp + s.Ap + 2) * 4 + (s.lap ? s.B * (64.0 * 8 + 64 * 4) + s.nblk * 8.0 : 0);
+      t.act_w += (double)s.B * ((s.ss.n != nullptr) + (s.ss.t != nullptr)) * 2 * s.Sp * 4 +
+                 (double)s.B * ((s.a.n != nullptr) + (s.a.t != nullptr)) * s.Ap * 4 + s.B * 20.0;
+      continue;
+    }
+    if (op.kind == OP_PRIORITY) {  // the scattered rows (a 64-B line each) and their two sums
+      t.other += (double)op.prio.B * (8 + 4) + op.prio.B * 64.0 * 3;
+      continue;
+    }
+    if (op.kind == OP_MAXRED && op.flat.stage == 0) {
+      t.other += 4.0 * 1e6;  // (the replay size is a device value: the 1M benchmark ring)
+      continue;
+    }
+    op_accesses(op, v);
+    for (const Access& a : v) {
+      const std::string what = a.what ? a.what : "";
+      const bool in_p = a.lo >= p0 && a.hi <= p1;
+      if (what.rfind("adam", 0) == 0) {
+        ad.push_back({a.lo, a.hi});
+        if (what == "adam w.t" || what == "adam bias") ad.push_back({a.lo, a.hi});  // (read and written)
+      } else if (a.w) {
+        aw.push_back({a.lo, a.hi});
+      } else if (in_p) {
+        wr.push_back({a.lo, a.hi});
+      } else {
+        ar.push_back({a.lo, a.hi});
+      }
+    }
+  }
+  t.act_r += union_bytes(ar);
+  t.act_w += union_bytes(aw);
+  t.w_r += union_bytes(wr);
+  // Adam ranges: each listed range once per direction (reads p, m, v; writes p T, m, v, p N)
+  double adam = 0;
+  for (auto& r : ad) adam += (double)(r.second - r.first);
+  t.adam = adam;
+  return t;
+}
+
 struct Prog {
   struct Item {
     std::vector<Op> ops;  // one op, or a group writing disjoint parts of the same buffers
@@ -862,8 +935,16 @@ struct Prog {
     int level = 0;
   };
   std::vector<Item> items;
+  // ops per level: one launch each (kLevelOps preloaded entries, kWideOps in a wide launch)
+  int max_ops = kLevelOps;
+  // added to every resource id (packed programs of several engines: disjoint id spaces)
+  int id_off = 0;
   void add(const Op& op, std::vector<int> rd, std::vector<int> wr) { add_group({op}, std::move(rd), std::move(wr)); }
   void add_group(std::vector<Op> ops, std::vector<int> rd, std::vector<int> wr) {
+    if (id_off) {
+      for (int& r : rd) r = r >= 0 ? r + id_off : r;
+      for (int& w : wr) w = w >= 0 ? w + id_off : w;
+    }
     for (Op& op : ops)
       if (op.kind == OP_GEMM) {
         gemm_finalize(op.gemm);
@@ -941,7 +1022,7 @@ struct Prog {
       const int wfac = balance >= 3 ? 2 : 1;
       int best = -1;
       for (int l = cur + 1; l <= hi; ++l) {
-        if (nops[l] + (int)it.ops.size() > kLevelOps || wt * wfac > wmax[l] || nwg[l] + wg > cap) continue;
+        if (nops[l] + (int)it.ops.size() > max_ops || wt * wfac > wmax[l] || nwg[l] + wg > cap) continue;
         if (nwg[l] + wg >= nwg[cur]) continue;
         if (best < 0 || nwg[l] < nwg[best]) best = l;
       }
@@ -966,12 +1047,12 @@ struct Prog {
         if (lw.count(w)) l = std::max(l, lw[w] + 1);
         if (lr.count(w)) l = std::max(l, lr[w] + 1);
       }
-      // a level of more than kLevelOps ops would take two launches: defer to the next level
+      // a level of more than max_ops ops would take two launches: defer to the next level
       // with room (every dependence is still met at a later level)
       int wg = 0;
       for (auto& op : it.ops) wg += op.wg_count;
       while (l < (int)nops.size() &&
-             (nops[l] + (int)it.ops.size() > kLevelOps || (nwg[l] > 0 && nwg[l] + wg > wg_cap)))
+             (nops[l] + (int)it.ops.size() > max_ops || (nwg[l] > 0 && nwg[l] + wg > wg_cap)))
         ++l;
       if (l >= (int)nops.size()) {
         nops.resize(l + 1, 0);
@@ -1915,10 +1996,12 @@ struct Engine {
   // workgroups), else the per-op default.  Returns the op's creation index too.
   std::vector<int> tn_plan;
   int tn_seq = 0;
+  int seq_base = 0;  // (packed programs of several engines: engine k's GEMMs are k << kSeqShift on)
+  static constexpr int kSeqShift = 20;
   std::pair<int, int> choose_tn(int M, int N) {
     const int seq = tn_seq++;
     const int t = seq < (int)tn_plan.size() ? tn_plan[seq] : pick_tn(M, N);
-    return {t, seq};
+    return {t, seq_base + seq};
   }
   // per-tile grad-square partial slots of a dW op (weights at the narrowest tile width,
   // so any plan fits; unused slots stay zero; bias)
@@ -3044,8 +3127,19 @@ struct Engine {
     static const char* kname[] = {"?", "gemm", "normbwd", "sreduce", "sgather", "head", "prio",
                                   "sacfwd", "sacbwd", "end", "polyak", "copy", "maxred", "ctrl", "noise",
                                   "foldbias"};
+    static const bool traffic = [] {
+      const char* e = std::getenv("RLE_TRAFFIC");
+      return e && e[0] == '1';
+    }();
     for (size_t l = 0; l < levels.size(); ++l) {
       G.desc += "L" + std::to_string(l) + " wg=" + std::to_string(G.nwg[l]) + ":";
+      if (traffic) {
+        const LevelTraffic t = level_traffic(levels[l], P, nP);
+        char buf[160];
+        snprintf(buf, sizeof buf, " [KB act_r %.0f act_w %.0f w_r %.0f adam %.0f other %.0f]", t.act_r / 1024,
+                 t.act_w / 1024, t.w_r / 1024, t.adam / 1024, t.other / 1024);
+        G.desc += buf;
+      }
       for (auto& op : levels[l]) {
         G.desc += std::string(" ") + kname[op.kind];
         if (op.kind == OP_GEMM) {
@@ -3065,7 +3159,7 @@ struct Engine {
     flat_ops.reserve(total);
     for (auto& lv : levels)
       for (auto& op : lv) flat_ops.push_back(op);
-    G.d_ops = mem.make<Op>(total);
+    G.d_ops = mem.make<Op>(total + kWideOps);  // (+ padding: wide launches read kWideOps headers)
     HIPCHK(hipMemcpy(G.d_ops, flat_ops.data(), total * sizeof(Op), hipMemcpyHostToDevice));
     const char* tr_env = std::getenv("RLE_TRACE");
     if (tr_env && tr_env[0] == '1') {
@@ -3137,25 +3231,33 @@ struct Engine {
   // Builds a step program twice: the first pass fixes the level schedule, then
   // GEMM tiles of any level with more workgroups than fit on the device at once
   // are widened (16 -> 32 -> 64 columns, fewer workgroups, longer reductions per
-  // wave) and the program is rebuilt with that tile plan.
+  // wave) and the program is rebuilt with that tile plan.  `es`: the engines whose ops
+  // f adds (one, or the seeds of a packed program: a tile plan per engine, indexed by the
+  // GEMM sequence numbers choose_tn hands out from each engine's seq_base).
   template <class F>
-  Prog plan_build(F&& f) {
-    tn_plan.clear();
-    tn_seq = 0;
+  static Prog plan_build_for(const std::vector<Engine*>& es, int max_ops, F&& f) {
+    for (size_t k = 0; k < es.size(); ++k) {
+      es[k]->tn_plan.clear();
+      es[k]->tn_seq = 0;
+      es[k]->seq_base = (int)k << kSeqShift;
+    }
     Prog p0;
+    p0.max_ops = max_ops;
     f(p0);
-    std::vector<int> plan(tn_seq, 16);
+    std::vector<std::vector<int>> plan(es.size());
+    for (size_t k = 0; k < es.size(); ++k) plan[k].assign(es[k]->tn_seq, 16);
+    auto at = [&](int seq) -> int& { return plan[seq >> kSeqShift][seq & ((1 << kSeqShift) - 1)]; };
     const char* tmin = std::getenv("RLE_TN_MIN");  // tuning experiments
     auto levels = p0.schedule();
     for (auto& lv : levels)
       for (auto& op : lv)
-        if (op.kind == OP_GEMM) plan[op.seq] = std::max(op.gemm.tn, tmin ? std::atoi(tmin) : 16);
+        if (op.kind == OP_GEMM) at(op.seq) = std::max(op.gemm.tn, tmin ? std::atoi(tmin) : 16);
     int cap = std::max(256, level_capacity());
     if (const char* e = std::getenv("RLE_LEVEL_CAP")) cap = std::max(1, std::atoi(e));  // tuning experiments
     auto wg_of = [&](const Op& op) {
       if (op.kind != OP_GEMM) return op.wg_count;
       const GemmArgs& g = op.gemm;
-      return g.tiles_m * (cdiv(g.N, plan[op.seq]) + (g.epi == EPI_ADAM ? 1 : 0));
+      return g.tiles_m * (cdiv(g.N, at(op.seq)) + (g.epi == EPI_ADAM ? 1 : 0));
     };
     for (auto& lv : levels) {
       while (true) {
@@ -3164,20 +3266,30 @@ struct Engine {
         if (total <= cap) break;
         int best = -1, best_wg = 0;
         for (auto& op : lv)
-          if (op.kind == OP_GEMM && plan[op.seq] < 64 && wg_of(op) > best_wg) {
+          if (op.kind == OP_GEMM && at(op.seq) < 64 && wg_of(op) > best_wg) {
             best = op.seq;
             best_wg = wg_of(op);
           }
         if (best < 0) break;
-        plan[best] *= 2;
+        at(best) *= 2;
       }
     }
-    tn_plan = plan;
-    tn_seq = 0;
+    for (size_t k = 0; k < es.size(); ++k) {
+      es[k]->tn_plan = plan[k];
+      es[k]->tn_seq = 0;
+    }
     Prog p;
+    p.max_ops = max_ops;
     f(p);
-    tn_plan.clear();
+    for (Engine* e : es) {
+      e->tn_plan.clear();
+      e->seq_base = 0;
+    }
     return p;
+  }
+  template <class F>
+  Prog plan_build(F&& f) {
+    return plan_build_for({this}, kLevelOps, std::forward<F>(f));
   }
 
   // steps per multi-step graph: RLE_PAIR=K (even; 0 = single-step graphs only)
@@ -3301,6 +3413,35 @@ struct Engine {
     }
     launches += G.nlaunch;
   }
+  // The next multi_k steps may run as one multi-step program: TD7 (counter bumped first,
+  // td7.py:295) / TD3 (td3.py:231) when its first step is a policy step (and, TD7, no step
+  // of it needs a hard update); SAC any multi_k steps.
+  bool pair_window_ok() const {
+    const int K = multi_k;
+    if (!K) return false;
+    const long long k1 = algo == RLE_TD7 ? n_runs + 1 : n_runs;
+    if (algo != RLE_SAC && k1 % 2) return false;
+    if (algo == RLE_TD7) {
+      const int tur = std::max(1, cfg.target_update_rate);
+      for (long long k = k1; k < k1 + K; ++k)
+        if (k % tur == 0) return false;
+    }
+    return true;
+  }
+  // host state after a multi-step program starting on batch set cur_set was enqueued
+  void pair_commit() {
+    const int p = cur_set;
+    n_runs += multi_k;
+    pol_set = p;
+    if (algo != RLE_SAC) pln_set = 1 - p;
+    last_set = 1 - p;
+    cur_set = p;
+    if (cfg.use_lap && algo != RLE_SAC) replay->version += multi_k;
+    primed = true;
+    primed_ver = replay->version;
+  }
+  int groups = 0;  // packed groups (rle_group) holding this engine
+
   void step(int n, float* info_out, float* gpu_ms = nullptr, bool async = false) {
     REQUIRE(replay, "no replay bound");
     REQUIRE(replay->size > 0, "replay is empty");
@@ -3337,28 +3478,15 @@ struct Engine {
         // drawn from has changed since (appends, other writers of the priorities, tapes)
         if (!primed || primed_ver != replay->version) launch_graph(g_prime[cur_set]);
         const int p = cur_set;
-        const int tur = std::max(1, cfg.target_update_rate);
-        // multi-step graph: TD7 (counter bumped first, td7.py:295) / TD3 (td3.py:231) when
-        // its first step is a policy step (and, TD7, no step of it needs a hard update);
-        // SAC any multi_k steps
+        // multi-step graph (pair_window_ok)
         const int K = multi_k;
-        const long long k1 = algo == RLE_TD7 ? n_runs + 1 : n_runs;
-        bool pair_ok = K && i + K - 1 < chunk && (!ctrl_tape_mode_host || tape_left >= K - 1);
-        if (pair_ok && algo != RLE_SAC) pair_ok = k1 % 2 == 0;
-        if (pair_ok && algo == RLE_TD7)
-          for (long long k = k1; k < k1 + K; ++k) pair_ok = pair_ok && k % tur != 0;
+        const bool pair_ok = K && i + K - 1 < chunk && (!ctrl_tape_mode_host || tape_left >= K - 1) &&
+                             pair_window_ok();
         if (pair_ok && g_pair[p].x) {
           if (ctrl_tape_mode_host) tape_left -= K - 1;
-          n_runs += K;
           launch_graph(g_pair[p]);
-          pol_set = p;
-          if (algo != RLE_SAC) pln_set = 1 - p;
-          last_set = 1 - p;
-          cur_set = p;
+          pair_commit();
           i += K - 1;
-          if (cfg.use_lap && algo != RLE_SAC) replay->version += K;
-          primed = true;
-          primed_ver = replay->version;
           continue;
         }
         if (algo == RLE_TD7) {
@@ -3405,6 +3533,113 @@ struct Engine {
   int ctrl_tape_mode_host = 0;
 };
 
+// Packed multi-seed stepping (rle_group): several engines -- independent seeds, each with
+// its own weights, optimiser state, replay and RNG stream -- whose multi-step programs are
+// merged into ONE level schedule (each engine's resource ids in a disjoint range, so only
+// its own dependencies order its ops).  A level then carries every seed's ops of that depth
+// in one (wide) launch: the per-launch cost is paid once for all seeds, and the device is
+// filled by several seeds' small GEMMs instead of one's.  Each engine's results are those
+// of stepping it alone (its ops and their order are unchanged; the tile plan may differ).
+// Steps that the packed program cannot run (a TD7 hard update, engines out of lockstep)
+// fall back to each engine's own graphs, all on the first engine's stream.
+struct Group {
+  std::vector<Engine*> es;
+  Graph g[2];
+  bool built = false;
+  int K = 0;
+  long long launches = 0, packed_steps = 0;  // rle_level dispatches / engine-steps of packed replays
+  std::vector<hipEvent_t> ev;                // per engine: the position of its own stream
+  static constexpr int kIdSpan = 1 << 24;    // resource ids per engine in the packed program
+
+  void build() {
+    for (Engine* e : es)
+      if (!e->built) e->build();
+    Engine& e0 = *es[0];
+    K = e0.multi_k;
+    for (int set = 0; K && set < 2; ++set) {
+      Prog p = Engine::plan_build_for(es, kWideOps, [&](Prog& pg) {
+        for (int j = 0; j < K; ++j)
+          for (size_t k = 0; k < es.size(); ++k) {
+            pg.id_off = (int)k * kIdSpan;
+            Engine& e = *es[k];
+            if (e.algo == RLE_TD7) e.build_td7(pg, j % 2 == 0, (set + j) % 2);
+            else e.build_mlp(pg, e.algo == RLE_SAC || j % 2 == 0, (set + j) % 2);
+          }
+        pg.id_off = 0;
+      });
+      g[set] = e0.capture(p);
+    }
+    for (Engine* e : es) e->use_set(0);
+    built = true;
+  }
+  // every engine at the same step, with its next batch prefetched on the same set, and the
+  // next K steps a multi-step window
+  bool lockstep() const {
+    const Engine& a = *es[0];
+    if (!K || !g[a.cur_set].x) return false;
+    for (const Engine* e : es)
+      if (e->ctrl_tape_mode_host || e->n_runs != a.n_runs || e->cur_set != a.cur_set || !e->pair_window_ok())
+        return false;
+    return true;
+  }
+  void step(int n, bool async) {
+    for (Engine* e : es) {
+      REQUIRE(e->replay && e->replay->size > 0, "group step: an engine has no (filled) replay");
+      HIPCHK(hipStreamSynchronize(e->replay->stream));
+    }
+    if (!built) build();
+    // everything of this call goes to the first engine's stream, after each engine's own work
+    hipStream_t s0 = es[0]->stream;
+    std::vector<hipStream_t> own(es.size());
+    for (size_t k = 0; k < es.size(); ++k) {
+      own[k] = es[k]->stream;
+      if (k) {
+        HIPCHK(hipEventRecord(ev[k], own[k]));
+        HIPCHK(hipStreamWaitEvent(s0, ev[k], 0));
+      }
+      es[k]->stream = s0;
+    }
+    auto restore = [&] {
+      for (size_t k = 0; k < es.size(); ++k) es[k]->stream = own[k];
+    };
+    try {
+      for (Engine* e : es) {
+        if (e->fold_dirty && e->g_fold.x) e->launch_graph(e->g_fold);
+        e->fold_dirty = false;
+      }
+      int done = 0;
+      while (done < n) {
+        if (n - done >= K && lockstep()) {
+          for (Engine* e : es) {
+            int zero = 0;
+            HIPCHK(hipMemcpyAsync(&e->ctrl->info_slot, &zero, sizeof(int), hipMemcpyHostToDevice, s0));
+            if (!e->primed || e->primed_ver != e->replay->version) e->launch_graph(e->g_prime[e->cur_set]);
+          }
+          const Graph& G = g[es[0]->cur_set];
+          HIPCHK(hipGraphLaunch(G.x, s0));
+          launches += G.nlaunch;
+          packed_steps += (long long)K * (long long)es.size();
+          for (Engine* e : es) {
+            e->pair_commit();
+            HIPCHK(hipEventRecord(e->done_ev, s0));
+          }
+          done += K;
+        } else {
+          for (Engine* e : es) e->step(1, nullptr, nullptr, true);  // (its own graphs, on s0)
+          done += 1;
+        }
+      }
+    } catch (...) {
+      restore();
+      throw;
+    }
+    restore();
+    HIPCHK(hipEventRecord(ev[0], s0));
+    for (size_t k = 1; k < es.size(); ++k) HIPCHK(hipStreamWaitEvent(own[k], ev[0], 0));
+    if (!async) HIPCHK(hipStreamSynchronize(s0));
+  }
+};
+
 }  // namespace rle
 
 // ====================================================================== C ABI
@@ -3418,6 +3653,9 @@ struct rle_replay {
 };
 struct rle_engine {
   std::unique_ptr<Engine> e;
+};
+struct rle_group {
+  rle::Group g;
 };
 
 template <class F>
@@ -3815,6 +4053,7 @@ int rle_destroy(rle_engine* h) {
   return guard([&] {
     if (!h) return;
     Engine& e = *h->e;
+    REQUIRE(e.groups == 0, "destroy: the engine is in a group (rle_group_destroy it first)");
     (void)hipStreamSynchronize(e.stream);
     if (e.replay) {
       auto& us = e.replay->users;
@@ -4465,6 +4704,73 @@ int rle_get_info(rle_engine* h, int n, float* out) {
 
 int rle_synchronize(rle_engine* h) {
   return guard([&] { HIPCHK(hipStreamSynchronize(h->e->stream)); });
+}
+
+int rle_group_create(rle_engine** engines, int n, rle_group** out) {
+  return guard([&] {
+    REQUIRE(engines && out && n >= 1 && n <= 16, "group_create: 1 to 16 engines");
+    auto h = std::make_unique<rle_group>();
+    rle::Group& G = h->g;
+    for (int i = 0; i < n; ++i) {
+      REQUIRE(engines[i], "group_create: null engine");
+      Engine* e = engines[i]->e.get();
+      REQUIRE(e->replay, "group_create: bind each engine's replay first");
+      for (Engine* o : G.es) {
+        REQUIRE(o != e, "group_create: an engine is listed twice");
+        REQUIRE(o->replay != e->replay, "group_create: each engine needs its own replay");
+        REQUIRE(o->cfg.device == e->cfg.device && o->algo == e->algo && o->cfg.policy_freq == e->cfg.policy_freq &&
+                    o->cfg.target_update_rate == e->cfg.target_update_rate && o->pair_k() == e->pair_k(),
+                "group_create: engines differ in device / algorithm / policy_freq / target_update_rate");
+      }
+      G.es.push_back(e);
+    }
+    HIPCHK(hipSetDevice(G.es[0]->cfg.device));
+    G.ev.assign(n, nullptr);
+    for (auto& ev : G.ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (Engine* e : G.es) ++e->groups;
+    *out = h.release();
+  });
+}
+
+int rle_group_step(rle_group* h, int n_steps, int async) {
+  return guard([&] {
+    REQUIRE(h && n_steps >= 0, "group_step: bad args");
+    HIPCHK(hipSetDevice(h->g.es[0]->cfg.device));
+    h->g.step(n_steps, async != 0);
+  });
+}
+
+int rle_group_stats(rle_group* h, long long* launches, long long* packed_steps, int* levels) {
+  return guard([&] {
+    REQUIRE(h, "group_stats: null group");
+    if (launches) *launches = h->g.launches;
+    if (packed_steps) *packed_steps = h->g.packed_steps;
+    if (levels) *levels = h->g.g[0].levels();
+  });
+}
+
+int rle_group_describe(rle_group* h, char* buf, int cap) {
+  return guard([&] {
+    REQUIRE(h && buf && cap > 0, "group_describe: bad args");
+    std::string d = h->g.built ? h->g.g[0].desc : std::string("(not built: step the group first)\n");
+    std::snprintf(buf, (size_t)cap, "%s", d.c_str());
+  });
+}
+
+int rle_group_destroy(rle_group* h) {
+  return guard([&] {
+    if (!h) return;
+    rle::Group& G = h->g;
+    (void)hipStreamSynchronize(G.es[0]->stream);
+    for (rle::Graph& g : G.g) {
+      if (g.x) (void)hipGraphExecDestroy(g.x);
+      if (g.g) (void)hipGraphDestroy(g.g);
+    }
+    for (auto& ev : G.ev)
+      if (ev) (void)hipEventDestroy(ev);
+    for (Engine* e : G.es) --e->groups;
+    delete h;
+  });
 }
 
 }  // extern "C"

@@ -328,6 +328,10 @@ __device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int off) {
   return as_f4(__builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 __device__ __forceinline__ f32x4 mfma4(const float4& a, const float4& b, f32x4 acc) {
+#ifdef RLE_EXP_NOMFMA  // timing experiment only: operands consumed by one VALU op instead of 4 MFMAs
+  acc.x += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+  return acc;
+#endif
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
@@ -853,7 +857,9 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   // instruction arbitration over the shorter ops sharing a CU (A/B: +0.2-0.3%; also raising the
   // pre-GEMM and fused-head consumers: no further gain)
   if constexpr (MODE == GEMM_DW) {
+#ifndef RLE_EXP_NO_SETPRIO
     if (tn == 64) __builtin_amdgcn_s_setprio(3);
+#endif
   }
   const bool bias_tile = EPI == EPI_ADAM && jt * tn >= bias_col;
   const bool lead = kp == 0;
@@ -2056,10 +2062,26 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     e = in ? x : e;
     k = in ? q : k;
   }
-  const int kind = (e >> 16) & 0xf, vid = e >> 20;
+  int kind = (e >> 16) & 0xf, vid = e >> 20;
   const CAS Op* ops = (const CAS Op*)ops_arg;
+  int wb = (int)(e & 0xffffu);
+  // Wide launch (a level of more than kLevelOps ops, packed multi-seed programs): entry 11 is
+  // kind 0 with the count of ops from 11 on.  Lane j reads op 11 + j's first workgroup from
+  // its descriptor header (one vector load); the op is the last one starting at or before
+  // this workgroup (ops are in workgroup order), its kind and variant come from its header.
+  if (kind == 0 && vid != 0) {
+    const int cnt = vid, lane = (int)(threadIdx.x & 63);
+    int wbl = 0x7fffffff;
+    if (lane < cnt) wbl = ((const Op*)ops_arg)[kLevelOps - 1 + lane].wg_begin;
+    const unsigned long long m = __ballot(wbl <= wg);
+    const int j = 63 - __clzll((long long)m);
+    k = kLevelOps - 1 + j;
+    wb = __builtin_amdgcn_readlane(wbl, j);
+    kind = ops[k].kind;
+    vid = kind == OP_GEMM ? ops[k].gemm.vid : 0;
+  }
   const CAS Op& op = ops[k];
-  const int t = wg - (int)(e & 0xffffu);
+  const int t = wg - wb;
   // (stamp 0 is taken on entry, before the kernel-argument loads)
   unsigned long long* tr = TRACE ? trace_arg + (size_t)wg * kTraceStride : nullptr;
   if (TRACE && threadIdx.x == 0) tr[0] = t_in;
@@ -2407,10 +2429,12 @@ const char* level_kernel_symbol() { return "_ZN3rle9rle_levelILb0EEEvjjjjjjjjjjj
 
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
                         unsigned long long* trace, const Op* next_ops, int next_nops) {
-  // a level of more than kLevelOps ops runs as consecutive launches of kLevelOps (its
-  // ops are independent, so any split is correct)
+  // a level of more than kLevelOps ops: one wide launch up to kWideOps (entry 11 refers the
+  // workgroups of ops 11.. to their descriptors), beyond that consecutive launches of
+  // kLevelOps (its ops are independent, so any split is correct)
+  const bool wide = nops > kLevelOps && nops <= kWideOps;
   for (int q0 = 0; q0 < nops; q0 += kLevelOps) {
-    const int n = nops - q0 < kLevelOps ? nops - q0 : kLevelOps;
+    const int n = wide ? nops : nops - q0 < kLevelOps ? nops - q0 : kLevelOps;
     const int w0 = h_ops[q0].wg_begin;
     const int w1 = q0 + n < nops ? h_ops[q0 + n].wg_begin : nwg;
     if (w1 - w0 + 8 > kMaxLevelWG) return hipErrorInvalidValue;
@@ -2420,12 +2444,15 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
     // the following launch's ops: the rest of this level, then the next level's
     const bool last = q0 + n >= nops;
     const int nn = !last ? (nops - q0 - n < kLevelOps ? nops - q0 - n : kLevelOps)
-                         : (next_nops < kLevelOps ? next_nops : kLevelOps);
+                         : (next_nops <= kWideOps ? next_nops : kLevelOps);
     const Op* next = !last ? d_ops + q0 + n : next_ops;
-    const unsigned next_lines = (unsigned)(nn * (int)(sizeof(Op) / 64));
+    // (the prefetch workgroups cover 2 x kThreads lines: the first ops of a wide launch)
+    const unsigned next_lines = (unsigned)(nn * (int)(sizeof(Op) / 64) < 2 * kThreads ? nn * (int)(sizeof(Op) / 64) : 2 * kThreads);
     const int npf = next_lines ? 8 : 0;  // leading prefetch workgroups (entry 0 bit 31)
     for (int q = 0; q < kLevelOps; ++q) {
-      if (q < n) {
+      if (wide && q == kLevelOps - 1) {
+        la.entry[q] = (unsigned)(h_ops[q0 + q].wg_begin - w0) | ((unsigned)(n - q) << 20);  // kind 0: wide
+      } else if (q < n) {
         const Op& o = h_ops[q0 + q];
         const unsigned vid = o.kind == OP_GEMM ? (unsigned)o.gemm.vid : 0u;
         la.entry[q] = (unsigned)(o.wg_begin - w0) | ((unsigned)o.kind << 16) | (vid << 20);
@@ -2452,6 +2479,7 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
 #undef RLE_LEVEL_ARGS
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (wide) break;
   }
   return hipSuccess;
 }

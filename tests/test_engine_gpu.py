@@ -9,6 +9,8 @@ parameter 2*lr away, so the bulk criterion is what catches a wrong gradient).  G
 themselves are pinned through the Adam moments in test_parity_gpu.py.
 """
 
+import re
+
 import numpy as np
 import pytest
 
@@ -297,6 +299,84 @@ def test_step_async_equals_step_and_seeds_overlap():
         for net, params in spec.agent_params(alg, *spec.TASKS[parse(g)[1]][:2], parse(g)[2], 0).items():
             for pname in params:
                 np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
+
+
+_OPS = re.compile(r"\b(gemm|normbwd|sreduce|sgather|head|prio|sacfwd|sacbwd|end|polyak|copy|maxred|ctrl|noise|"
+                  r"foldbias)\b")
+
+
+def _scaled(eng, alg, env, H, f):
+    for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
+        for pname in params:
+            eng.set_param(net, pname, eng.get_param(net, pname) * np.float32(f))
+
+
+# td7_tiny hard-updates every 4 steps: no 6-step window ever fits, so the group runs every step
+# through the engines' own graphs (the fallback path); the others replay the packed program
+@pytest.mark.parametrize("name", ["td7_tiny", "td7_tiny@tur250", "td3_tiny", "sac_tiny", "td7_humanoid"])
+def test_packed_group_equals_engines_alone(name):
+    """rle_group_step (packed): three seeds (different weights) merged into
+    one level schedule end bit-identical to each engine stepped alone -- parameters, counters,
+    priorities and last batch -- and, full size, the packed program's levels exceed the 12-op
+    launch table (wide launches)."""
+    g = dict(load_golden(name.split("@")[0]))
+    if name.endswith("@tur250"):
+        g["meta_extra_vals"] = np.array([250.0])
+    alg, env, H = parse(g)[:3]
+    n = 20
+
+    def make():
+        out = []
+        for k in range(3):
+            e, r, _ = engine_from_golden(g)
+            _scaled(e, alg, env, H, 1.0 - 0.05 * k)
+            out.append((e, r))
+        return out
+
+    alone = make()
+    for e, _ in alone:
+        e.step(n)
+    packed = make()
+    grp = E.EngineGroup([e for e, _ in packed])
+    grp.step(n)
+    launches, psteps, levels = grp.stats()
+    desc = grp.describe()
+    grp.close()
+    if name == "td7_tiny":
+        assert psteps == 0
+    else:
+        assert psteps >= 3 * (n // 2) and launches > 0 and levels > 0
+    if name == "td7_humanoid":
+        assert max(len(_OPS.findall(ln)) for ln in desc.splitlines() if ln.startswith("L")) > 12
+    for (e1, r1), (e2, r2) in zip(alone, packed):
+        np.testing.assert_array_equal(e1.counters(), e2.counters())
+        np.testing.assert_array_equal(e1.last_indices(), e2.last_indices())
+        np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
+        for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
+            for pname in params:
+                np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname), f"{net}.{pname}")
+
+
+@pytest.mark.parametrize("name", ["td7_tiny"])
+def test_group_rejects_shared_replay_and_grouped_destroy(name):
+    g = load_golden(name)
+    (e1, r1, _), (e2, r2, _) = engine_from_golden(g), engine_from_golden(g)
+    e3 = E.Engine(E.make_config(E.RLE_TD3, 17, 6, 32, 16))
+    r3 = E.Replay(64, 17, 6, False)
+    e3.bind(r3)
+    with pytest.raises(RuntimeError, match="twice"):
+        E.EngineGroup([e1, e1])
+    e2.bind(r1)  # (not built yet: rebinding moves it)
+    with pytest.raises(RuntimeError, match="own replay"):
+        E.EngineGroup([e1, e2])
+    e2.bind(r2)
+    with pytest.raises(RuntimeError, match="differ"):
+        E.EngineGroup([e1, e3])
+    grp = E.EngineGroup([e1, e2])
+    with pytest.raises(RuntimeError, match="group"):
+        e1.close()
+    grp.close()
+    e1.close()
 
 
 # (td7_tiny hard-updates every 4 steps, so its bursts run single-step graphs around the hard

@@ -45,11 +45,35 @@ def main():
         return child(a.child, a.threads, a.seconds, {int(c) for c in a.cpus.split(",")})
     allowed = sorted(os.sched_getaffinity(0))
     need = a.procs * a.threads
-    if need > len(allowed):
-        raise SystemExit(f"need {need} CPUs, {len(allowed)} allowed")
+    # one logical CPU per physical core (SMT siblings left idle), socket by socket, so each
+    # process owns whole cores of one socket (/proc/cpuinfo physical id / core id)
+    phys, seen = [], set()
+    try:
+        ent, cur = [], {}
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if not k:
+                if cur:
+                    ent.append(cur)
+                cur = {}
+            elif k in ("processor", "physical id", "core id"):
+                cur[k] = int(v)
+        if cur:
+            ent.append(cur)
+        for e in sorted(ent, key=lambda e: (e.get("physical id", 0), e.get("core id", 0), e["processor"])):
+            key = (e.get("physical id", 0), e.get("core id", e["processor"]))
+            if e["processor"] in allowed and key not in seen:
+                seen.add(key)
+                phys.append(e["processor"])
+    except OSError:
+        phys = []
+    pool = phys if len(phys) >= need else allowed
+    if need > len(pool):
+        raise SystemExit(f"need {need} CPUs, {len(pool)} allowed")
     procs = []
     for i in range(a.procs):
-        cpus = allowed[i * a.threads:(i + 1) * a.threads]
+        cpus = pool[i * a.threads:(i + 1) * a.threads]
         env = dict(os.environ, OMP_NUM_THREADS=str(a.threads))
         procs.append(subprocess.Popen([sys.executable, __file__, "--child", str(i), "--threads", str(a.threads),
                                        "--seconds", str(a.seconds), "--cpus", ",".join(map(str, cpus))],
@@ -66,7 +90,8 @@ def main():
     print(json.dumps({"metric": "gradient-steps/sec, TD7 Humanoid-v4 B=256, torch-CPU oracle, independent seeds",
                       "value": round(agg, 3), "unit": "gradient-steps/s", "procs": a.procs,
                       "threads_per_proc": a.threads, "cores": need, "kind": "port", "host": bench.host_cpu(),
-                      "per_proc": [r["value"] for r in rows]}), flush=True)
+                      "one_cpu_per_physical_core": pool is phys,
+                      "per_proc": [r["value"] for r in rows], "cpus": [r["cpus"] for r in rows]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -63,6 +63,13 @@ if len(sys.argv) > 2:  # level descriptions (engine describe of the multi-step g
         if line.startswith("L"):
             k, _, rest = line.partition(" ")
             DESC[int(k[1:])] = rest.strip()
+import re
+
+MODEL = {}  # level -> {kind: KB} from RLE_TRAFFIC=1 descriptions
+for k, d in DESC.items():
+    m = re.search(r"\[KB act_r (\d+) act_w (\d+) w_r (\d+) adam (\d+) other (\d+)\]", d)
+    if m:
+        MODEL[k] = dict(zip(("act_r", "act_w", "w_r", "adam", "other"), map(float, m.groups())))
 cols = [c for c in ("FETCH_SIZE", "WRITE_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY",
                     "SQ_WAVE_CYCLES", "TCC_HIT_sum", "TCC_MISS_sum") if any(c in r for r in merged.values())]
 print("per level of the multi-step graph (means over its replays); traffic KB = 2 x FETCH_SIZE + WRITE_SIZE "
@@ -80,3 +87,22 @@ for q in sorted(merged):
     print(f"{q:3d} {r.get('grid', 0):5d} {us:6.1f} {tr:9.0f} " + " ".join(f"{r.get(c, 0):12.0f}" for c in cols) +
           "  " + DESC.get(q, "")[:160])
 print(f"sum     {tot['us']:6.1f} {tot['traffic']:9.0f} " + " ".join(f"{tot[c]:12.0f}" for c in cols))
+if MODEL:
+    print("\ntraffic model (RLE_TRAFFIC=1: unique bytes the level's ops must move) against the counters, KB")
+    print(f"{'lvl':>3} {'act_r':>7} {'act_w':>7} {'w_r':>7} {'adam':>7} {'other':>7} {'model':>8} {'pmc':>8} {'x':>5}")
+    mt = defaultdict(float)
+    for q in sorted(merged):
+        m = MODEL.get(q)
+        if not m:
+            continue
+        r = merged[q]
+        tr = 2 * r.get("FETCH_SIZE", 0) + r.get("WRITE_SIZE", 0)
+        tot_m = sum(m.values())
+        for kk, vv in m.items():
+            mt[kk] += vv
+        mt["pmc"] += tr
+        print(f"{q:3d} " + " ".join(f"{m[kk]:7.0f}" for kk in ("act_r", "act_w", "w_r", "adam", "other")) +
+              f" {tot_m:8.0f} {tr:8.0f} {tr / max(tot_m, 1):5.2f}")
+    tm = sum(mt[kk] for kk in ("act_r", "act_w", "w_r", "adam", "other"))
+    print("sum " + " ".join(f"{mt[kk]:7.0f}" for kk in ("act_r", "act_w", "w_r", "adam", "other")) +
+          f" {tm:8.0f} {mt['pmc']:8.0f} {mt['pmc'] / max(tm, 1):5.2f}")
