@@ -905,6 +905,7 @@ static LevelTraffic level_traffic(const std::vector<Op>& ops, const float* P, si
     op_accesses(op, v);
     for (const Access& a : v) {
       const std::string what = a.what ? a.what : "";
+      if (what.rfind("tape", 0) == 0) continue;  // (declared whole; read only in tape mode, one row)
       const bool in_p = a.lo >= p0 && a.hi <= p1;
       if (what.rfind("adam", 0) == 0) {
         ad.push_back({a.lo, a.hi});
@@ -3116,7 +3117,8 @@ struct Engine {
     Graph G;
     size_t total = 0;
     for (auto& lv : levels) {
-      G.nlaunch += (int)((lv.size() + kLevelOps - 1) / kLevelOps);
+      // (launch_level: one launch up to kWideOps ops, else ceil(ops / kLevelOps))
+      G.nlaunch += lv.size() <= (size_t)kWideOps ? 1 : (int)((lv.size() + kLevelOps - 1) / kLevelOps);
       G.off.push_back((int)total);
       G.nops.push_back((int)lv.size());
       int wg = 0;
@@ -3289,7 +3291,9 @@ struct Engine {
   }
   template <class F>
   Prog plan_build(F&& f) {
-    return plan_build_for({this}, kLevelOps, std::forward<F>(f));
+    const char* e = std::getenv("RLE_MAX_OPS");  // A/B: wide launches for one engine's levels
+    const int mo = e ? std::min(std::max(std::atoi(e), 1), kWideOps) : kLevelOps;
+    return plan_build_for({this}, mo, std::forward<F>(f));
   }
 
   // steps per multi-step graph: RLE_PAIR=K (even; 0 = single-step graphs only)

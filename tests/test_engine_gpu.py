@@ -313,12 +313,18 @@ def _scaled(eng, alg, env, H, f):
 
 # td7_tiny hard-updates every 4 steps: no 6-step window ever fits, so the group runs every step
 # through the engines' own graphs (the fallback path); the others replay the packed program
-@pytest.mark.parametrize("name", ["td7_tiny", "td7_tiny@tur250", "td3_tiny", "sac_tiny", "td7_humanoid"])
-def test_packed_group_equals_engines_alone(name):
+@pytest.mark.parametrize("name", ["td7_tiny", "td7_tiny@tur250", "td3_tiny", "sac_tiny", "td7_humanoid",
+                                  "td7_humanoid@widened", "td3_halfcheetah@widened"])
+def test_packed_group_equals_engines_alone(name, monkeypatch):
     """rle_group_step (packed): three seeds (different weights) merged into
     one level schedule end bit-identical to each engine stepped alone -- parameters, counters,
     priorities and last batch -- and, full size, the packed program's levels exceed the 12-op
-    launch table (wide launches)."""
+    launch table (wide launches).  Bitwise with the tile planner's widening off (a wider tile
+    splits a reduction differently over its waves); '@widened' (the default planner, as the
+    bench runs it): same batches, parameters within the bulk criterion of this module."""
+    exact = not name.endswith("@widened")
+    if exact:
+        monkeypatch.setenv("RLE_LEVEL_CAP", "1000000")
     g = dict(load_golden(name.split("@")[0]))
     if name.endswith("@tur250"):
         g["meta_extra_vals"] = np.array([250.0])
@@ -346,15 +352,23 @@ def test_packed_group_equals_engines_alone(name):
         assert psteps == 0
     else:
         assert psteps >= 3 * (n // 2) and launches > 0 and levels > 0
-    if name == "td7_humanoid":
+    if name.startswith("td7_humanoid"):
         assert max(len(_OPS.findall(ln)) for ln in desc.splitlines() if ln.startswith("L")) > 12
     for (e1, r1), (e2, r2) in zip(alone, packed):
         np.testing.assert_array_equal(e1.counters(), e2.counters())
-        np.testing.assert_array_equal(e1.last_indices(), e2.last_indices())
-        np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
+        if exact:
+            np.testing.assert_array_equal(e1.last_indices(), e2.last_indices())
+            np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
+        else:
+            np.testing.assert_allclose(r1.get_priority(), r2.get_priority(), rtol=1e-4)
         for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
             for pname in params:
-                np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname), f"{net}.{pname}")
+                a, b = e1.get_param(net, pname), e2.get_param(net, pname)
+                if exact:
+                    np.testing.assert_array_equal(a, b, f"{net}.{pname}")
+                else:
+                    # (two fp32 summation orders over 20 steps: 99% bulk, as for the H=32 tensors)
+                    assert_params_close(a, b, 2 * 3e-4 * n + 1e-4, f"{net}.{pname}", bulk=0.99)
 
 
 @pytest.mark.parametrize("name", ["td7_tiny"])

@@ -18,6 +18,7 @@ for K in 3 2; do
 done
 timeout -k 10 200 python bench.py --steps 3000 --warmup 60 --no-cpu-baseline > gpurun_out/r03_single.json 2>&1 || exit 1
 cut -c1-200 gpurun_out/r03_single.json
+AB_TAG=_maxops bash tools/abenv.sh 2 3000 - RLE_MAX_OPS=32 RLE_MAX_OPS=16 || exit 1
 for v in nomfma noprio; do
   AB_TAG=_$v bash tools/ablib.sh sac-td3-td7_amd/lib/librle.so sac-td3-td7_amd/lib/librle_$v.so 2 3000 || exit 1
 done
