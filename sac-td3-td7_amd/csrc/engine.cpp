@@ -324,11 +324,20 @@ static void gemm_finalize(GemmArgs& g) {
                                g.A.seg[g.prea.seg].r1 - g.A.seg[g.prea.seg].r0 <= 32 && g.prea.mode == g.mode &&
                                g.prea.R % 16 == 0),
           "gemm: pre-GEMM layout");
-  REQUIRE(g.has_pre != 2 || (g.mode == GEMM_DX && g.epi == EPI_STORE && act == ACT_ELU && !norm && g.A.nseg == 1 &&
-                             g.hd.mode == HEAD_TD7_LOSS && g.hd.tgt_mode == HEAD_TD7_TARGET && g.hd.dact == ACT_ELU &&
-                             g.hd.H <= 256 && g.hd.H % 4 == 0 && g.R == r16(g.hd.H) && g.M % 16 == 0 &&
-                             g.hd.rows == g.M && (g.head_n == 0 || g.head_n == 1)),
-          "gemm: fused loss head layout");
+  {  // the fused head (kernels.hip headdx_reduce): q of every twin from EPI_QDOT partials
+    const HeadArgs& h = g.hd;
+    const bool pol = h.mode == HEAD_MLP_POLICY;
+    const bool modes = (h.mode == HEAD_TD7_LOSS && h.tgt_mode == HEAD_TD7_TARGET && h.vt && h.vmax_key && h.vmin_key) ||
+                       (h.mode == HEAD_MLP_LOSS && h.tgt_mode == HEAD_MLP_TARGET && !h.vt) ||
+                       (pol && h.tgt_mode < 0 && !h.lap && h.tp_n[0] == 0 && h.tp_n[1] == 0);
+    const bool parts = h.qp[0] && h.qp[1] && h.qp_n[0] <= 64 && h.qp_n[1] <= 64 &&
+                       (pol || (h.tp[0] && h.tp[1] && h.tp_n[0] <= 64 && h.tp_n[1] <= 64));
+    REQUIRE(g.has_pre != 2 || (g.mode == GEMM_DX && g.epi == EPI_STORE && (act == ACT_ELU || act == ACT_RELU) &&
+                               !norm && g.A.nseg == 1 && modes && parts && h.dact == act && (!h.sac || h.logpi) &&
+                               (!h.lap || h.prio) && h.H <= 256 && h.H % 4 == 0 && g.R == r16(h.H) &&
+                               g.M % 16 == 0 && h.rows == g.M && (g.head_n == 0 || g.head_n == 1)),
+            "gemm: fused loss head layout");
+  }
   REQUIRE(g.has_pre >= 0 && g.has_pre <= 2, "gemm: pre kind");
   g.vid = gemm_vid(g.mode, g.epi, act, norm, g.has_pre);
   REQUIRE(g.tn == 16 || g.tn == 32 || g.tn == 64, "gemm: tile width");
@@ -596,9 +605,10 @@ static void audit_gemm(const GemmArgs& g) {
     audit_range(h.w[hn], 0, (long long)h.w_cbn * 1024, "head w3", g);
     for (int n = 0; n < 2; ++n) {
       audit_range(h.b[n], 0, 4, "head b3", g);
-      audit_range(h.tb[n], 0, 4, "head tb3", g);
+      if (h.tb[n]) audit_range(h.tb[n], 0, 4, "head tb3", g);
     }
     if (h.vt) audit_range(h.vt, 0, 8, "head vt", g);
+    if (h.sac) audit_range(h.log_alpha, 0, 4, "head alpha", g);
     for (int it = 0; it < g.tiles_m; ++it) {
       const int i0 = it * 16;
       for (int n = 0; n < 2; ++n) {
@@ -607,14 +617,16 @@ static void audit_gemm(const GemmArgs& g) {
       }
       if (h.reward) audit_range(h.reward, (long long)i0 * 4, 64, "head reward", g);
       if (h.notdone) audit_range(h.notdone, (long long)i0 * 4, 64, "head notdone", g);
+      if (h.sac) audit_range(h.logpi, (long long)i0 * 4, 64, "head logpi", g);
       // tile column 0 stores the head's outputs of its rows
       if (hn == 0 && h.lap) audit_range(h.prio, (long long)i0 * 4, 64, "head prio", g, 1);
       if (h.dq[hn].t) audit_range(h.dq[hn].t, h_tblk(h.dq[hn].rbs, i0, 0), 1024, "head dq", g, 1);
-      for (int c = 0; c < g.R; c += 16) audit_mat(h.dz[hn], i0, c, "head dz", g, false, false, 1);
+      if (h.dz[hn].n || h.dz[hn].t)
+        for (int c = 0; c < g.R; c += 16) audit_mat(h.dz[hn], i0, c, "head dz", g, false, false, 1);
       if (hn == 0) {
         if (h.loss_part) audit_range(h.loss_part, (long long)(i0 / 4) * 16, 64, "head loss", g, 1);
-        audit_range(h.vmax_key, 0, 4, "head vmax", g, 1);
-        audit_range(h.vmin_key, 0, 4, "head vmin", g, 1);
+        if (h.vmax_key) audit_range(h.vmax_key, 0, 4, "head vmax", g, 1);
+        if (h.vmin_key) audit_range(h.vmin_key, 0, 4, "head vmin", g, 1);
       }
     }
   }
@@ -1810,7 +1822,8 @@ struct Engine {
     }
     float* qpart = nullptr;
     if (qdot) {  // EPI_QDOT: row partials of the H -> 1 layer qdot applied to this output
-      REQUIRE(!normed && qdot->out == 1 && qdot->K == L.out && act == ACT_ELU, "fwd: q-dot partial layout");
+      REQUIRE(!normed && qdot->out == 1 && qdot->K == L.out && (act == ACT_ELU || act == ACT_RELU),
+              "fwd: q-dot partial layout");
       qpart = mem.make<float>((size_t)tiles_n * M);
       out.qd = qpart;
       out.qd_ld = M;
@@ -2808,13 +2821,38 @@ struct Engine {
   }
 
   // MLP critic stack forward: returns (h0, h1)
+  // qd: the last hidden layer also emits EPI_QDOT row partials of q (a fused head reads them)
   void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, View& h0, View& h1,
-                      const PreUse* pre = nullptr, bool h1_t = true) {
+                      const PreUse* pre = nullptr, bool h1_t = true, bool qd = false) {
     h0 = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pre);
     const bool keep = out_t;
     out_t = keep && h1_t;  // (h1_t = false: only the head reads h1, in the N image)
-    h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false);
+    h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, nullptr,
+             qd ? &Q.layers[2] : nullptr);
     out_t = keep;
+  }
+  // TD3 / SAC: the critic loss head and the actor objective's head fused into the DX of each
+  // critic's last hidden layer (GemmArgs::has_pre 2; one level fewer on the critic chain and on
+  // the policy chain).  RLE_NO_HEADDX=1: the standalone heads (tests, A/B).
+  bool mlp_headdx() const {
+    const char* e = std::getenv("RLE_NO_HEADDX");
+    return !(e && e[0] == '1') && B % 16 == 0 && H <= 256 && H % 4 == 0;
+  }
+  // q partials of the twins (and target twins) into a head fused by headdx
+  static void set_head_parts(HeadArgs& h, const View* q, const View* t, std::vector<int>& rd) {
+    for (int n = 0; n < 2; ++n) {
+      h.qp[n] = q[n].qd;
+      h.qp_n[n] = q[n].qd_n;
+      rd.push_back(q[n].qd_id);
+      if (t) {
+        h.tp[n] = t[n].qd;
+        h.tp_n[n] = t[n].qd_n;
+        rd.push_back(t[n].qd_id);
+      }
+    }
+    h.qp_ld = q[0].qd_ld;
+    h.tp_ld = t ? t[0].qd_ld : 0;
+    REQUIRE(q[1].qd_ld == h.qp_ld && (!t || t[1].qd_ld == h.tp_ld), "head: q partial layout");
   }
 
   // SAC temperature operand of the heads and the actor backward: log_alpha (autotune, the
@@ -2879,12 +2917,17 @@ struct Engine {
     // target critics + y
     View th0[2], th1[2];
     out_t = false;  // (forward only)
-    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n], prea ? &pn1 : nullptr);
+    const bool hdx = mlp_headdx();
+    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n], prea ? &pn1 : nullptr, true, hdx);
     out_t = true;
     // online critics
     View c0[2], c1[2];
-    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c0[n], c1[n]);
-    View dz1[2] = {buf(B, H), buf(B, H)}, dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
+    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c0[n], c1[n], nullptr, true, hdx);
+    // (dZ of the critics' last hidden layers: with the fused head only their weight gradients read
+    // it, in the T image)
+    View dz1[2] = {buf(B, H, !hdx, true), buf(B, H, !hdx, true)},
+         dq[2] = {buf(B, 1, false, true), buf(B, 1, false, true)};
+    View d0f[2];  // (hdx) dZ of each critic's first hidden layer from the fused head + DX
     View prio = vec(B);
     const int hw = cdiv(B, 4);
     qloss_part = mem.make<float>((size_t)hw * 4);
@@ -2916,7 +2959,19 @@ struct Engine {
       h.dq[1] = dq[1].m;
       h.loss_part = qloss_part;
       h.prio = prio.p;
-      pg.add(op, rd, {dz1[0].id, dz1[1].id, dq[0].id, dq[1].id, prio.id, qloss_id = next_id++});
+      qloss_id = next_id++;
+      if (!hdx) {
+        pg.add(op, rd, {dz1[0].id, dz1[1].id, dq[0].id, dq[1].id, prio.id, qloss_id});
+      } else {
+        // the head runs inside the DX of each critic's last hidden layer; critic 0's op stores the
+        // priorities and loss partials
+        set_head_parts(h, c1, th1, rd);
+        for (int n = 0; n < 2; ++n) {
+          HeadUse hu{h, n, rd, {dz1[n].id, dq[n].id}};
+          if (n == 0) hu.wr.insert(hu.wr.end(), {prio.id, qloss_id});
+          d0f[n] = dx(pg, {{c1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &c0[n], nullptr, nullptr, nullptr, &hu);
+        }
+      }
     }
     if (lap) {
       Op op{};
@@ -2935,7 +2990,7 @@ struct Engine {
     for (int n = 0; n < 2; ++n) {
       Net& Q = *q[n];
       dw(pg, Q.layers[2], dq[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
-      View d0 = dx(pg, {{dz1[n], &Q.layers[1], 0}}, H, B, ACT_RELU, &c0[n]);
+      View d0 = hdx ? d0f[n] : dx(pg, {{dz1[n], &Q.layers[1], 0}}, H, B, ACT_RELU, &c0[n]);
       dw(pg, Q.layers[1], dz1[n], {c0[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
       dw(pg, Q.layers[0], d0, {s, act_in}, B, CNT_ADAM_Q, cfg.critic_lr);
     }
@@ -2944,11 +2999,37 @@ struct Engine {
     int ngsq = 0;
     if (policy) {
       View p0[2], p1[2];
-      for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, a_pi, p0[n], p1[n], nullptr, false);
+      for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, a_pi, p0[n], p1[n], nullptr, false, hdx);
       // (no weight gradient of the critics in the policy pass: the gradients keep N images only)
-      View dzp1[2] = {buf(B, H, true, false), buf(B, H, true, false)};
+      View dzp1[2];
+      if (!hdx) dzp1[0] = buf(B, H, true, false), dzp1[1] = buf(B, H, true, false);
       ploss_part = mem.make<float>((size_t)hw * 4);
-      {
+      View dzp0[2];
+      if (hdx) {  // the objective's head inside the DX of each critic's last hidden layer
+        Op op = head_op(HEAD_MLP_POLICY, B);
+        HeadArgs& h = op.head;
+        set_head_twin(h, p1[0], p1[1], q[0]->layers[2], q[1]->layers[2]);
+        h.dact = ACT_RELU;
+        h.loss_part = ploss_part;
+        std::vector<int> rd{p1[0].id, p1[1].id, q[0]->layers[2].res, q[1]->layers[2].res};
+        if (sac) {
+          h.sac = 1;
+          h.logpi = logpi.p;
+          h.log_alpha = alpha_src();
+          h.alpha_lin = cfg.tmp >= 0.f;
+          rd.push_back(logpi.id);
+          rd.push_back(R_LA);
+        }
+        set_head_parts(h, p1, nullptr, rd);
+        ploss_id = next_id++;
+        out_t = false;
+        for (int n = 0; n < 2; ++n) {
+          HeadUse hu{h, n, rd, {}};
+          if (n == 0) hu.wr.push_back(ploss_id);
+          dzp0[n] = dx(pg, {{p1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &p0[n], nullptr, nullptr, nullptr, &hu);
+        }
+        out_t = true;
+      } else {
         Op op = head_op(HEAD_MLP_POLICY, B);
         HeadArgs& h = op.head;
         set_head_twin(h, p1[0], p1[1], q[0]->layers[2], q[1]->layers[2]);
@@ -2968,11 +3049,10 @@ struct Engine {
           rd.push_back(R_LA);
         }
         pg.add(op, rd, {dzp1[0].id, dzp1[1].id, ploss_id = next_id++});
+        out_t = false;
+        for (int n = 0; n < 2; ++n) dzp0[n] = dx(pg, {{dzp1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &p0[n]);
+        out_t = true;
       }
-      View dzp0[2];
-      out_t = false;
-      for (int n = 0; n < 2; ++n) dzp0[n] = dx(pg, {{dzp1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &p0[n]);
-      out_t = true;
       View dout;
       PreUse pdout{};  // TD3: d1 recomputes dout in-tile
       if (!sac) {

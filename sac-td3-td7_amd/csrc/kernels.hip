@@ -650,29 +650,34 @@ __device__ __forceinline__ float lap_priority(float d) {
   return f;
 }
 
-// ---- fused loss head (GemmArgs::has_pre 2): the TD7 critic head (op_head_t, HEAD_TD7_LOSS with
-// the target twins fused, q from EPI_QDOT partials) for the tile's 16 rows, one per lane, then the
-// DX reduction of critic head_n whose A operand dZ = (dq * w3) * act'(z) is formed from z
-// (segment 0) as op_head_t formed dz.  own_wg: this workgroup stores the head's outputs of its
-// rows (tile column 0); own_dz: this wave also stores its dZ chunks (column group 0).
+// ---- fused loss head (GemmArgs::has_pre 2): a critic head for the tile's 16 rows, one per
+// lane, from EPI_QDOT partials of q -- HEAD_TD7_LOSS / HEAD_MLP_LOSS (op_head_t with the target
+// twins fused) or HEAD_MLP_POLICY (TD3 / SAC actor objective, min of the twins) -- then the DX
+// reduction of critic head_n whose A operand dZ = (dq * w) * act'(z) is formed from z (segment
+// 0) as op_head_t formed dz.  own_wg: this workgroup stores the head's outputs of its rows (tile
+// column 0); own_dz: this wave also stores its dZ chunks (column group 0), when dz has an image.
+template <int DACT>
 __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, int j0, bool active, bool own_wg,
                                                bool own_dz, int c0, int c1, int nch, const float* a0p, int a0xs,
                                                const float* b0p, int b0xs, float* smem, f32x4 acc) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const CAS HeadArgs& h = g.hd;
   const int hn = g.head_n;
+  const bool pol = h.mode == HEAD_MLP_POLICY, td7 = h.mode == HEAD_TD7_LOSS;  // (uniform)
   float* dqs = smem + 64 + 1024;  // [16] dq of critic hn per tile row (the tabs region)
   float* w3s = dqs + 16;          // [H] critic hn's last-layer weights
   for (int c = 4 * tid; c < h.H; c += 4 * kThreads) *(float4*)(w3s + c) = ld4g(G(h.w[hn]) + nidx(h.w_cbn, 0, c));
-  // q of the twins and of the target twins for the tile's 16 rows from their EPI_QDOT row
-  // partials: wave w sums quantity w (0 / 1: q of critic 0 / 1, 2 / 3: the target critics' q),
-  // lane l adds partials 16 (l / 16) .. +15 of row l % 16 in order, then the 4 lane groups
+  // q of the twins and (loss heads) of the target twins for the tile's 16 rows from their
+  // EPI_QDOT row partials: wave w sums quantity w (0 / 1: q of critic 0 / 1, 2 / 3: the target
+  // critics' q), lane l adds partials 16 (l / 16) .. +15 of row l % 16 in order, then the 4 lane
+  // groups
   float* qv = w3s + 256;        // [4][16] the quantities (+ bias)
   float* acs = qv + 64;         // [2][16] loss terms
   int* kq = (int*)(acs + 32);   // [16] value keys
   const int row = lane & 15, grp = lane >> 4;
+  const bool tw = wave >= 2;    // a target twin's quantity (none in the policy head)
   const float* src = wave == 0 ? h.qp[0] : (wave == 1 ? h.qp[1] : (wave == 2 ? h.tp[0] : h.tp[1]));
-  const int np = wave == 0 ? h.qp_n[0] : (wave == 1 ? h.qp_n[1] : (wave == 2 ? h.tp_n[0] : h.tp_n[1]));
+  const int np = (pol && tw) ? 0 : (wave == 0 ? h.qp_n[0] : (wave == 1 ? h.qp_n[1] : (wave == 2 ? h.tp_n[0] : h.tp_n[1])));
   const int ld = wave < 2 ? h.qp_ld : h.tp_ld;
   float pv[16];
 #pragma unroll
@@ -680,13 +685,15 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
     const int p = grp * 16 + k;
     pv[k] = p < np ? G(src)[(size_t)p * ld + i0 + row] : 0.f;
   }
-  float rw = 0.f, ndn = 0.f;
+  float rw = 0.f, ndn = 0.f, lpv = 0.f;
   if (wave == 0 && lane < 16) {
     if (h.reward) rw = G(h.reward)[i0 + lane];
     if (h.notdone) ndn = G(h.notdone)[i0 + lane];
+    if (h.sac) lpv = G(h.logpi)[i0 + lane];
   }
-  const float bq = sload(wave == 0 ? h.b[0] : (wave == 1 ? h.b[1] : (wave == 2 ? h.tb[0] : h.tb[1])));
+  const float bq = (pol && tw) ? 0.f : sload(wave == 0 ? h.b[0] : (wave == 1 ? h.b[1] : (wave == 2 ? h.tb[0] : h.tb[1])));
   const float vtmax = h.vt ? sload(h.vt) : 0.f, vtmin = h.vt ? sload(h.vt + 1) : 0.f;
+  const float alpha = h.sac ? (h.alpha_lin ? sload(h.log_alpha) : expf(sload(h.log_alpha))) : 0.f;
   float sm = 0.f;
 #pragma unroll
   for (int k = 0; k < 16; ++k) sm += pv[k];
@@ -694,35 +701,50 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
   sm += __shfl_xor(sm, 32);
   if (lane < 16) qv[wave * 16 + lane] = sm + bq;
   __syncthreads();
-  if (wave == 0 && lane < 16) {  // one row per lane (op_head_t HEAD_TD7_LOSS, target fused)
+  if (wave == 0 && lane < 16) {  // one row per lane (op_head_t, target fused)
     const int b = i0 + lane;
     const float q[2] = {qv[lane], qv[16 + lane]};
-    float v = fminf(qv[32 + lane], qv[48 + lane]);
-    v = fminf(fmaxf(v, vtmin), vtmax);
-    const float yv = rw + (h.gamma * v) * ndn;
-    float dq[2], ac[2], dmax = 0.f;
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {  // td7.py:231-244
-      const float diff = q[n] - yv;
-      if (h.lap) {
-        const float d = fabsf(diff);
-        ac[n] = d < 1.f ? 0.5f * (d * d) : d;
-        const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-        dq[n] = (d < 1.f ? d : 1.f) * sg * h.inv_b;
-        dmax = fmaxf(dmax, d);
+    float dq[2], ac[2] = {0.f, 0.f}, dmax = 0.f;
+    if (pol) {  // HEAD_MLP_POLICY: td3.py:191, sac.py:227-229
+      const float mn = fminf(q[0], q[1]);
+      const float gq = -h.inv_b;  // torch.minimum backward: ties split the gradient
+      dq[0] = q[0] < q[1] ? gq : (q[0] == q[1] ? 0.5f * gq : 0.f);
+      dq[1] = q[1] < q[0] ? gq : (q[0] == q[1] ? 0.5f * gq : 0.f);
+      if (h.sac) {
+        ac[0] = -mn + lpv * alpha;
+        ac[1] = lpv;
       } else {
-        const float e = yv - q[n];
-        ac[n] = e * e;
-        dq[n] = -e * h.inv_b;
+        ac[0] = mn;
       }
+      kq[lane] = 0;
+    } else {
+      float v = fminf(qv[32 + lane], qv[48 + lane]);
+      if (td7) v = fminf(fmaxf(v, vtmin), vtmax);  // td7.py:211-218
+      else if (h.sac) v = v - alpha * lpv;         // sac.py:188-193 (td3.py:160-164: neither)
+      const float yv = rw + (h.gamma * v) * ndn;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {  // td7.py:231-244, td3.py:169-182
+        const float diff = q[n] - yv;
+        if (h.lap) {
+          const float d = fabsf(diff);
+          ac[n] = d < 1.f ? 0.5f * (d * d) : d;
+          const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+          dq[n] = (d < 1.f ? d : 1.f) * sg * h.inv_b;
+          dmax = fmaxf(dmax, d);
+        } else {
+          const float e = yv - q[n];
+          ac[n] = e * e;
+          dq[n] = -e * h.inv_b;
+        }
+      }
+      if (own_wg && hn == 0 && h.lap) GW(h.prio)[b] = lap_priority(dmax);
+      kq[lane] = fkey(yv);
     }
-    if (own_wg && hn == 0 && h.lap) GW(h.prio)[b] = lap_priority(dmax);
     const float dqn = hn ? dq[1] : dq[0];
     if (own_wg && h.dq[hn].t) GW(h.dq[hn].t)[tidx(h.dq[hn].rbs, b, 0)] = dqn;
     dqs[lane] = dqn;
     acs[lane] = ac[0];
     acs[16 + lane] = ac[1];
-    kq[lane] = fkey(yv);
   }
   __syncthreads();
   if (own_wg && hn == 0 && wave == 0) {
@@ -734,7 +756,7 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
       lp[2] = 0.f;
       lp[3] = 0.f;
     }
-    if (lane == 0) {  // value_max / value_min (td7.py:217-218)
+    if (lane == 0 && td7) {  // value_max / value_min (td7.py:217-218)
       int kmax = kq[0], kmin = kq[0];
       for (int r = 1; r < 16; ++r) {
         kmax = max(kmax, kq[r]);
@@ -744,6 +766,7 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
       atomicMin(h.vmin_key, kmin);
     }
   }
+  own_dz = own_dz && (h.dz[hn].n != nullptr || h.dz[hn].t != nullptr);
   __syncthreads();
   // ---- the DX reduction over this wave's chunks [c0, c1) of the single A segment
   if (!active || c0 >= c1) return acc;
@@ -762,8 +785,8 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
       if (c + r >= n) break;  // (uniform, as ring_run)
       const int k = c0 + c + r;  // absolute chunk
       const float4 z = xa[r], w = *(const float4*)(w3s + k * 16 + cq);
-      const float4 y = make_float4((dqr * w.x) * act_b<ACT_ELU>(z.x), (dqr * w.y) * act_b<ACT_ELU>(z.y),
-                                   (dqr * w.z) * act_b<ACT_ELU>(z.z), (dqr * w.w) * act_b<ACT_ELU>(z.w));
+      const float4 y = make_float4((dqr * w.x) * act_b<DACT>(z.x), (dqr * w.y) * act_b<DACT>(z.y),
+                                   (dqr * w.z) * act_b<DACT>(z.z), (dqr * w.w) * act_b<DACT>(z.w));
       if (own_dz) mat_str4(h.dz[hn], i0 + (lane & 15), k * 16 + cq, y);
       if (r & 1) acc1 = mfma4(y, xb[r], acc1);
       else acc = mfma4(y, xb[r], acc);
@@ -956,8 +979,8 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       acc = ring_run<NORM ? 1 : 0, 0>(ra, rb, rsrc(sap), va, rsrc(sbp), vb, k1 - k0, acc, inva, nullptr, nullptr, false);
     };
     if constexpr (PK == 2) {  // fused loss head: one A segment, dZ of the critic's last hidden layer
-      acc = headdx_reduce(g, i0, j0, active, jt == 0, jt == 0 && cg == 0, c0, c1, nch, a0p, a0xs, b0p, b0xs, smem,
-                          acc);
+      acc = headdx_reduce<ACT>(g, i0, j0, active, jt == 0, jt == 0 && cg == 0, c0, c1, nch, a0p, a0xs, b0p, b0xs,
+                               smem, acc);
     } else if constexpr (PK == 1) {  // segment g.prea.seg comes from the pre-GEMM in LDS
       float* pimg = smem + 64 + 2048;
       PreRing pr;
@@ -1200,17 +1223,14 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         gg += ok ? gv * gv : 0.f;
       }
       GAS float* pw = bias_tile ? GW(ad.b) + ib : GW(ad.w.t) + wt;
-#ifdef RLE_EXP_ADAM_NT_P  // experiment: the weights' T image as a streaming store too
-      {
+      {  // the weights' T image (+ bias) too: +0.3% over 3 A/B pairs
         f32x4 w;
         w.x = po[0]; w.y = po[1]; w.z = po[2]; w.w = po[3];
         __builtin_nontemporal_store(w, (GAS f32x4*)pw);
       }
-#else
-      st4g(pw, make_float4(po[0], po[1], po[2], po[3]));
-#endif
       // Adam moments: read again only by the next step's Adam of this tile, so streaming
-      // (nontemporal) stores -- measured +0.45% (3 A/B pairs, tools/ablib.sh)
+      // (nontemporal) stores -- measured +0.45% (3 A/B pairs, tools/ablib.sh); the T image above
+      // is read by the next step's input-gradient GEMMs, long after
       {
         f32x4 w;
         w.x = mo[0]; w.y = mo[1]; w.z = mo[2]; w.w = mo[3];
@@ -1270,6 +1290,7 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, true)
     RLE_V(GEMM_FWD, EPI_ACT, ACT_TANH, false)
     RLE_V(GEMM_FWD, EPI_QDOT, ACT_ELU, false)
+    RLE_V(GEMM_FWD, EPI_QDOT, ACT_RELU, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_NONE, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_RELU, false)
     RLE_V(GEMM_DX, EPI_STORE, ACT_ELU, false)
@@ -1283,6 +1304,7 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_VP(GEMM_FWD, EPI_STORE, ACT_ELU, true)
     RLE_VP(GEMM_DX, EPI_STORE, ACT_RELU, false)
     RLE_VH(GEMM_DX, EPI_STORE, ACT_ELU, false)
+    RLE_VH(GEMM_DX, EPI_STORE, ACT_RELU, false)
     default: break;
   }
 #undef RLE_V

@@ -9,7 +9,7 @@ for i in $(seq 1 $R); do
   line=""
   for e in "$@"; do
     [ "$e" = "-" ] && ev="" || ev="$e"
-    x=$(env $ev timeout -k 10 120 python bench.py --steps $N --warmup 100 --no-cpu-baseline | python -c "import json,sys; d=json.load(sys.stdin); print(round(d['value'],1), round(d['roofline']['launches_per_step'],2))") || exit 1
+    x=$(env $ev timeout -k 10 120 python bench.py --steps $N --warmup 100 --no-cpu-baseline $BENCH_ARGS | python -c "import json,sys; d=json.load(sys.stdin); print(round(d['value'],1), round(d['roofline']['launches_per_step'],2))") || exit 1
     line="$line | $e: $x"
   done
   echo "$line" | tee -a $ROOT/gpurun_out/abenv${AB_TAG}.txt
