@@ -338,6 +338,14 @@ static void gemm_finalize(GemmArgs& g) {
                                g.M % 16 == 0 && h.rows == g.M && (g.head_n == 0 || g.head_n == 1)),
             "gemm: fused loss head layout");
   }
+  REQUIRE(g.epi != EPI_SACFWD || (g.mode == GEMM_FWD && act == ACT_NONE && !norm && g.has_pre == 0 && g.tn == 64 &&
+                                   g.tiles_n == 1 && g.sf.A <= 32 && g.sf.ls_off + g.sf.A <= g.N && g.sf.eps.t &&
+                                   g.sf.eps2.t && (g.sf.act.n || g.sf.act.t) && g.sf.logpi),
+          "gemm: SAC actor forward epilogue operands");
+  REQUIRE(g.epi != EPI_SACBWD || (g.mode == GEMM_DX && act == ACT_NONE && !norm && g.has_pre == 0 && g.sb.raw.t &&
+                                   g.sb.eps2.t && (g.sb.dout.n || g.sb.dout.t) && g.sb.log_alpha &&
+                                   g.sb.ls_off >= g.sb.mean_off + g.N),
+          "gemm: SAC actor backward epilogue operands");
   REQUIRE(g.has_pre >= 0 && g.has_pre <= 2, "gemm: pre kind");
   g.vid = gemm_vid(g.mode, g.epi, act, norm, g.has_pre);
   REQUIRE(g.tn == 16 || g.tn == 32 || g.tn == 64, "gemm: tile width");
@@ -583,6 +591,25 @@ static void audit_gemm(const GemmArgs& g) {
             audit_range(g.noise.t, h_tblk(g.noise.rbs, i0 + 15 - g.noise_row0, j0), 1024, "noise", g);
           }
           if (g.epi == EPI_NBDOT) audit_mat(g.nbx, i0, j0, "nbx", g, false, true);
+          if (g.epi == EPI_SACFWD && w == 0) {  // the tile's rows: noise, action, log pi
+            const SacFwdArgs& sf = g.sf;
+            for (int c : {0, sf.A - 1}) {
+              if (i0 < sf.eps_row_split) audit_mat(sf.eps2, i0, c, "sac eps2", g, false, true);
+              else audit_mat(sf.eps, i0 - sf.eps_row_split, c, "sac eps", g, false, true);
+              audit_mat(sf.act, i0, c, "sac act", g, false, false, 1);
+            }
+            audit_range(sf.logpi, (long long)i0 * 4, 64, "sac logpi", g, 1);
+          }
+          if (g.epi == EPI_SACBWD) {  // columns j0 .. j0 + ncol - 1 of the mean and log_std blocks
+            const SacBwdArgs& sb = g.sb;
+            audit_mat(sb.eps2, i0, j0, "sac eps2", g, false, true);
+            for (int off : {sb.mean_off, sb.ls_off})
+              for (int c : {off + j0, off + j0 + ncol - 1}) {
+                audit_mat(sb.raw, i0, c, "sac raw", g, false, true);
+                audit_mat(sb.dout, i0, c, "sac dout", g, false, false, 1);
+              }
+            audit_range(sb.log_alpha, 0, 4, "sac alpha", g);
+          }
           if (g.epi == EPI_MSE) {
             audit_mat(g.tgt, i0, j0, "tgt", g, false, true);
             audit_norm(g.tgt_norm, i0, 16, g);
@@ -1705,6 +1732,16 @@ struct Engine {
     int n;
     std::vector<int> rd, wr;  // the head's resources (beyond the DX's own)
   };
+  // The SAC actor rsample (OP_SAC_ACTOR) as the epilogue of its raw head GEMM (EPI_SACFWD)
+  struct SacFwdUse {
+    SacFwdArgs a;
+    std::vector<int> rd, wr;
+  };
+  // The SAC actor backward (OP_SAC_ACTOR_BWD) as the epilogue of the DX producing da (EPI_SACBWD)
+  struct SacBwdUse {
+    SacBwdArgs a;
+    std::vector<int> rd, wr;
+  };
   // The actor's tanh output layer L over rows x (+ target smoothing noise) as a pre-GEMM
   // (sale.py:77-83 / mlp.py:55-62, td7.py:188-194, td3.py:154-158).
   PreUse pre_actor_fwd(const Layer& L, const View& x, const View* noise, int seg) {
@@ -1770,7 +1807,7 @@ struct Engine {
   View fwd(Prog& pg, const Layer& L, const std::vector<std::vector<View>>& ins, int M, int act, View* pre_out,
            bool normed, const View* noise = nullptr, int noise_row0 = 0, const std::vector<WSeg>* wsegs = nullptr,
            const View* bias_ovr = nullptr, const PreUse* pre = nullptr, const Layer* qdot = nullptr,
-           bool pre_n = false) {
+           bool pre_n = false, const SacFwdUse* sfu = nullptr) {
     REQUIRE(ins.size() == L.seg_p.size(), "fwd: input segment count mismatch for " + L.wname);
     REQUIRE(M % kTileM == 0, "fwd: rows must be a multiple of 16");
     REQUIRE(!wsegs || wsegs->size() == ins.size(), "fwd: one weight block per input segment");
@@ -1799,9 +1836,14 @@ struct Engine {
       rd.insert(rd.end(), pre->rd.begin(), pre->rd.end());
     }
     const auto tq = choose_tn(M, L.out);
-    const int tn = tq.first;
+    const int tn = sfu ? 64 : tq.first;  // (EPI_SACFWD: one tile column holds whole rows)
     const int tiles_n = cdiv(L.out, tn);
     View out = buf(M, L.out, true, out_t);
+    if (sfu) {
+      REQUIRE(!pre && !qdot && !normed && !noise && act == ACT_NONE && L.out <= 64, "fwd: SAC forward epilogue");
+      rd.insert(rd.end(), sfu->rd.begin(), sfu->rd.end());
+      wr.insert(wr.end(), sfu->wr.begin(), sfu->wr.end());
+    }
     wr.push_back(out.id);
     if (pre_out) {
       // T: DX epilogue masks; N (pre_n) only where the loss head reads the rows: 4 scattered
@@ -1892,6 +1934,11 @@ struct Engine {
         g.norm_out = part + ra;
         g.norm_ld = M;
       }
+      if (sfu) {
+        REQUIRE(cuts.size() == 2, "fwd: SAC forward epilogue over one row piece");
+        g.epi = EPI_SACFWD;
+        g.sf = sfu->a;
+      }
       if (qdot) {
         g.epi = EPI_QDOT;
         g.qw = P + qdot->wn_off;
@@ -1922,7 +1969,7 @@ struct Engine {
   // dX[:, 0:ncols] = sum_t dZ_t W_t[:, col0_t : col0_t + ncols]  (* act'(saved))
   View dx(Prog& pg, const std::vector<DxTerm>& terms, int ncols, int M, int dact, const View* saved,
           const View* into = nullptr, const View* nb_x = nullptr, const PreUse* pre = nullptr,
-          const HeadUse* head = nullptr) {
+          const HeadUse* head = nullptr, const SacBwdUse* sbu = nullptr) {
     Op op{};
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;
@@ -1999,6 +2046,14 @@ struct Engine {
       g.head_n = head->n;
       rd.insert(rd.end(), head->rd.begin(), head->rd.end());
       wr.insert(wr.end(), head->wr.begin(), head->wr.end());
+    }
+    if (sbu) {  // the output is sbu->a.dout (d / d(mean | log_std)), not da
+      REQUIRE(!head && !pre && !nb_x && !saved, "dx: SAC backward epilogue is a plain DX");
+      g.epi = EPI_SACBWD;
+      g.out = Mat{};
+      g.sb = sbu->a;
+      rd.insert(rd.end(), sbu->rd.begin(), sbu->rd.end());
+      wr.insert(wr.end(), sbu->wr.begin(), sbu->wr.end());
     }
     op.wg_count = g.tiles_m * g.tiles_n;
     pg.add(op, rd, wr);
@@ -2834,6 +2889,16 @@ struct Engine {
   // TD3 / SAC: the critic loss head and the actor objective's head fused into the DX of each
   // critic's last hidden layer (GemmArgs::has_pre 2; one level fewer on the critic chain and on
   // the policy chain).  RLE_NO_HEADDX=1: the standalone heads (tests, A/B).
+  // SAC: the rsample as the epilogue of the actor's raw head (RLE_NO_SACFWD=1: OP_SAC_ACTOR, A/B)
+  bool sac_fwd_fused() const {
+    const char* e = std::getenv("RLE_NO_SACFWD");
+    return !(e && e[0] == '1') && 2 * A <= 64 && A <= 32;
+  }
+  // SAC: the actor backward as the epilogue of the da DX (RLE_NO_SACBWD=1: OP_SAC_ACTOR_BWD, A/B)
+  bool sac_bwd_fused() const {
+    const char* e = std::getenv("RLE_NO_SACBWD");
+    return !(e && e[0] == '1');
+  }
   bool mlp_headdx() const {
     const char* e = std::getenv("RLE_NO_HEADDX");
     return !(e && e[0] == '1') && B % 16 == 0 && H <= 256 && H % 4 == 0;
@@ -2891,6 +2956,25 @@ struct Engine {
     if (!sac) {
       actv = prea ? fwd(pg, pi.layers[2], {{h1.sub(0, B)}}, B, ACT_TANH, nullptr, false)
                   : fwd(pg, pi.layers[2], {{h1}}, B2, ACT_TANH, nullptr, false, &eps, B);
+    } else if (sac_fwd_fused()) {  // the rsample in the raw head's epilogue (one level fewer)
+      actv = buf(B2, A);
+      logpi = vec(B2);
+      SacFwdUse sfu{};
+      SacFwdArgs& a = sfu.a;
+      a.eps = eps.m;
+      a.eps2 = eps2.m;
+      a.act = actv.m;
+      a.logpi = logpi.p;
+      a.min_log_std = cfg.min_log_std;
+      a.max_log_std = cfg.max_log_std;
+      a.A = A;
+      a.mean_off = 0;
+      a.ls_off = A;
+      a.eps_row_split = B;
+      sfu.rd = {eps.id, eps2.id};
+      sfu.wr = {actv.id, logpi.id};
+      raw = fwd(pg, pi.layers[2], {{h1}}, B2, ACT_NONE, nullptr, false, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
+                false, &sfu);
     } else {
       raw = fwd(pg, pi.layers[2], {{h1}}, B2, ACT_NONE, nullptr, false);
       actv = buf(B2, A);
@@ -3059,9 +3143,29 @@ struct Engine {
         dout = dx(pg, {{dzp0[0], &q[0]->layers[0], Sp}, {dzp0[1], &q[1]->layers[0], Sp}}, A, B, ACT_TANH, &a_pi);
         if (prea) pdout = pre_actor_dx({{dzp0[0], &q[0]->layers[0], Sp}, {dzp0[1], &q[1]->layers[0], Sp}}, A, a_pi, 0);
       } else {
+        dout = buf(B, 2 * A);
+        if (sac_bwd_fused()) {  // the backward in the epilogue of the DX that forms da (one level fewer)
+          SacBwdUse sbu{};
+          SacBwdArgs& a = sbu.a;
+          a.raw = raw.m;
+          a.eps2 = eps2.m;
+          a.dout = dout.m;
+          a.log_alpha = alpha_src();
+          a.alpha_lin = cfg.tmp >= 0.f;
+          a.inv_b = 1.f / (float)B;
+          a.min_log_std = cfg.min_log_std;
+          a.max_log_std = cfg.max_log_std;
+          a.mean_off = 0;
+          a.ls_off = A;
+          sbu.rd = {raw.id, eps2.id, R_LA};
+          sbu.wr = {dout.id};
+          dx(pg, {{dzp0[0], &q[0]->layers[0], Sp}, {dzp0[1], &q[1]->layers[0], Sp}}, A, B, ACT_NONE, nullptr,
+             nullptr, nullptr, nullptr, nullptr, &sbu);
+        }
+      }
+      if (sac && !sac_bwd_fused()) {
         View da = dx(pg, {{dzp0[0], &q[0]->layers[0], Sp}, {dzp0[1], &q[1]->layers[0], Sp}}, A, B, ACT_NONE,
                      nullptr);
-        dout = buf(B, 2 * A);
         Op op{};
         op.kind = OP_SAC_ACTOR_BWD;
         SacActorArgs& a = op.sac;
@@ -3225,8 +3329,8 @@ struct Engine {
       for (auto& op : levels[l]) {
         G.desc += std::string(" ") + kname[op.kind];
         if (op.kind == OP_GEMM) {
-          static const char* kepi[] = {"st", "adam", "mse", "qhead", "nbdot", "act", "qdot"};
-          static_assert(sizeof(kepi) / sizeof(kepi[0]) == EPI_QDOT + 1, "every epilogue has a name");
+          static const char* kepi[] = {"st", "adam", "mse", "qhead", "nbdot", "act", "qdot", "sacbwd", "sacfwd"};
+          static_assert(sizeof(kepi) / sizeof(kepi[0]) == EPI_SACFWD + 1, "every epilogue has a name");
           const char* ep = op.gemm.mode == GEMM_DW && op.gemm.act == kDwNb ? "adam+nb"
                            : op.gemm.has_pre == 2                         ? "head+dx"
                                                                            : kepi[op.gemm.epi];

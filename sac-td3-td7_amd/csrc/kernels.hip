@@ -1123,6 +1123,81 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
               (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
       }
     }
+  } else if constexpr (EPI == EPI_SACFWD) {  // op_sac_actor for the tile's 16 rows (sac.py:132-152)
+    const CAS SacFwdArgs& s = g.sf;
+    float y[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] = acc[q] + pre_b;
+    if (jok) mat_st4(g.out, ib, j, make_float4(y[0], y[1], y[2], y[3]));  // raw (the backward reads it)
+    __syncthreads();  // (the split-K scratch is free)
+    float* rt = smem;                // [16][64] the tile's raw rows
+    float* lpt = smem + 1024;        // [16][32] log-density terms
+    float* crt = lpt + 512;          // [16][32] tanh corrections
+    if (active && lead) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rt[(ib - i0 + q) * 64 + (j - jt * 64)] = jok ? y[q] : 0.f;
+    }
+    __syncthreads();
+    const float c = (float)0.9189385332046727;  // log(sqrt(2*pi))
+    for (int it = tid; it < 16 * s.A; it += kThreads) {
+      const int r = it / s.A, jj = it - r * s.A, b = i0 + r;
+      if (b >= g.M) continue;
+      const bool pol = b < s.eps_row_split;
+      const float mu = rt[r * 64 + s.mean_off + jj];
+      const float ls = fminf(fmaxf(rt[r * 64 + s.ls_off + jj], s.min_log_std), s.max_log_std);
+      const float sd = expf(ls);
+      const float ej = pol ? mat_ld(s.eps2, b, jj) : mat_ld(s.eps, b - s.eps_row_split, jj);
+      const float u = mu + ej * sd;
+      const float a = tanhf(u);
+      const float var = sd * sd;
+      const float d = u - mu;
+      lpt[r * 32 + jj] = -(d * d) / (2.f * var) - logf(sd) - c;
+      crt[r * 32 + jj] = logf((1.f - a * a) + 1e-6f);
+      mat_st(s.act, b, jj, a);
+    }
+    __syncthreads();
+    if (tid < 16 && i0 + tid < g.M) {  // the row sums in op_sac_actor's order
+      float lp = 0.f, corr = 0.f;
+      for (int jj = 0; jj < s.A; ++jj) {
+        lp += lpt[tid * 32 + jj];
+        corr += crt[tid * 32 + jj];
+      }
+      GW(s.logpi)[i0 + tid] = lp - corr;
+    }
+  } else if constexpr (EPI == EPI_SACBWD) {  // sac.py:227-229 through rsample, tanh and log pi (op_sac_actor_bwd)
+    if (jok) {
+      const CAS SacBwdArgs& s = g.sb;
+      const float w = (s.alpha_lin ? sload(s.log_alpha) : expf(sload(s.log_alpha))) * s.inv_b;  // d obj / d logpi_b
+      const float4 mu4 = mat_ld4(s.raw, ib, s.mean_off + j), ls4 = mat_ld4(s.raw, ib, s.ls_off + j),
+                   e4 = mat_ld4(s.eps2, ib, j);
+      const float muv[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, lsv[4] = {ls4.x, ls4.y, ls4.z, ls4.w},
+                  ev[4] = {e4.x, e4.y, e4.z, e4.w};
+      float gm[4], gl[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float mu = muv[q], lsr = lsv[q], ej = ev[q];
+        const float ls = fminf(fmaxf(lsr, s.min_log_std), s.max_log_std);
+        const float sd = expf(ls);
+        const float u = mu + ej * sd;
+        const float a = tanhf(u);
+        const float var = sd * sd;
+        const float d = u - mu;
+        const float ga = acc[q] + (w / ((1.f - a * a) + 1e-6f)) * (2.f * a);
+        float gu = ga * (1.f - a * a);
+        gu += -(w / (2.f * var)) * (2.f * d);
+        float gmu = (w / (2.f * var)) * (2.f * d);
+        const float gvar = (w * (d * d)) / ((2.f * var) * (2.f * var)) * 2.f;
+        float gsd = gvar * (2.f * sd) - w / sd;
+        gmu += gu;
+        gsd += gu * ej;
+        float gls = gsd * sd;
+        if (!(lsr >= s.min_log_std && lsr <= s.max_log_std)) gls = 0.f;
+        gm[q] = gmu;
+        gl[q] = gls;
+      }
+      mat_st4(s.dout, ib, s.mean_off + j, make_float4(gm[0], gm[1], gm[2], gm[3]));
+      mat_st4(s.dout, ib, s.ls_off + j, make_float4(gl[0], gl[1], gl[2], gl[3]));
+    }
   } else if constexpr (EPI == EPI_QHEAD) {  // td7.py:268-275: Q = w3 . act(z) + b3, L = -mean(cat Q)
     float ls = 0.f;
     if (jok) {
@@ -1303,6 +1378,8 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_VP(GEMM_FWD, EPI_STORE, ACT_RELU, false)
     RLE_VP(GEMM_FWD, EPI_STORE, ACT_ELU, true)
     RLE_VP(GEMM_DX, EPI_STORE, ACT_RELU, false)
+    RLE_V(GEMM_DX, EPI_SACBWD, ACT_NONE, false)
+    RLE_V(GEMM_FWD, EPI_SACFWD, ACT_NONE, false)
     RLE_VH(GEMM_DX, EPI_STORE, ACT_ELU, false)
     RLE_VH(GEMM_DX, EPI_STORE, ACT_RELU, false)
     default: break;
@@ -2106,7 +2183,11 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
   // kind 0 with the count of ops from 11 on.  Lane j reads op 11 + j's first workgroup from
   // its descriptor header (one vector load); the op is the last one starting at or before
   // this workgroup (ops are in workgroup order), its kind and variant come from its header.
+#ifndef RLE_EXP_NO_WIDE  // (timing experiment: without the wide-launch lookup)
   if (kind == 0 && vid != 0) {
+#else
+  if (false) {
+#endif
     const int cnt = vid, lane = (int)(threadIdx.x & 63);
     int wbl = 0x7fffffff;
     if (lane < cnt) wbl = ((const Op*)ops_arg)[kLevelOps - 1 + lane].wg_begin;

@@ -91,6 +91,10 @@ enum Epi : int {
   EPI_ACT = 5,     // act graph (TD7 / TD3 actor's tanh layer): environment action, ActArgs
   EPI_QDOT = 6,    // EPI_STORE (forward) + per-tile row partials of sum_j act(z)_j w_j (w: qw, a
                    // critic's H -> 1 head row) into norm_out: the loss head's q without a row load
+  EPI_SACBWD = 7,  // DX of the SAC actor objective's action gradient da: the squashed-Gaussian
+                   // backward (as OP_SAC_ACTOR_BWD) per element in the epilogue -> d / d(mean | log_std)
+  EPI_SACFWD = 8,  // the SAC actor's raw head (tile = whole rows, tn 64 >= 2A): raw stored, then the
+                   // rsample, tanh action and log pi of the tile's rows (as OP_SAC_ACTOR)
 };
 
 // Environment action of an act graph (td7.py:141-156, td3.py:114-129, sac.py:132-152), written
@@ -127,13 +131,15 @@ struct AdamArgs {
   float* gsq_b;          // optional: per-tile sum of squared grads (bias), [tiles_m]
 };
 
-// Variant id of a GEMM op = pre * 256 + mode * 64 + epi * 8 + act * 2 + norm (pre: one A
+// Variant id of a GEMM op = pre * 512 + mode * 128 + epi * 8 + act * 2 + norm (pre: one A
 // segment is the actor's tanh output layer recomputed in the workgroup, PreArgs; act: the forward
 // activation for GEMM_FWD, the derivative mask for GEMM_DX, kDwNb or 0 for GEMM_DW; norm: some operand
 // segment carries a deferred AvgL1Norm).
 constexpr int gemm_vid(int mode, int epi, int act, int norm, int pre = 0) {
-  return pre * 256 + mode * 64 + epi * 8 + act * 2 + norm;
+  return pre * 512 + mode * 128 + epi * 8 + act * 2 + norm;
 }
+// (the level-launch entry keeps it in bits 20-30: bit 31 of entry 0 is the descriptor-prefetch flag)
+static_assert(gemm_vid(2, 2, 15, 3, 1) < 2048, "GEMM variant ids fit 11 bits");
 
 enum GemmMode : int {
   GEMM_FWD = 0,   // A contiguous (activations), B contiguous (W rows):  Y = X W^T
@@ -242,6 +248,25 @@ struct HeadArgs {                   // 4 rows per workgroup (1 per wave)
   int qp_ld, tp_ld;
 };
 
+// EPI_SACBWD operands (the policy rows of the actor's raw head and their rsample draws)
+struct SacBwdArgs {
+  Mat raw;                           // raw head output [2B][2A(p)]: mean | log_std (T image)
+  Mat eps2;                          // policy rsample noise [B][Ap] (T image)
+  Mat dout;                          // grad wrt the raw output [B][2A(p)]
+  const float* log_alpha;            // log alpha, or alpha itself (alpha_lin)
+  float inv_b, min_log_std, max_log_std;
+  int alpha_lin, mean_off, ls_off;
+};
+
+// EPI_SACFWD operands (sac.py:132-152 rsample of both row halves: policy rows < eps_row_split)
+struct SacFwdArgs {
+  Mat eps, eps2;                     // target / policy rsample noise (T images)
+  Mat act;                           // tanh action [2B][Ap]
+  float* logpi;                      // [2B]
+  float min_log_std, max_log_std;
+  int A, mean_off, ls_off, eps_row_split;
+};
+
 struct GemmArgs {
   GemmHot hot;           // (first: two s_load_dwordx16)
   int mode;              // GemmMode (operand layouts; every segment of an operand shares it)
@@ -279,6 +304,8 @@ struct GemmArgs {
     // tile-column-0 workgroups store what the standalone head stored (dz / dq of critic head_n;
     // head_n 0 also the priorities, loss partials and value bounds)
     HeadArgs hd;
+    SacBwdArgs sb;  // EPI_SACBWD (has_pre 0)
+    SacFwdArgs sf;  // EPI_SACFWD (has_pre 0)
   };
   int head_n;
   AdamArgs adam;
