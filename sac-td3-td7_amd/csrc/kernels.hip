@@ -2138,7 +2138,7 @@ __device__ __forceinline__ void op_foldbias(const CAS FoldBiasArgs& f) {
 // (-mllvm -amdgpu-kernarg-preload-count=14, Makefile): a workgroup knows its op without
 // a kernel-argument load; its first memory access is its op's descriptor.
 static_assert(kLevelOps == 12, "rle_level takes the op table as 12 scalar arguments");
-template <bool TRACE>
+template <bool TRACE, bool WIDE>
 #ifndef RLE_WAVES
 #define RLE_WAVES 4  // waves per SIMD the register allocation must allow (4 workgroups per CU)
 #endif
@@ -2183,11 +2183,8 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
   // kind 0 with the count of ops from 11 on.  Lane j reads op 11 + j's first workgroup from
   // its descriptor header (one vector load); the op is the last one starting at or before
   // this workgroup (ops are in workgroup order), its kind and variant come from its header.
-#ifndef RLE_EXP_NO_WIDE  // (timing experiment: without the wide-launch lookup)
-  if (kind == 0 && vid != 0) {
-#else
-  if (false) {
-#endif
+  // (its own kernel instance: the branch alone in the production instance measured -1.2%)
+  if (WIDE && kind == 0 && vid != 0) {
     const int cnt = vid, lane = (int)(threadIdx.x & 63);
     int wbl = 0x7fffffff;
     if (lane < cnt) wbl = ((const Op*)ops_arg)[kLevelOps - 1 + lane].wg_begin;
@@ -2533,7 +2530,7 @@ int trace_stride() { return kTraceStride; }
 int level_capacity() {
   int per_cu = 0, cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false>, kThreads, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false, false>, kThreads, 0) != hipSuccess)
     return 1024;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
   return per_cu * cus;
@@ -2543,7 +2540,7 @@ int level_capacity() {
 // AQL launch lists; traced launches are never recorded)
 std::vector<LevelLaunch>* g_level_rec = nullptr;
 // the production kernel's HSA symbol name (AQL dispatch)
-const char* level_kernel_symbol() { return "_ZN3rle9rle_levelILb0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"; }
+const char* level_kernel_symbol() { return "_ZN3rle9rle_levelILb0ELb0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"; }
 
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
                         unsigned long long* trace, const Op* next_ops, int next_nops) {
@@ -2579,7 +2576,7 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
       }
     }
     if (npf) la.entry[0] |= 0x80000000u;
-    if (g_level_rec && !trace) {
+    if (g_level_rec && !trace && !wide) {  // (direct dispatch runs the narrow instance only)
       LevelLaunch L{};
       std::memcpy(L.ka, la.entry, sizeof la.entry);
       std::memcpy(L.ka + 48, &la.ops, 8);
@@ -2592,8 +2589,10 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
 #define RLE_LEVEL_ARGS                                                                                         \
   la.entry[0], la.entry[1], la.entry[2], la.entry[3], la.entry[4], la.entry[5], la.entry[6], la.entry[7], \
       la.entry[8], la.entry[9], la.entry[10], la.entry[11], la.ops, la.trace, next, next_lines
-    if (trace) hipLaunchKernelGGL(rle_level<true>, dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
-    else hipLaunchKernelGGL(rle_level<false>, dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    if (wide && trace) hipLaunchKernelGGL((rle_level<true, true>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    else if (wide) hipLaunchKernelGGL((rle_level<false, true>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    else if (trace) hipLaunchKernelGGL((rle_level<true, false>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    else hipLaunchKernelGGL((rle_level<false, false>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
 #undef RLE_LEVEL_ARGS
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -18,12 +18,15 @@ sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd")]
 from rl import _engine as E  # noqa: E402
 from rl.nn.layout import init_agent  # noqa: E402
 
-S, A, H, B = 376, 17, 256, 256
-eng = E.Engine(E.make_config(E.RLE_TD7, S, A, H, B, use_lap=True))
-for net, params in init_agent("td7", S, A, H, 1).items():
+# RLE_TRACE_ALGO=td3 / sac: the secondary configs (TD3 HalfCheetah, SAC Humanoid; uniform replay)
+ALGO = os.environ.get("RLE_TRACE_ALGO", "td7")
+S, A, H, B = (17, 6, 256, 256) if ALGO == "td3" else (376, 17, 256, 256)
+LAP = ALGO == "td7"
+eng = E.Engine(E.make_config({"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[ALGO], S, A, H, B, use_lap=LAP))
+for net, params in init_agent(ALGO, S, A, H, 1).items():
     for k, v in params.items():
         eng.set_param(net, k, v)
-rep = E.Replay(1000000, S, A, True)
+rep = E.Replay(1000000, S, A, LAP)
 rep.fill_random(1000000, 1)
 eng.bind(rep)
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
