@@ -1005,12 +1005,29 @@ struct Prog {
   // Relative per-workgroup duration of an item (its longest op): a GEMM workgroup's
   // dependent MFMA chain grows with reduction length x tile width (4 waves share it); Adam
   // epilogues, the loss head and the sampler are long for their size (level traces).
+  // weight of the step-end op (RLE_TINY_W, A/B; 0 = no tiny-op moves)
+  static int tiny_weight() {
+    static const int w = [] {
+      const char* e = std::getenv("RLE_TINY_W");
+      return e ? std::atoi(e) : 30;  // (A/B 0 / 20 / 30: TD7 8021 / 8050 / 8054, SAC 12249 / 12235 / 12328)
+    }();
+    return w ? w : 8;
+  }
+  static bool tiny_moves() {
+    static const bool on = [] {
+      const char* e = std::getenv("RLE_TINY_W");
+      return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+  }
   static int item_weight(const Item& it) {
     int w = 0;
     for (const Op& op : it.ops) {
       int x = 8;
       if (op.kind == OP_GEMM) x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? 8 : 0);
       else if (op.kind == OP_HEAD || op.kind == OP_SAMPLE_GATHER) x = 60;
+      else if (op.kind == OP_STEP_END) x = tiny_weight();  // (one workgroup, ~4 KB of straight-line
+                                                           // code fetched at L2 latency: 7-8 us)
       w = std::max(w, x);
     }
     return w;
@@ -1065,6 +1082,12 @@ struct Prog {
         if (nops[l] + (int)it.ops.size() > max_ops || wt * wfac > wmax[l] || nwg[l] + wg > cap) continue;
         if (nwg[l] + wg >= nwg[cur]) continue;
         if (best < 0 || nwg[l] < nwg[best]) best = l;
+      }
+      // a one-workgroup op that is the longest of its level (the step end): into the first level
+      // of its window that has a longer op, so its time hides under that op's
+      if (best < 0 && tiny_moves() && wg <= 2 && wt >= wmax[cur]) {
+        for (int l = cur + 1; l <= hi && best < 0; ++l)
+          if (wmax[l] > wt && nops[l] + (int)it.ops.size() <= max_ops && nwg[l] + wg <= cap) best = l;
       }
       if (best < 0) continue;
       nops[cur] -= (int)it.ops.size();

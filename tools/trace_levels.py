@@ -91,6 +91,9 @@ for which in graphs:
                         if (tt[:, 4] > 0).all() and (tt[:, 6] > 0).all():  # pre-GEMM consumer phases
                             extra += (f" [pre issue {f(ph(1, 4))} segs {f(ph(4, 5))} finish {f(ph(5, 6))}"
                                       f" lds {f(ph(6, 2))}]")
+                    if tr.shape[1] == 16 and name == "end" and (tt[:, 8] > 0).all():  # op_step_end marks
+                        extra = (f" [loads {f(ph(0, 4))} sums {f(ph(4, 5))} sync {f(ph(5, 6))} reduce {f(ph(6, 7))}"
+                                 f" info {f(ph(7, 8))} tail {f(ph(8, 3))}]")
                     print(f"        {name.replace(' ', '_'):32s} start {f((tt[:, 0] - t0) * 10 / 1000)} pro {f(ph(0, 1))}"
                           f" loop {f(ph(1, 2))} epi {f(ph(2, 3))}{extra}")
         if tr.shape[1] == 16 and line.rstrip().endswith("head/64"):  # fine build: loss head phases
