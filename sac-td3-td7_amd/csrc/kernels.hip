@@ -1967,7 +1967,6 @@ __device__ __forceinline__ void adam_scalars(long long t, float lr, GAS float* s
 // per-sum partials in LDS, then wave w reduces sums w, w+4, ... (fixed order).
 __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* smem, unsigned long long* tr) {
   constexpr int kSums = kInfoMax + 1 + 9;  // info sums, logpi, grad-norm tensors
-  float* th = smem;                        // [kSums][kThreads]
   float* res = smem + kSums * kThreads;    // [kSums]
   float* vals = res + kSums;               // [kInfoMax]
   const float nanv = __int_as_float(0x7FC00000);
@@ -2006,30 +2005,34 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
       }
     }
   };
-#ifdef RLE_EXP_END_ROLL  // experiment: rolled loops (code fetched once per dispatch by one workgroup)
-#pragma unroll 1
-#endif
-  for (int j = 0; j < kSums; ++j) {
+  // each wave sums every 4th list entry: lane l adds the entry's elements l + 64 k (k = 0..3,
+  // + 256 m) in the order thread 64 k + l of the former one-pass layout did, then the 4 quarters
+  // and the wave as that layout's LDS reduction did -- the same float operations, with the 4
+  // quarters' first loads in flight together and 4 lists at once (one list at a time paid one
+  // dependent round trip per list: 3-4 us of the op's ~7, the longest op of its level)
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int j = wave; j < kSums; j += 4) {
     const float* p;
     int n, stride;
     sum_src(j, p, n, stride);
-    float v = 0.f;
-    for (int i = tid; i < n; i += kThreads) v += G(p)[(size_t)i * stride];
-    th[j * kThreads + tid] = v;
-  }
-  FINE_MARK(1);
-  __syncthreads();
-  FINE_MARK(2);
-  const int lane = tid & 63, wave = tid >> 6;
-#ifdef RLE_EXP_END_ROLL
-#pragma unroll 1
-#endif
-  for (int j = wave; j < kSums; j += 4) {
-    const float* r = th + j * kThreads;
-    float v = (r[lane] + r[lane + 64]) + (r[lane + 128] + r[lane + 192]);
+    float x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = lane + 64 * k;
+      x[k] = i < n ? G(p)[(size_t)i * stride] : 0.f;
+    }
+    float q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v = 0.f + x[k];
+      for (int i = lane + 64 * k + kThreads; i < n; i += kThreads) v += G(p)[(size_t)i * stride];
+      q[k] = v;
+    }
+    float v = (q[0] + q[1]) + (q[2] + q[3]);
     v = wave_sum(v);
     if (lane == 0) res[j] = v;
   }
+  FINE_MARK(1);
   __syncthreads();
   FINE_MARK(3);
   if (!w0) return;
