@@ -925,6 +925,18 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   if constexpr (EPI == EPI_NBDOT) {
     if (jok) nbxv = mat_ld4(g.nbx, ib, j);
   }
+  // EPI_SACFWD: the rsample noise of this thread's (row, column) items of the epilogue (16 A <= 2
+  // kThreads of them), fetched before the main loop
+  float sfe[2] = {0.f, 0.f};
+  if constexpr (EPI == EPI_SACFWD) {
+    const CAS SacFwdArgs& s = g.sf;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int it2 = tid + k * kThreads, r = it2 / s.A, jj = it2 - r * s.A, b = i0 + r;
+      if (it2 < 16 * s.A && b < g.M)
+        sfe[k] = b < s.eps_row_split ? mat_ld(s.eps2, b, jj) : mat_ld(s.eps, b - s.eps_row_split, jj);
+    }
+  }
   if constexpr (EPI != EPI_ADAM) {
     if (jok && biasp) pre_b = G(biasp)[j];
     if constexpr (MODE == GEMM_DX && ACT != ACT_NONE) {
@@ -1142,14 +1154,14 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     }
     __syncthreads();
     const float c = (float)0.9189385332046727;  // log(sqrt(2*pi))
-    for (int it = tid; it < 16 * s.A; it += kThreads) {
-      const int r = it / s.A, jj = it - r * s.A, b = i0 + r;
-      if (b >= g.M) continue;
-      const bool pol = b < s.eps_row_split;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int it = tid + k * kThreads, r = it / s.A, jj = it - r * s.A, b = i0 + r;
+      if (it >= 16 * s.A || b >= g.M) continue;
       const float mu = rt[r * 64 + s.mean_off + jj];
       const float ls = fminf(fmaxf(rt[r * 64 + s.ls_off + jj], s.min_log_std), s.max_log_std);
       const float sd = expf(ls);
-      const float ej = pol ? mat_ld(s.eps2, b, jj) : mat_ld(s.eps, b - s.eps_row_split, jj);
+      const float ej = sfe[k];
       const float u = mu + ej * sd;
       const float a = tanhf(u);
       const float var = sd * sd;
