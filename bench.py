@@ -356,14 +356,11 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
     }
 
 
-def multi_seed(args, K, world, rank, local, dist, algo_id, lap, chunk=25):
+def multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, cuda_sync, chunk=25):
     """K independent seeds per GPU: K engines, each with its own replay,
-    weights, Philox stream and HIP stream, stepped round-robin in chunks without host syncs.
+    weights, Philox stream and HIP stream, stepped round-robin in chunks without host syncs
+    (--packed: one packed level schedule, rle_group).
     value = steps of all seeds on all ranks / max-rank wall time."""
-    import torch
-
-    from rl import _engine as E
-    from rl.nn.layout import init_agent
 
     s_dim, a_dim, _ = TASKS[args.env]
     engs = []
@@ -396,11 +393,11 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, chunk=25):
     run(args.warmup)
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(local)
+    cuda_sync(local)
     st0 = group.stats() if group is not None else None
     t0 = time.perf_counter()
     run(args.steps)
-    torch.cuda.synchronize(local)
+    cuda_sync(local)
     wall = max_over_ranks([time.perf_counter() - t0], dist)[0]
     packed = None
     if group is not None:
@@ -554,7 +551,7 @@ def main():
     algo_id = {"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[args.algo]
     K = max(1, args.seeds_per_gpu)
     if K > 1:
-        return multi_seed(args, K, world, rank, local, dist, algo_id, lap)
+        return multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, cuda_sync)
     cfg = E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=111 * (rank + 1), device=local)
     eng = E.Engine(cfg)
     for net, params in init_agent(args.algo, s_dim, a_dim, H, 123 + rank).items():
