@@ -253,6 +253,20 @@ __device__ __forceinline__ float4 mat_ld4(const CAS Mat& m, int r, int c) {
   return ld4g(G(m.t) + tidx(m.rbs, r, c));
 }
 __device__ __forceinline__ void mat_st4(const CAS Mat& m, int r, int c, float4 v) {
+#ifdef RLE_EXP_ACT_NT  // experiment: activation / gradient tile stores as streaming stores
+  if (m.t) {
+    f32x4 w;
+    w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+    __builtin_nontemporal_store(w, (GAS f32x4*)(GW(m.t) + tidx(m.rbs, r, c)));
+  }
+  if (m.n) {
+    GAS float* q = GW(m.n) + nidx(m.cbn, r, c);
+    __builtin_nontemporal_store(v.x, q);
+    __builtin_nontemporal_store(v.y, q + 4);
+    __builtin_nontemporal_store(v.z, q + 8);
+    __builtin_nontemporal_store(v.w, q + 12);
+  }
+#else
   if (m.t) st4g(GW(m.t) + tidx(m.rbs, r, c), v);
   if (m.n) {
     GAS float* q = GW(m.n) + nidx(m.cbn, r, c);  // rows r..r+3 are 4 floats apart in the N image
@@ -261,6 +275,7 @@ __device__ __forceinline__ void mat_st4(const CAS Mat& m, int r, int c, float4 v
     q[8] = v.z;
     q[12] = v.w;
   }
+#endif
 }
 
 // Phase timestamps of one workgroup (wave 0, lane 0): [0] entry, [1] main loop
@@ -369,25 +384,32 @@ constexpr int kRing = RLE_RING;  // chunks in flight per wave
 
 // The ring in two halves, so that work with its own memory round trip (AvgL1Norm scalars
 // and tables) can run between issuing the first kRing chunks and consuming them.
-__device__ __forceinline__ void ring_issue(float4 (&a)[kRing], float4 (&b)[kRing], __amdgpu_buffer_rsrc_t ra, int va,
+// (RG: ring depth; the weight-gradient variants may run a deeper one, RLE_DW_RING.  An even RG
+// keeps chunk k on accumulator k & 1 in order, so the sums do not depend on it.)
+#ifndef RLE_DW_RING
+#define RLE_DW_RING 4
+#endif
+constexpr int kRingDW = RLE_DW_RING;
+template <int RG = kRing>
+__device__ __forceinline__ void ring_issue(float4 (&a)[RG], float4 (&b)[RG], __amdgpu_buffer_rsrc_t ra, int va,
                                            __amdgpu_buffer_rsrc_t rb, int vb, int n, bool bias_ones) {
 #pragma unroll
-  for (int r = 0; r < kRing; ++r) {
+  for (int r = 0; r < RG; ++r) {
     if (r >= n) break;  // (uniform: no load past the last chunk)
     a[r] = bload(ra, va + r * 1024);
     b[r] = bias_ones ? make_float4(1.f, 1.f, 1.f, 1.f) : bload(rb, vb + r * 1024);
   }
 }
-template <int SA, int SB>
-__device__ __forceinline__ f32x4 ring_run(float4 (&a)[kRing], float4 (&b)[kRing], __amdgpu_buffer_rsrc_t ra, int va,
+template <int SA, int SB, int RG = kRing>
+__device__ __forceinline__ f32x4 ring_run(float4 (&a)[RG], float4 (&b)[RG], __amdgpu_buffer_rsrc_t ra, int va,
                                           __amdgpu_buffer_rsrc_t rb, int vb, int n, f32x4 acc, float inva,
                                           const float* taba, const float* tabb, bool bias_ones) {
   const int rl = ((threadIdx.x & 63) >> 4) << 2;
   f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-  for (int c = 0; c < n; c += kRing) {
+  for (int c = 0; c < n; c += RG) {
 #pragma unroll
-    for (int r = 0; r < kRing; ++r) {
+    for (int r = 0; r < RG; ++r) {
       // (uniform branches: no MFMA of a chunk past the last and no load past it -- an
       // out-of-range load still occupies the memory pipeline and the in-order load counter:
       // +2.9% steps/s over loading zeros)
@@ -399,7 +421,7 @@ __device__ __forceinline__ f32x4 ring_run(float4 (&a)[kRing], float4 (&b)[kRing]
       if constexpr (SB == 2) y = mul4(y, *(const float4*)(tabb + min(c + r, n - 1) * 16 + rl));
       if (r & 1) acc1 = mfma4(x, y, acc1);
       else acc = mfma4(x, y, acc);
-      const int nx = c + r + kRing;
+      const int nx = c + r + RG;
       if (nx >= n) continue;
       a[r] = bload(ra, va + nx * 1024);
       if (!bias_ones) b[r] = bload(rb, vb + nx * 1024);
@@ -426,16 +448,17 @@ __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f
 // x read from (rx, vx) in the same T-image layout as g and inv / gm from LDS tables
 // (ti / tg: float offset of chunk k0's first row).  Same ring as chunk_loop.
 // (x ring issued by the caller together with ring_issue for a / b, ahead of the tables)
-__device__ __forceinline__ f32x4 ring_run_nb(float4 (&a)[kRing], float4 (&x)[kRing], float4 (&b)[kRing],
+template <int RG = kRing>
+__device__ __forceinline__ f32x4 ring_run_nb(float4 (&a)[RG], float4 (&x)[RG], float4 (&b)[RG],
                                              __amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rx, int vx,
                                              __amdgpu_buffer_rsrc_t rb, int vb, int n, f32x4 acc, const float* ti,
                                              const float* tg, bool bias_ones) {
   const int rl = ((threadIdx.x & 63) >> 4) << 2;
   f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-  for (int c = 0; c < n; c += kRing) {
+  for (int c = 0; c < n; c += RG) {
 #pragma unroll
-    for (int r = 0; r < kRing; ++r) {
+    for (int r = 0; r < RG; ++r) {
       if (c + r >= n) break;  // (as ring_run)
       const int k = c + r;
       const float4 iv = *(const float4*)(ti + k * 16 + rl), gv = *(const float4*)(tg + k * 16 + rl);
@@ -443,7 +466,7 @@ __device__ __forceinline__ f32x4 ring_run_nb(float4 (&a)[kRing], float4 (&x)[kRi
                                    a[r].z * iv.z + sgnf(x[r].z) * gv.z, a[r].w * iv.w + sgnf(x[r].w) * gv.w);
       if (r & 1) acc1 = mfma4(y, b[r], acc1);
       else acc = mfma4(y, b[r], acc);
-      const int nx = c + r + kRing;
+      const int nx = c + r + RG;
       if (nx >= n) continue;
       a[r] = bload(ra, va + nx * 1024);
       x[r] = bload(rx, vx + nx * 1024);
@@ -947,6 +970,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     early_step = sload(g.adam.step);
     early_bc2s = sload(g.adam.bc2s);
 #endif
+#ifndef RLE_EXP_ADAM_LATE  // (experiment: p / m / v loaded after the main loop, registers for a deeper ring)
     if (jok) {
       const CAS AdamArgs& ad = g.adam;
       if (bias_tile) {
@@ -960,6 +984,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         vv = ld4g(G(ad.w.t) + wt + ad.vo);
       }
     }
+#endif
   }
   trace_mark(tr, 1);
 
@@ -1048,11 +1073,12 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
 #else
     const int nrun = run ? c1 - c0 : 0;
 #endif
-    float4 ra[kRing], rb[kRing], rx[kRing];
-    ring_issue(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, bias_tile);
+    constexpr int RGD = ACT == kDwNb ? kRing : kRingDW;  // (the kDwNb ring carries a third operand)
+    float4 ra[RGD], rb[RGD], rx[RGD];
+    ring_issue<RGD>(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, bias_tile);
     if constexpr (ACT == kDwNb) {
 #pragma unroll
-      for (int r = 0; r < kRing; ++r)
+      for (int r = 0; r < RGD; ++r)
         if (r < nrun) rx[r] = bload(rsrc(g.nbx.t), vx + r * 1024);
     }
     const float* tb = nullptr;
@@ -1077,12 +1103,12 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     }
     if (run) {
       if constexpr (ACT == kDwNb) {
-        acc = ring_run_nb(ra, rx, rb, rsrc(a0p), va, rsrc(g.nbx.t), vx, rsrc(sb.p), vb, nrun, acc, tabs + c0 * 16,
-                          tabs + tgo + c0 * 16, bias_tile);
+        acc = ring_run_nb<RGD>(ra, rx, rb, rsrc(a0p), va, rsrc(g.nbx.t), vx, rsrc(sb.p), vb, nrun, acc,
+                               tabs + c0 * 16, tabs + tgo + c0 * 16, bias_tile);
       } else if (NORM && tb && !bias_tile)  // the bias column's B is ones: never scaled
-        acc = ring_run<0, 2>(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, acc, 1.f, nullptr, tb, bias_tile);
+        acc = ring_run<0, 2, RGD>(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, acc, 1.f, nullptr, tb, bias_tile);
       else
-        acc = ring_run<0, 0>(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, acc, 1.f, nullptr, nullptr, bias_tile);
+        acc = ring_run<0, 0, RGD>(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, acc, 1.f, nullptr, nullptr, bias_tile);
     }
   }
   trace_mark(tr, 2);
@@ -1292,6 +1318,20 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   } else {  // EPI_ADAM (torch.optim.Adam single-tensor law, see oracle/agents.py)
     const CAS AdamArgs& ad = g.adam;
     float gg = 0.f;
+#ifdef RLE_EXP_ADAM_LATE
+    if (jok) {
+      if (bias_tile) {
+        pp = ld4g(G(ad.b) + ib);
+        mm = ld4g(G(ad.b) + ib + ad.mo);
+        vv = ld4g(G(ad.b) + ib + ad.vo);
+      } else {
+        wt = tidx(ad.w.rbs, ib, j);
+        pp = ld4g(G(ad.w.t) + wt);
+        mm = ld4g(G(ad.w.t) + wt + ad.mo);
+        vv = ld4g(G(ad.w.t) + wt + ad.vo);
+      }
+    }
+#endif
     if (jok) {
 #ifdef RLE_EXP_EARLY_ADAM
       const float step_size = early_step, bc2s = early_bc2s;

@@ -91,6 +91,9 @@ for which in graphs:
                         if (tt[:, 4] > 0).all() and (tt[:, 6] > 0).all():  # pre-GEMM consumer phases
                             extra += (f" [pre issue {f(ph(1, 4))} segs {f(ph(4, 5))} finish {f(ph(5, 6))}"
                                       f" lds {f(ph(6, 2))}]")
+                    if tr.shape[1] == 16 and name == "sgather" and (tt[:, 10] > 0).all():  # sampler marks
+                        extra = (f" [ctrl {f(ph(0, 4))} sums+u {f(ph(4, 5))} blocks {f(ph(5, 6))} sub {f(ph(6, 7))}"
+                                 f" elems {f(ph(7, 2))} gather {f(ph(2, 10))} tail {f(ph(10, 3))}]")
                     if tr.shape[1] == 16 and name == "end" and (tt[:, 8] > 0).all():  # op_step_end marks
                         extra = (f" [loads {f(ph(0, 4))} sums {f(ph(4, 5))} sync {f(ph(5, 6))} reduce {f(ph(6, 7))}"
                                  f" info {f(ph(7, 8))} tail {f(ph(8, 3))}]")
