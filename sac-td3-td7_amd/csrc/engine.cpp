@@ -795,21 +795,24 @@ static void op_accesses(const Op& op, std::vector<Access>& v) {
       }
       break;
     }
-    case OP_STEP_END: {
+    case OP_STEP_END: {  // (mode 1: counters + temperature; mode 2: the info row; 0: both)
       const StepEndArgs& a = op.end;
-      for (int k = 0; k < a.ninfo; ++k)
-        if (a.part[k]) acc_bytes(v, a.part[k], (long long)a.npart[k] * a.stride[k] * 4, 0, "info part");
-      if (a.logpi_part) acc_bytes(v, a.logpi_part, (long long)a.nlogpi * 16, 0, "logpi part");
-      if (a.gsq && a.ngsq_t > 0) acc_bytes(v, a.gsq, (long long)a.gsq_off[a.ngsq_t] * 4, 0, "gsq");
-      acc_bytes(v, a.counters, 16 * 8, 1, "counters");
-      acc_bytes(v, a.info_slot, 4, 1, "info slot");
-      acc_whole(v, a.info, 1, "info ring");
-      if (a.log_alpha) acc_bytes(v, a.log_alpha, 4, a.la_lr > 0.f, "log_alpha");
-      if (a.la_lr > 0.f) {
+      const bool info = a.mode != 1, ctr = a.mode != 2, scr = a.mode == 2 && a.sac_scratch;
+      if (info)
+        for (int k = 0; k < a.ninfo; ++k)
+          if (a.part[k]) acc_bytes(v, a.part[k], (long long)a.npart[k] * a.stride[k] * 4, 0, "info part");
+      if (a.logpi_part && !scr) acc_bytes(v, a.logpi_part, (long long)a.nlogpi * 16, 0, "logpi part");
+      if (info && a.gsq && a.ngsq_t > 0) acc_bytes(v, a.gsq, (long long)a.gsq_off[a.ngsq_t] * 4, 0, "gsq");
+      if (ctr) acc_bytes(v, a.counters, 16 * 8, 1, "counters");
+      if (info) acc_bytes(v, a.info_slot, 4, 1, "info slot");
+      if (info) acc_whole(v, a.info, 1, "info ring");
+      if (a.log_alpha && !scr) acc_bytes(v, a.log_alpha, 4, ctr && a.la_lr > 0.f, "log_alpha");
+      if (ctr && a.la_lr > 0.f) {
         acc_bytes(v, a.la_m, 4, 1, "la_m");
         acc_bytes(v, a.la_v, 4, 1, "la_v");
         acc_bytes(v, a.la_t, 8, 1, "la_t");
       }
+      if (a.sac_scratch) acc_bytes(v, a.sac_scratch, 8, a.mode == 1, "sac scratch");
       break;
     }
     case OP_POLYAK:
@@ -1026,7 +1029,7 @@ struct Prog {
       int x = 8;
       if (op.kind == OP_GEMM) x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? 8 : 0);
       else if (op.kind == OP_HEAD || op.kind == OP_SAMPLE_GATHER) x = 60;
-      else if (op.kind == OP_STEP_END) x = tiny_weight();  // (one workgroup, ~4 KB of straight-line
+      else if (op.kind == OP_STEP_END && op.end.mode != 1) x = tiny_weight();  // (one workgroup, ~4 KB of straight-line
                                                            // code fetched at L2 latency: 7-8 us)
       w = std::max(w, x);
     }
@@ -2391,14 +2394,49 @@ struct Engine {
 
   // STEP_END writes the info row and bumps the step counters; every reader of a
   // counter (Adam t, RNG step, tape position) is therefore scheduled before it.
+  // Split in two (RLE_END_SPLIT=0: one op): the counters (+ the SAC temperature update), which
+  // the next step reads, at the step's end; the info row, which only the host reads, after it,
+  // free to sit under a longer op (the rebalance pass's one-workgroup rule).
+  float* sac_scr = nullptr;
+  int sac_scr_id = -1;
+  static bool end_split() {
+    static const bool on = [] {
+      const char* e = std::getenv("RLE_END_SPLIT");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   void add_step_end(Prog& pg, Op op, std::vector<int> rd, const std::vector<int>& counters) {
     StepEndArgs& a = op.end;
     a.cmask = 0;
     for (int c : counters) a.cmask |= 1 << c;
+    const std::vector<int> rd_info = rd;  // (the info op does not touch the counters)
     rd.push_back(R_CNT);
-    std::vector<int> wr{R_INFO, R_CNT};
-    if (a.log_alpha) wr.push_back(R_LA);
-    pg.add(op, rd, wr);
+    if (!end_split()) {
+      std::vector<int> wr{R_INFO, R_CNT};
+      if (a.log_alpha) wr.push_back(R_LA);
+      pg.add(op, rd, wr);
+      return;
+    }
+    const bool sac_tmp = a.log_alpha && a.la_lr > 0.f;
+    if (sac_tmp && !sac_scr) {
+      sac_scr = mem.make<float>(4);
+      sac_scr_id = next_id++;
+    }
+    Op c = op, i = op;
+    c.end.mode = 1;
+    c.end.sac_scratch = sac_tmp ? sac_scr : nullptr;
+    std::vector<int> cw{R_CNT};
+    if (a.log_alpha) cw.push_back(R_LA);
+    if (sac_tmp) cw.push_back(sac_scr_id);
+    pg.add(c, rd, cw);
+    i.end.mode = 2;
+    i.end.cmask = 0;
+    i.end.sac_scratch = sac_tmp ? sac_scr : nullptr;
+    std::vector<int> ir = rd_info;
+    if (sac_tmp) ir.push_back(sac_scr_id);
+    else if (a.log_alpha) ir.push_back(R_LA);  // (fixed temperature: read, never written)
+    pg.add(i, ir, {R_INFO});
   }
 
   // TD7 (td7.py:287-332)

@@ -2025,12 +2025,15 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
   const int tid = threadIdx.x;
   // tail operands loaded up front (independent of the sums: one round trip overall)
   const bool w0 = tid < 64;
-  const long long cnt = (w0 && tid < 16) ? G(a.counters)[tid] : 0;
-  const int slot0 = (w0 && a.info_slot) ? G(a.info_slot)[0] : 0;
-  const bool sac_tmp = a.log_alpha && a.la_lr > 0.f;
-  const float la = a.log_alpha ? G(a.log_alpha)[0] : 0.f;
+  const long long cnt = (w0 && tid < 16 && a.mode != 2) ? G(a.counters)[tid] : 0;
+  const int slot0 = (w0 && a.info_slot && a.mode != 1) ? G(a.info_slot)[0] : 0;
+  const int mode = a.mode;
+  const bool scr = mode == 2 && a.sac_scratch;  // (alpha and the logpi sum from the counters op)
+  const bool sac_tmp = a.log_alpha && a.la_lr > 0.f && mode != 2;
+  const float la = a.log_alpha && !scr ? G(a.log_alpha)[0] : 0.f;
   const float la_m = sac_tmp ? G(a.la_m)[0] : 0.f, la_v = sac_tmp ? G(a.la_v)[0] : 0.f;
   const long long la_t = sac_tmp ? G(a.la_t)[0] : 0;
+  const float scr_alpha = scr ? G(a.sac_scratch)[0] : 0.f, scr_slp = scr ? G(a.sac_scratch)[1] : 0.f;
   FINE_MARK(0);
   // sum list: j < ninfo -> info k (if summed); kInfoMax -> logpi; kInfoMax+1+q -> gsq tensor q
   auto sum_src = [&](int j, const float*& p, int& n, int& stride) {
@@ -2064,6 +2067,8 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
   // dependent round trip per list: 3-4 us of the op's ~7, the longest op of its level)
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   for (int j = wave; j < kSums; j += 4) {
+    // (mode 1 sums only the logpi list; mode 2 takes it from the scratch when there is one)
+    if ((mode == 1 && j != kInfoMax) || (scr && j == kInfoMax)) continue;
     const float* p;
     int n, stride;
     sum_src(j, p, n, stride);
@@ -2090,22 +2095,29 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
   if (!w0) return;
   // wave 0, every lane (uniform values from LDS); lane-parallel stores
   if (tid < 16 && (a.cmask & (1 << tid))) GW(a.counters)[tid] = cnt + 1;
-  const float slp = res[kInfoMax];
-  for (int k = 0; k < a.ninfo; ++k) {
-    float v = res[k];
-    if (a.kind[k] == INFO_GNORM) {
-      // per-tensor sum of squares -> sqrt -> sum (rl/nn/utils.py:13-19)
-      v = 0.f;
-      for (int q = 0; q < a.ngsq_t; ++q) v += sqrtf(res[kInfoMax + 1 + q]);
+  const float slp = scr ? scr_slp : res[kInfoMax];
+  const float alpha = scr ? scr_alpha : expf(la);
+  if (mode == 1) {
+    if (a.sac_scratch && tid == 0) {  // (for the info op)
+      GW(a.sac_scratch)[0] = alpha;
+      GW(a.sac_scratch)[1] = slp;
     }
-    vals[k] = v;
+  } else {
+    for (int k = 0; k < a.ninfo; ++k) {
+      float v = res[k];
+      if (a.kind[k] == INFO_GNORM) {
+        // per-tensor sum of squares -> sqrt -> sum (rl/nn/utils.py:13-19)
+        v = 0.f;
+        for (int q = 0; q < a.ngsq_t; ++q) v += sqrtf(res[kInfoMax + 1 + q]);
+      }
+      vals[k] = v;
+    }
   }
-  const float alpha = expf(la);
   // mean_b(-lp_b - target_entropy); d/dla mean(exp(la) * c) = exp(la) * mean(c)
   const float gmean = (-slp) * a.inv_b - a.target_entropy;
   const float tmp_obj = alpha * gmean;
   float mine = 0.f;  // lane k < ninfo: info value k
-  for (int k = 0; k < a.ninfo; ++k) {
+  for (int k = 0; k < (mode == 1 ? 0 : a.ninfo); ++k) {
     float v = vals[k];
     switch (a.kind[k]) {
       case INFO_SUM: v *= a.scale[k]; break;
@@ -2132,7 +2144,7 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
     GW(a.log_alpha)[0] = la + (-bc.x * m) / denom;
     GW(a.la_t)[0] = la_t + 1;
   }
-  if (a.info_slot) {
+  if (a.info_slot && mode != 1) {
     const int slot = slot0 >= a.info_cap ? a.info_cap - 1 : slot0;
     if (tid < a.ninfo) GW(a.info)[(size_t)slot * kInfoMax + tid] = mine;
     if (tid == 0) GW(a.info_slot)[0] = slot + 1;

@@ -388,6 +388,12 @@ struct StepEndArgs {
   float* adam_step; float* adam_bc2s; float adam_lr[4];  // next-step Adam scalars of counters 0..2
   const float* logpi_part; int nlogpi; float inv_b;
   const float* gsq; int gsq_off[9]; int ngsq_t;      // TD3 grad norm: tensor t = tiles [off[t], off[t+1])
+  // 0: the whole step end; 1: counters (+ the SAC temperature update, which needs the logpi sum)
+  // -- what the next step depends on; 2: the info row -- what only the host reads, scheduled
+  // wherever it is not the longest op.  sac_scratch: {alpha before the update, logpi sum},
+  // written by mode 1 for mode 2 (autotuned SAC temperature)
+  int mode;
+  float* sac_scratch;
 };
 
 enum InfoKind : int {
