@@ -1016,6 +1016,20 @@ struct Prog {
     }();
     return w ? w : 8;
   }
+  static int uniform_weight() {  // RLE_UNI_W, A/B (60: as the LAP sampler)
+    static const int w = [] {
+      const char* e = std::getenv("RLE_UNI_W");
+      return e ? std::atoi(e) : 60;  // (12 with RLE_TINY_WG=64: SAC +-0, TD3 -0.5%)
+    }();
+    return w;
+  }
+  static int tiny_wg() {  // RLE_TINY_WG, A/B: the workgroup bound of the rule below
+    static const int w = [] {
+      const char* e = std::getenv("RLE_TINY_WG");
+      return e ? std::atoi(e) : 2;
+    }();
+    return w;
+  }
   static bool tiny_moves() {
     static const bool on = [] {
       const char* e = std::getenv("RLE_TINY_W");
@@ -1028,7 +1042,9 @@ struct Prog {
     for (const Op& op : it.ops) {
       int x = 8;
       if (op.kind == OP_GEMM) x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? 8 : 0);
-      else if (op.kind == OP_HEAD || op.kind == OP_SAMPLE_GATHER) x = 60;
+      else if (op.kind == OP_HEAD) x = 60;
+      else if (op.kind == OP_SAMPLE_GATHER) x = op.sample.lap ? 60 : uniform_weight();  // (uniform: a
+                                                                                         // ~6 us gather)
       else if (op.kind == OP_STEP_END && op.end.mode != 1) x = tiny_weight();  // (one workgroup, ~4 KB of straight-line
                                                            // code fetched at L2 latency: 7-8 us)
       w = std::max(w, x);
@@ -1086,9 +1102,9 @@ struct Prog {
         if (nwg[l] + wg >= nwg[cur]) continue;
         if (best < 0 || nwg[l] < nwg[best]) best = l;
       }
-      // a one-workgroup op that is the longest of its level (the step end): into the first level
-      // of its window that has a longer op, so its time hides under that op's
-      if (best < 0 && tiny_moves() && wg <= 2 && wt >= wmax[cur]) {
+      // a one-workgroup op (the step end) that is the longest of its level: into the first level
+      // of its window that has a longer op, so its time hides there
+      if (best < 0 && tiny_moves() && wg <= tiny_wg() && wt >= wmax[cur]) {
         for (int l = cur + 1; l <= hi && best < 0; ++l)
           if (wmax[l] > wt && nops[l] + (int)it.ops.size() <= max_ops && nwg[l] + wg <= cap) best = l;
       }
@@ -3501,7 +3517,14 @@ struct Engine {
         if (op.kind == OP_GEMM) at(op.seq) = std::max(op.gemm.tn, tmin ? std::atoi(tmin) : 16);
     int cap = std::max(256, level_capacity());
     if (const char* e = std::getenv("RLE_LEVEL_CAP")) cap = std::max(1, std::atoi(e));  // tuning experiments
+    // elementwise ops (Polyak, copies) are short: they free their slots long before the level's
+    // GEMMs do, so they count at 1 / flat_div of their workgroups (RLE_FLAT_DIV, A/B; 1 = full)
+    static const int flat_div = [] {
+      const char* e = std::getenv("RLE_FLAT_DIV");
+      return e ? std::max(1, std::atoi(e)) : 4;  // (A/B 1 / 4 / 1000: SAC 12675 / 13135 / 13122)
+    }();
     auto wg_of = [&](const Op& op) {
+      if (op.kind == OP_POLYAK || op.kind == OP_COPY) return op.wg_count / flat_div;
       if (op.kind != OP_GEMM) return op.wg_count;
       const GemmArgs& g = op.gemm;
       return g.tiles_m * (cdiv(g.N, at(op.seq)) + (g.epi == EPI_ADAM ? 1 : 0));
