@@ -551,6 +551,11 @@ def main():
     algo_id = {"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[args.algo]
     K = max(1, args.seeds_per_gpu)
     if K > 1:
+        # K seeds on streams: the tile planner sizes each seed's levels for 512 resident workgroups
+        # (half the device) so two seeds' levels co-reside (A/B, 3 seeds: 13.1k default, 14.1k at 512,
+        # 13.9k at 384; profiles/r03_ab.txt "multiseed_cap").  RLE_LEVEL_CAP overrides.
+        if not args.packed:
+            os.environ.setdefault("RLE_LEVEL_CAP", "512")
         return multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, cuda_sync)
     cfg = E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=111 * (rank + 1), device=local)
     eng = E.Engine(cfg)

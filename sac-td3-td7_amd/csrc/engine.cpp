@@ -1055,7 +1055,8 @@ struct Prog {
   // successor at least two levels later) to the lightest level of its window where it is
   // not the longest op, so wide ASAP levels (contended CUs) shed work into thin levels of
   // the critical chain.  Dependencies are the RAW / WAW / WAR edges of the ASAP pass.
-  void rebalance(int maxl, std::vector<int>& nops, std::vector<int>& nwg, int wg_cap) {
+  // RAW / WAW / WAR successors of every item (program order)
+  std::vector<std::vector<int>> successors() const {
     const int n = (int)items.size();
     std::vector<std::vector<int>> succ(n);
     std::map<int, int> lastw;
@@ -1080,6 +1081,23 @@ struct Prog {
       for (int r : it.rd)
         if (r >= 0) readers[r].push_back(i);
     }
+    return succ;
+  }
+  // (describe, RLE_DESC_CRIT=1) items on a longest dependency chain of the ASAP placement: their
+  // level + the longest chain after them = the last level (every dependence edge is one level)
+  std::vector<char> crit;
+  void mark_critical(int maxl) {
+    const int n = (int)items.size();
+    const auto succ = successors();
+    std::vector<int> tail(n, 0);
+    for (int i = n - 1; i >= 0; --i)
+      for (int s : succ[i]) tail[i] = std::max(tail[i], tail[s] + 1);
+    crit.assign(n, 0);
+    for (int i = 0; i < n; ++i) crit[i] = items[i].level + tail[i] == maxl;
+  }
+  void rebalance(int maxl, std::vector<int>& nops, std::vector<int>& nwg, int wg_cap) {
+    const int n = (int)items.size();
+    const auto succ = successors();
     std::vector<int> wmax(maxl + 1, 0);
     for (auto& it : items) wmax[it.level] = std::max(wmax[it.level], item_weight(it));
     const int cap = std::min(wg_cap, 1024);
@@ -1116,6 +1134,7 @@ struct Prog {
       it.level = best;
     }
   }
+  std::vector<std::vector<char>> crit_lv;  // (describe) per level, per op: on a longest chain
   std::vector<std::vector<Op>> schedule(int wg_cap = 1 << 30) {
     std::map<int, int> lw, lr;
     int maxl = -1;
@@ -1149,13 +1168,16 @@ struct Prog {
         if (r >= 0) lr[r] = std::max(lr.count(r) ? lr[r] : -1, l);
       maxl = std::max(maxl, l);
     }
+    if (const char* c = std::getenv("RLE_DESC_CRIT"); c && c[0] == '1') mark_critical(maxl);
     if (balance) rebalance(maxl, nops, nwg, wg_cap);
     std::vector<std::vector<Op>> levels(maxl + 1);
     std::vector<std::vector<int>> owner(maxl + 1);
+    crit_lv.assign(maxl + 1, {});
     for (size_t i = 0; i < items.size(); ++i)
       for (auto& op : items[i].ops) {
         levels[items[i].level].push_back(op);
         owner[items[i].level].push_back((int)i);
+        crit_lv[items[i].level].push_back(crit.empty() ? 0 : crit[i]);
       }
     if (const char* hz = std::getenv("RLE_HAZARD"); hz && hz[0] == '1')
       for (size_t l = 0; l < levels.size(); ++l) level_hazards(levels[l], owner[l], (int)l);
@@ -2166,6 +2188,7 @@ struct Engine {
     ad.bias_col = cdiv(L.K, g.tn) * g.tn;
     ad.gsq = gsq;
     ad.gsq_b = gsq_b;
+    ad.ptau = adam_ptau;
     if (nb_x) {  // dZ = AvgL1Norm backward of (dz = g, x), applied on load (kDwNb)
       REQUIRE(dz.nbdot && nb_x->norm && nb_x->m.t && nb_x->rows >= Brows, "dw: deferred AvgL1Norm backward operands");
       g.act = kDwNb;
@@ -2181,6 +2204,15 @@ struct Engine {
     }
     op.wg_count = g.tiles_m * g.tiles_n;
     pg.add(op, rd, wr);
+  }
+
+  // (TD3 policy steps) tau of the self-aliased target-policy Polyak fused into the actor's Adam
+  // epilogues (AdamArgs::ptau), 0 elsewhere
+  float adam_ptau = 0.f;
+  // RLE_NO_PIPOLYAK=1: the standalone OP_POLYAK over the policy instead (tests, A/B)
+  static bool pi_polyak_fused() {
+    const char* e = std::getenv("RLE_NO_PIPOLYAK");
+    return !(e && e[0] == '1');
   }
 
   View normbwd(Prog& pg, const View& gv, const View& x) {
@@ -3284,11 +3316,15 @@ struct Engine {
       auto g1 = gsq_for(pi.layers[1], 2, 3);
       auto g2 = gsq_for(pi.layers[2], 4, 5);
       View h1s = h1.sub(0, B), h0s = h0.sub(0, B);
+      // TD3: the aliased target policy's Polyak (td3.py:200-204) in the Adam epilogues: one level
+      // fewer between the actor update and the next step's target action
+      adam_ptau = !sac && pi_polyak_fused() ? cfg.tau : 0.f;
       View d1 = dx(pg, {{dout, &pi.layers[2], 0}}, H, B, ACT_RELU, &h1s, nullptr, nullptr, prea ? &pdout : nullptr);
       dw(pg, pi.layers[2], dout, {h1s}, B, CNT_ADAM_PI, cfg.policy_lr, g2.first, g2.second);
       View d0 = dx(pg, {{d1, &pi.layers[1], 0}}, H, B, ACT_RELU, &h0s);
       dw(pg, pi.layers[1], d1, {h0s}, B, CNT_ADAM_PI, cfg.policy_lr, g1.first, g1.second);
       dw(pg, pi.layers[0], d0, {s}, B, CNT_ADAM_PI, cfg.policy_lr, g0.first, g0.second);
+      adam_ptau = 0.f;
       if (gsq) {
         // tensor t owns tiles [gsq_offs[t], gsq_offs[t+1]) (params() order: w0, b0, w1, b1, w2, b2)
         gsq_offs.assign(1, 0);
@@ -3300,7 +3336,7 @@ struct Engine {
     if (!sac && policy) {
       flat(pg, OP_POLYAK, *tq[0], q[0], cfg.tau, false);
       flat(pg, OP_POLYAK, *tq[1], q[1], cfg.tau, false);
-      flat(pg, OP_POLYAK, pi, nullptr, cfg.tau, true);
+      if (!pi_polyak_fused()) flat(pg, OP_POLYAK, pi, nullptr, cfg.tau, true);
     }
     if (sac) {
       flat(pg, OP_POLYAK, *tq[0], q[0], cfg.tau, false);
@@ -3403,8 +3439,9 @@ struct Engine {
                  t.act_w / 1024, t.w_r / 1024, t.adam / 1024, t.other / 1024);
         G.desc += buf;
       }
-      for (auto& op : levels[l]) {
-        G.desc += std::string(" ") + kname[op.kind];
+      for (size_t k = 0; k < levels[l].size(); ++k) {
+        const Op& op = levels[l][k];
+        G.desc += std::string(" ") + (pg.crit_lv[l][k] ? "*" : "") + kname[op.kind];
         if (op.kind == OP_GEMM) {
           static const char* kepi[] = {"st", "adam", "mse", "qhead", "nbdot", "act", "qdot", "sacbwd", "sacfwd"};
           static_assert(sizeof(kepi) / sizeof(kepi[0]) == EPI_SACFWD + 1, "every epilogue has a name");

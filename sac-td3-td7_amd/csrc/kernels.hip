@@ -1352,6 +1352,11 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         vo[q] = ok ? v2 : v4[q];
         gg += ok ? gv * gv : 0.f;
       }
+      if (ad.ptau != 0.f) {  // TD3 policy step: the Polyak of the aliased target policy (op_polyak's law)
+        const float omt = 1.f - ad.ptau;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) po[q] = __fadd_rn(__fmul_rn(ad.ptau, po[q]), __fmul_rn(po[q], omt));
+      }
       GAS float* pw = bias_tile ? GW(ad.b) + ib : GW(ad.w.t) + wt;
       {  // the weights' T image (+ bias) too: +0.3% over 3 A/B pairs
         f32x4 w;

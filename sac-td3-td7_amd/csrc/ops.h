@@ -127,6 +127,8 @@ struct AdamArgs {
   float lr, beta1, beta2, eps;
   float omb1, omb2;      // (float)(1 - beta1), (float)(1 - beta2) as torch casts the Python scalars
   int bias_col;          // first column of the bias tile = K rounded up to the tile width tn
+  float ptau;            // != 0: the self-aliased Polyak p <- tau p + p (1 - tau) applied to the updated
+                         // value (TD3's target policy is the policy, td3.py:200-204)
   float* gsq;            // optional: per-tile sum of squared grads (weights), [tiles]
   float* gsq_b;          // optional: per-tile sum of squared grads (bias), [tiles_m]
 };

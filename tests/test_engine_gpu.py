@@ -418,6 +418,26 @@ def test_multistep_graphs_equal_single_steps(name):
             np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
 
 
+@pytest.mark.parametrize("name", ["td3_tiny", "td3_tiny_lap", "td3_halfcheetah"])
+def test_td3_fused_policy_polyak_bitwise(name, monkeypatch):
+    """TD3's self-aliased target-policy Polyak (td3.py:200-204, SURVEY Q1/Q2) applied in the actor's
+    Adam epilogues (AdamArgs::ptau) is bit-identical to the standalone OP_POLYAK over the policy
+    (RLE_NO_PIPOLYAK=1), through single-step and 16-step graphs."""
+    g = load_golden(name)
+    n = 20
+    e1, r1, _ = engine_from_golden(g)
+    info1 = e1.step(n)
+    monkeypatch.setenv("RLE_NO_PIPOLYAK", "1")
+    e2, r2, _ = engine_from_golden(g)
+    info2 = e2.step(n)
+    np.testing.assert_array_equal(info1, info2)
+    np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
+    alg, env, H = parse(g)[:3]
+    for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
+        for pname in params:
+            np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
+
+
 @pytest.mark.parametrize("alg,env,n", [("td3", "HalfCheetah-v4", 18), ("sac", "Humanoid-v4", 9),
                                        ("td7", "Ant-v4", 8)])
 def test_multistep_burst_matches_oracle(alg, env, n):
