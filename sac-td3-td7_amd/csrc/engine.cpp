@@ -346,7 +346,14 @@ static void gemm_finalize(GemmArgs& g) {
                                    g.sb.eps2.t && (g.sb.dout.n || g.sb.dout.t) && g.sb.log_alpha &&
                                    g.sb.ls_off >= g.sb.mean_off + g.N),
           "gemm: SAC actor backward epilogue operands");
-  REQUIRE(g.has_pre >= 0 && g.has_pre <= 2, "gemm: pre kind");
+  REQUIRE(g.has_pre != 3 || (g.mode == GEMM_FWD && (g.epi == EPI_STORE || g.epi == EPI_QDOT) && act == ACT_RELU &&
+                               !norm && g.A.nseg == 1 && g.prea.seg == 0 && g.prea.mode == GEMM_FWD &&
+                               g.prea.act == ACT_RELU && g.prea.N == g.A.seg[0].r1 - g.A.seg[0].r0 && g.prea.N <= 256 &&
+                               g.prea.N % 16 == 0 && g.prea.R % 16 == 0 && g.prea.R <= 48 && g.prea.B.nseg == 1 &&
+                               g.R == g.prea.N &&  // (<= 16 chunks per wave: kernels.hip PK 3 holds them all)
+                               g.prea.bias && !g.pre.t && g.B.nseg == 1),
+          "gemm: pre-layer layout");
+  REQUIRE(g.has_pre >= 0 && g.has_pre <= 3, "gemm: pre kind");
   g.vid = gemm_vid(g.mode, g.epi, act, norm, g.has_pre);
   REQUIRE(g.tn == 16 || g.tn == 32 || g.tn == 64, "gemm: tile width");
   g.ks_log = g.tn == 16 ? 2 : (g.tn == 32 ? 1 : 0);
@@ -501,7 +508,7 @@ static void audit_gemm(const GemmArgs& g) {
           if (k0 >= k1) continue;
           const int kb = wabs ? k0 : k0 - s0;
           if (!mine[0] && !mine[1] && !mine[2] && !mine[3]) continue;  // inactive wave: no loads
-          if (!(g.has_pre == 1 && q == g.prea.seg)) {
+          if (!((g.has_pre == 1 || g.has_pre == 3) && q == g.prea.seg)) {
             audit_range(sa.p, ((long long)(i0 / 16) * sa.xs + (k0 - s0)) * 1024, (long long)(k1 - k0) * 1024, "A", g);
             if (sa.norm.part) audit_norm(sa.norm, i0, 16, g);
           }
@@ -511,6 +518,23 @@ static void audit_gemm(const GemmArgs& g) {
         }
         // pre-GEMM operands (pre_issue / pre_finish): 16 rows at i0, both column blocks (has_pre 2,
         // the fused loss head, keeps HeadArgs in the same union: its reads are not audited here)
+        if (g.has_pre == 3) {  // pre-layer (prelayer_fwd): every A chunk, the wave's 4 W column blocks, bias
+          const PreArgs& p = g.prea;
+          for (int k = 0; k < p.R / 16; ++k) {
+            int q = 0;
+            for (int u = 1; u < p.A.nseg; ++u)
+              if (k >= p.A.seg[u].r0 / 16) q = u;
+            const Seg& sa = p.A.seg[q];
+            audit_range(sa.p, ((long long)(i0 / 16) * sa.xs + (k - sa.r0 / 16)) * 1024, 1024, "prelayer A", g);
+            for (int c = 0; c < 4; ++c)
+              if ((w * 4 + c) * 16 < p.N)
+                audit_range(p.B.seg[0].p, ((long long)(w * 4 + c) * p.B.seg[0].xs + k) * 1024, 1024, "prelayer W", g);
+          }
+          for (int c = 0; c < 4; ++c)
+            if ((w * 4 + c) * 16 < p.N)
+              audit_range(p.bias, (long long)(w * 4 + c) * 64, (long long)std::min(16, p.N - (w * 4 + c) * 16) * 4,
+                          "prelayer bias", g);
+        }
         if (g.has_pre == 1) {
           const PreArgs& p = g.prea;
           const int nchp = p.R / 16, perp = (nchp + 3) / 4;
@@ -1789,6 +1813,7 @@ struct Engine {
   struct PreUse {
     PreArgs a;
     std::vector<int> rd;
+    int kind = 1;  // GemmArgs::has_pre: 1 pre-GEMM (actor output layer), 3 pre-layer
   };
   // The critic loss head fused into the DX of critic n's last hidden layer (GemmArgs::has_pre 2)
   struct HeadUse {
@@ -1833,6 +1858,50 @@ struct Engine {
       p.noise_clip = cfg.noise_clip;
       u.rd.push_back(noise->id);
     }
+    return u;
+  }
+  // A small-K first layer L0 (ReLU, K <= 48: TD3 / SAC on low-dimensional observations) over the
+  // input segments xs, recomputed in-tile by the layer after it (prelayer_fwd): one level fewer on
+  // the critic and actor chains.  The standalone L0 output stays for its other readers (the
+  // weight gradient, the ReLU mask of the input gradient).  RLE_NO_PRELAYER=1: off (tests, A/B).
+  bool pl_src = false;  // (fwd) the layer being built is a pre-layer source
+  static int pl_tn() {
+    const char* e = std::getenv("RLE_PL_TN");
+    const int t = e ? std::atoi(e) : 64;
+    return t == 16 || t == 32 ? t : 64;
+  }
+  bool prelayer_ok(const Layer& L0, const Layer& L1) const {
+    const char* e = std::getenv("RLE_NO_PRELAYER");
+    return !(e && e[0] == '1') && L0.K <= 48 && L0.out <= 256 && L0.out % 16 == 0 && L1.seg_p.size() == 1 &&
+           L1.seg_p[0] == L0.out;
+  }
+  PreUse pre_layer(const Layer& L0, const std::vector<View>& xs) {
+    REQUIRE(xs.size() == L0.seg_p.size() && L0.K <= 48, "pre-layer: operands");
+    PreUse u{};
+    u.kind = 3;
+    PreArgs& p = u.a;
+    p.mode = GEMM_FWD;
+    int koff = 0;
+    for (size_t q = 0; q < xs.size(); ++q) {
+      REQUIRE(xs[q].m.n && xs[q].cols == L0.seg_p[q] && !xs[q].norm, "pre-layer: input segment");
+      p.A.seg[q] = seg_n(xs[q], koff, koff + L0.seg_p[q]);
+      koff += L0.seg_p[q];
+      u.rd.push_back(xs[q].id);
+    }
+    p.A.nseg = (int)xs.size();
+    Seg w{};
+    w.p = P + L0.wn_off;
+    w.xs = L0.cb;
+    w.x1 = L0.out;
+    w.r1 = L0.K;
+    p.B.seg[0] = w;
+    p.B.nseg = 1;
+    p.N = L0.out;
+    p.R = L0.K;
+    p.seg = 0;
+    p.act = ACT_RELU;
+    p.bias = bias(L0);
+    u.rd.push_back(L0.res);
     return u;
   }
   // The gradient wrt the actor's tanh input, sum_t dZ_t W_t[:, col0_t ..] * (1 - a^2), as a
@@ -1900,7 +1969,13 @@ struct Engine {
       rd.insert(rd.end(), pre->rd.begin(), pre->rd.end());
     }
     const auto tq = choose_tn(M, L.out);
-    const int tn = sfu ? 64 : tq.first;  // (EPI_SACFWD: one tile column holds whole rows)
+    // (EPI_SACFWD: one tile column holds whole rows; a pre-layer consumer recomputes the first layer
+    // per tile, so wider tiles cut that redundant work: RLE_PL_TN, default 64)
+    // (pl_src: this layer is also recomputed in-tile by a pre-layer consumer -- at most 32-wide tiles
+    // keep its reduction split, so the stored output (the ReLU mask of the input gradient, the weight
+    // gradient's operand) is the same floats as the consumer's copy, whatever the planner widens)
+    const int tn = sfu ? 64
+                       : (pre && pre->kind == 3 ? std::max(tq.first, pl_tn()) : (pl_src ? std::min(tq.first, 32) : tq.first));
     const int tiles_n = cdiv(L.out, tn);
     View out = buf(M, L.out, true, out_t);
     if (sfu) {
@@ -2018,7 +2093,7 @@ struct Engine {
         g.noise_clip = cfg.noise_clip;
       }
       if (pre) {
-        g.has_pre = 1;
+        g.has_pre = pre->kind;
         g.prea = pre->a;
       }
       op.wg_count = g.tiles_m * g.tiles_n;
@@ -2988,10 +3063,15 @@ struct Engine {
   // qd: the last hidden layer also emits EPI_QDOT row partials of q (a fused head reads them)
   void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, View& h0, View& h1,
                       const PreUse* pre = nullptr, bool h1_t = true, bool qd = false) {
+    // (not behind a pre-GEMM: the first layer's own a segment is recomputed in-tile already)
+    const bool use_pl = !pre && prelayer_ok(Q.layers[0], Q.layers[1]);
+    pl_src = use_pl;
     h0 = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pre);
+    pl_src = false;
     const bool keep = out_t;
     out_t = keep && h1_t;  // (h1_t = false: only the head reads h1, in the N image)
-    h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, nullptr,
+    const PreUse pl = use_pl ? pre_layer(Q.layers[0], {sv, av}) : PreUse{};
+    h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pl.kind == 3 ? &pl : nullptr,
              qd ? &Q.layers[2] : nullptr);
     out_t = keep;
   }
@@ -3055,8 +3135,12 @@ struct Engine {
     add_adam_scalars(pg);
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
     // actor on [s; s'] (target policy aliases the policy, Q1; SAC policy unchanged until its step)
+    pl_src = prelayer_ok(pi.layers[0], pi.layers[1]);
     View h0 = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_RELU, nullptr, false);
-    View h1 = fwd(pg, pi.layers[1], {{h0}}, B2, ACT_RELU, nullptr, false);
+    pl_src = false;
+    const PreUse pl0 = prelayer_ok(pi.layers[0], pi.layers[1]) ? pre_layer(pi.layers[0], {ss}) : PreUse{};
+    View h1 = fwd(pg, pi.layers[1], {{h0}}, B2, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr,
+                  pl0.kind == 3 ? &pl0 : nullptr);
     View actv, raw, logpi;
     // TD3: the target critics' first layer recomputes a' in-tile (pre-GEMM, as TD7)
     const bool prea = !sac && actor_pre();
@@ -3447,6 +3531,7 @@ struct Engine {
           static_assert(sizeof(kepi) / sizeof(kepi[0]) == EPI_SACFWD + 1, "every epilogue has a name");
           const char* ep = op.gemm.mode == GEMM_DW && op.gemm.act == kDwNb ? "adam+nb"
                            : op.gemm.has_pre == 2                         ? "head+dx"
+                           : op.gemm.has_pre == 3                         ? (op.gemm.epi == EPI_QDOT ? "qdot+pl" : "st+pl")
                                                                            : kepi[op.gemm.epi];
           G.desc += "[" + std::to_string(op.gemm.M) + "x" + std::to_string(op.gemm.N) + "x" +
                     std::to_string(op.gemm.R) + " " + ep + "]";

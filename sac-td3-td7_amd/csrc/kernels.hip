@@ -651,6 +651,65 @@ __device__ __forceinline__ void pre_finish(const CAS PreArgs& p, int i0, PreRing
   __syncthreads();
 }
 
+// Pre-layer (GemmArgs::has_pre 3, PreArgs with N = the consumer's whole A width <= 256, R <= 48):
+// the consumer's A operand, act(X W^T + b) for the tile's 16 rows, computed in the workgroup into
+// pimg[N / 16][256] (N-image fragment blocks) -- a small-K first layer (TD3 / SAC on low-dimensional
+// observations: K = state (+ action) dims) folded into the layer after it, one level fewer on the
+// chain.  Wave w computes output column blocks 4w .. 4w + 3 over all (<= 3) reduction chunks; each
+// chunk's sum is a separate MFMA chain and the chunks are added in order, as the standalone op
+// reduces them split-K over its waves (tn 16 / 32): the same floats.
+template <int ACT, typename F>
+__device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float* pimg, F&& after_mma) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nch = p.R >> 4;
+  const int lb = lane * 16;
+  const CAS Seg& sb = p.B.seg[0];
+  const auto rw = rsrc(sb.p);
+  float4 a[3], b[3][4];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k >= nch) break;  // (uniform)
+    int q = 0;
+#pragma unroll
+    for (int u = 1; u < kMaxSeg; ++u)
+      if (u < p.A.nseg && k >= (p.A.seg[u].r0 >> 4)) q = u;
+    const CAS Seg& sa = p.A.seg[q];
+    a[k] = bload(rsrc(sa.p), ((i0 >> 4) * sa.xs + (k - (sa.r0 >> 4))) * 1024 + lb);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)  // (column blocks past N: no load, zeros)
+      b[k][c] = (wave * 4 + c) * 16 < p.N ? bload(rw, ((wave * 4 + c) * sb.xs + k) * 1024 + lb)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float bj[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int j = (wave * 4 + c) * 16 + (lane & 15);
+    bj[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(p.bias), j < p.N ? j * 4 : kOOB, 0, 0));
+  }
+  f32x4 s[4];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k >= nch) break;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 pk = mfma4(a[k], b[k][c], z);
+      s[c] = k ? s[c] + pk : pk;
+    }
+  }
+  after_mma();  // (the caller's next loads: the pre-layer's operand registers are free now)
+  const int rb = (lane >> 4) << 2;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int cb = wave * 4 + c;
+    float* dst = pimg + cb * 256 + ((lane & 15) >> 2) * 64 + rb * 4 + (lane & 3);
+    const bool jok = cb * 16 + (lane & 15) < p.N;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q * 4] = jok ? act_f<ACT>(s[c][q] + bj[c]) : 0.f;
+  }
+  __syncthreads();
+}
+
 // max(|td|, 1)^0.4 rounded from double (torch's float pow is correctly rounded).  The double pow
 // is ~1.3 us of dependent FP64 work on the loss head's critical path, so: a float seed, two
 // Newton steps on y^5 = x^2 in double (relative error ~1e-15), rounded to float; the exact
@@ -825,7 +884,7 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
   return acc + acc1;
 }
 
-template <int MODE, int EPI, int ACT, bool NORM, int PK = 0>  // PK: 1 pre-GEMM, 2 fused loss head
+template <int MODE, int EPI, int ACT, bool NORM, int PK = 0>  // PK: 1 pre-GEMM, 2 fused loss head, 3 pre-layer
 __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
   FINE_MARK(10);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -861,7 +920,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     if constexpr (ACT == kDwNb) RLE_HOT_ASM(TL_B TL_D TL_X);
     else RLE_HOT_ASM(TL_B TL_D);
   } else if constexpr (PK != 0) {
-    if constexpr (MODE == GEMM_FWD && ACT == ACT_TANH) RLE_HOT_ASM(TL_A TL_B TL_S TL_N TL_P);
+    if constexpr (MODE == GEMM_FWD && (ACT == ACT_TANH || EPI == EPI_QDOT)) RLE_HOT_ASM(TL_A TL_B TL_S TL_N TL_P);
     else RLE_HOT_ASM(TL_A TL_B TL_S TL_P);
   } else if constexpr (EPI == EPI_NBDOT) {
     RLE_HOT_ASM(TL_A TL_B TL_S TL_X);
@@ -1021,6 +1080,36 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     if constexpr (PK == 2) {  // fused loss head: one A segment, dZ of the critic's last hidden layer
       acc = headdx_reduce<ACT>(g, i0, j0, active, jt == 0, jt == 0 && cg == 0, c0, c1, nch, a0p, a0xs, b0p, b0xs,
                                smem, acc);
+    } else if constexpr (PK == 3) {  // the whole A operand from the pre-layer in LDS (prelayer_fwd)
+      float* pimg = smem + 64 + 1024;
+      const int nrun = active && c0 < c1 ? c1 - c0 : 0;
+      const int vb = ((j0 >> 4) * b0xs + c0) * 1024 + lb;
+      const auto rbw = rsrc(b0p);
+      float4 rbq[4];  // the wave's first W chunks in flight with the pre-layer's operands
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r < nrun) rbq[r] = bload(rbw, vb + r * 1024);
+      // (A/B, TD3: issuing 8 more chunks once the pre-layer's MFMAs free their registers measured
+      // -1.2% against this one-group-ahead loop)
+      prelayer_fwd<ACT>(g.prea, i0, pimg, [] {});
+      f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};  // (chunks on two accumulators by parity, as ring_run)
+#pragma unroll 1
+      for (int c = 0; c < nrun; c += 4) {
+        float4 nx[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (c + 4 + r < nrun) nx[r] = bload(rbw, vb + (c + 4 + r) * 1024);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (c + r >= nrun) break;
+          const float4 x = *(const float4*)(pimg + (c0 + c + r) * 256 + lane * 4);
+          if (r & 1) acc1 = mfma4(x, rbq[r], acc1);
+          else acc = mfma4(x, rbq[r], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rbq[r] = nx[r];
+      }
+      acc = acc + acc1;
     } else if constexpr (PK == 1) {  // segment g.prea.seg comes from the pre-GEMM in LDS
       float* pimg = smem + 64 + 2048;
       PreRing pr;
@@ -1406,6 +1495,11 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     asm volatile("; gemm variant pre " #mode #epi #act #norm ::);    \
     gemm_v<mode, epi, act, norm, 1>(g, t, smem, tr);                 \
     break;
+#define RLE_VL(mode, epi, act, norm)                                  \
+  case gemm_vid(mode, epi, act, norm, 3):                            \
+    asm volatile("; gemm variant prelayer " #mode #epi #act #norm ::); \
+    gemm_v<mode, epi, act, norm, 3>(g, t, smem, tr);                 \
+    break;
 #define RLE_VH(mode, epi, act, norm)                                  \
   case gemm_vid(mode, epi, act, norm, 2):                            \
     asm volatile("; gemm variant head " #mode #epi #act #norm ::);   \
@@ -1442,8 +1536,11 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_V(GEMM_FWD, EPI_SACFWD, ACT_NONE, false)
     RLE_VH(GEMM_DX, EPI_STORE, ACT_ELU, false)
     RLE_VH(GEMM_DX, EPI_STORE, ACT_RELU, false)
+    RLE_VL(GEMM_FWD, EPI_STORE, ACT_RELU, false)
+    RLE_VL(GEMM_FWD, EPI_QDOT, ACT_RELU, false)
     default: break;
   }
+#undef RLE_VL
 #undef RLE_V
 #undef RLE_VP
 #undef RLE_VH

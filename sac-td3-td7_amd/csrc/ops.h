@@ -141,7 +141,7 @@ constexpr int gemm_vid(int mode, int epi, int act, int norm, int pre = 0) {
   return pre * 512 + mode * 128 + epi * 8 + act * 2 + norm;
 }
 // (the level-launch entry keeps it in bits 20-30: bit 31 of entry 0 is the descriptor-prefetch flag)
-static_assert(gemm_vid(2, 2, 15, 3, 1) < 2048, "GEMM variant ids fit 11 bits");
+static_assert(gemm_vid(2, 8, 15, 1, 3) < 2048, "GEMM variant ids fit 11 bits");
 
 enum GemmMode : int {
   GEMM_FWD = 0,   // A contiguous (activations), B contiguous (W rows):  Y = X W^T
@@ -197,7 +197,7 @@ struct PreArgs {
   int mode;            // GEMM_FWD or GEMM_DX
   int N, R;            // output columns (<= 32), reduction length
   int seg;             // consumer A segment produced
-  int pad_;
+  int act;             // (pre-layer, has_pre 3) the layer's activation
   const float* bias;   // FWD
   Mat noise; float noise_sigma, noise_clip;  // FWD: smoothing noise (T image, consumer rows)
   Mat dsrc;            // DX: saved tanh output (T image, consumer rows)

@@ -151,7 +151,7 @@ def test_level_hazards(name, monkeypatch):
     run_with_tapes(eng, tp, 1, lambda t: None)
 
 
-@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid"])
+@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah"])
 def test_gemm_address_audit(name, monkeypatch):
     """RLE_AUDIT=1: every byte range each GEMM op's workgroups can load or store (the kernel's
     address arithmetic replayed on the host, engine.cpp audit_gemm) lies inside one live device
@@ -367,8 +367,14 @@ def test_packed_group_equals_engines_alone(name, monkeypatch):
                 if exact:
                     np.testing.assert_array_equal(a, b, f"{net}.{pname}")
                 else:
-                    # (two fp32 summation orders over 20 steps: 99% bulk, as for the H=32 tensors)
-                    assert_params_close(a, b, 2 * 3e-4 * n + 1e-4, f"{net}.{pname}", bulk=0.99)
+                    # (two fp32 summation orders over 20 steps: 99% bulk, as for the H=32 tensors.  TD3
+                    # with its first layers recomputed in-tile (pre-layer, 64-wide consumer tiles) gets
+                    # a different widening plan packed than alone inside its 16-step graph, and Adam's
+                    # early sign-like steps turn the rounding differences into 2 lr moves of the
+                    # near-zero-gradient entries: 95.1% of policy.mlp.0.weight at n = 20, against 99.6%
+                    # without the pre-layer (tools/diag_packed.py); the exact case above stays bitwise)
+                    bulk = 0.94 if alg == "td3" else 0.99
+                    assert_params_close(a, b, 2 * 3e-4 * n + 1e-4, f"{net}.{pname}", bulk=bulk)
 
 
 @pytest.mark.parametrize("name", ["td7_tiny"])
@@ -428,6 +434,31 @@ def test_td3_fused_policy_polyak_bitwise(name, monkeypatch):
     e1, r1, _ = engine_from_golden(g)
     info1 = e1.step(n)
     monkeypatch.setenv("RLE_NO_PIPOLYAK", "1")
+    e2, r2, _ = engine_from_golden(g)
+    info2 = e2.step(n)
+    np.testing.assert_array_equal(info1, info2)
+    np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
+    alg, env, H = parse(g)[:3]
+    for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
+        for pname in params:
+            np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
+
+
+@pytest.mark.parametrize("name", ["td3_tiny", "td3_tiny_lap", "td3_halfcheetah"])
+def test_td3_prelayer_bitwise(name, monkeypatch):
+    """The small-K first layers (TD3 actor and critics, K <= 48) recomputed in-tile by the layer
+    after them (GemmArgs::has_pre 3, kernels.hip prelayer_fwd) give the same floats as reading the
+    standalone layer's output (RLE_NO_PRELAYER=1): chunk sums in the standalone op's split-K order,
+    consumer chunks on ring_run's two accumulators.  Tile widening off in both (RLE_LEVEL_CAP), so
+    the standalone first layers keep 16-wide tiles, and the consumers take the same 16-wide tiles
+    (RLE_PL_TN=16; production widens them to 64, covered by the golden trajectories)."""
+    g = load_golden(name)
+    n = 20
+    monkeypatch.setenv("RLE_LEVEL_CAP", "100000")
+    monkeypatch.setenv("RLE_PL_TN", "16")
+    e1, r1, _ = engine_from_golden(g)
+    info1 = e1.step(n)
+    monkeypatch.setenv("RLE_NO_PRELAYER", "1")
     e2, r2, _ = engine_from_golden(g)
     info2 = e2.step(n)
     np.testing.assert_array_equal(info1, info2)
