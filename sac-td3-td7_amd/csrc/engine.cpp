@@ -346,12 +346,13 @@ static void gemm_finalize(GemmArgs& g) {
                                    g.sb.eps2.t && (g.sb.dout.n || g.sb.dout.t) && g.sb.log_alpha &&
                                    g.sb.ls_off >= g.sb.mean_off + g.N),
           "gemm: SAC actor backward epilogue operands");
-  REQUIRE(g.has_pre != 3 || (g.mode == GEMM_FWD && (g.epi == EPI_STORE || g.epi == EPI_QDOT) && act == ACT_RELU &&
-                               !norm && g.A.nseg == 1 && g.prea.seg == 0 && g.prea.mode == GEMM_FWD &&
+  REQUIRE(g.has_pre != 3 || (((g.mode == GEMM_FWD && (g.epi == EPI_STORE || g.epi == EPI_QDOT) && g.prea.bias) ||
+                                (g.mode == GEMM_DX && g.epi == EPI_STORE && g.prea.dsrc.t)) &&
+                               act == ACT_RELU && !norm && g.A.nseg == 1 && g.prea.seg == 0 && g.prea.mode == g.mode &&
                                g.prea.act == ACT_RELU && g.prea.N == g.A.seg[0].r1 - g.A.seg[0].r0 && g.prea.N <= 256 &&
                                g.prea.N % 16 == 0 && g.prea.R % 16 == 0 && g.prea.R <= 48 && g.prea.B.nseg == 1 &&
                                g.R == g.prea.N &&  // (<= 16 chunks per wave: kernels.hip PK 3 holds them all)
-                               g.prea.bias && !g.pre.t && g.B.nseg == 1),
+                               !g.pre.t && g.B.nseg == 1),
           "gemm: pre-layer layout");
   REQUIRE(g.has_pre >= 0 && g.has_pre <= 3, "gemm: pre kind");
   g.vid = gemm_vid(g.mode, g.epi, act, norm, g.has_pre);
@@ -531,9 +532,13 @@ static void audit_gemm(const GemmArgs& g) {
                 audit_range(p.B.seg[0].p, ((long long)(w * 4 + c) * p.B.seg[0].xs + k) * 1024, 1024, "prelayer W", g);
           }
           for (int c = 0; c < 4; ++c)
-            if ((w * 4 + c) * 16 < p.N)
-              audit_range(p.bias, (long long)(w * 4 + c) * 64, (long long)std::min(16, p.N - (w * 4 + c) * 16) * 4,
-                          "prelayer bias", g);
+            if ((w * 4 + c) * 16 < p.N) {
+              if (p.mode == GEMM_FWD)
+                audit_range(p.bias, (long long)(w * 4 + c) * 64, (long long)std::min(16, p.N - (w * 4 + c) * 16) * 4,
+                            "prelayer bias", g);
+              else
+                audit_range(p.dsrc.t, h_tblk(p.dsrc.rbs, i0, (w * 4 + c) * 16), 1024, "prelayer dsrc", g);
+            }
         }
         if (g.has_pre == 1) {
           const PreArgs& p = g.prea;
@@ -1875,6 +1880,11 @@ struct Engine {
     return !(e && e[0] == '1') && L0.K <= 48 && L0.out <= 256 && L0.out % 16 == 0 && L1.seg_p.size() == 1 &&
            L1.seg_p[0] == L0.out;
   }
+  bool prelayer_ok_dx(const Layer& L, const Layer& Lprev) const {
+    const char* e = std::getenv("RLE_NO_PRELAYER");
+    return !(e && e[0] == '1') && r16(L.out) <= 48 && L.K <= 256 && L.K % 16 == 0 && Lprev.out == L.K &&
+           Lprev.out <= 256;
+  }
   PreUse pre_layer(const Layer& L0, const std::vector<View>& xs) {
     REQUIRE(xs.size() == L0.seg_p.size() && L0.K <= 48, "pre-layer: operands");
     PreUse u{};
@@ -1902,6 +1912,32 @@ struct Engine {
     p.act = ACT_RELU;
     p.bias = bias(L0);
     u.rd.push_back(L0.res);
+    return u;
+  }
+  // The input gradient through layer L (small fan-out: L.out <= 48, e.g. SAC's raw head 2 x action
+  // dims) masked by act'(saved), dZ W * act'(saved), recomputed in-tile by the input-gradient GEMM of
+  // the layer before (prelayer_fwd, GEMM_DX).  The standalone op stays for the weight gradient.
+  PreUse pre_layer_dx(const Layer& L, const View& dz, const View& saved) {
+    REQUIRE(r16(L.out) <= 48 && dz.m.n && dz.cols == r16(L.out) && saved.m.t && L.K <= 256, "pre-layer dx: operands");
+    PreUse u{};
+    u.kind = 3;
+    PreArgs& p = u.a;
+    p.mode = GEMM_DX;
+    p.A.seg[0] = seg_n(dz, 0, L.out);
+    p.A.nseg = 1;
+    Seg b{};
+    b.p = P + L.wt_off;
+    b.xs = L.rb;
+    b.x1 = L.K;
+    b.r1 = L.out;
+    p.B.seg[0] = b;
+    p.B.nseg = 1;
+    p.N = L.K;
+    p.R = r16(L.out);
+    p.seg = 0;
+    p.act = ACT_RELU;
+    p.dsrc = saved.m;
+    u.rd = {dz.id, L.res, saved.id};
     return u;
   }
   // The gradient wrt the actor's tanh input, sum_t dZ_t W_t[:, col0_t ..] * (1 - a^2), as a
@@ -2143,7 +2179,7 @@ struct Engine {
     g.N = ncols;
     g.R = roff;
     const auto tq = choose_tn(M, ncols);
-    g.tn = tq.first;
+    g.tn = pre && pre->kind == 3 ? std::max(tq.first, pl_tn()) : (pl_src ? std::min(tq.first, 32) : tq.first);
     op.seq = tq.second;
     g.tiles_m = cdiv(M, kTileM);
     g.tiles_n = cdiv(ncols, g.tn);
@@ -2175,7 +2211,7 @@ struct Engine {
     }
     wr.push_back(out.id);
     if (pre) {
-      g.has_pre = 1;
+      g.has_pre = pre->kind;
       g.prea = pre->a;
       rd.insert(rd.end(), pre->rd.begin(), pre->rd.end());
     }
@@ -3403,9 +3439,17 @@ struct Engine {
       // TD3: the aliased target policy's Polyak (td3.py:200-204) in the Adam epilogues: one level
       // fewer between the actor update and the next step's target action
       adam_ptau = !sac && pi_polyak_fused() ? cfg.tau : 0.f;
+      // SAC: d1 (the gradient through the raw head, K = 2A <= 48) recomputed in-tile by d0's DX
+      const bool pld = sac && sac_bwd_fused() && prelayer_ok_dx(pi.layers[2], pi.layers[1]);
+      pl_src = pld;
       View d1 = dx(pg, {{dout, &pi.layers[2], 0}}, H, B, ACT_RELU, &h1s, nullptr, nullptr, prea ? &pdout : nullptr);
+      pl_src = false;
+      // (d0 reads the raw head's pre-update weights when it recomputes d1: emitted before that Adam)
+      const PreUse pd1 = pld ? pre_layer_dx(pi.layers[2], dout, h1s) : PreUse{};
+      View d0;
+      if (pld) d0 = dx(pg, {{d1, &pi.layers[1], 0}}, H, B, ACT_RELU, &h0s, nullptr, nullptr, &pd1);
       dw(pg, pi.layers[2], dout, {h1s}, B, CNT_ADAM_PI, cfg.policy_lr, g2.first, g2.second);
-      View d0 = dx(pg, {{d1, &pi.layers[1], 0}}, H, B, ACT_RELU, &h0s);
+      if (!pld) d0 = dx(pg, {{d1, &pi.layers[1], 0}}, H, B, ACT_RELU, &h0s);
       dw(pg, pi.layers[1], d1, {h0s}, B, CNT_ADAM_PI, cfg.policy_lr, g1.first, g1.second);
       dw(pg, pi.layers[0], d0, {s}, B, CNT_ADAM_PI, cfg.policy_lr, g0.first, g0.second);
       adam_ptau = 0.f;

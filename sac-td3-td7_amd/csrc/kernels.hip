@@ -658,7 +658,9 @@ __device__ __forceinline__ void pre_finish(const CAS PreArgs& p, int i0, PreRing
 // chain.  Wave w computes output column blocks 4w .. 4w + 3 over all (<= 3) reduction chunks; each
 // chunk's sum is a separate MFMA chain and the chunks are added in order, as the standalone op
 // reduces them split-K over its waves (tn 16 / 32): the same floats.
-template <int ACT, typename F>
+// (GEMM_DX: the same over dZ (N image) and W's T image, no bias, the output scaled by act'(saved)
+// (p.dsrc, T image) -- SAC's gradient through the actor's raw head, K = 2 x action dims.)
+template <int MODE, int ACT, typename F>
 __device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float* pimg, F&& after_mma) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nch = p.R >> 4;
@@ -681,10 +683,18 @@ __device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float bj[4];
+  float4 ev[4];  // (DX) act'(saved) sources: 4 rows of column j per lane
+  const int rb = (lane >> 4) << 2;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int j = (wave * 4 + c) * 16 + (lane & 15);
-    bj[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(p.bias), j < p.N ? j * 4 : kOOB, 0, 0));
+    if constexpr (MODE == GEMM_FWD) {
+      bj[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(p.bias), j < p.N ? j * 4 : kOOB, 0, 0));
+      ev[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      bj[c] = 0.f;
+      ev[c] = bload(rsrc(p.dsrc.t), j < p.N ? (int)tidx(p.dsrc.rbs, i0 + rb, j) * 4 : kOOB);
+    }
   }
   f32x4 s[4];
 #pragma unroll
@@ -698,14 +708,19 @@ __device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float
     }
   }
   after_mma();  // (the caller's next loads: the pre-layer's operand registers are free now)
-  const int rb = (lane >> 4) << 2;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int cb = wave * 4 + c;
     float* dst = pimg + cb * 256 + ((lane & 15) >> 2) * 64 + rb * 4 + (lane & 3);
     const bool jok = cb * 16 + (lane & 15) < p.N;
+    const float e4[4] = {ev[c].x, ev[c].y, ev[c].z, ev[c].w};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q * 4] = jok ? act_f<ACT>(s[c][q] + bj[c]) : 0.f;
+    for (int q = 0; q < 4; ++q) {
+      float y;
+      if constexpr (MODE == GEMM_FWD) y = act_f<ACT>(s[c][q] + bj[c]);
+      else y = s[c][q] * act_b<ACT>(e4[q]);
+      dst[q * 4] = jok ? y : 0.f;
+    }
   }
   __syncthreads();
 }
@@ -1091,7 +1106,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         if (r < nrun) rbq[r] = bload(rbw, vb + r * 1024);
       // (A/B, TD3: issuing 8 more chunks once the pre-layer's MFMAs free their registers measured
       // -1.2% against this one-group-ahead loop)
-      prelayer_fwd<ACT>(g.prea, i0, pimg, [] {});
+      prelayer_fwd<MODE, ACT>(g.prea, i0, pimg, [] {});
       f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};  // (chunks on two accumulators by parity, as ring_run)
 #pragma unroll 1
       for (int c = 0; c < nrun; c += 4) {
@@ -1538,6 +1553,7 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_VH(GEMM_DX, EPI_STORE, ACT_RELU, false)
     RLE_VL(GEMM_FWD, EPI_STORE, ACT_RELU, false)
     RLE_VL(GEMM_FWD, EPI_QDOT, ACT_RELU, false)
+    RLE_VL(GEMM_DX, EPI_STORE, ACT_RELU, false)
     default: break;
   }
 #undef RLE_VL

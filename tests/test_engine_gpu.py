@@ -444,12 +444,14 @@ def test_td3_fused_policy_polyak_bitwise(name, monkeypatch):
             np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
 
 
-@pytest.mark.parametrize("name", ["td3_tiny", "td3_tiny_lap", "td3_halfcheetah"])
-def test_td3_prelayer_bitwise(name, monkeypatch):
+@pytest.mark.parametrize("name", ["td3_tiny", "td3_tiny_lap", "td3_halfcheetah", "sac_tiny", "sac_humanoid"])
+def test_prelayer_bitwise(name, monkeypatch):
     """The small-K first layers (TD3 actor and critics, K <= 48) recomputed in-tile by the layer
-    after them (GemmArgs::has_pre 3, kernels.hip prelayer_fwd) give the same floats as reading the
-    standalone layer's output (RLE_NO_PRELAYER=1): chunk sums in the standalone op's split-K order,
-    consumer chunks on ring_run's two accumulators.  Tile widening off in both (RLE_LEVEL_CAP), so
+    after them, and SAC's gradient through the actor's raw head (K = 2A <= 48) recomputed in-tile by
+    the next input-gradient GEMM (GemmArgs::has_pre 3, kernels.hip prelayer_fwd), give the same
+    floats as reading the standalone op's output (RLE_NO_PRELAYER=1): chunk sums in the standalone
+    op's split-K order, consumer chunks on ring_run's two accumulators, and the consumer ordered
+    before the Adam update of the weights it recomputes with.  Tile widening off in both (RLE_LEVEL_CAP), so
     the standalone first layers keep 16-wide tiles, and the consumers take the same 16-wide tiles
     (RLE_PL_TN=16; production widens them to 64, covered by the golden trajectories)."""
     g = load_golden(name)
