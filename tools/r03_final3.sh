@@ -15,3 +15,4 @@ bash tools/secondary.sh || exit 1
 RLE_TRACE_ALGO=td3 timeout -k 10 120 python tools/trace_levels.py > gpurun_out/r03_level_trace_td3.txt 2>&1 || exit 1
 RLE_DESC_CRIT=1 RLE_DESC_WG=1 timeout -k 10 120 python tools/describe.py td3 > gpurun_out/r03_crit_td3.txt 2>&1 || exit 1
 RLE_DESC_CRIT=1 RLE_DESC_WG=1 timeout -k 10 120 python tools/describe.py td7 > gpurun_out/r03_crit_td7.txt 2>&1 || exit 1
+RLE_TRACE_ALGO=sac timeout -k 10 120 python tools/trace_levels.py > gpurun_out/r03_level_trace_sac.txt 2>&1 || exit 1
