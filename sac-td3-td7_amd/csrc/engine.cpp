@@ -3682,7 +3682,14 @@ struct Engine {
       for (auto& op : lv)
         if (op.kind == OP_GEMM) at(op.seq) = std::max(op.gemm.tn, tmin ? std::atoi(tmin) : 16);
     int cap = std::max(256, level_capacity());
-    if (const char* e = std::getenv("RLE_LEVEL_CAP")) cap = std::max(1, std::atoi(e));  // tuning experiments
+    // TD3 (its first layers folded into 64-wide pre-layer consumers) plans its levels for 3/4 of the
+    // resident workgroups: A/B on HalfCheetah, capacity 1024 / 832 / 768 / 640 -> 23.18k / 23.47k /
+    // 23.47k / 23.37k steps/s (TD7: 1024 best, 896 -1.2%; SAC: 1024 best, 768 -0.8%)
+    bool all_td3 = true;
+    for (Engine* e : es) all_td3 = all_td3 && e->algo == RLE_TD3;
+    if (all_td3) cap = cap * 3 / 4;
+    // (RLE_LEVEL_CAP: tuning experiments, and seeds per GPU on streams -- bench.py)
+    if (const char* e = std::getenv("RLE_LEVEL_CAP")) cap = std::max(1, std::atoi(e));
     // elementwise ops (Polyak, copies) are short: they free their slots long before the level's
     // GEMMs do, so they count at 1 / flat_div of their workgroups (RLE_FLAT_DIV, A/B; 1 = full)
     static const int flat_div = [] {
