@@ -660,8 +660,8 @@ __device__ __forceinline__ void pre_finish(const CAS PreArgs& p, int i0, PreRing
 // reduces them split-K over its waves (tn 16 / 32): the same floats.
 // (GEMM_DX: the same over dZ (N image) and W's T image, no bias, the output scaled by act'(saved)
 // (p.dsrc, T image) -- SAC's gradient through the actor's raw head, K = 2 x action dims.)
-template <int MODE, int ACT, typename F>
-__device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float* pimg, F&& after_mma) {
+template <int MODE, int ACT>
+__device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float* pimg) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nch = p.R >> 4;
   const int lb = lane * 16;
@@ -707,7 +707,6 @@ __device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float
       s[c] = k ? s[c] + pk : pk;
     }
   }
-  after_mma();  // (the caller's next loads: the pre-layer's operand registers are free now)
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int cb = wave * 4 + c;
@@ -1106,7 +1105,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         if (r < nrun) rbq[r] = bload(rbw, vb + r * 1024);
       // (A/B, TD3: issuing 8 more chunks once the pre-layer's MFMAs free their registers measured
       // -1.2% against this one-group-ahead loop)
-      prelayer_fwd<MODE, ACT>(g.prea, i0, pimg, [] {});
+      prelayer_fwd<MODE, ACT>(g.prea, i0, pimg);
       f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};  // (chunks on two accumulators by parity, as ring_run)
 #pragma unroll 1
       for (int c = 0; c < nrun; c += 4) {
