@@ -151,7 +151,7 @@ def test_level_hazards(name, monkeypatch):
     run_with_tapes(eng, tp, 1, lambda t: None)
 
 
-@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah"])
+@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah", "sac_humanoid"])
 def test_gemm_address_audit(name, monkeypatch):
     """RLE_AUDIT=1: every byte range each GEMM op's workgroups can load or store (the kernel's
     address arithmetic replayed on the host, engine.cpp audit_gemm) lies inside one live device
