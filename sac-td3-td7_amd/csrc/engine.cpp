@@ -1870,6 +1870,14 @@ struct Engine {
   // the critic and actor chains.  The standalone L0 output stays for its other readers (the
   // weight gradient, the ReLU mask of the input gradient).  RLE_NO_PRELAYER=1: off (tests, A/B).
   bool pl_src = false;  // (fwd) the layer being built is a pre-layer source
+  // minimum tile width of a pre-GEMM consumer: each tile recomputes the actor output layer for its
+  // 16 rows, so wider tiles cut that redundant work (A/B, RLE_PRE_TN 16 / 32 / 64: TD3 HalfCheetah
+  // 23.37k / 23.79k / 23.91k, TD7 Humanoid 8069 / 8094 / 8060 steps/s)
+  int pre_tn() const {
+    const char* e = std::getenv("RLE_PRE_TN");
+    const int t = e ? std::atoi(e) : (algo == RLE_TD3 ? 64 : 32);
+    return t == 32 || t == 64 ? t : 16;
+  }
   static int pl_tn() {
     const char* e = std::getenv("RLE_PL_TN");
     const int t = e ? std::atoi(e) : 64;
@@ -2011,7 +2019,9 @@ struct Engine {
     // keep its reduction split, so the stored output (the ReLU mask of the input gradient, the weight
     // gradient's operand) is the same floats as the consumer's copy, whatever the planner widens)
     const int tn = sfu ? 64
-                       : (pre && pre->kind == 3 ? std::max(tq.first, pl_tn()) : (pl_src ? std::min(tq.first, 32) : tq.first));
+                       : (pre && pre->kind == 3 ? std::max(tq.first, pl_tn())
+                          : pre && pre->kind == 1 ? std::max(tq.first, pre_tn())
+                                                  : (pl_src ? std::min(tq.first, 32) : tq.first));
     const int tiles_n = cdiv(L.out, tn);
     View out = buf(M, L.out, true, out_t);
     if (sfu) {
@@ -2179,7 +2189,9 @@ struct Engine {
     g.N = ncols;
     g.R = roff;
     const auto tq = choose_tn(M, ncols);
-    g.tn = pre && pre->kind == 3 ? std::max(tq.first, pl_tn()) : (pl_src ? std::min(tq.first, 32) : tq.first);
+    g.tn = pre && pre->kind == 3 ? std::max(tq.first, pl_tn())
+           : pre && pre->kind == 1 ? std::max(tq.first, pre_tn())
+                                   : (pl_src ? std::min(tq.first, 32) : tq.first);
     op.seq = tq.second;
     g.tiles_m = cdiv(M, kTileM);
     g.tiles_n = cdiv(ncols, g.tn);
