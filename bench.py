@@ -358,8 +358,7 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
 
 def multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, cuda_sync, chunk=25):
     """K independent seeds per GPU: K engines, each with its own replay,
-    weights, Philox stream and HIP stream, stepped round-robin in chunks without host syncs
-    (--packed: one packed level schedule, rle_group).
+    weights, Philox stream and HIP stream, stepped round-robin in chunks without host syncs.
     value = steps of all seeds on all ranks / max-rank wall time."""
 
     s_dim, a_dim, _ = TASKS[args.env]
@@ -375,12 +374,7 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, c
         eng.bind(rep)
         engs.append((eng, rep))
 
-    group = E.EngineGroup([e for e, _ in engs]) if args.packed else None
-
     def run(n):
-        if group is not None:  # one packed level schedule for all K seeds (rle_group_step)
-            group.step(n)
-            return
         done = 0
         while done < n:
             c = min(chunk, n - done)
@@ -394,23 +388,16 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, c
     if dist:
         dist.barrier()
     cuda_sync(local)
-    st0 = group.stats() if group is not None else None
     t0 = time.perf_counter()
     run(args.steps)
     cuda_sync(local)
     wall = max_over_ranks([time.perf_counter() - t0], dist)[0]
-    packed = None
-    if group is not None:
-        st1 = group.stats()
-        packed = {"launches_per_step": round((st1[0] - st0[0]) / args.steps, 3),
-                  "packed_fraction": round((st1[1] - st0[1]) / (K * args.steps), 4),
-                  "levels_per_program": st1[2]}
     if rank == 0:
         gflop, mb = (SURVEY_MACS_PER_SAMPLE * 2.0 * B / 1e9, None) if (args.algo, args.env, args.batch) == (
             "td7", "Humanoid-v4", B) else WORK[(args.algo, args.env, args.batch)]
         value = world * K * args.steps / wall
         out = {
-            "metric": f"gradient-steps/sec, {K} independent seeds per GPU{' (packed)' if group else ''}, "
+            "metric": f"gradient-steps/sec, {K} independent seeds per GPU, "
                       f"{args.algo.upper()} {args.env} "
                       f"batch={args.batch} (secondary: SURVEY §8(f) rank 4)",
             "value": round(value, 2), "unit": "gradient-steps/s", "n_gpus": world, "steps": args.steps,
@@ -418,17 +405,13 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, c
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": f"{K} x {args.algo.upper()} {args.env} gradient step per GPU",
                        "seeds_per_gpu": K, "batch": args.batch, "replay": N_REPLAY, "lap": lap,
-                       "parallelism": f"replicas x{world * K} ({K} seeds per GPU, " + (
-                           "one packed level schedule)" if group is not None else "one HIP stream each)"),
-                       "packed": packed},
+                       "parallelism": f"replicas x{world * K} ({K} seeds per GPU, one HIP stream each)"},
             "roofline": {"bound": "mfma", "achieved": round(gflop * 1e9 * value / world / 1e12, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(gflop * 1e9 * value / world / 1e12 / PEAK_FP32_TFLOPS, 5),
                          "traffic": None, "note": "device aggregate over the K seeds (wall clock)"},
         }
         print(json.dumps(out), flush=True)
-    if group is not None:
-        group.close()
     if dist:
         dist.barrier()
 
@@ -510,8 +493,6 @@ def main():
     ap.add_argument("--batch", type=int, default=B)
     ap.add_argument("--seeds-per-gpu", type=int, default=1,
                     help="independent seeds (engines, one stream each) sharing each GPU (SURVEY §8(f) rank 4)")
-    ap.add_argument("--packed", action="store_true",
-                    help="with --seeds-per-gpu K: step the K seeds as one packed level schedule (rle_group)")
     args = ap.parse_args()
     if (args.algo, args.env, args.batch) not in WORK:
         ap.error(f"no SURVEY §8(d) work figures for {args.algo} {args.env} B={args.batch}")
@@ -554,8 +535,7 @@ def main():
         # K seeds on streams: the tile planner sizes each seed's levels for 512 resident workgroups
         # (half the device) so two seeds' levels co-reside (A/B, 3 seeds: 13.1k default, 14.1k at 512,
         # 13.9k at 384; profiles/r03_ab.txt "multiseed_cap").  RLE_LEVEL_CAP overrides.
-        if not args.packed:
-            os.environ.setdefault("RLE_LEVEL_CAP", "512")
+        os.environ.setdefault("RLE_LEVEL_CAP", "512")
         return multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, cuda_sync)
     cfg = E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=111 * (rank + 1), device=local)
     eng = E.Engine(cfg)

@@ -33,7 +33,6 @@ extern "C" {
 
 typedef struct rle_replay rle_replay;
 typedef struct rle_engine rle_engine;
-typedef struct rle_group rle_group;
 
 typedef struct rle_config {
   int algo;                 /* RLE_TD7 / RLE_TD3 / RLE_SAC */
@@ -124,19 +123,6 @@ int rle_step_timed(rle_engine* e, int n_steps, float* gpu_ms);
  * independent seeds (engines, each on its own stream) on one GPU concurrently -- SURVEY
  * §8(f) rank 4, beyond the reference's one agent per process (scripts/td7_exp.sh:1-4). */
 int rle_step_async(rle_engine* e, int n_steps);
-/* Packed multi-seed stepping: n (<= 16) engines on one device, each bound
- * to its own replay, same algorithm / policy_freq / target_update_rate (dims may differ).  Their
- * multi-step programs are merged into one level schedule, so each level launch carries every
- * seed's ops of that depth.  rle_group_step(g, n, async) = rle_step_async(e, n) for each engine
- * (each engine's results are those of stepping it alone), on the first engine's stream; async 0
- * waits for it.  Steps the packed program cannot take (TD7 hard-update windows, engines not at
- * the same step) run each engine's own graphs.  Destroy the group before its engines. */
-int rle_group_create(rle_engine** engines, int n, rle_group** out);
-int rle_group_step(rle_group* g, int n_steps, int async);
-/* level launches enqueued by packed replays, engine-steps they ran, levels of the packed program */
-int rle_group_stats(rle_group* g, long long* launches, long long* packed_steps, int* levels);
-int rle_group_describe(rle_group* g, char* buf, int len);
-int rle_group_destroy(rle_group* g);
 /* Parity / explicit-batch mode: replace draws of the next n_steps with tapes; each tape
  * is optional and a NULL one keeps its Philox stream.  u [n][B] (torch.rand in sample),
  * eps [n][B][A] (randn_like target noise, or SAC next-state rsample noise), eps_pi [n][B][A]

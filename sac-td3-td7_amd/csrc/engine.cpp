@@ -1007,16 +1007,10 @@ struct Prog {
     int level = 0;
   };
   std::vector<Item> items;
-  // ops per level: one launch each (kLevelOps preloaded entries, kWideOps in a wide launch)
-  int max_ops = kLevelOps;
-  // added to every resource id (packed programs of several engines: disjoint id spaces)
-  int id_off = 0;
+  // ops per level: one launch each (kLevelOps preloaded entries)
+  static constexpr int max_ops = kLevelOps;
   void add(const Op& op, std::vector<int> rd, std::vector<int> wr) { add_group({op}, std::move(rd), std::move(wr)); }
   void add_group(std::vector<Op> ops, std::vector<int> rd, std::vector<int> wr) {
-    if (id_off) {
-      for (int& r : rd) r = r >= 0 ? r + id_off : r;
-      for (int& w : wr) w = w >= 0 ? w + id_off : w;
-    }
     for (Op& op : ops)
       if (op.kind == OP_GEMM) {
         gemm_finalize(op.gemm);
@@ -2252,12 +2246,10 @@ struct Engine {
   // workgroups), else the per-op default.  Returns the op's creation index too.
   std::vector<int> tn_plan;
   int tn_seq = 0;
-  int seq_base = 0;  // (packed programs of several engines: engine k's GEMMs are k << kSeqShift on)
-  static constexpr int kSeqShift = 20;
   std::pair<int, int> choose_tn(int M, int N) {
     const int seq = tn_seq++;
     const int t = seq < (int)tn_plan.size() ? tn_plan[seq] : pick_tn(M, N);
-    return {t, seq_base + seq};
+    return {t, seq};
   }
   // per-tile grad-square partial slots of a dW op (weights at the narrowest tile width,
   // so any plan fits; unused slots stay zero; bias)
@@ -3554,8 +3546,8 @@ struct Engine {
     Graph G;
     size_t total = 0;
     for (auto& lv : levels) {
-      // (launch_level: one launch up to kWideOps ops, else ceil(ops / kLevelOps))
-      G.nlaunch += lv.size() <= (size_t)kWideOps ? 1 : (int)((lv.size() + kLevelOps - 1) / kLevelOps);
+      // (launch_level: ceil(ops / kLevelOps) launches)
+      G.nlaunch += (int)((lv.size() + kLevelOps - 1) / kLevelOps);
       G.off.push_back((int)total);
       G.nops.push_back((int)lv.size());
       int wg = 0;
@@ -3600,7 +3592,7 @@ struct Engine {
     flat_ops.reserve(total);
     for (auto& lv : levels)
       for (auto& op : lv) flat_ops.push_back(op);
-    G.d_ops = mem.make<Op>(total + kWideOps);  // (+ padding: wide launches read kWideOps headers)
+    G.d_ops = mem.make<Op>(total);
     HIPCHK(hipMemcpy(G.d_ops, flat_ops.data(), total * sizeof(Op), hipMemcpyHostToDevice));
     const char* tr_env = std::getenv("RLE_TRACE");
     if (tr_env && tr_env[0] == '1') {
@@ -3672,22 +3664,16 @@ struct Engine {
   // Builds a step program twice: the first pass fixes the level schedule, then
   // GEMM tiles of any level with more workgroups than fit on the device at once
   // are widened (16 -> 32 -> 64 columns, fewer workgroups, longer reductions per
-  // wave) and the program is rebuilt with that tile plan.  `es`: the engines whose ops
-  // f adds (one, or the seeds of a packed program: a tile plan per engine, indexed by the
-  // GEMM sequence numbers choose_tn hands out from each engine's seq_base).
+  // wave) and the program is rebuilt with that tile plan (indexed by the GEMM sequence
+  // numbers choose_tn hands out).
   template <class F>
-  static Prog plan_build_for(const std::vector<Engine*>& es, int max_ops, F&& f) {
-    for (size_t k = 0; k < es.size(); ++k) {
-      es[k]->tn_plan.clear();
-      es[k]->tn_seq = 0;
-      es[k]->seq_base = (int)k << kSeqShift;
-    }
+  Prog plan_build(F&& f) {
+    tn_plan.clear();
+    tn_seq = 0;
     Prog p0;
-    p0.max_ops = max_ops;
     f(p0);
-    std::vector<std::vector<int>> plan(es.size());
-    for (size_t k = 0; k < es.size(); ++k) plan[k].assign(es[k]->tn_seq, 16);
-    auto at = [&](int seq) -> int& { return plan[seq >> kSeqShift][seq & ((1 << kSeqShift) - 1)]; };
+    std::vector<int> plan(tn_seq, 16);
+    auto at = [&](int seq) -> int& { return plan[seq]; };
     const char* tmin = std::getenv("RLE_TN_MIN");  // tuning experiments
     auto levels = p0.schedule();
     for (auto& lv : levels)
@@ -3697,9 +3683,7 @@ struct Engine {
     // TD3 (its first layers folded into 64-wide pre-layer consumers) plans its levels for 3/4 of the
     // resident workgroups: A/B on HalfCheetah, capacity 1024 / 832 / 768 / 640 -> 23.18k / 23.47k /
     // 23.47k / 23.37k steps/s (TD7: 1024 best, 896 -1.2%; SAC: 1024 best, 768 -0.8%)
-    bool all_td3 = true;
-    for (Engine* e : es) all_td3 = all_td3 && e->algo == RLE_TD3;
-    if (all_td3) cap = cap * 3 / 4;
+    if (algo == RLE_TD3) cap = cap * 3 / 4;
     // (RLE_LEVEL_CAP: tuning experiments, and seeds per GPU on streams -- bench.py)
     if (const char* e = std::getenv("RLE_LEVEL_CAP")) cap = std::max(1, std::atoi(e));
     // elementwise ops (Polyak, copies) are short: they free their slots long before the level's
@@ -3729,24 +3713,12 @@ struct Engine {
         at(best) *= 2;
       }
     }
-    for (size_t k = 0; k < es.size(); ++k) {
-      es[k]->tn_plan = plan[k];
-      es[k]->tn_seq = 0;
-    }
+    tn_plan = plan;
+    tn_seq = 0;
     Prog p;
-    p.max_ops = max_ops;
     f(p);
-    for (Engine* e : es) {
-      e->tn_plan.clear();
-      e->seq_base = 0;
-    }
+    tn_plan.clear();
     return p;
-  }
-  template <class F>
-  Prog plan_build(F&& f) {
-    const char* e = std::getenv("RLE_MAX_OPS");  // A/B: wide launches for one engine's levels
-    const int mo = e ? std::min(std::max(std::atoi(e), 1), kWideOps) : kLevelOps;
-    return plan_build_for({this}, mo, std::forward<F>(f));
   }
 
   // steps per multi-step graph: RLE_PAIR=K (even; 0 = single-step graphs only)
@@ -3897,7 +3869,6 @@ struct Engine {
     primed = true;
     primed_ver = replay->version;
   }
-  int groups = 0;  // packed groups (rle_group) holding this engine
 
   void step(int n, float* info_out, float* gpu_ms = nullptr, bool async = false) {
     REQUIRE(replay, "no replay bound");
@@ -3990,113 +3961,6 @@ struct Engine {
   int ctrl_tape_mode_host = 0;
 };
 
-// Packed multi-seed stepping (rle_group): several engines -- independent seeds, each with
-// its own weights, optimiser state, replay and RNG stream -- whose multi-step programs are
-// merged into ONE level schedule (each engine's resource ids in a disjoint range, so only
-// its own dependencies order its ops).  A level then carries every seed's ops of that depth
-// in one (wide) launch: the per-launch cost is paid once for all seeds, and the device is
-// filled by several seeds' small GEMMs instead of one's.  Each engine's results are those
-// of stepping it alone (its ops and their order are unchanged; the tile plan may differ).
-// Steps that the packed program cannot run (a TD7 hard update, engines out of lockstep)
-// fall back to each engine's own graphs, all on the first engine's stream.
-struct Group {
-  std::vector<Engine*> es;
-  Graph g[2];
-  bool built = false;
-  int K = 0;
-  long long launches = 0, packed_steps = 0;  // rle_level dispatches / engine-steps of packed replays
-  std::vector<hipEvent_t> ev;                // per engine: the position of its own stream
-  static constexpr int kIdSpan = 1 << 24;    // resource ids per engine in the packed program
-
-  void build() {
-    for (Engine* e : es)
-      if (!e->built) e->build();
-    Engine& e0 = *es[0];
-    K = e0.multi_k;
-    for (int set = 0; K && set < 2; ++set) {
-      Prog p = Engine::plan_build_for(es, kWideOps, [&](Prog& pg) {
-        for (int j = 0; j < K; ++j)
-          for (size_t k = 0; k < es.size(); ++k) {
-            pg.id_off = (int)k * kIdSpan;
-            Engine& e = *es[k];
-            if (e.algo == RLE_TD7) e.build_td7(pg, j % 2 == 0, (set + j) % 2);
-            else e.build_mlp(pg, e.algo == RLE_SAC || j % 2 == 0, (set + j) % 2);
-          }
-        pg.id_off = 0;
-      });
-      g[set] = e0.capture(p);
-    }
-    for (Engine* e : es) e->use_set(0);
-    built = true;
-  }
-  // every engine at the same step, with its next batch prefetched on the same set, and the
-  // next K steps a multi-step window
-  bool lockstep() const {
-    const Engine& a = *es[0];
-    if (!K || !g[a.cur_set].x) return false;
-    for (const Engine* e : es)
-      if (e->ctrl_tape_mode_host || e->n_runs != a.n_runs || e->cur_set != a.cur_set || !e->pair_window_ok())
-        return false;
-    return true;
-  }
-  void step(int n, bool async) {
-    for (Engine* e : es) {
-      REQUIRE(e->replay && e->replay->size > 0, "group step: an engine has no (filled) replay");
-      HIPCHK(hipStreamSynchronize(e->replay->stream));
-    }
-    if (!built) build();
-    // everything of this call goes to the first engine's stream, after each engine's own work
-    hipStream_t s0 = es[0]->stream;
-    std::vector<hipStream_t> own(es.size());
-    for (size_t k = 0; k < es.size(); ++k) {
-      own[k] = es[k]->stream;
-      if (k) {
-        HIPCHK(hipEventRecord(ev[k], own[k]));
-        HIPCHK(hipStreamWaitEvent(s0, ev[k], 0));
-      }
-      es[k]->stream = s0;
-    }
-    auto restore = [&] {
-      for (size_t k = 0; k < es.size(); ++k) es[k]->stream = own[k];
-    };
-    try {
-      for (Engine* e : es) {
-        if (e->fold_dirty && e->g_fold.x) e->launch_graph(e->g_fold);
-        e->fold_dirty = false;
-      }
-      int done = 0;
-      while (done < n) {
-        if (n - done >= K && lockstep()) {
-          for (Engine* e : es) {
-            int zero = 0;
-            HIPCHK(hipMemcpyAsync(&e->ctrl->info_slot, &zero, sizeof(int), hipMemcpyHostToDevice, s0));
-            if (!e->primed || e->primed_ver != e->replay->version) e->launch_graph(e->g_prime[e->cur_set]);
-          }
-          const Graph& G = g[es[0]->cur_set];
-          HIPCHK(hipGraphLaunch(G.x, s0));
-          launches += G.nlaunch;
-          packed_steps += (long long)K * (long long)es.size();
-          for (Engine* e : es) {
-            e->pair_commit();
-            HIPCHK(hipEventRecord(e->done_ev, s0));
-          }
-          done += K;
-        } else {
-          for (Engine* e : es) e->step(1, nullptr, nullptr, true);  // (its own graphs, on s0)
-          done += 1;
-        }
-      }
-    } catch (...) {
-      restore();
-      throw;
-    }
-    restore();
-    HIPCHK(hipEventRecord(ev[0], s0));
-    for (size_t k = 1; k < es.size(); ++k) HIPCHK(hipStreamWaitEvent(own[k], ev[0], 0));
-    if (!async) HIPCHK(hipStreamSynchronize(s0));
-  }
-};
-
 }  // namespace rle
 
 // ====================================================================== C ABI
@@ -4110,9 +3974,6 @@ struct rle_replay {
 };
 struct rle_engine {
   std::unique_ptr<Engine> e;
-};
-struct rle_group {
-  rle::Group g;
 };
 
 template <class F>
@@ -4510,7 +4371,6 @@ int rle_destroy(rle_engine* h) {
   return guard([&] {
     if (!h) return;
     Engine& e = *h->e;
-    REQUIRE(e.groups == 0, "destroy: the engine is in a group (rle_group_destroy it first)");
     (void)hipStreamSynchronize(e.stream);
     if (e.replay) {
       auto& us = e.replay->users;
@@ -5161,73 +5021,6 @@ int rle_get_info(rle_engine* h, int n, float* out) {
 
 int rle_synchronize(rle_engine* h) {
   return guard([&] { HIPCHK(hipStreamSynchronize(h->e->stream)); });
-}
-
-int rle_group_create(rle_engine** engines, int n, rle_group** out) {
-  return guard([&] {
-    REQUIRE(engines && out && n >= 1 && n <= 16, "group_create: 1 to 16 engines");
-    auto h = std::make_unique<rle_group>();
-    rle::Group& G = h->g;
-    for (int i = 0; i < n; ++i) {
-      REQUIRE(engines[i], "group_create: null engine");
-      Engine* e = engines[i]->e.get();
-      REQUIRE(e->replay, "group_create: bind each engine's replay first");
-      for (Engine* o : G.es) {
-        REQUIRE(o != e, "group_create: an engine is listed twice");
-        REQUIRE(o->replay != e->replay, "group_create: each engine needs its own replay");
-        REQUIRE(o->cfg.device == e->cfg.device && o->algo == e->algo && o->cfg.policy_freq == e->cfg.policy_freq &&
-                    o->cfg.target_update_rate == e->cfg.target_update_rate && o->pair_k() == e->pair_k(),
-                "group_create: engines differ in device / algorithm / policy_freq / target_update_rate");
-      }
-      G.es.push_back(e);
-    }
-    HIPCHK(hipSetDevice(G.es[0]->cfg.device));
-    G.ev.assign(n, nullptr);
-    for (auto& ev : G.ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    for (Engine* e : G.es) ++e->groups;
-    *out = h.release();
-  });
-}
-
-int rle_group_step(rle_group* h, int n_steps, int async) {
-  return guard([&] {
-    REQUIRE(h && n_steps >= 0, "group_step: bad args");
-    HIPCHK(hipSetDevice(h->g.es[0]->cfg.device));
-    h->g.step(n_steps, async != 0);
-  });
-}
-
-int rle_group_stats(rle_group* h, long long* launches, long long* packed_steps, int* levels) {
-  return guard([&] {
-    REQUIRE(h, "group_stats: null group");
-    if (launches) *launches = h->g.launches;
-    if (packed_steps) *packed_steps = h->g.packed_steps;
-    if (levels) *levels = h->g.g[0].levels();
-  });
-}
-
-int rle_group_describe(rle_group* h, char* buf, int cap) {
-  return guard([&] {
-    REQUIRE(h && buf && cap > 0, "group_describe: bad args");
-    std::string d = h->g.built ? h->g.g[0].desc : std::string("(not built: step the group first)\n");
-    std::snprintf(buf, (size_t)cap, "%s", d.c_str());
-  });
-}
-
-int rle_group_destroy(rle_group* h) {
-  return guard([&] {
-    if (!h) return;
-    rle::Group& G = h->g;
-    (void)hipStreamSynchronize(G.es[0]->stream);
-    for (rle::Graph& g : G.g) {
-      if (g.x) (void)hipGraphExecDestroy(g.x);
-      if (g.g) (void)hipGraphDestroy(g.g);
-    }
-    for (auto& ev : G.ev)
-      if (ev) (void)hipEventDestroy(ev);
-    for (Engine* e : G.es) --e->groups;
-    delete h;
-  });
 }
 
 }  // extern "C"

@@ -2336,7 +2336,7 @@ __device__ __forceinline__ void op_foldbias(const CAS FoldBiasArgs& f) {
 // (-mllvm -amdgpu-kernarg-preload-count=14, Makefile): a workgroup knows its op without
 // a kernel-argument load; its first memory access is its op's descriptor.
 static_assert(kLevelOps == 12, "rle_level takes the op table as 12 scalar arguments");
-template <bool TRACE, bool WIDE>
+template <bool TRACE>
 #ifndef RLE_WAVES
 #define RLE_WAVES 4  // waves per SIMD the register allocation must allow (4 workgroups per CU)
 #endif
@@ -2374,25 +2374,9 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     e = in ? x : e;
     k = in ? q : k;
   }
-  int kind = (e >> 16) & 0xf, vid = e >> 20;
+  const int kind = (e >> 16) & 0xf, vid = e >> 20;
   const CAS Op* ops = (const CAS Op*)ops_arg;
-  int wb = (int)(e & 0xffffu);
-  // Wide launch (a level of more than kLevelOps ops, packed multi-seed programs): entry 11 is
-  // kind 0 with the count of ops from 11 on.  Lane j reads op 11 + j's first workgroup from
-  // its descriptor header (one vector load); the op is the last one starting at or before
-  // this workgroup (ops are in workgroup order), its kind and variant come from its header.
-  // (its own kernel instance: the branch alone in the production instance measured -1.2%)
-  if (WIDE && kind == 0 && vid != 0) {
-    const int cnt = vid, lane = (int)(threadIdx.x & 63);
-    int wbl = 0x7fffffff;
-    if (lane < cnt) wbl = ((const Op*)ops_arg)[kLevelOps - 1 + lane].wg_begin;
-    const unsigned long long m = __ballot(wbl <= wg);
-    const int j = 63 - __clzll((long long)m);
-    k = kLevelOps - 1 + j;
-    wb = __builtin_amdgcn_readlane(wbl, j);
-    kind = ops[k].kind;
-    vid = kind == OP_GEMM ? ops[k].gemm.vid : 0;
-  }
+  const int wb = (int)(e & 0xffffu);
   const CAS Op& op = ops[k];
   const int t = wg - wb;
   // (stamp 0 is taken on entry, before the kernel-argument loads)
@@ -2728,7 +2712,7 @@ int trace_stride() { return kTraceStride; }
 int level_capacity() {
   int per_cu = 0, cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false, false>, kThreads, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false>, kThreads, 0) != hipSuccess)
     return 1024;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
   return per_cu * cus;
@@ -2738,16 +2722,14 @@ int level_capacity() {
 // AQL launch lists; traced launches are never recorded)
 std::vector<LevelLaunch>* g_level_rec = nullptr;
 // the production kernel's HSA symbol name (AQL dispatch)
-const char* level_kernel_symbol() { return "_ZN3rle9rle_levelILb0ELb0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"; }
+const char* level_kernel_symbol() { return "_ZN3rle9rle_levelILb0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"; }
 
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
                         unsigned long long* trace, const Op* next_ops, int next_nops) {
-  // a level of more than kLevelOps ops: one wide launch up to kWideOps (entry 11 refers the
-  // workgroups of ops 11.. to their descriptors), beyond that consecutive launches of
-  // kLevelOps (its ops are independent, so any split is correct)
-  const bool wide = nops > kLevelOps && nops <= kWideOps;
+  // a level of more than kLevelOps ops: consecutive launches of kLevelOps (its ops are
+  // independent, so any split is correct)
   for (int q0 = 0; q0 < nops; q0 += kLevelOps) {
-    const int n = wide ? nops : nops - q0 < kLevelOps ? nops - q0 : kLevelOps;
+    const int n = nops - q0 < kLevelOps ? nops - q0 : kLevelOps;
     const int w0 = h_ops[q0].wg_begin;
     const int w1 = q0 + n < nops ? h_ops[q0 + n].wg_begin : nwg;
     if (w1 - w0 + 8 > kMaxLevelWG) return hipErrorInvalidValue;
@@ -2757,15 +2739,12 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
     // the following launch's ops: the rest of this level, then the next level's
     const bool last = q0 + n >= nops;
     const int nn = !last ? (nops - q0 - n < kLevelOps ? nops - q0 - n : kLevelOps)
-                         : (next_nops <= kWideOps ? next_nops : kLevelOps);
+                         : (next_nops <= kLevelOps ? next_nops : kLevelOps);
     const Op* next = !last ? d_ops + q0 + n : next_ops;
-    // (the prefetch workgroups cover 2 x kThreads lines: the first ops of a wide launch)
     const unsigned next_lines = (unsigned)(nn * (int)(sizeof(Op) / 64) < 2 * kThreads ? nn * (int)(sizeof(Op) / 64) : 2 * kThreads);
     const int npf = next_lines ? 8 : 0;  // leading prefetch workgroups (entry 0 bit 31)
     for (int q = 0; q < kLevelOps; ++q) {
-      if (wide && q == kLevelOps - 1) {
-        la.entry[q] = (unsigned)(h_ops[q0 + q].wg_begin - w0) | ((unsigned)(n - q) << 20);  // kind 0: wide
-      } else if (q < n) {
+      if (q < n) {
         const Op& o = h_ops[q0 + q];
         const unsigned vid = o.kind == OP_GEMM ? (unsigned)o.gemm.vid : 0u;
         la.entry[q] = (unsigned)(o.wg_begin - w0) | ((unsigned)o.kind << 16) | (vid << 20);
@@ -2774,7 +2753,7 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
       }
     }
     if (npf) la.entry[0] |= 0x80000000u;
-    if (g_level_rec && !trace && !wide) {  // (direct dispatch runs the narrow instance only)
+    if (g_level_rec && !trace) {  // (traced launches are never recorded)
       LevelLaunch L{};
       std::memcpy(L.ka, la.entry, sizeof la.entry);
       std::memcpy(L.ka + 48, &la.ops, 8);
@@ -2787,14 +2766,11 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
 #define RLE_LEVEL_ARGS                                                                                         \
   la.entry[0], la.entry[1], la.entry[2], la.entry[3], la.entry[4], la.entry[5], la.entry[6], la.entry[7], \
       la.entry[8], la.entry[9], la.entry[10], la.entry[11], la.ops, la.trace, next, next_lines
-    if (wide && trace) hipLaunchKernelGGL((rle_level<true, true>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
-    else if (wide) hipLaunchKernelGGL((rle_level<false, true>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
-    else if (trace) hipLaunchKernelGGL((rle_level<true, false>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
-    else hipLaunchKernelGGL((rle_level<false, false>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    if (trace) hipLaunchKernelGGL((rle_level<true>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    else hipLaunchKernelGGL((rle_level<false>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
 #undef RLE_LEVEL_ARGS
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (wide) break;
   }
   return hipSuccess;
 }

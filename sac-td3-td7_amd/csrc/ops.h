@@ -515,10 +515,6 @@ struct LevelArgs {
   // variant id << 20 (GemmArgs::vid: the variant is chosen before any descriptor load)
   unsigned entry[kLevelOps];
 };
-// Wide launches (packed multi-seed programs): up to kWideOps ops, entry 11 = kind 0 with the
-// count of ops from 11 on (bits 20-31); those ops' first workgroups are read from their
-// descriptors.  Op tables are padded by kWideOps ops so those reads stay in bounds.
-constexpr int kWideOps = 32;
 constexpr int kMaxLevelWG = 0xfffe;  // workgroups per launch (16-bit entry field)
 
 // One rle_level dispatch as an AQL packet needs it (engine.cpp direct dispatch, RLE_AQL): the

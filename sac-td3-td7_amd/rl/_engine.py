@@ -90,12 +90,6 @@ SIGNATURES = {
     "rle_get_info": (_int, [_vp, _int, _f32p]),
     "rle_copy_state": (_int, [_vp, _vp]),
     "rle_synchronize": (_int, [_vp]),
-    "rle_group_create": (_int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]),
-    "rle_group_step": (_int, [_vp, _int, _int]),
-    "rle_group_stats": (_int, [_vp, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong),
-                                ctypes.POINTER(_int)]),
-    "rle_group_describe": (_int, [_vp, ctypes.c_char_p, _int]),
-    "rle_group_destroy": (_int, [_vp]),
 }
 
 
@@ -428,43 +422,6 @@ class Engine:
 
     def synchronize(self):
         _check(lib().rle_synchronize(self.h))
-
-
-class EngineGroup:
-    """Packed multi-seed stepping (rle_group_*): the engines' multi-step programs merged into one
-    level schedule on the first engine's stream.  step(n) = step_async(n) on every engine, each
-    engine's results those of stepping it alone.  Close before the engines."""
-
-    def __init__(self, engines):
-        self.engines = list(engines)
-        arr = (_vp * len(self.engines))(*[e.h for e in self.engines])
-        self.h = _vp()
-        _check(lib().rle_group_create(arr, len(self.engines), ctypes.byref(self.h)))
-
-    def step(self, n, wait=True):
-        _check(lib().rle_group_step(self.h, n, 0 if wait else 1))
-
-    def stats(self):
-        """(level launches of packed replays, engine-steps they ran, levels of the packed program)"""
-        a, b, c = ctypes.c_longlong(), ctypes.c_longlong(), _int()
-        _check(lib().rle_group_stats(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
-        return a.value, b.value, c.value
-
-    def describe(self):
-        buf = ctypes.create_string_buffer(1 << 18)
-        _check(lib().rle_group_describe(self.h, buf, len(buf)))
-        return buf.value.decode()
-
-    def close(self):
-        if self.h:
-            _check(lib().rle_group_destroy(self.h))
-            self.h = _vp()
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 def make_config(algo, state_dim, action_dim, hidden, batch, use_lap=False, discount=0.99,

@@ -57,21 +57,3 @@ class Engine:
 
     def synchronize(self):
         pass
-
-
-class EngineGroup:
-    """rle_group stand-in: steps every engine, counts one launch per level of a 97-level program."""
-
-    def __init__(self, engines):
-        self.engines, self.steps = list(engines), 0
-
-    def step(self, n, wait=True):
-        for e in self.engines:
-            e.step_async(n)
-        self.steps += n
-
-    def stats(self):
-        return self.steps * 16, self.steps * len(self.engines), 97
-
-    def close(self):
-        pass

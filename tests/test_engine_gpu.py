@@ -9,8 +9,6 @@ parameter 2*lr away, so the bulk criterion is what catches a wrong gradient).  G
 themselves are pinned through the Adam moments in test_parity_gpu.py.
 """
 
-import re
-
 import numpy as np
 import pytest
 
@@ -210,11 +208,12 @@ def _trajectory(name, burst):
                                    rtol=1e-5, atol=1e-7)
 
 
-def _synthetic_golden(alg, env, H, B, ncap, n_fill, n_steps, use_lap, seed):
+def _synthetic_golden(alg, env, H, B, ncap, n_fill, n_steps, use_lap, seed, **extra):
     S, A, _ = spec.TASKS[env]
     g = {"meta_alg": np.array(alg), "meta_env": np.array(env),
          "meta": np.array([H, B, ncap, n_fill, n_steps, int(use_lap), seed]),
-         "meta_extra_keys": np.array([], dtype="<U1"), "meta_extra_vals": np.array([], np.float64)}
+         "meta_extra_keys": np.array(list(extra), dtype="<U32"),
+         "meta_extra_vals": np.array(list(extra.values()), np.float64)}
     for k, v in spec.tapes(alg, B, A, n_steps, seed + 3).items():
         g["tape_" + k] = v
     return g
@@ -301,104 +300,6 @@ def test_step_async_equals_step_and_seeds_overlap():
                 np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
 
 
-_OPS = re.compile(r"\b(gemm|normbwd|sreduce|sgather|head|prio|sacfwd|sacbwd|end|polyak|copy|maxred|ctrl|noise|"
-                  r"foldbias)\b")
-
-
-def _scaled(eng, alg, env, H, f):
-    for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
-        for pname in params:
-            eng.set_param(net, pname, eng.get_param(net, pname) * np.float32(f))
-
-
-# td7_tiny hard-updates every 4 steps: no 6-step window ever fits, so the group runs every step
-# through the engines' own graphs (the fallback path); the others replay the packed program
-@pytest.mark.parametrize("name", ["td7_tiny", "td7_tiny@tur250", "td3_tiny", "sac_tiny", "td7_humanoid",
-                                  "td7_humanoid@widened", "td3_halfcheetah@widened"])
-def test_packed_group_equals_engines_alone(name, monkeypatch):
-    """rle_group_step (packed): three seeds (different weights) merged into
-    one level schedule end bit-identical to each engine stepped alone -- parameters, counters,
-    priorities and last batch -- and, full size, the packed program's levels exceed the 12-op
-    launch table (wide launches).  Bitwise with the tile planner's widening off (a wider tile
-    splits a reduction differently over its waves); '@widened' (the default planner, as the
-    bench runs it): same batches, parameters within the bulk criterion of this module."""
-    exact = not name.endswith("@widened")
-    if exact:
-        monkeypatch.setenv("RLE_LEVEL_CAP", "1000000")
-    g = dict(load_golden(name.split("@")[0]))
-    if name.endswith("@tur250"):
-        g["meta_extra_vals"] = np.array([250.0])
-    alg, env, H = parse(g)[:3]
-    n = 20
-
-    def make():
-        out = []
-        for k in range(3):
-            e, r, _ = engine_from_golden(g)
-            _scaled(e, alg, env, H, 1.0 - 0.05 * k)
-            out.append((e, r))
-        return out
-
-    alone = make()
-    for e, _ in alone:
-        e.step(n)
-    packed = make()
-    grp = E.EngineGroup([e for e, _ in packed])
-    grp.step(n)
-    launches, psteps, levels = grp.stats()
-    desc = grp.describe()
-    grp.close()
-    if name == "td7_tiny":
-        assert psteps == 0
-    else:
-        assert psteps >= 3 * (n // 2) and launches > 0 and levels > 0
-    if name.startswith("td7_humanoid"):
-        assert max(len(_OPS.findall(ln)) for ln in desc.splitlines() if ln.startswith("L")) > 12
-    for (e1, r1), (e2, r2) in zip(alone, packed):
-        np.testing.assert_array_equal(e1.counters(), e2.counters())
-        if exact:
-            np.testing.assert_array_equal(e1.last_indices(), e2.last_indices())
-            np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
-        else:
-            np.testing.assert_allclose(r1.get_priority(), r2.get_priority(), rtol=1e-4)
-        for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
-            for pname in params:
-                a, b = e1.get_param(net, pname), e2.get_param(net, pname)
-                if exact:
-                    np.testing.assert_array_equal(a, b, f"{net}.{pname}")
-                else:
-                    # (two fp32 summation orders over 20 steps: 99% bulk, as for the H=32 tensors.  TD3
-                    # with its first layers recomputed in-tile (pre-layer, 64-wide consumer tiles) gets
-                    # a different widening plan packed than alone inside its 16-step graph, and Adam's
-                    # early sign-like steps turn the rounding differences into 2 lr moves of the
-                    # near-zero-gradient entries: 95.1% of policy.mlp.0.weight at n = 20, against 99.6%
-                    # without the pre-layer (tools/diag_packed.py); the exact case above stays bitwise)
-                    bulk = 0.94 if alg == "td3" else 0.99
-                    assert_params_close(a, b, 2 * 3e-4 * n + 1e-4, f"{net}.{pname}", bulk=bulk)
-
-
-@pytest.mark.parametrize("name", ["td7_tiny"])
-def test_group_rejects_shared_replay_and_grouped_destroy(name):
-    g = load_golden(name)
-    (e1, r1, _), (e2, r2, _) = engine_from_golden(g), engine_from_golden(g)
-    e3 = E.Engine(E.make_config(E.RLE_TD3, 17, 6, 32, 16))
-    r3 = E.Replay(64, 17, 6, False)
-    e3.bind(r3)
-    with pytest.raises(RuntimeError, match="twice"):
-        E.EngineGroup([e1, e1])
-    e2.bind(r1)  # (not built yet: rebinding moves it)
-    with pytest.raises(RuntimeError, match="own replay"):
-        E.EngineGroup([e1, e2])
-    e2.bind(r2)
-    with pytest.raises(RuntimeError, match="differ"):
-        E.EngineGroup([e1, e3])
-    grp = E.EngineGroup([e1, e2])
-    with pytest.raises(RuntimeError, match="group"):
-        e1.close()
-    grp.close()
-    e1.close()
-
-
 # (td7_tiny hard-updates every 4 steps, so its bursts run single-step graphs around the hard
 # updates; with target_update_rate 250 it replays the 6-step graph, LAP included)
 @pytest.mark.parametrize("name", ["td7_tiny", "td7_tiny@tur250", "td7_tiny_nolap", "td3_tiny", "sac_tiny"])
@@ -471,18 +372,30 @@ def test_prelayer_bitwise(name, monkeypatch):
             np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
 
 
-@pytest.mark.parametrize("alg,env,n", [("td3", "HalfCheetah-v4", 18), ("sac", "Humanoid-v4", 9),
-                                       ("td7", "Ant-v4", 8)])
-def test_multistep_burst_matches_oracle(alg, env, n):
+# (TD7 with policy_freq 2 starts a 6-step graph at every odd step count n_runs whose window holds no
+# hard update: n_runs = 1 -> steps 2..7 as one graph.  Humanoid 13: 1 + 6 + 6 steps, the headline
+# program (B = 256, default planner, LAP over 4096 rows); B = 1024: 1 + 6 + 1, BASELINE config 4;
+# target_update_rate 8, 16 steps: 1 + 6 + 1 (hard update) + 1 + 6 + 1 (hard update), so both
+# 6-step graphs run on either side of a hard update)
+BURSTS = [("td3", "HalfCheetah-v4", 18, 256, {}), ("sac", "Humanoid-v4", 9, 256, {}),
+          ("td7", "Ant-v4", 8, 256, {}), ("td7", "Humanoid-v4", 13, 256, {}),
+          ("td7", "Humanoid-v4", 8, 1024, {}), ("td7", "Humanoid-v4", 16, 256, {"target_update_rate": 8})]
+
+
+@pytest.mark.parametrize("alg,env,n,B,extra", BURSTS,
+                         ids=[f"{a}-{e.split('-')[0]}-n{n}-B{b}" + ("-tur8" if x else "") for a, e, n, b, x in BURSTS])
+def test_multistep_burst_matches_oracle(alg, env, n, B, extra):
     """Full-size burst through the multi-step graphs (TD3: one 16-step graph + 2 single steps;
-    SAC: one 8-step graph + 1; TD7: 1 single + one 6-step graph + 1) against the oracle
-    stepped one taped step at a time on the same draws."""
+    SAC: one 8-step graph + 1; TD7: single steps + 6-step graphs, with the production tile planner)
+    against the oracle stepped one taped step at a time on the same draws."""
     from oracle import agents
     from test_oracle import build_from_golden
 
-    g = _synthetic_golden(alg, env, 256, 256, 4096, 4096, n, alg == "td7", 91)
+    ncap = 8192 if B > 256 else 4096
+    g = _synthetic_golden(alg, env, 256, B, ncap, ncap, n, alg == "td7", 91, **extra)
     _, orc, orep, tp, n_steps, B = build_from_golden(g)
     eng, rep, tp2 = engine_from_golden(g)
+    launches0 = eng.launch_count()
     infos_ref = []
     for t in range(n_steps):
         i1, n1 = agents.run_steps(orc, alg, orep, {k: v[t:t + 1] for k, v in tp.items()}, 1, B)
@@ -491,6 +404,9 @@ def test_multistep_burst_matches_oracle(alg, env, n):
                   eps_pi=tp2.get("eps_pi", None) if "eps_pi" in tp2 else None)
     infos = np.array(eng.step(n_steps))
     eng.set_tapes()
+    if alg == "td7":  # the multi-step graphs ran: fewer launches than single-step graphs would take
+        lp, lpl = eng.graph_stats()
+        assert eng.launch_count() - launches0 < (n_steps // 2) * (lp + lpl), "no multi-step graph ran"
     np.testing.assert_array_equal(eng.last_indices(), n1[-1])
     keys = {"td7": ["train/encoder", "train/q_fn", "train/policy"],
             "td3": ["train/q_fn", "train/policy", "norm/policy"],
@@ -499,7 +415,9 @@ def test_multistep_burst_matches_oracle(alg, env, n):
     k = ref.shape[1]
     np.testing.assert_allclose(infos[:, :k], ref, rtol=2e-3, atol=1e-4, equal_nan=True)
     if alg == "td7":
-        np.testing.assert_allclose(rep.get_priority(4096), orep.priority, rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(rep.get_priority(ncap), orep.priority, rtol=1e-4, atol=1e-5)
+        vb = np.array([orc.value_max, orc.value_min, orc.vt_max, orc.vt_min], np.float32)  # td7.py:325-331
+        np.testing.assert_allclose(eng.value_bounds(), vb, rtol=1e-4, atol=1e-4)
     tol = 2 * 3e-4 * n_steps + 1e-4
     for net, d in orc.nets().items():
         for name, v in d.items():

@@ -152,18 +152,16 @@ def test_bench_gpus_n_launches_its_own_ranks():
     assert out["value"] > 0
 
 
-def test_bench_packed_seeds_line():
-    """``bench.py --seeds-per-gpu 2 --packed`` (stub engine): one JSON line whose value counts both
-    seeds and whose config carries the packed program's launch statistics."""
+def test_bench_seeds_per_gpu_line():
+    """``bench.py --seeds-per-gpu 2`` (stub engine): one JSON line whose value counts both seeds."""
     env = dict(os.environ, RLE_BENCH_STUB=os.path.join(REPO, "tests", "bench_stub.py"))
     env.pop("WORLD_SIZE", None)
-    res = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--seeds-per-gpu", "2", "--packed",
+    res = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--seeds-per-gpu", "2",
                           "--steps", "40", "--warmup", "2", "--no-cpu-baseline"], capture_output=True, text=True,
                          timeout=240, env=env)
     assert res.returncode == 0, res.stderr[-2000:]
     out = json.loads([ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1])
-    assert "(packed)" in out["metric"] and out["config"]["seeds_per_gpu"] == 2
-    assert out["config"]["packed"] == {"launches_per_step": 16.0, "packed_fraction": 1.0, "levels_per_program": 97}
+    assert out["config"]["seeds_per_gpu"] == 2 and "one HIP stream each" in out["config"]["parallelism"]
     assert out["value"] > 0
 
 
