@@ -239,7 +239,12 @@ def _latest_profile(name):
     return c[-1] if c else None
 
 
-def pmc_evidence():
+PMC_FILES = {("td7", "Humanoid-v4", 256): "pmc.json", ("td7", "Humanoid-v4", 1024): "pmc_td7_b1024.json",
+             ("td7", "Ant-v4", 256): "pmc_td7_ant.json", ("td3", "HalfCheetah-v4", 256): "pmc_td3_halfcheetah.json",
+             ("sac", "Humanoid-v4", 256): "pmc_sac_humanoid.json"}
+
+
+def pmc_evidence(cfg=("td7", "Humanoid-v4", 256)):
     """Counters of the dominant kernel from the committed PMC summary of the same command
     (tools/pmc.sh + tools/pmc_summary.py --json; mean per rle_level dispatch of a
     `bench.py --steps 200` run), NOT measured in this process:
@@ -249,7 +254,7 @@ def pmc_evidence():
       GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs; it reads high on dispatches this short,
       MI355X_MICROARCH.md 'DVFS', so this fraction is a lower bound; summarize() adds the same
       cycles over the measured launch time)."""
-    path = _latest_profile("pmc.json")
+    path = _latest_profile(PMC_FILES[cfg])
     if path is None:
         return {"traffic": None}
     with open(path) as f:
@@ -263,8 +268,8 @@ def pmc_evidence():
     return out
 
 
-def _pmc_value(key):
-    path = _latest_profile("pmc.json")
+def _pmc_value(key, cfg=("td7", "Humanoid-v4", 256)):
+    path = _latest_profile(PMC_FILES[cfg])
     if path is None:
         return None
     with open(path) as f:
@@ -272,25 +277,42 @@ def _pmc_value(key):
 
 
 def gather_evidence(s_dim, a_dim, batch, n_replay, lap):
-    """Achieved GB/s of the replay sampler op (OP_SAMPLE_GATHER: index search + row gather)
-    from the committed level trace (tools/trace_levels.py --json: mean op span from in-kernel
-    s_memrealtime stamps).  Bytes per launch: the rows read and written into the batch images,
-    B x [(2 S + A + 2) x 4 x 2 + 8 index], plus the LAP search reads, B x (4096 x 4 block +
-    8 x block sums)."""
-    path = _latest_profile("level_trace.json")
-    if path is None:
+    """Achieved GB/s of the replay sampler (OP_SAMPLE_GATHER: three-level LAP index search + row
+    gather, kernels.hip op_sample_gather) from the committed rocprofv3 kernel trace of standalone
+    sampler dispatches (tools/sampler_prof.py -> tools/sampler_summary.py: B = 256 queries over a
+    1M-row TD7 Humanoid replay, one rle_level launch each; mean duration after warm-up).
+
+    Bytes per query are what the kernel issues: the block sums its lanes load (64 lanes x
+    ceil(blocks / 64) x 8 B), the 64 sub-block sums (8 B) and 64 priorities (4 B) of the chosen
+    block / sub-block, the row (2 Sp + Ap floats + reward + notdone) and its stores into the
+    batch's T images (+ reward, notdone, index, uniform).  The PMC traffic of the same dispatches
+    (2 x FETCH_SIZE + WRITE_SIZE, profiles/rNN_sampler_pmc.json) is reported beside it."""
+    path = _latest_profile("sampler.csv")
+    if path is None or (s_dim, a_dim, batch, n_replay) != (S, A, B, N_REPLAY):
         return {}
     with open(path) as f:
-        tr = json.load(f)
-    if "sgather_all" not in tr:
-        return {}
+        durs = [int(r.split(",")[2]) for r in f.read().splitlines()[2:] if r]
+    durs = durs[10:]  # (tools/sampler_summary.py: the first 10 dispatches are warm-up)
+    us = sum(durs) / len(durs) / 1e3
     sp = (s_dim + 15) // 16 * 16
     ap = (a_dim + 15) // 16 * 16
-    rows = batch * ((2 * sp + ap + 2) * 4 * 2 + 8)
-    search = batch * (4096 * 4 + 8 * math.ceil(n_replay / 4096)) if lap else 0
-    us = tr["sgather_all"]["mean_us"]
-    return {"gather_GBs": round((rows + search) / (us * 1e-6) / 1e9, 2), "gather_bytes": rows + search,
-            "gather_us": round(us, 3), "gather_source": f"profiles/{os.path.basename(path)}"}
+    nblk = math.ceil(n_replay / 4096)
+    search = (64 * math.ceil(nblk / 64) * 8 + 64 * 8 + 64 * 4) if lap else 0
+    row_rd = (2 * sp + ap) * 4 + 8
+    row_wr = (2 * sp + ap) * 4 + 4 + 4 + 8 + 4
+    q = search + row_rd + row_wr
+    out = {"gather_GBs": round(batch * q / (us * 1e-6) / 1e9, 2), "gather_bytes": batch * q,
+           "gather_bytes_per_query": {"search": search, "row_read": row_rd, "row_write": row_wr},
+           "gather_us": round(us, 3), "gather_frac_hbm": round(batch * q / (us * 1e-6) / 1e9 / PEAK_HBM_GBS, 5),
+           "gather_source": f"profiles/{os.path.basename(path)} (rocprofv3 --kernel-trace, standalone sampler "
+                            f"dispatches, B={batch})"}
+    pm = _latest_profile("sampler_pmc.json")
+    if pm is not None:
+        with open(pm) as f:
+            c = json.load(f)
+        out["gather_traffic"] = round((2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0)
+        out["gather_traffic_source"] = f"profiles/{os.path.basename(pm)} (rocprofv3 --pmc, same dispatches)"
+    return out
 
 
 def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7", env="Humanoid-v4",
@@ -318,7 +340,7 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
         "peak": PEAK_FP32_TFLOPS,
         "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_FP32_TFLOPS, 5),
-        **(pmc_evidence() if headline else {"traffic": None}),
+        **pmc_evidence((algo, env, batch)),
         "traffic_algorithmic": round(bytes_step / launches),
         "kernel": "rle_level (one launch per dependency level of the step graph)",
         "flop_per_step": flop_step,
@@ -329,9 +351,9 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
     }
     if headline:
         roofline.update(gather_evidence(s_dim, a_dim, batch, N_REPLAY, lap))
-        busy = _pmc_value("SQ_VALU_MFMA_BUSY_CYCLES")
-        if busy is not None:  # the same counter over this run's measured launch duration, 2.4 GHz
-            roofline["mfma_busy_vs_launch_time"] = round(busy / (1024 * 2.4e9 * per_launch_s), 5)
+    busy = _pmc_value("SQ_VALU_MFMA_BUSY_CYCLES", (algo, env, batch))
+    if busy is not None:  # the same counter over this run's measured launch duration, 2.4 GHz
+        roofline["mfma_busy_vs_launch_time"] = round(busy / (1024 * 2.4e9 * per_launch_s), 5)
     metric = METRIC if headline else (f"gradient-steps/sec, {algo.upper()} {env} batch={batch}"
                                       f"{' LAP' if lap else ''} (secondary config)")
     return {
