@@ -387,7 +387,8 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, c
     engs = []
     for k in range(K):
         seed = 111 * (rank * K + k + 1)
-        eng = E.Engine(E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=seed, device=local))
+        eng = E.Engine(E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=seed, device=local),
+                       E.parse_plan(args.plan))
         for net, params in init_agent(args.algo, s_dim, a_dim, H, 123 + rank * K + k).items():
             for name, v in params.items():
                 eng.set_param(net, name, v)
@@ -427,7 +428,8 @@ def multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, c
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": f"{K} x {args.algo.upper()} {args.env} gradient step per GPU",
                        "seeds_per_gpu": K, "batch": args.batch, "replay": N_REPLAY, "lap": lap,
-                       "parallelism": f"replicas x{world * K} ({K} seeds per GPU, one HIP stream each)"},
+                       "parallelism": f"replicas x{world * K} ({K} seeds per GPU, one HIP stream each)",
+                       "plan": engs[0][0].plan()},
             "roofline": {"bound": "mfma", "achieved": round(gflop * 1e9 * value / world / 1e12, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(gflop * 1e9 * value / world / 1e12 / PEAK_FP32_TFLOPS, 5),
@@ -515,6 +517,9 @@ def main():
     ap.add_argument("--batch", type=int, default=B)
     ap.add_argument("--seeds-per-gpu", type=int, default=1,
                     help="independent seeds (engines, one stream each) sharing each GPU (SURVEY §8(f) rank 4)")
+    ap.add_argument("--plan", default=os.environ.get("RLE_PLAN", ""),
+                    help="step-program plan (rle_plan) fields, e.g. 'level_cap=512,fuse_off=headdx' (A/B tools; "
+                         "default: the engine's default plan, or $RLE_PLAN); reported in the JSON line's config")
     args = ap.parse_args()
     if (args.algo, args.env, args.batch) not in WORK:
         ap.error(f"no SURVEY §8(d) work figures for {args.algo} {args.env} B={args.batch}")
@@ -556,11 +561,12 @@ def main():
     if K > 1:
         # K seeds on streams: the tile planner sizes each seed's levels for 512 resident workgroups
         # (half the device) so two seeds' levels co-reside (A/B, 3 seeds: 13.1k default, 14.1k at 512,
-        # 13.9k at 384; profiles/r03_ab.txt "multiseed_cap").  RLE_LEVEL_CAP overrides.
-        os.environ.setdefault("RLE_LEVEL_CAP", "512")
+        # 13.9k at 384; profiles/r03_ab.txt "multiseed_cap").  --plan overrides.
+        if "level_cap" not in args.plan:
+            args.plan = ",".join(filter(None, [args.plan, "level_cap=512"]))
         return multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, cuda_sync)
     cfg = E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=111 * (rank + 1), device=local)
-    eng = E.Engine(cfg)
+    eng = E.Engine(cfg, E.parse_plan(args.plan))
     for net, params in init_agent(args.algo, s_dim, a_dim, H, 123 + rank).items():
         for name, v in params.items():
             eng.set_param(net, name, v)
@@ -588,6 +594,7 @@ def main():
         return
     out = summarize(world, args.steps, args.warmup, wall, gpu_s, lv_policy, lv_plain, args.algo, args.env,
                     args.batch, lap, launches)
+    out["config"]["plan"] = eng.plan()
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.algo, args.env, args.batch, lap)
     print(json.dumps(out), flush=True)

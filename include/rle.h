@@ -52,6 +52,33 @@ typedef struct rle_config {
   int device;
 } rle_config;
 
+/* Step-program plan: the schedule and tile-plan choices that decide how the step's reductions are
+ * split (so its fp32 summation order) and how its ops are fused.  Every engine starts from the
+ * defaults (rle_plan_default); rle_set_plan changes them before the engine's first step, and
+ * rle_get_plan reports the values in effect.  No environment variable changes a plan. */
+#define RLE_FUSE_PRELAYER (1u << 0)  /* small-K first layers recomputed in-tile by the next layer   */
+#define RLE_FUSE_PRE      (1u << 1)  /* actor output layer recomputed in-tile by its consumers      */
+#define RLE_FUSE_QDOT     (1u << 2)  /* TD7 q from per-tile row partials of the last hidden layers  */
+#define RLE_FUSE_HEADDX   (1u << 3)  /* critic loss heads fused into the DX of the last hidden layer */
+#define RLE_FUSE_NBDEFER  (1u << 4)  /* TD7 AvgL1Norm backward deferred into the weight gradient    */
+#define RLE_FUSE_SACFWD   (1u << 5)  /* SAC rsample in the actor raw head's epilogue                */
+#define RLE_FUSE_SACBWD   (1u << 6)  /* SAC squashed-Gaussian backward in the da DX's epilogue      */
+#define RLE_FUSE_FOLD     (1u << 7)  /* TD7 fixed target encoder's zsa3 folded into target critics  */
+#define RLE_FUSE_PIPOLYAK (1u << 8)  /* TD3 aliased target-policy Polyak in the actor's Adam         */
+#define RLE_FUSE_ENDSPLIT (1u << 9)  /* step end split into counters and info row                  */
+typedef struct rle_plan {
+  int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity, TD3 3/4) */
+  int steps_per_graph;  /* steps per multi-step graph (-1: TD7 6, SAC 8, TD3 16; 0: single-step only)  */
+  int pre_tn;           /* tile width of pre-GEMM consumers (0: TD3 64, else 32)                         */
+  int pl_tn;            /* tile width of pre-layer consumers (0: 64)                                     */
+  int tn_min;           /* narrowest GEMM tile (0: 16)                                                   */
+  int flat_div;         /* Polyak / copy workgroups count 1 / flat_div in the planner (0: 4)            */
+  int balance;          /* rebalance pass (-1: 1 = on; 0 off)                                            */
+  int tiny_w, uni_w, tiny_wg;  /* rebalance weights: step end, uniform sampler, tiny-op bound (-1: 30, 60, 2) */
+  int sched_cap;        /* 1: the scheduler defers ops past level_cap workgroups to a later level       */
+  unsigned fuse_off;    /* RLE_FUSE_* bits switched off (A/B, tests); 0 = every fusion on               */
+} rle_plan;
+
 /* ---- replay memory: rl/replay_memory/{lap,simple}.py ---------------------- */
 
 /* LAPReplayMemory.__init__ (lap.py:15-29) / SimpleReplayMemory.__init__ (simple.py:15-27). */
@@ -85,6 +112,11 @@ int rle_replay_gather(rle_replay* r, int n, const long long* ind, float* state, 
 /* TD7.__init__ (td7.py:34-87) / TD3.__init__ (td3.py:33-74) / SAC.__init__ (sac.py:27-77). */
 int rle_create(const rle_config* cfg, rle_engine** out);
 int rle_destroy(rle_engine* e);
+/* The default plan (every field "default"); the engine's plan before its first step; the plan in
+ * effect (defaults resolved for this engine's algorithm and device). */
+int rle_plan_default(rle_plan* out);
+int rle_set_plan(rle_engine* e, const rle_plan* plan);
+int rle_get_plan(rle_engine* e, rle_plan* out);
 /* Bind the replay the step samples from (the replay_buffer arg of train_ops). */
 int rle_bind_replay(rle_engine* e, rle_replay* r);
 /* Parameter import/export in the reference's state_dict layout (Agent.load_state_dict,

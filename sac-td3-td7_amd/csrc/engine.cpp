@@ -1032,35 +1032,13 @@ struct Prog {
   // dependent MFMA chain grows with reduction length x tile width (4 waves share it); Adam
   // epilogues, the loss head and the sampler are long for their size (level traces).
   // weight of the step-end op (RLE_TINY_W, A/B; 0 = no tiny-op moves)
-  static int tiny_weight() {
-    static const int w = [] {
-      const char* e = std::getenv("RLE_TINY_W");
-      return e ? std::atoi(e) : 30;  // (A/B 0 / 20 / 30: TD7 8021 / 8050 / 8054, SAC 12249 / 12235 / 12328)
-    }();
-    return w ? w : 8;
-  }
-  static int uniform_weight() {  // RLE_UNI_W, A/B (60: as the LAP sampler)
-    static const int w = [] {
-      const char* e = std::getenv("RLE_UNI_W");
-      return e ? std::atoi(e) : 60;  // (12 with RLE_TINY_WG=64: SAC +-0, TD3 -0.5%)
-    }();
-    return w;
-  }
-  static int tiny_wg() {  // RLE_TINY_WG, A/B: the workgroup bound of the rule below
-    static const int w = [] {
-      const char* e = std::getenv("RLE_TINY_WG");
-      return e ? std::atoi(e) : 2;
-    }();
-    return w;
-  }
-  static bool tiny_moves() {
-    static const bool on = [] {
-      const char* e = std::getenv("RLE_TINY_W");
-      return !(e && std::atoi(e) == 0);
-    }();
-    return on;
-  }
-  static int item_weight(const Item& it) {
+  // (rle_plan tiny_w / uni_w / tiny_wg; A/B tiny_w 0 / 20 / 30: TD7 8021 / 8050 / 8054, SAC 12249 /
+  // 12235 / 12328; uni_w 60 as the LAP sampler, 12 with tiny_wg 64: SAC +-0, TD3 -0.5%)
+  int tiny_w = 30, uni_w = 60, tiny_wg = 2;
+  int tiny_weight() const { return tiny_w ? tiny_w : 8; }
+  int uniform_weight() const { return uni_w; }
+  bool tiny_moves() const { return tiny_w != 0; }
+  int item_weight(const Item& it) const {
     int w = 0;
     for (const Op& op : it.ops) {
       int x = 8;
@@ -1145,7 +1123,7 @@ struct Prog {
       }
       // a one-workgroup op (the step end) that is the longest of its level: into the first level
       // of its window that has a longer op, so its time hides there
-      if (best < 0 && tiny_moves() && wg <= tiny_wg() && wt >= wmax[cur]) {
+      if (best < 0 && tiny_moves() && wg <= tiny_wg && wt >= wmax[cur]) {
         for (int l = cur + 1; l <= hi && best < 0; ++l)
           if (wmax[l] > wt && nops[l] + (int)it.ops.size() <= max_ops && nwg[l] + wg <= cap) best = l;
       }
@@ -1397,8 +1375,34 @@ enum Res : int {
   R_FIRST_DYNAMIC = 100,
 };
 
+// The default plan: every field "default" (resolved per engine by Engine::resolve_plan).
+static rle_plan plan_defaults() {
+  rle_plan p{};
+  p.steps_per_graph = -1;
+  p.balance = -1;
+  p.tiny_w = p.uni_w = p.tiny_wg = -1;
+  return p;
+}
+
 struct Engine {
   rle_config cfg;
+  rle_plan plan = plan_defaults();  // (resolved: no field left "default")
+  // Defaults of the fields left at "default" for this engine's algorithm (rle.h rle_plan).
+  void resolve_plan() {
+    if (plan.steps_per_graph < 0) plan.steps_per_graph = algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 6;
+    if (plan.pre_tn == 0) plan.pre_tn = algo == RLE_TD3 ? 64 : 32;
+    plan.pre_tn = plan.pre_tn == 32 || plan.pre_tn == 64 ? plan.pre_tn : 16;
+    if (plan.pl_tn == 0) plan.pl_tn = 64;
+    plan.pl_tn = plan.pl_tn == 16 || plan.pl_tn == 32 ? plan.pl_tn : 64;
+    plan.tn_min = plan.tn_min == 32 || plan.tn_min == 64 ? plan.tn_min : 16;
+    if (plan.flat_div <= 0) plan.flat_div = 4;
+    if (plan.balance < 0) plan.balance = 1;
+    if (plan.tiny_w < 0) plan.tiny_w = 30;
+    if (plan.uni_w < 0) plan.uni_w = 60;
+    if (plan.tiny_wg < 0) plan.tiny_wg = 2;
+    plan.sched_cap = plan.sched_cap ? 1 : 0;
+    if (plan.level_cap < 0) plan.level_cap = 0;
+  }
   int S, Sp, A, Ap, H, Hp, B;
   int algo;
   hipStream_t stream = nullptr;
@@ -1867,24 +1871,15 @@ struct Engine {
   // minimum tile width of a pre-GEMM consumer: each tile recomputes the actor output layer for its
   // 16 rows, so wider tiles cut that redundant work (A/B, RLE_PRE_TN 16 / 32 / 64: TD3 HalfCheetah
   // 23.37k / 23.79k / 23.91k, TD7 Humanoid 8069 / 8094 / 8060 steps/s)
-  int pre_tn() const {
-    const char* e = std::getenv("RLE_PRE_TN");
-    const int t = e ? std::atoi(e) : (algo == RLE_TD3 ? 64 : 32);
-    return t == 32 || t == 64 ? t : 16;
-  }
-  static int pl_tn() {
-    const char* e = std::getenv("RLE_PL_TN");
-    const int t = e ? std::atoi(e) : 64;
-    return t == 16 || t == 32 ? t : 64;
-  }
+  int pre_tn() const { return plan.pre_tn; }
+  int pl_tn() const { return plan.pl_tn; }
+  bool fused(unsigned bit) const { return !(plan.fuse_off & bit); }
   bool prelayer_ok(const Layer& L0, const Layer& L1) const {
-    const char* e = std::getenv("RLE_NO_PRELAYER");
-    return !(e && e[0] == '1') && L0.K <= 48 && L0.out <= 256 && L0.out % 16 == 0 && L1.seg_p.size() == 1 &&
+    return fused(RLE_FUSE_PRELAYER) && L0.K <= 48 && L0.out <= 256 && L0.out % 16 == 0 && L1.seg_p.size() == 1 &&
            L1.seg_p[0] == L0.out;
   }
   bool prelayer_ok_dx(const Layer& L, const Layer& Lprev) const {
-    const char* e = std::getenv("RLE_NO_PRELAYER");
-    return !(e && e[0] == '1') && r16(L.out) <= 48 && L.K <= 256 && L.K % 16 == 0 && Lprev.out == L.K &&
+    return fused(RLE_FUSE_PRELAYER) && r16(L.out) <= 48 && L.K <= 256 && L.K % 16 == 0 && Lprev.out == L.K &&
            Lprev.out <= 256;
   }
   PreUse pre_layer(const Layer& L0, const std::vector<View>& xs) {
@@ -2324,11 +2319,8 @@ struct Engine {
   // (TD3 policy steps) tau of the self-aliased target-policy Polyak fused into the actor's Adam
   // epilogues (AdamArgs::ptau), 0 elsewhere
   float adam_ptau = 0.f;
-  // RLE_NO_PIPOLYAK=1: the standalone OP_POLYAK over the policy instead (tests, A/B)
-  static bool pi_polyak_fused() {
-    const char* e = std::getenv("RLE_NO_PIPOLYAK");
-    return !(e && e[0] == '1');
-  }
+  // (plan without RLE_FUSE_PIPOLYAK: the standalone OP_POLYAK over the policy instead, tests, A/B)
+  bool pi_polyak_fused() const { return fused(RLE_FUSE_PIPOLYAK); }
 
   View normbwd(Prog& pg, const View& gv, const View& x) {
     REQUIRE(x.norm, "normbwd: x is not a normed view");
@@ -2557,18 +2549,12 @@ struct Engine {
 
   // STEP_END writes the info row and bumps the step counters; every reader of a
   // counter (Adam t, RNG step, tape position) is therefore scheduled before it.
-  // Split in two (RLE_END_SPLIT=0: one op): the counters (+ the SAC temperature update), which
+  // Split in two (plan without RLE_FUSE_ENDSPLIT: one op): the counters (+ the SAC temperature update), which
   // the next step reads, at the step's end; the info row, which only the host reads, after it,
   // free to sit under a longer op (the rebalance pass's one-workgroup rule).
   float* sac_scr = nullptr;
   int sac_scr_id = -1;
-  static bool end_split() {
-    static const bool on = [] {
-      const char* e = std::getenv("RLE_END_SPLIT");
-      return !(e && e[0] == '0');
-    }();
-    return on;
-  }
+  bool end_split() const { return fused(RLE_FUSE_ENDSPLIT); }
   void add_step_end(Prog& pg, Op op, std::vector<int> rd, const std::vector<int>& counters) {
     StepEndArgs& a = op.end;
     a.cmask = 0;
@@ -3002,34 +2988,23 @@ struct Engine {
   // Algebraic folds of TD7's linear zsa3 layer into its consumers (build_td7): on when
   // every block is 16-aligned.  RLE_NO_FOLD=1 keeps the unfolded programs (tests).
   bool td7_fold() const {
-    const char* e = std::getenv("RLE_NO_FOLD");
-    return algo == RLE_TD7 && H % 16 == 0 && !(e && e[0] == '1');
+    return algo == RLE_TD7 && H % 16 == 0 && fused(RLE_FUSE_FOLD);
   }
   // The actor's tanh output layer (N = act_dim <= 32) recomputed in-tile by the consumers on
-  // the critical path (PreArgs).  RLE_NO_PRE=1: separate ops (tests).
-  bool actor_pre() const {
-    const char* e = std::getenv("RLE_NO_PRE");
-    return A <= 32 && !(e && e[0] == '1');
-  }
+  // the critical path (PreArgs).  Without RLE_FUSE_PRE: separate ops (tests).
+  bool actor_pre() const { return A <= 32 && fused(RLE_FUSE_PRE); }
   // The critics' and target critics' last hidden layers emit EPI_QDOT row partials of q, so the
   // loss head reads 2 x 16 floats per row instead of 4 rows of H.  RLE_NO_QDOT=1: row loads (A/B).
-  bool td7_qdot() const {
-    const char* e = std::getenv("RLE_NO_QDOT");
-    return !(e && e[0] == '1');
-  }
+  bool td7_qdot() const { return fused(RLE_FUSE_QDOT); }
   // The critic loss head fused into the DX of the critics' second hidden layers (HeadUse):
-  // H <= 256, B a multiple of 16.  RLE_NO_HEADDX=1: the standalone head (tests, A/B).
+  // H <= 256, B a multiple of 16.  without RLE_FUSE_HEADDX: the standalone head (tests, A/B).
   bool td7_headdx() const {
-    const char* e = std::getenv("RLE_NO_HEADDX");
-    return algo == RLE_TD7 && H <= 256 && H % 16 == 0 && B % 16 == 0 && !(e && e[0] == '1');
+    return algo == RLE_TD7 && H <= 256 && H % 16 == 0 && B % 16 == 0 && fused(RLE_FUSE_HEADDX);
   }
   // AvgL1Norm backwards that feed only a weight-gradient GEMM are applied inside it
   // (EPI_NBDOT producer + kDwNb consumer: one level fewer).  RLE_NO_NBDEFER=1: separate
   // OP_NORMBWD (tests).
-  bool td7_nb_defer() const {
-    const char* e = std::getenv("RLE_NO_NBDEFER");
-    return B <= 1024 && !(e && e[0] == '1');
-  }
+  bool td7_nb_defer() const { return B <= 1024 && fused(RLE_FUSE_NBDEFER); }
   View tfold_w[2], tfold_b[2];  // per target critic: q1[:, zsa block] x fet.zsa3, folded q1 bias
   bool fold_dirty = true;       // parameters written from the host since the last fold
   Graph g_fold;
@@ -3117,21 +3092,12 @@ struct Engine {
   }
   // TD3 / SAC: the critic loss head and the actor objective's head fused into the DX of each
   // critic's last hidden layer (GemmArgs::has_pre 2; one level fewer on the critic chain and on
-  // the policy chain).  RLE_NO_HEADDX=1: the standalone heads (tests, A/B).
-  // SAC: the rsample as the epilogue of the actor's raw head (RLE_NO_SACFWD=1: OP_SAC_ACTOR, A/B)
-  bool sac_fwd_fused() const {
-    const char* e = std::getenv("RLE_NO_SACFWD");
-    return !(e && e[0] == '1') && 2 * A <= 64 && A <= 32;
-  }
-  // SAC: the actor backward as the epilogue of the da DX (RLE_NO_SACBWD=1: OP_SAC_ACTOR_BWD, A/B)
-  bool sac_bwd_fused() const {
-    const char* e = std::getenv("RLE_NO_SACBWD");
-    return !(e && e[0] == '1');
-  }
-  bool mlp_headdx() const {
-    const char* e = std::getenv("RLE_NO_HEADDX");
-    return !(e && e[0] == '1') && B % 16 == 0 && H <= 256 && H % 4 == 0;
-  }
+  // the policy chain).  without RLE_FUSE_HEADDX: the standalone heads (tests, A/B).
+  // SAC: the rsample as the epilogue of the actor's raw head (without RLE_FUSE_SACFWD: OP_SAC_ACTOR, A/B)
+  bool sac_fwd_fused() const { return fused(RLE_FUSE_SACFWD) && 2 * A <= 64 && A <= 32; }
+  // SAC: the actor backward as the epilogue of the da DX (without RLE_FUSE_SACBWD: OP_SAC_ACTOR_BWD, A/B)
+  bool sac_bwd_fused() const { return fused(RLE_FUSE_SACBWD); }
+  bool mlp_headdx() const { return fused(RLE_FUSE_HEADDX) && B % 16 == 0 && H <= 256 && H % 4 == 0; }
   // q partials of the twins (and target twins) into a head fused by headdx
   static void set_head_parts(HeadArgs& h, const View* q, const View* t, std::vector<int>& rd) {
     for (int n = 0; n < 2; ++n) {
@@ -3529,19 +3495,19 @@ struct Engine {
   // B = 256 (6494 vs 6481 steps/s) and -12% at B = 1024 (2706 vs 3067), where most levels
   // exceed the resident capacity and deferral only adds levels.  RLE_SCHED_CAP=1 enables it.
   int sched_cap() const {
-    const char* e = std::getenv("RLE_SCHED_CAP");
-    if (!(e && e[0] == '1')) return 1 << 30;
-    int cap = std::max(256, level_capacity());
-    if (const char* c = std::getenv("RLE_LEVEL_CAP")) cap = std::max(1, std::atoi(c));  // tuning experiments
-    return cap;
+    if (!plan.sched_cap) return 1 << 30;
+    return plan.level_cap > 0 ? plan.level_cap : std::max(256, level_capacity());
   }
   Graph capture(Prog& pg) {
-    const char* eb = std::getenv("RLE_BALANCE");  // A/B
+    // (rle_plan balance, A/B)
     // measured on MI355X (tools/abk.sh, RLE_BALANCE 0/1/2/3): TD3 HalfCheetah 15481/16050/15911/
     // 15637, SAC Humanoid 7674/8025/7997/7801, TD7 Humanoid 6532/6478/6498/6517 steps/s (round 1);
     // TD7 after the guarded operand rings: 7744/7774/7720/7754 (4-step graphs), and 6-step
     // graphs with mode 1: 7822 (tools/abenv.sh)
-    pg.balance = eb ? std::atoi(eb) : 1;
+    pg.balance = plan.balance;
+    pg.tiny_w = plan.tiny_w;
+    pg.uni_w = plan.uni_w;
+    pg.tiny_wg = plan.tiny_wg;
     auto levels = pg.schedule(sched_cap());
     Graph G;
     size_t total = 0;
@@ -3672,26 +3638,22 @@ struct Engine {
     tn_seq = 0;
     Prog p0;
     f(p0);
-    std::vector<int> plan(tn_seq, 16);
-    auto at = [&](int seq) -> int& { return plan[seq]; };
-    const char* tmin = std::getenv("RLE_TN_MIN");  // tuning experiments
+    std::vector<int> tplan(tn_seq, 16);
+    auto at = [&](int seq) -> int& { return tplan[seq]; };
     auto levels = p0.schedule();
     for (auto& lv : levels)
       for (auto& op : lv)
-        if (op.kind == OP_GEMM) at(op.seq) = std::max(op.gemm.tn, tmin ? std::atoi(tmin) : 16);
-    int cap = std::max(256, level_capacity());
+        if (op.kind == OP_GEMM) at(op.seq) = std::max(op.gemm.tn, plan.tn_min);
+    int cap = std::max(256, level_capacity());  // (plan.level_cap 0)
     // TD3 (its first layers folded into 64-wide pre-layer consumers) plans its levels for 3/4 of the
     // resident workgroups: A/B on HalfCheetah, capacity 1024 / 832 / 768 / 640 -> 23.18k / 23.47k /
     // 23.47k / 23.37k steps/s (TD7: 1024 best, 896 -1.2%; SAC: 1024 best, 768 -0.8%)
     if (algo == RLE_TD3) cap = cap * 3 / 4;
-    // (RLE_LEVEL_CAP: tuning experiments, and seeds per GPU on streams -- bench.py)
-    if (const char* e = std::getenv("RLE_LEVEL_CAP")) cap = std::max(1, std::atoi(e));
+    // (plan.level_cap: tuning experiments, and seeds per GPU on streams -- bench.py)
+    if (plan.level_cap > 0) cap = plan.level_cap;
     // elementwise ops (Polyak, copies) are short: they free their slots long before the level's
     // GEMMs do, so they count at 1 / flat_div of their workgroups (RLE_FLAT_DIV, A/B; 1 = full)
-    static const int flat_div = [] {
-      const char* e = std::getenv("RLE_FLAT_DIV");
-      return e ? std::max(1, std::atoi(e)) : 4;  // (A/B 1 / 4 / 1000: SAC 12675 / 13135 / 13122)
-    }();
+    const int flat_div = plan.flat_div;  // (A/B 1 / 4 / 1000: SAC 12675 / 13135 / 13122)
     auto wg_of = [&](const Op& op) {
       if (op.kind == OP_POLYAK || op.kind == OP_COPY) return op.wg_count / flat_div;
       if (op.kind != OP_GEMM) return op.wg_count;
@@ -3713,7 +3675,7 @@ struct Engine {
         at(best) *= 2;
       }
     }
-    tn_plan = plan;
+    tn_plan = tplan;
     tn_seq = 0;
     Prog p;
     f(p);
@@ -3721,14 +3683,13 @@ struct Engine {
     return p;
   }
 
-  // steps per multi-step graph: RLE_PAIR=K (even; 0 = single-step graphs only)
+  // steps per multi-step graph: plan.steps_per_graph (even; 0 = single-step graphs only)
   int pair_k() const {
-    const char* e = std::getenv("RLE_PAIR");  // A/B experiments
     // measured on MI355X (tools/abk.sh): TD7 Humanoid K=2/4/6/8 -> 6370/6513/6440/6290
     // steps/s (round 1), K=4/6/8 -> 7744/7785/7789 after the guarded operand rings (with the
     // rebalance pass: K=6/8 -> 7822/7825); TD3 HalfCheetah K=2/4/8/12/16 -> 14072/14885/16066/
     // 16203/16348 and SAC Humanoid K=2/4/8 -> 7874/7977/8052 (with the rebalance pass)
-    int k = e ? std::atoi(e) : (algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 6);
+    int k = plan.steps_per_graph;
     if (algo != RLE_SAC && cfg.policy_freq != 2) k = 0;  // the pattern assumes policy_freq 2
     return k >= 2 ? k & ~1 : 0;
   }
@@ -4339,6 +4300,7 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
     e.H = cfg->hidden;
     e.Hp = rle::r16(e.H);
     e.B = cfg->batch;
+    e.resolve_plan();
     HIPCHK(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
     if (e.algo == RLE_TD7) {
       for (const char* n : {"encoder", "fixed_encoder", "fixed_encoder_target"}) e.nets.push_back(e.make_net(n, "sale_enc"));
@@ -4364,6 +4326,30 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
     e.alloc_step_buffers();
     e.refresh_adam_scalars();
     *out = h.release();
+  });
+}
+
+int rle_plan_default(rle_plan* out) {
+  return guard([&] {
+    REQUIRE(out, "plan_default: null");
+    *out = rle::plan_defaults();
+  });
+}
+
+int rle_set_plan(rle_engine* h, const rle_plan* plan) {
+  return guard([&] {
+    REQUIRE(h && plan, "set_plan: null");
+    Engine& e = *h->e;
+    REQUIRE(!e.built, "set_plan: the engine has already built its step programs (set the plan before the first step)");
+    e.plan = *plan;
+    e.resolve_plan();
+  });
+}
+
+int rle_get_plan(rle_engine* h, rle_plan* out) {
+  return guard([&] {
+    REQUIRE(h && out, "get_plan: null");
+    *out = h->e->plan;
   });
 }
 

@@ -43,6 +43,55 @@ class Config(ctypes.Structure):
     ]
 
 
+class Plan(ctypes.Structure):
+    """Mirror of ``rle_plan`` (include/rle.h): the schedule / tile-plan / fusion choices that
+    decide the step's fp32 summation order.  No environment variable changes it."""
+
+    _fields_ = [
+        ("level_cap", _int), ("steps_per_graph", _int), ("pre_tn", _int), ("pl_tn", _int), ("tn_min", _int),
+        ("flat_div", _int), ("balance", _int), ("tiny_w", _int), ("uni_w", _int), ("tiny_wg", _int),
+        ("sched_cap", _int), ("fuse_off", ctypes.c_uint),
+    ]
+
+
+# RLE_FUSE_* bits of rle_plan.fuse_off
+FUSE = {"prelayer": 1 << 0, "pre": 1 << 1, "qdot": 1 << 2, "headdx": 1 << 3, "nbdefer": 1 << 4, "sacfwd": 1 << 5,
+        "sacbwd": 1 << 6, "fold": 1 << 7, "pipolyak": 1 << 8, "endsplit": 1 << 9}
+
+
+def make_plan(fuse_off=(), **kw) -> Plan:
+    """rle_plan_default() with the given fields changed; fuse_off: names of FUSE to switch off."""
+    p = Plan()
+    _check(lib().rle_plan_default(ctypes.byref(p)))
+    for k, v in kw.items():
+        if k not in dict(Plan._fields_):
+            raise ValueError(f"unknown plan field {k!r}")
+        setattr(p, k, int(v))
+    bits = 0
+    for name in ([fuse_off] if isinstance(fuse_off, str) else fuse_off):
+        bits |= FUSE[name]
+    p.fuse_off = bits
+    return p
+
+
+def parse_plan(text: str) -> Plan:
+    """'level_cap=512,steps_per_graph=4,fuse_off=headdx+qdot' -> Plan (bench.py --plan, tools)."""
+    kw, off = {}, ()
+    for item in filter(None, (t.strip() for t in (text or "").split(","))):
+        k, _, v = item.partition("=")
+        if k == "fuse_off":
+            off = tuple(filter(None, v.split("+")))
+        else:
+            kw[k] = int(v)
+    return make_plan(off, **kw)
+
+
+def plan_dict(p: Plan) -> dict:
+    d = {k: getattr(p, k) for k, _ in Plan._fields_}
+    d["fuse_off"] = [n for n, b in FUSE.items() if p.fuse_off & b]
+    return d
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "rle_last_error": (_cs, []),
@@ -59,6 +108,9 @@ SIGNATURES = {
     "rle_replay_gather": (_int, [_vp, _int, _i64p, _f32p, _f32p, _f32p, _f32p, _f32p]),
     "rle_create": (_int, [ctypes.POINTER(Config), ctypes.POINTER(_vp)]),
     "rle_destroy": (_int, [_vp]),
+    "rle_plan_default": (_int, [ctypes.POINTER(Plan)]),
+    "rle_set_plan": (_int, [_vp, ctypes.POINTER(Plan)]),
+    "rle_get_plan": (_int, [_vp, ctypes.POINTER(Plan)]),
     "rle_bind_replay": (_int, [_vp, _vp]),
     "rle_param_numel": (_int, [_vp, _cs, _cs, _i64p]),
     "rle_get_param": (_int, [_vp, _cs, _cs, _f32p, _ll]),
@@ -202,12 +254,24 @@ class Replay:
 class Engine:
     """One agent's device state + captured step graphs."""
 
-    def __init__(self, cfg: Config):
+    def __init__(self, cfg: Config, plan: Plan | None = None):
         self.cfg = cfg
         self.h = _vp()
         _check(lib().rle_create(ctypes.byref(cfg), ctypes.byref(self.h)))
         self.replay = None
         self._act_out = {}
+        if plan is not None:
+            self.set_plan(plan)
+
+    def set_plan(self, plan: Plan):
+        """Before the first step (the step programs are built with it)."""
+        _check(lib().rle_set_plan(self.h, ctypes.byref(plan)))
+
+    def plan(self) -> dict:
+        """The plan in effect (defaults resolved)."""
+        p = Plan()
+        _check(lib().rle_get_plan(self.h, ctypes.byref(p)))
+        return plan_dict(p)
 
     def close(self):
         if self.h:

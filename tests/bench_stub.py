@@ -22,6 +22,10 @@ def init_agent(algo, s, a, h, seed):
     return {}
 
 
+def parse_plan(text):
+    return dict(item.split("=") for item in filter(None, text.split(",")))
+
+
 class Replay:
     def __init__(self, n, s, a, lap, device=0):
         self.device = device
@@ -31,8 +35,11 @@ class Replay:
 
 
 class Engine:
-    def __init__(self, cfg):
-        self.cfg, self.n = cfg, 0
+    def __init__(self, cfg, plan=None):
+        self.cfg, self.n, self._plan = cfg, 0, dict(plan or {})
+
+    def plan(self):
+        return self._plan
 
     def set_param(self, *a):
         pass

@@ -28,7 +28,7 @@ def fill_replay(rep, S, A, hi, n_fill, seed):
                data["next_state"].astype(np.float32), data["done"].astype(np.float32))
 
 
-def engine_from_golden(g, device=0):
+def engine_from_golden(g, device=0, plan=None):
     alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
     S, A, hi = spec.TASKS[env]
     kw = {}
@@ -37,7 +37,7 @@ def engine_from_golden(g, device=0):
     if "tmp" in extra:  # SAC fixed temperature (sac.py:55-60)
         kw["tmp"] = float(extra["tmp"])
     cfg = E.make_config(ALGO[alg], S, A, H, B, use_lap=use_lap, seed=seed, device=device, **kw)
-    eng = E.Engine(cfg)
+    eng = E.Engine(cfg, plan)
     for net, params in spec.agent_params(alg, S, A, H, seed).items():
         for name, v in params.items():
             eng.set_param(net, name, v)

@@ -126,14 +126,13 @@ def test_step_trajectory_matches_reference(name, burst):
     _trajectory(name, burst)
 
 
-@pytest.mark.parametrize("variant", ["RLE_NO_HEADDX", "RLE_NO_QDOT"])
+@pytest.mark.parametrize("variant", ["headdx", "qdot"])
 @pytest.mark.parametrize("name", ["td7_tiny", "td7_tiny_nolap", "td7_humanoid"])
-def test_td7_head_variants_match_reference(name, variant, monkeypatch):
-    """The TD7 critic loss head's alternative schedules, read at engine build: RLE_NO_HEADDX
-    runs the head as its own op (q from the EPI_QDOT row partials), RLE_NO_QDOT (implies no
-    fusion) runs it from the critics' last hidden activations with row dot products."""
-    monkeypatch.setenv(variant, "1")
-    _trajectory(name, False)
+def test_td7_head_variants_match_reference(name, variant):
+    """The TD7 critic loss head's alternative schedules (rle_plan fuse_off): without HEADDX the
+    head runs as its own op (q from the EPI_QDOT row partials), without QDOT (implies no fusion)
+    from the critics' last hidden activations with row dot products."""
+    _trajectory(name, False, E.make_plan(fuse_off=[variant]))
 
 
 @pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah",
@@ -160,10 +159,10 @@ def test_gemm_address_audit(name, monkeypatch):
     run_with_tapes(eng, tp, 1, lambda t: None)
 
 
-def _trajectory(name, burst):
+def _trajectory(name, burst, plan=None):
     g = load_golden(name)
     alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
-    eng, rep, tp = engine_from_golden(g)
+    eng, rep, tp = engine_from_golden(g, plan=plan)
 
     def check(t):
         np.testing.assert_array_equal(eng.last_indices(), g["ind"][t])
@@ -326,16 +325,15 @@ def test_multistep_graphs_equal_single_steps(name):
 
 
 @pytest.mark.parametrize("name", ["td3_tiny", "td3_tiny_lap", "td3_halfcheetah"])
-def test_td3_fused_policy_polyak_bitwise(name, monkeypatch):
+def test_td3_fused_policy_polyak_bitwise(name):
     """TD3's self-aliased target-policy Polyak (td3.py:200-204, SURVEY Q1/Q2) applied in the actor's
     Adam epilogues (AdamArgs::ptau) is bit-identical to the standalone OP_POLYAK over the policy
-    (RLE_NO_PIPOLYAK=1), through single-step and 16-step graphs."""
+    (plan fuse_off pipolyak), through single-step and 16-step graphs."""
     g = load_golden(name)
     n = 20
     e1, r1, _ = engine_from_golden(g)
     info1 = e1.step(n)
-    monkeypatch.setenv("RLE_NO_PIPOLYAK", "1")
-    e2, r2, _ = engine_from_golden(g)
+    e2, r2, _ = engine_from_golden(g, plan=E.make_plan(fuse_off=["pipolyak"]))
     info2 = e2.step(n)
     np.testing.assert_array_equal(info1, info2)
     np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
@@ -346,23 +344,20 @@ def test_td3_fused_policy_polyak_bitwise(name, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["td3_tiny", "td3_tiny_lap", "td3_halfcheetah", "sac_tiny", "sac_humanoid"])
-def test_prelayer_bitwise(name, monkeypatch):
+def test_prelayer_bitwise(name):
     """The small-K first layers (TD3 actor and critics, K <= 48) recomputed in-tile by the layer
     after them, and SAC's gradient through the actor's raw head (K = 2A <= 48) recomputed in-tile by
     the next input-gradient GEMM (GemmArgs::has_pre 3, kernels.hip prelayer_fwd), give the same
-    floats as reading the standalone op's output (RLE_NO_PRELAYER=1): chunk sums in the standalone
+    floats as reading the standalone op's output (plan fuse_off prelayer): chunk sums in the standalone
     op's split-K order, consumer chunks on ring_run's two accumulators, and the consumer ordered
-    before the Adam update of the weights it recomputes with.  Tile widening off in both (RLE_LEVEL_CAP), so
+    before the Adam update of the weights it recomputes with.  Tile widening off in both (level_cap), so
     the standalone first layers keep 16-wide tiles, and the consumers take the same 16-wide tiles
-    (RLE_PL_TN=16; production widens them to 64, covered by the golden trajectories)."""
+    (pl_tn 16; production widens them to 64, covered by the golden trajectories)."""
     g = load_golden(name)
     n = 20
-    monkeypatch.setenv("RLE_LEVEL_CAP", "100000")
-    monkeypatch.setenv("RLE_PL_TN", "16")
-    e1, r1, _ = engine_from_golden(g)
+    e1, r1, _ = engine_from_golden(g, plan=E.make_plan(level_cap=100000, pl_tn=16))
     info1 = e1.step(n)
-    monkeypatch.setenv("RLE_NO_PRELAYER", "1")
-    e2, r2, _ = engine_from_golden(g)
+    e2, r2, _ = engine_from_golden(g, plan=E.make_plan(["prelayer"], level_cap=100000, pl_tn=16))
     info2 = e2.step(n)
     np.testing.assert_array_equal(info1, info2)
     np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
@@ -422,3 +417,43 @@ def test_multistep_burst_matches_oracle(alg, env, n, B, extra):
     for net, d in orc.nets().items():
         for name, v in d.items():
             assert_params_close(eng.get_param(net, name, tuple(v.shape)), v.detach().numpy(), tol, (net, name))
+
+
+@pytest.mark.parametrize("name", ["td7_humanoid", "td3_halfcheetah"])
+def test_plan_is_explicit_and_env_free(name, monkeypatch):
+    """The step program's plan (tile plan, schedule, fusions: everything that sets the fp32 summation
+    order) comes only from rle_plan: the old environment switches change nothing, the plan given as
+    fields or as bench.py's --plan text builds the same program bitwise, and a different level
+    capacity builds a different one."""
+    g = load_golden(name)
+    n = 18
+
+    def run(plan=None):
+        e, r, _ = engine_from_golden(g, plan=plan)
+        info = np.array(e.step(n))
+        params = {(net, p): e.get_param(net, p) for net, ps in spec.agent_params(*_alg_dims(g)).items() for p in ps}
+        return e, info, params
+
+    def same(a, b):
+        np.testing.assert_array_equal(a[1], b[1])
+        for k in a[2]:
+            np.testing.assert_array_equal(a[2][k], b[2][k], str(k))
+
+    base = run()
+    for var, val in (("RLE_LEVEL_CAP", "512"), ("RLE_PL_TN", "16"), ("RLE_PRE_TN", "16"), ("RLE_PAIR", "2"),
+                     ("RLE_NO_HEADDX", "1"), ("RLE_FLAT_DIV", "1"), ("RLE_TN_MIN", "64")):
+        monkeypatch.setenv(var, val)
+    env = run()
+    assert env[0].plan() == base[0].plan()
+    same(base, env)
+    monkeypatch.undo()
+    fields = run(E.make_plan(level_cap=512))
+    text = run(E.parse_plan("level_cap=512"))
+    assert fields[0].plan()["level_cap"] == 512 and fields[0].plan() == text[0].plan()
+    same(fields, text)
+    assert fields[0].describe(0) != base[0].describe(0)  # (a narrower level capacity widens other tiles)
+
+
+def _alg_dims(g):
+    alg, env, H = parse(g)[:3]
+    return (alg, *spec.TASKS[env][:2], H, 0)
