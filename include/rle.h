@@ -66,6 +66,11 @@ typedef struct rle_config {
 #define RLE_FUSE_FOLD     (1u << 7)  /* TD7 fixed target encoder's zsa3 folded into target critics  */
 #define RLE_FUSE_PIPOLYAK (1u << 8)  /* TD3 aliased target-policy Polyak in the actor's Adam         */
 #define RLE_FUSE_ENDSPLIT (1u << 9)  /* step end split into counters and info row                  */
+#define RLE_FUSE_PRIOSAMPLE (1u << 10) /* LAP priority update applied by the next batch's sampler (opt-in,
+                                        fuse_on): one level fewer per step pair, but the heavy critic
+                                        weight-gradient ops then share a level with the next batch's
+                                        first layers (TD7 Humanoid A/B: -4.5%)                        */
+#define RLE_FUSE_OPT_IN RLE_FUSE_PRIOSAMPLE  /* fusions off unless set in fuse_on                      */
 typedef struct rle_plan {
   int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity, TD3 3/4) */
   int steps_per_graph;  /* steps per multi-step graph (-1: TD7 6, SAC 8, TD3 16; 0: single-step only)  */
@@ -76,7 +81,10 @@ typedef struct rle_plan {
   int balance;          /* rebalance pass (-1: 1 = on; 0 off)                                            */
   int tiny_w, uni_w, tiny_wg;  /* rebalance weights: step end, uniform sampler, tiny-op bound (-1: 30, 60, 2) */
   int sched_cap;        /* 1: the scheduler defers ops past level_cap workgroups to a later level       */
-  unsigned fuse_off;    /* RLE_FUSE_* bits switched off (A/B, tests); 0 = every fusion on               */
+  unsigned fuse_off;    /* RLE_FUSE_* bits switched off (A/B, tests); 0 = every default fusion on       */
+  unsigned fuse_on;     /* RLE_FUSE_OPT_IN bits switched on                                             */
+  int rb;               /* 1: 32 / 64-wide weight-gradient tiles register-blocked (the 4 waves split the batch
+                           rows, each accumulates every column block; -1: default)                       */
 } rle_plan;
 
 /* ---- replay memory: rl/replay_memory/{lap,simple}.py ---------------------- */

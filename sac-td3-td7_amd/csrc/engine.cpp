@@ -758,6 +758,10 @@ static void op_accesses(const Op& op, std::vector<Access>& v) {
         acc_whole(v, r, 0, "replay");
       acc_whole(v, s.tape_u, 0, "tape u");
       acc_whole(v, s.tape_ind, 0, "tape ind");
+      if (s.pend_n) {
+        acc_bytes(v, s.pend_ind, 8LL * s.pend_n, 0, "pending ind");
+        acc_bytes(v, s.pend_p, 4LL * s.pend_n, 0, "pending p");
+      }
       acc_mat(v, s.ss, 1, "batch ss");
       acc_mat(v, s.a, 1, "batch a");
       acc_whole(v, s.r, 1, "batch r");
@@ -1009,10 +1013,18 @@ struct Prog {
   std::vector<Item> items;
   // ops per level: one launch each (kLevelOps preloaded entries)
   static constexpr int max_ops = kLevelOps;
+  // register-blocked wide weight-gradient tiles (rle_plan rb)
+  int rb = 0;
+  static bool rb_eligible(const GemmArgs& g) {
+    bool seg_ok = true;  // (the tile's column blocks lie in one X segment, kernels.hip rb path)
+    for (int q = 0; q < g.B.nseg; ++q) seg_ok = seg_ok && g.B.seg[q].x0 % g.tn == 0;
+    return g.mode == GEMM_DW && (g.tn == 32 || g.tn == 64) && g.has_pre == 0 && seg_ok;
+  }
   void add(const Op& op, std::vector<int> rd, std::vector<int> wr) { add_group({op}, std::move(rd), std::move(wr)); }
   void add_group(std::vector<Op> ops, std::vector<int> rd, std::vector<int> wr) {
     for (Op& op : ops)
       if (op.kind == OP_GEMM) {
+        op.gemm.hot.rb = rb && rb_eligible(op.gemm) ? 1 : 0;
         gemm_finalize(op.gemm);
         check_gemm(op.gemm);
         if (std::getenv("RLE_AUDIT")) audit_gemm(op.gemm);  // (read per op: tests set it per engine)
@@ -1381,6 +1393,7 @@ static rle_plan plan_defaults() {
   p.steps_per_graph = -1;
   p.balance = -1;
   p.tiny_w = p.uni_w = p.tiny_wg = -1;
+  p.rb = -1;
   return p;
 }
 
@@ -1401,6 +1414,7 @@ struct Engine {
     if (plan.uni_w < 0) plan.uni_w = 60;
     if (plan.tiny_wg < 0) plan.tiny_wg = 2;
     plan.sched_cap = plan.sched_cap ? 1 : 0;
+    plan.rb = plan.rb < 0 ? 0 : (plan.rb ? 1 : 0);
     if (plan.level_cap < 0) plan.level_cap = 0;
   }
   int S, Sp, A, Ap, H, Hp, B;
@@ -1873,7 +1887,9 @@ struct Engine {
   // 23.37k / 23.79k / 23.91k, TD7 Humanoid 8069 / 8094 / 8060 steps/s)
   int pre_tn() const { return plan.pre_tn; }
   int pl_tn() const { return plan.pl_tn; }
-  bool fused(unsigned bit) const { return !(plan.fuse_off & bit); }
+  bool fused(unsigned bit) const {
+    return (bit & RLE_FUSE_OPT_IN) ? (plan.fuse_on & bit) != 0 : !(plan.fuse_off & bit);
+  }
   bool prelayer_ok(const Layer& L0, const Layer& L1) const {
     return fused(RLE_FUSE_PRELAYER) && L0.K <= 48 && L0.out <= 256 && L0.out % 16 == 0 && L1.seg_p.size() == 1 &&
            L1.seg_p[0] == L0.out;
@@ -2434,7 +2450,13 @@ struct Engine {
   }
 
   // ---------------------------------------------------------------- step programs
-  void add_sampling(Prog& pg, bool sac, int ahead) {
+  // The previous step's LAP priority update, applied by the sampler (SampleArgs::pend_*)
+  struct PendUpd {
+    const long long* ind;
+    const float* p;
+    int ind_id, p_id;
+  };
+  void add_sampling(Prog& pg, bool sac, int ahead, const PendUpd* pu = nullptr) {
     // LAP block sums are maintained by every priority write (OP_PRIORITY, appends)
     Op op{};
     op.kind = OP_SAMPLE_GATHER;
@@ -2442,7 +2464,15 @@ struct Engine {
     op.sample.ahead = ahead;
     op.wg_count = cdiv(B, 4);  // one wave per query
     // reads the RNG step / tape position counters -> ordered before STEP_END (WAR)
-    pg.add(op, {bsum_id, R_PRIO, R_REPLAY, R_CNT}, {ss.id, act_in.id, rw.id, nd.id, ind_id});
+    std::vector<int> rd{bsum_id, R_PRIO, R_REPLAY, R_CNT};
+    if (pu) {
+      op.sample.pend_ind = pu->ind;
+      op.sample.pend_p = pu->p;
+      op.sample.pend_n = B;
+      rd.push_back(pu->ind_id);
+      rd.push_back(pu->p_id);
+    }
+    pg.add(op, rd, {ss.id, act_in.id, rw.id, nd.id, ind_id});
     Op nz{};
     nz.kind = OP_NOISE;
     fill_sample_args(nz.sample, sac);
@@ -2591,10 +2621,42 @@ struct Engine {
   // TD7 (td7.py:287-332)
   // Next step's batch into the other buffer set, after this step's priority update
   // (RAW on the priorities) and before STEP_END bumps the counters (WAR).
-  void add_prefetch(Prog& pg, bool sac, int set) {
+  void add_prefetch(Prog& pg, bool sac, int set, const PendUpd* pu = nullptr) {
     use_set(1 - set);
-    add_sampling(pg, sac, 1);
+    add_sampling(pg, sac, 1, pu);
     use_set(set);
+  }
+  // LAPReplayMemory.update_priority (lap.py:66-69) of this step's batch, then the next step's batch.
+  // Fused (RLE_FUSE_PRIOSAMPLE): the sampler applies the update to what its search reads, and the
+  // OP_PRIORITY that persists it runs after the sampler, off the step-to-step chain.
+  bool prio_sample_fused() const {
+    int ns = 64;  // (kernels.hip pend_prepare's LDS layout, within rle_level's 24 KB)
+    while (ns < 2 * B) ns <<= 1;
+    return fused(RLE_FUSE_PRIOSAMPLE) && replay->lap && B <= 1024 &&
+           std::max(8 * ns, 20 * B) + 12 * replay->nblk <= 24 * 1024;
+  }
+  void add_update_and_prefetch(Prog& pg, bool sac, int set, bool lap, const View& prio) {
+    Op op{};
+    op.kind = OP_PRIORITY;
+    op.prio.priority = replay->priority;
+    op.prio.ind = ind;
+    op.prio.p = prio.p;
+    op.prio.B = B;
+    op.prio.max_priority = replay->maxp_d;
+    op.prio.bsum = replay->lap ? replay->bsum : nullptr;
+    op.prio.ssum = replay->ssum;
+    op.wg_count = 1;
+    const std::vector<int> rd{prio.id, ind_id}, wr{R_PRIO, R_MAXP, bsum_id};
+    if (!lap) {
+      add_prefetch(pg, sac, set);
+    } else if (prio_sample_fused()) {
+      const PendUpd pu{ind, prio.p, ind_id, prio.id};
+      add_prefetch(pg, sac, set, &pu);
+      pg.add(op, rd, wr);
+    } else {
+      pg.add(op, rd, wr);
+      add_prefetch(pg, sac, set);
+    }
   }
   void build_prime(Prog& pg, bool sac, int set) {
     use_set(set);
@@ -2811,20 +2873,7 @@ struct Engine {
         }
       }
     }
-    if (lap) {
-      Op op{};
-      op.kind = OP_PRIORITY;
-      op.prio.priority = replay->priority;
-      op.prio.ind = ind;
-      op.prio.p = prio.p;
-      op.prio.B = B;
-      op.prio.max_priority = replay->maxp_d;
-      op.prio.bsum = replay->lap ? replay->bsum : nullptr;
-      op.prio.ssum = replay->ssum;
-      op.wg_count = 1;
-      pg.add(op, {prio.id, ind_id}, {R_PRIO, R_MAXP, bsum_id});
-    }
-    add_prefetch(pg, false, set);
+    add_update_and_prefetch(pg, false, set, lap, prio);
     for (int n = 0; n < 2; ++n) {  // critic backward + Adam (optim_q_fns spans q1 + q2)
       Net& Q = *q[n];
       dw(pg, Q.layers[3], dq[n], {c2[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
@@ -3256,20 +3305,7 @@ struct Engine {
         }
       }
     }
-    if (lap) {
-      Op op{};
-      op.kind = OP_PRIORITY;
-      op.prio.priority = replay->priority;
-      op.prio.ind = ind;
-      op.prio.p = prio.p;
-      op.prio.B = B;
-      op.prio.max_priority = replay->maxp_d;
-      op.prio.bsum = replay->lap ? replay->bsum : nullptr;
-      op.prio.ssum = replay->ssum;
-      op.wg_count = 1;
-      pg.add(op, {prio.id, ind_id}, {R_PRIO, R_MAXP, bsum_id});
-    }
-    add_prefetch(pg, sac, set);
+    add_update_and_prefetch(pg, sac, set, lap, prio);
     for (int n = 0; n < 2; ++n) {
       Net& Q = *q[n];
       dw(pg, Q.layers[2], dq[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
@@ -3637,6 +3673,7 @@ struct Engine {
     tn_plan.clear();
     tn_seq = 0;
     Prog p0;
+    p0.rb = plan.rb;
     f(p0);
     std::vector<int> tplan(tn_seq, 16);
     auto at = [&](int seq) -> int& { return tplan[seq]; };
@@ -3678,6 +3715,7 @@ struct Engine {
     tn_plan = tplan;
     tn_seq = 0;
     Prog p;
+    p.rb = plan.rb;
     f(p);
     tn_plan.clear();
     return p;

@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "ops.h"
@@ -517,6 +518,86 @@ __device__ __forceinline__ void chunk_loop2(__amdgpu_buffer_rsrc_t ra, int va, _
   }
 }
 
+// ---- register-blocked wide weight-gradient tiles (GemmHot::rb, tn = 16 NB): the 4 waves split the
+// reduction (batch rows) in quarters and each wave accumulates all NB column blocks of the tile on NB
+// independent chains, so one A chunk (and, kDwNb, its AvgL1Norm-backward transform) serves NB MFMA
+// groups and a wave's operand ring covers its whole quarter in one or two rounds; the quarters are
+// summed through LDS in wave order (rb_exchange).  B block cb of chunk k at (rbr, vbv[cb] + k KB) (the
+// tile's blocks lie in one X segment: engine.cpp rb_eligible); blocks cb >= nb are outside the tile
+// (no load, no MFMA).  tabb: B scaled per reduction row from an LDS table (deferred AvgL1Norm of X);
+// NBX: A = g * ti + sgn(x) * tg per reduction row (kDwNb), x from (rx, vx).
+constexpr int kRbOff = 3200;  // LDS floats: [4 waves][NB][64 lanes][4] partials (after the tables)
+template <int NB, int RG>
+struct RbRing {
+  float4 a[RG], x[RG], b[RG][NB];
+};
+template <int NB, int RG, bool NBX>
+__device__ __forceinline__ void rb_issue(RbRing<NB, RG>& R, __amdgpu_buffer_rsrc_t ra, int va,
+                                         __amdgpu_buffer_rsrc_t rbr, const int (&vbv)[NB], int nb, int n,
+                                         __amdgpu_buffer_rsrc_t rx, int vx, bool bias_ones) {
+  const float4 ones = make_float4(1.f, 1.f, 1.f, 1.f);
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    if (r >= n) break;  // (uniform)
+    R.a[r] = bload(ra, va + r * 1024);
+    if constexpr (NBX) R.x[r] = bload(rx, vx + r * 1024);
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb)
+      if (cb < nb) R.b[r][cb] = bias_ones ? ones : bload(rbr, vbv[cb] + r * 1024);
+  }
+}
+template <int NB, int RG, bool NBX>
+__device__ __forceinline__ void rb_run(RbRing<NB, RG>& R, __amdgpu_buffer_rsrc_t ra, int va,
+                                       __amdgpu_buffer_rsrc_t rbr, const int (&vbv)[NB], int nb, int n,
+                                       f32x4 (&acc)[NB], const float* tabb, __amdgpu_buffer_rsrc_t rx, int vx,
+                                       const float* ti, const float* tg, bool bias_ones) {
+  const int rl = ((threadIdx.x & 63) >> 4) << 2;
+#pragma unroll 1
+  for (int c = 0; c < n; c += RG) {
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      const int k = c + r;
+      if (k >= n) break;  // (uniform)
+      float4 y = R.a[r];
+      if constexpr (NBX) {
+        const float4 iv = *(const float4*)(ti + k * 16 + rl), gv = *(const float4*)(tg + k * 16 + rl);
+        const float4 xv = R.x[r];
+        y = make_float4(y.x * iv.x + sgnf(xv.x) * gv.x, y.y * iv.y + sgnf(xv.y) * gv.y,
+                        y.z * iv.z + sgnf(xv.z) * gv.z, y.w * iv.w + sgnf(xv.w) * gv.w);
+      }
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) {
+        if (cb >= nb) break;
+        float4 bb = R.b[r][cb];
+        if (tabb) bb = mul4(bb, *(const float4*)(tabb + k * 16 + rl));
+        acc[cb] = mfma4(y, bb, acc[cb]);
+      }
+      const int nx = k + RG;
+      if (nx >= n) continue;
+      R.a[r] = bload(ra, va + nx * 1024);
+      if constexpr (NBX) R.x[r] = bload(rx, vx + nx * 1024);
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb)
+        if (cb < nb && !bias_ones) R.b[r][cb] = bload(rbr, vbv[cb] + nx * 1024);
+    }
+  }
+}
+// The quarters of column block cg summed in wave order (q = 0..3) into the lead wave of cg.
+template <int NB>
+__device__ __forceinline__ f32x4 rb_exchange(const f32x4 (&acc)[NB], float* smem, int cg, bool lead) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* xr = smem + kRbOff;
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb) *(f32x4*)(xr + ((wave * NB + cb) * 64 + lane) * 4) = acc[cb];
+  __syncthreads();
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (lead) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s += *(const f32x4*)(xr + ((q * NB + cg) * 64 + lane) * 4);
+  }
+  return s;
+}
+
 // A chunks from an LDS fragment image (pre-GEMM output), B from memory.
 __device__ __forceinline__ f32x4 chunk_loop_lds(const float* la, __amdgpu_buffer_rsrc_t rb, int vb, int n, f32x4 acc) {
   const int lane = threadIdx.x & 63;
@@ -899,7 +980,7 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
 }
 
 template <int MODE, int EPI, int ACT, bool NORM, int PK = 0>  // PK: 1 pre-GEMM, 2 fused loss head, 3 pre-layer
-__device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
+__device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr, unsigned hpf) {
   FINE_MARK(10);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -909,7 +990,8 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   // The same batch also touches (one dword each) every other 64-byte line of the descriptor
   // this variant reads later (segments, epilogue, Adam, pre-GEMM fields), so those loads hit
   // the scalar cache instead of each paying a dependent L2/MALL round trip (+2% steps/s).
-  // Early-clobber outputs: the base must not share SGPRs with a load still being issued.
+  // Early-clobber outputs: the base must not share SGPRs with a load still being issued.  (hpf: the
+  // hot lines' touch loads rle_level issued before the variant dispatch, kept live until this wait)
   u32x16 h0, h1;
   unsigned dsink;
 #define RLE_HOT_ASM(TOUCH)                                  \
@@ -917,7 +999,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
                "s_load_dwordx16 %1, %3, 0x40\n\t" TOUCH     \
                "s_waitcnt lgkmcnt(0)"                       \
                : "=&s"(h0), "=&s"(h1), "=&s"(dsink)         \
-               : "s"(&g.hot))
+               : "s"(&g.hot), "s"(hpf))
 #define TL(off) "s_load_dword %2, %3, " #off "\n\t"
 #define TL_A TL(0xb0) TL(0xf0) TL(0x130) TL(0x170)
 #define TL_B TL(0x1b0) TL(0x1f0) TL(0x230) TL(0x270)
@@ -966,6 +1048,9 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   const float* b0p = ptr(h1[0], h1[1]);
   const float* biasp = ptr(h1[2], h1[3]);
   const int cg = wave >> ksl, kp = wave & ((1 << ksl) - 1);
+  // register-blocked wide weight-gradient tile (GemmHot::rb; the host sets it only for tn 32 / 64)
+  constexpr bool RBOK = PK == 0 && MODE == GEMM_DW;
+  const bool rbm = RBOK && h1[10] != 0;
   int it, jt;
   if (h1[4]) {  // XCD-aware order (GemmHot::xb): residue class t % 8 -> a contiguous run p
     xcd_tile(t, (int)h0[13], tiles_n, (int)h1[4], (int)h1[5], (int)h1[9], __uint_as_float(h1[6]),
@@ -1158,6 +1243,53 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         seg(sa.p, sa.xs, sa.r0, sa.r1, wabs ? b0p : sb.p, wabs ? b0xs : sb.xs, q);
       }
     }
+  } else if (RBOK && rbm) {
+    // DW, register-blocked: every wave reduces its quarter of the batch rows for all tn / 16 column
+    // blocks; the bias tile is one block of ones
+    auto rbw = [&](auto nbt) {
+      constexpr int NB = decltype(nbt)::value, RG = NB == 4 ? 2 : 4;
+      constexpr bool NBX = ACT == kDwNb;
+      const int nq = (nch + 3) >> 2, q0 = wave * nq, q1 = min(nch, q0 + nq), nrun = max(0, q1 - q0);
+      const int jc0 = jt * tn;
+      int nb = 0;
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) nb = jc0 + cb * 16 < gN ? cb + 1 : nb;
+      if (bias_tile) nb = 1;
+      // (the tile's column blocks lie in one X segment: every segment starts at a multiple of tn)
+      int qb = 0;
+#pragma unroll
+      for (int q = 1; q < kMaxSeg; ++q)
+        if (q < nseg_b && min(jc0, gN - 1) >= g.B.seg[q].x0) qb = q;
+      const CAS Seg& sbq = g.B.seg[qb];
+      int vbv[NB];
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) vbv[cb] = ((((jc0 - sbq.x0) >> 4) + cb) * sbq.xs + q0) * 1024 + lb;
+      const int va = ((i0 >> 4) * a0xs + q0) * 1024 + lb;
+      const int vx = NBX ? ((i0 >> 4) * g.nbx_xs + q0) * 1024 + lb : 0;
+      const auto rx = NBX ? rsrc(g.nbx.t) : rsrc(a0p);
+      RbRing<NB, RG> R;
+      rb_issue<NB, RG, NBX>(R, rsrc(a0p), va, rsrc(sbq.p), vbv, nb, nrun, rx, vx, bias_tile);
+      const float* tabb = nullptr;
+      if constexpr (NORM) {  // 1/m of the reduction rows of the tile's X segment
+        if (sbq.norm.part) build_norm_tab(sbq.norm, sbq.r1 - sbq.r0, tabs);
+        __syncthreads();
+        if (sbq.norm.part && !bias_tile) tabb = tabs + q0 * 16;
+      }
+      int tgo = 0;
+      if constexpr (NBX) {
+        tgo = (gR + 15) & ~15;
+        build_nb_tab(g, gR, tabs, tabs + tgo);
+        __syncthreads();
+      }
+      f32x4 ac[NB];
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) ac[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      rb_run<NB, RG, NBX>(R, rsrc(a0p), va, rsrc(sbq.p), vbv, nb, nrun, ac, tabb, rx, vx, tabs + q0 * 16,
+                          tabs + tgo + q0 * 16, bias_tile);
+      acc = rb_exchange<NB>(ac, smem, cg, lead);
+    };
+    if (tn == 64) rbw(std::integral_constant<int, 4>{});
+    else rbw(std::integral_constant<int, 2>{});
   } else {
     // DW: A = dZ (T image, x = output row), B = X (T image, x = output column; the
     // wave's 16 columns lie in one column segment); both reduce over batch rows
@@ -1215,7 +1347,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     }
   }
   trace_mark(tr, 2);
-  if (ksl) {  // split-K: partials of splits 1.. through LDS, summed by split 0 in fixed order
+  if (ksl && !rbm) {  // split-K: partials of splits 1.. through LDS, summed by split 0 in fixed order
     if (!lead) *(f32x4*)(part + (wave * 64 + lane) * 4) = acc;
     __syncthreads();
     if (lead) {
@@ -1498,26 +1630,27 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   }
 }
 
-__device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, float* smem, unsigned long long* tr) {
+__device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, float* smem, unsigned long long* tr,
+                                        unsigned hpf) {
 #define RLE_V(mode, epi, act, norm)                      \
   case gemm_vid(mode, epi, act, norm):                   \
     asm volatile("; gemm variant " #mode #epi #act #norm ::); \
-    gemm_v<mode, epi, act, norm>(g, t, smem, tr);        \
+    gemm_v<mode, epi, act, norm>(g, t, smem, tr, hpf);   \
     break;
 #define RLE_VP(mode, epi, act, norm)                                  \
   case gemm_vid(mode, epi, act, norm, 1):                            \
     asm volatile("; gemm variant pre " #mode #epi #act #norm ::);    \
-    gemm_v<mode, epi, act, norm, 1>(g, t, smem, tr);                 \
+    gemm_v<mode, epi, act, norm, 1>(g, t, smem, tr, hpf);            \
     break;
 #define RLE_VL(mode, epi, act, norm)                                  \
   case gemm_vid(mode, epi, act, norm, 3):                            \
     asm volatile("; gemm variant prelayer " #mode #epi #act #norm ::); \
-    gemm_v<mode, epi, act, norm, 3>(g, t, smem, tr);                 \
+    gemm_v<mode, epi, act, norm, 3>(g, t, smem, tr, hpf);            \
     break;
 #define RLE_VH(mode, epi, act, norm)                                  \
   case gemm_vid(mode, epi, act, norm, 2):                            \
     asm volatile("; gemm variant head " #mode #epi #act #norm ::);   \
-    gemm_v<mode, epi, act, norm, 2>(g, t, smem, tr);                 \
+    gemm_v<mode, epi, act, norm, 2>(g, t, smem, tr, hpf);            \
     break;
   switch (vid) {
     RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, false)
@@ -1862,12 +1995,98 @@ __device__ __forceinline__ int first_lane(bool p) {
 __device__ __forceinline__ double readlane_d(double v, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
 }
+// The previous step's priority update applied in LDS by every sampler workgroup (SampleArgs::pend_n;
+// its OP_PRIORITY persists it one level later, off the chain): duplicates resolved as op_priority
+// (LDS hash, last writer wins), each winner's fp64 delta added to its 4096-block's delta (exact in
+// any order, as the block sums are: SURVEY Q8) and pushed on its block's list, so a query patches the
+// block sums it scans, the sub-block sums of its block and the priorities of its sub-block with the
+// values the search would read after the update.  LDS (bytes): [0, r0) the hash (2 ns ints), then
+// the winner records by batch row (key, next, new value, delta); at r0 the block deltas, then the
+// block list heads (engine.cpp prio_sample_fused checks the sizes).
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global
+// loads in flight (__syncthreads' workgroup fences would wait for those too).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+struct PendTab {
+  const int* wkey; const int* wnext; const float* wnew; const double* wdel; const double* bdel; const int* bhead;
+};
+__device__ __forceinline__ PendTab pend_prepare(const CAS SampleArgs& s, float* smem) {
+  const int tid = threadIdx.x, n = s.pend_n;
+  int ns = 64;
+  while (ns < 2 * n) ns <<= 1;  // hash slots: load factor <= 1/2
+  const int r0 = max(8 * ns, 20 * n);
+  char* L = (char*)smem;
+  int* keys = (int*)L;
+  int* last = keys + ns;
+  int* wkey = (int*)L;  // (records: after the hash is dead)
+  int* wnext = wkey + n;
+  float* wnew = (float*)(wnext + n);
+  double* wdel = (double*)(L + 12 * n);  // (12 n: 8-aligned, n a multiple of 16)
+  const int nbc = (int)((s.cap + kBlk - 1) / kBlk);
+  double* bdel = (double*)(L + r0);
+  int* bhead = (int*)(bdel + nbc);
+  int key[4];
+  float pn[4], po[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {  // (B <= 1024: at most 4 updates per thread)
+    const int b = tid + u * kThreads;
+    key[u] = b < n ? (int)G(s.pend_ind)[b] : 0;
+    pn[u] = b < n ? G(s.pend_p)[b] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) po[u] = tid + u * kThreads < n ? G(s.priority)[key[u]] : 0.f;  // (every update's)
+  for (int i = tid; i < ns; i += kThreads) {
+    keys[i] = -1;
+    last[i] = -1;
+  }
+  for (int i = tid; i < nbc; i += kThreads) {
+    bdel[i] = 0.0;
+    bhead[i] = -1;
+  }
+  lds_barrier();
+  int slot[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int b = tid + u * kThreads;
+    slot[u] = 0;
+    if (b >= n) continue;
+    int h = (int)(((unsigned)key[u] * 2654435761u) >> 21) & (ns - 1);
+    while (true) {
+      const int old = atomicCAS(&keys[h], -1, key[u]);
+      if (old == -1 || old == key[u]) break;
+      h = (h + 1) & (ns - 1);
+    }
+    atomicMax(&last[h], b);
+    slot[u] = h;
+  }
+  lds_barrier();
+  bool win[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) win[u] = tid + u * kThreads < n && last[slot[u]] == tid + u * kThreads;
+  lds_barrier();  // (the hash is dead)
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (win[u]) {
+      const int b = tid + u * kThreads, blk = key[u] / kBlk;
+      const double d = (double)pn[u] - (double)po[u];
+      atomicAdd(&bdel[blk], d);
+      wkey[b] = key[u];
+      wnew[b] = pn[u];
+      wdel[b] = d;
+      wnext[b] = atomicExch(&bhead[blk], b);  // (list order: any -- every use below is exact in any order)
+    }
+  lds_barrier();
+  return PendTab{wkey, wnext, wnew, wdel, bdel, bhead};
+}
+
 __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t, float* smem, unsigned long long* tr) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = t * 4 + wave;  // query (wave-uniform)
-  if (b >= s.B) return;
-  const long long size = sload(s.size);
   const int tape = sload(s.tape_mode);
+  // (uniform over the workgroup: every wave takes part in the fused update's LDS phases)
+  const bool pend = s.pend_n > 0 && s.lap && !(tape & kTapeInd);
+  if (!pend && b >= s.B) return;
+  const bool live = b < s.B;  // (wave-uniform; a wave past the batch only helps with the update)
+  const long long size = sload(s.size);
   const long long pos = sload(s.tape_pos) + s.ahead;
   const uint2 key = make_uint2((unsigned)s.seed, (unsigned)(s.seed >> 32));
   const unsigned long long step = (unsigned long long)sload(s.ctrl_rng) + s.ahead;
@@ -1884,9 +2103,16 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t,
     for (int q = 0; q < 16; ++q) bs[q] = q < per ? G(s.bsum)[min(lane * per + q, nbc - 1)] : 0.0;  // (per: uniform)
   }
   float u = 0.f;
-  if (!tind) {
+  if (!tind && live) {
     if (tape & kTapeU) u = sload(s.tape_u + (size_t)pos * s.B + b);
     else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
+  }
+  PendTab pt{};
+  if (pend) {  // (after the block-sum loads and u: they stay in flight through its LDS phases)
+    pt = pend_prepare(s, smem);
+    if (!live) return;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) bs[q] += q < per ? pt.bdel[min(lane * per + q, nbc - 1)] : 0.0;
   }
   FINE_MARK(1);
   long long ind;
@@ -1933,7 +2159,10 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t,
       FINE_MARK(2);
       // level 2: the block's 64 sub-blocks, one per lane
       const int nsub = (int)min((long long)(kBlk / kSub), (size - (long long)blk * kBlk + kSub - 1) / kSub);
-      const double sv = lane < nsub ? G(s.ssum)[(size_t)blk * (kBlk / kSub) + lane] : 0.0;
+      double sv = lane < nsub ? G(s.ssum)[(size_t)blk * (kBlk / kSub) + lane] : 0.0;
+      const int pj0 = pend ? pt.bhead[blk] : -1;
+      for (int j = pj0; j >= 0; j = pt.wnext[j])  // (the update's rows in this block: ~B / blocks of them)
+        if (((pt.wkey[j] & (kBlk - 1)) >> 6) == lane) sv += pt.wdel[j];
       inc = wave_scan_incl_d(sv);
       const int l2 = first_lane(lane < nsub && ((float)(base + inc) >= v || lane == nsub - 1));
       const int sub = max(l2, 0);
@@ -1941,7 +2170,9 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t,
       FINE_MARK(3);
       // level 3: the sub-block's 64 priorities, one per lane
       const long long e = (long long)blk * kBlk + (long long)sub * kSub + lane;
-      const float pv = e < size ? G(s.priority)[e] : 0.f;
+      float pv = e < size ? G(s.priority)[e] : 0.f;
+      for (int j = pj0; j >= 0; j = pt.wnext[j])
+        if (pt.wkey[j] == (int)e) pv = pt.wnew[j];
       inc = wave_scan_incl_d((double)pv);
       const int l3 = first_lane(e < size && (float)(base + inc) >= v);
       ind = l3 < 0 ? size - 1 : (long long)blk * kBlk + (long long)sub * kSub + l3;
@@ -2336,6 +2567,11 @@ __device__ __forceinline__ void op_foldbias(const CAS FoldBiasArgs& f) {
 // (-mllvm -amdgpu-kernarg-preload-count=14, Makefile): a workgroup knows its op without
 // a kernel-argument load; its first memory access is its op's descriptor.
 static_assert(kLevelOps == 12, "rle_level takes the op table as 12 scalar arguments");
+#ifndef RLE_NO_HOT_EARLY
+#define HOT_EARLY 1
+#else
+#define HOT_EARLY 0
+#endif
 template <bool TRACE>
 #ifndef RLE_WAVES
 #define RLE_WAVES 4  // waves per SIMD the register allocation must allow (4 workgroups per CU)
@@ -2345,7 +2581,7 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
                                                                   unsigned e8, unsigned e9, unsigned e10, unsigned e11,
                                                                   const Op* ops_arg, unsigned long long* trace_arg,
                                                                   const Op* next_arg, unsigned next_lines) {
-  __shared__ __attribute__((aligned(16))) float smem[6144];  // 24 KB
+  __shared__ __attribute__((aligned(16))) float smem[kRbOff + 4096];  // 28.5 KB
   // op of this workgroup from the (preloaded) entry table: straight-line selects over SGPRs
   const unsigned long long t_in = TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;  // before any load
   // Entry 0 bit 31: the launch leads with 8 workgroups that only load the next launch's
@@ -2402,6 +2638,17 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
         : "s"(&op));
     (void)dsink;
   }
+  // GEMM: the descriptor lines of the hot header (GemmHot: op + 0x10 .. 0x8f) requested before the
+  // variant dispatch (a compare tree of far branches, instruction-cache misses at each): gemm_v's hot
+  // batch then finds them in flight or in the scalar cache.  hpf stays live until that batch's wait.
+  unsigned hpf = 0;
+  if (kind == OP_GEMM && HOT_EARLY)
+    asm volatile(
+        "s_load_dword %0, %1, 0x10\n\t"
+        "s_load_dword %0, %1, 0x50\n\t"
+        "s_load_dword %0, %1, 0x80"
+        : "=&s"(hpf)
+        : "s"(&op));
   FINE_MARK(7);
   switch (kind) {
 #define RLE_OP(K, call)                       \
@@ -2410,9 +2657,9 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     call;                                     \
     break;
 #ifdef RLE_EXP_TWICE_GEMM  // diagnostics: the stamps of a second, cache-warm pass overwrite the first
-    RLE_OP(OP_GEMM, op_gemm(op.gemm, vid, t, smem, tr); __syncthreads(); op_gemm(op.gemm, vid, t, smem, tr))
+    RLE_OP(OP_GEMM, op_gemm(op.gemm, vid, t, smem, tr, hpf); __syncthreads(); op_gemm(op.gemm, vid, t, smem, tr, hpf))
 #else
-    RLE_OP(OP_GEMM, op_gemm(op.gemm, vid, t, smem, tr))
+    RLE_OP(OP_GEMM, op_gemm(op.gemm, vid, t, smem, tr, hpf))
 #endif
 #ifndef RLE_EXP_GEMM_ONLY
     RLE_OP(OP_NORMBWD, op_normbwd(op.nb, t))

@@ -167,7 +167,11 @@ struct GemmHot {
   int xb, tmb;                    // band width in tiles, tiles per full band (tiles_m * xb)
   float inv_tmb, inv_xb, inv_blast;
   int nfull;                      // full bands; the last band is tiles_n - nfull * xb wide
-  int pad_[6];
+  // register-blocked wide weight-gradient tile (tn 32 / 64): the 4 waves split the reduction in
+  // quarters and each accumulates every column block of the tile (kernels.hip rb_run); 0: column
+  // groups x splits
+  int rb;
+  int pad_[5];
 };
 static_assert(sizeof(GemmHot) == 128, "GemmHot is loaded as 2 x 16 dwords");
 
@@ -353,6 +357,10 @@ struct SampleArgs {
   const long long* tape_pos;
   const float* tape_u; const float* tape_eps; const float* tape_eps2; const long long* tape_ind;
   int ahead;                         // 1: draws of the NEXT step (prefetch at the end of a step)
+  // LAP: the previous step's priority update not yet applied to priority / bsum / ssum (its
+  // OP_PRIORITY runs after this op): pend_p[b] for row pend_ind[b], b < pend_n, last duplicate
+  // wins (lap.py:66-69); the search reads the sums and priorities as that update leaves them
+  const long long* pend_ind; const float* pend_p; int pend_n;
 };
 
 struct PriorityArgs {

@@ -50,45 +50,52 @@ class Plan(ctypes.Structure):
     _fields_ = [
         ("level_cap", _int), ("steps_per_graph", _int), ("pre_tn", _int), ("pl_tn", _int), ("tn_min", _int),
         ("flat_div", _int), ("balance", _int), ("tiny_w", _int), ("uni_w", _int), ("tiny_wg", _int),
-        ("sched_cap", _int), ("fuse_off", ctypes.c_uint),
+        ("sched_cap", _int), ("fuse_off", ctypes.c_uint), ("fuse_on", ctypes.c_uint), ("rb", _int),
     ]
 
 
 # RLE_FUSE_* bits of rle_plan.fuse_off
 FUSE = {"prelayer": 1 << 0, "pre": 1 << 1, "qdot": 1 << 2, "headdx": 1 << 3, "nbdefer": 1 << 4, "sacfwd": 1 << 5,
-        "sacbwd": 1 << 6, "fold": 1 << 7, "pipolyak": 1 << 8, "endsplit": 1 << 9}
+        "sacbwd": 1 << 6, "fold": 1 << 7, "pipolyak": 1 << 8, "endsplit": 1 << 9, "priosample": 1 << 10}
 
 
-def make_plan(fuse_off=(), **kw) -> Plan:
-    """rle_plan_default() with the given fields changed; fuse_off: names of FUSE to switch off."""
+def make_plan(fuse_off=(), fuse_on=(), **kw) -> Plan:
+    """rle_plan_default() with the given fields changed; fuse_off / fuse_on: names of FUSE to switch off
+    / on (fuse_on: the opt-in fusions, FUSE_OPT_IN)."""
     p = Plan()
     _check(lib().rle_plan_default(ctypes.byref(p)))
     for k, v in kw.items():
         if k not in dict(Plan._fields_):
             raise ValueError(f"unknown plan field {k!r}")
         setattr(p, k, int(v))
-    bits = 0
-    for name in ([fuse_off] if isinstance(fuse_off, str) else fuse_off):
-        bits |= FUSE[name]
-    p.fuse_off = bits
+    def bits(names):
+        b = 0
+        for name in ([names] if isinstance(names, str) else names):
+            b |= FUSE[name]
+        return b
+
+    p.fuse_off, p.fuse_on = bits(fuse_off), bits(fuse_on)
     return p
 
 
 def parse_plan(text: str) -> Plan:
     """'level_cap=512,steps_per_graph=4,fuse_off=headdx+qdot' -> Plan (bench.py --plan, tools)."""
-    kw, off = {}, ()
+    kw, off, on = {}, (), ()
     for item in filter(None, (t.strip() for t in (text or "").split(","))):
         k, _, v = item.partition("=")
         if k == "fuse_off":
             off = tuple(filter(None, v.split("+")))
+        elif k == "fuse_on":
+            on = tuple(filter(None, v.split("+")))
         else:
             kw[k] = int(v)
-    return make_plan(off, **kw)
+    return make_plan(off, on, **kw)
 
 
 def plan_dict(p: Plan) -> dict:
     d = {k: getattr(p, k) for k, _ in Plan._fields_}
     d["fuse_off"] = [n for n, b in FUSE.items() if p.fuse_off & b]
+    d["fuse_on"] = [n for n, b in FUSE.items() if p.fuse_on & b]
     return d
 
 

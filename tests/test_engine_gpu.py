@@ -383,13 +383,40 @@ def test_multistep_burst_matches_oracle(alg, env, n, B, extra):
     """Full-size burst through the multi-step graphs (TD3: one 16-step graph + 2 single steps;
     SAC: one 8-step graph + 1; TD7: single steps + 6-step graphs, with the production tile planner)
     against the oracle stepped one taped step at a time on the same draws."""
+    _burst_vs_oracle(alg, env, n, B, extra)
+
+
+OPT_PLANS = {"priosample": dict(fuse_on=["priosample"]), "rb": dict(rb=1),
+             "priosample+rb": dict(fuse_on=["priosample"], rb=1)}
+
+
+@pytest.mark.parametrize("plan", list(OPT_PLANS))
+@pytest.mark.parametrize("alg,env,n,B", [("td7", "Humanoid-v4", 13, 256), ("td7", "Humanoid-v4", 8, 1024),
+                                         ("td3", "HalfCheetah-v4", 18, 256), ("sac", "Humanoid-v4", 9, 256)])
+def test_opt_in_plans_match_oracle(alg, env, n, B, plan):
+    """The opt-in plan choices on full-size bursts against the oracle: the LAP priority update applied by
+    the next batch's sampler (RLE_FUSE_PRIOSAMPLE, exact: the same indices) and the register-blocked
+    weight-gradient tiles (rle_plan rb)."""
+    _burst_vs_oracle(alg, env, n, B, {}, E.make_plan(**OPT_PLANS[plan]))
+
+
+@pytest.mark.parametrize("burst", [False, True], ids=["per_step", "burst"])
+@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "td7_humanoid", "td7_humanoid_64k"])
+def test_fused_priority_sampler_matches_reference(name, burst):
+    """RLE_FUSE_PRIOSAMPLE against the reference goldens: the sampler applies the step's priority
+    update (duplicates: last writer wins) to the block sums, sub-block sums and priorities it reads,
+    so every drawn index is the reference's (lap.py:45-69); the persisted priorities follow."""
+    _trajectory(name, burst, E.make_plan(fuse_on=["priosample"]))
+
+
+def _burst_vs_oracle(alg, env, n, B, extra, plan=None):
     from oracle import agents
     from test_oracle import build_from_golden
 
     ncap = 8192 if B > 256 else 4096
     g = _synthetic_golden(alg, env, 256, B, ncap, ncap, n, alg == "td7", 91, **extra)
     _, orc, orep, tp, n_steps, B = build_from_golden(g)
-    eng, rep, tp2 = engine_from_golden(g)
+    eng, rep, tp2 = engine_from_golden(g, plan=plan)
     launches0 = eng.launch_count()
     infos_ref = []
     for t in range(n_steps):

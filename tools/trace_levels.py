@@ -22,7 +22,8 @@ from rl.nn.layout import init_agent  # noqa: E402
 ALGO = os.environ.get("RLE_TRACE_ALGO", "td7")
 S, A, H, B = (17, 6, 256, 256) if ALGO == "td3" else (376, 17, 256, 256)
 LAP = ALGO == "td7"
-eng = E.Engine(E.make_config({"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[ALGO], S, A, H, B, use_lap=LAP))
+eng = E.Engine(E.make_config({"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[ALGO], S, A, H, B, use_lap=LAP),
+               E.parse_plan(os.environ.get("RLE_PLAN", "")))  # (RLE_PLAN: the plan to trace, bench.py --plan syntax)
 for net, params in init_agent(ALGO, S, A, H, 1).items():
     for k, v in params.items():
         eng.set_param(net, k, v)
