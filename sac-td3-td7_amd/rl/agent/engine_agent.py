@@ -252,6 +252,10 @@ class EngineAgent(Agent, Sampler):
         s, a = arr("state", (B, self.state_dim)), arr("action", (B, self.action_dim))
         r, s2, d = arr("reward", (B,)), arr("next_state", (B, self.state_dim)), arr("done", (B,))
         lap = bool(self._cfg.get("use_lap")) and self.ALG != "sac"
+        # td7.py:310 / td3.py:221 assert a LAP replay before update_priority (here before the step,
+        # which runs as one device program: the reference would have stepped the encoder first)
+        assert not lap or (replay_buffer is not None and getattr(replay_buffer, "LAP", hasattr(replay_buffer, "update_priority"))), \
+            "a LAP agent's train_ops needs the LAPReplayMemory its priorities go to (td7.py:310)"
         ring = getattr(self, "_host_ring", None)
         if ring is None or ring.capacity != B or getattr(ring, "device", None) != self._device:
             ring = self._host_ring = E.Replay(B, self.state_dim, self.action_dim, lap, self._device)
@@ -269,7 +273,7 @@ class EngineAgent(Agent, Sampler):
             row = self.engine.step(1)[0]
         finally:
             self.engine.set_tapes()
-        if lap and replay_buffer is not None and hasattr(replay_buffer, "update_priority"):
+        if lap:
             import torch
 
             replay_buffer.update_priority(torch.from_numpy(ring.get_priority(B).copy()))

@@ -85,7 +85,10 @@ def _mlp(fin: int, fout: int, hidden_sizes) -> nn.Sequential:
 
 
 def _sizes(hidden_sizes):
-    return [hidden_sizes] * 2 if isinstance(hidden_sizes, int) else list(hidden_sizes)
+    sizes = [hidden_sizes] * 2 if isinstance(hidden_sizes, int) else list(hidden_sizes)
+    if len(sizes) != 2:  # (make_mlp takes any depth, mlp.py:10-35; the engine's step programs have two)
+        raise NotImplementedError(f"hidden_sizes {sizes}: the engine builds MLPs of two hidden layers")
+    return sizes
 
 
 class MLPActor(nn.Module):

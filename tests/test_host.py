@@ -66,7 +66,9 @@ def test_info_rows_map_to_reference_keys():
     assert math.isnan(nan_loss["train/q_fn"])  # a diverged loss stays NaN, only policy keys go None
 
 
-def test_train_ops_rejects_batches_not_drawn_from_a_device_replay():
+def test_train_ops_rejects_malformed_batches_and_foreign_replays():
+    """A BATCH dict without the reference's keys (annotation.py:23-30), or a device batch drawn from
+    another replay than the one passed, is a ValueError."""
     td7 = TD7.__new__(TD7)
     with pytest.raises(ValueError):
         td7.train_ops({"state": np.zeros((4, 3))}, None)
@@ -76,15 +78,21 @@ def test_train_ops_rejects_batches_not_drawn_from_a_device_replay():
         td7.train_ops(batch, rep_b)
 
 
-def test_engine_agents_reject_custom_nets():
-    """make_nn hooks must return the reference's default net types (rl.nn.*), checked before any
-    engine exists."""
+def test_engine_agents_reject_non_default_net_types():
+    """make_nn hooks must return the reference's default net types (rl.nn.*) of two hidden layers of one
+    width, checked before any engine exists; anything else is a clear NotImplementedError."""
     with pytest.raises(TypeError):
         TD3("HalfCheetah-v4", make_nn=lambda **k: None)
     import torch
 
+    from rl.nn import MLPActor, MLPCritic
+
     with pytest.raises(NotImplementedError):
         TD3("HalfCheetah-v4", make_nn=lambda state_dim, action_dim, **k: (torch.nn.Linear(1, 1),) * 3)
+    with pytest.raises(NotImplementedError, match="two hidden layers"):
+        TD3("HalfCheetah-v4", make_nn=lambda state_dim, action_dim, **k: (
+            MLPActor(state_dim, action_dim, [64, 64, 64]), MLPCritic(state_dim, action_dim, 64),
+            MLPCritic(state_dim, action_dim, 64)))
 
 
 def test_missing_library_fails_loudly(tmp_path, monkeypatch):
