@@ -32,12 +32,14 @@
 namespace rle {
 // next_ops / next_nops: descriptors of the level launched after this one (prefetched into
 // every XCD's L2 during this level; 0: none)
+// ext: the extended kernel instance (register-blocked / 32-row tiles, fused priority sampler)
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
-                        unsigned long long* trace = nullptr, const Op* next_ops = nullptr, int next_nops = 0);
+                        unsigned long long* trace = nullptr, const Op* next_ops = nullptr, int next_nops = 0,
+                        bool ext = false);
 int level_capacity();
 int trace_stride();
 extern std::vector<LevelLaunch>* g_level_rec;
-const char* level_kernel_symbol();
+const char* level_kernel_symbol(bool ext);
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count,
@@ -1205,7 +1207,7 @@ struct Prog {
   }
 };
 
-// ---- Direct AQL dispatch (RLE_AQL=1, an A/B of the launch path): the step graphs' level
+// ---- Direct AQL dispatch (default; RLE_AQL=0 for the hipGraph path): the step graphs' level
 // launches written as kernel-dispatch packets into the engine's own HSA queue instead of
 // hipGraph replays, with chosen fence scopes (RLE_AQL_ACQ / RLE_AQL_REL: 0 none, 1 agent,
 // 2 system; default agent / agent, as HIP's own).  The first packet of a flush acquires and its
@@ -1215,12 +1217,13 @@ struct AqlQueue {
   hsa_agent_t agent{};
   hsa_queue_t* q = nullptr;
   hsa_signal_t sig{};
-  uint64_t kobj = 0;
-  uint32_t gseg = 0, pseg = 0;
+  uint64_t kobj[2] = {0, 0};  // rle_level<false, ext>
+  uint32_t gseg[2] = {0, 0}, pseg[2] = {0, 0};
   int acq = HSA_FENCE_SCOPE_AGENT, rel = HSA_FENCE_SCOPE_AGENT;
   struct Pending {
     const void* ka;
     unsigned grid;
+    int ext;
   };
   std::vector<Pending> pending;
   ~AqlQueue() {
@@ -1249,13 +1252,14 @@ static hsa_status_t aql_find_gpu(hsa_agent_t a, void* data) {
 }
 struct AqlFind {
   hsa_agent_t agent;
+  const char* name;
   uint64_t kobj;
   uint32_t gseg, pseg;
 };
 static hsa_status_t aql_find_kernel(hsa_executable_t exe, void* data) {
   auto* f = static_cast<AqlFind*>(data);
   hsa_executable_symbol_t sym;
-  if (hsa_executable_get_symbol_by_name(exe, level_kernel_symbol(), &f->agent, &sym) == HSA_STATUS_SUCCESS) {
+  if (hsa_executable_get_symbol_by_name(exe, f->name, &f->agent, &sym) == HSA_STATUS_SUCCESS) {
     hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &f->kobj);
     hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &f->gseg);
     hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &f->pseg);
@@ -1276,12 +1280,14 @@ static std::unique_ptr<AqlQueue> aql_open(int dev) {
   A->agent = want.second;
   hsa_ven_amd_loader_1_03_pfn_t tbl;
   HSACHK(hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof(tbl), &tbl));
-  AqlFind f{A->agent, 0, 0, 0};
-  tbl.hsa_ven_amd_loader_iterate_executables(aql_find_kernel, &f);
-  REQUIRE(f.kobj, "aql: rle_level's kernel object is not loaded");
-  A->kobj = f.kobj;
-  A->gseg = f.gseg;
-  A->pseg = f.pseg;
+  for (int x = 0; x < 2; ++x) {
+    AqlFind f{A->agent, level_kernel_symbol(x != 0), 0, 0, 0};
+    tbl.hsa_ven_amd_loader_iterate_executables(aql_find_kernel, &f);
+    REQUIRE(f.kobj, "aql: rle_level's kernel object is not loaded");
+    A->kobj[x] = f.kobj;
+    A->gseg[x] = f.gseg;
+    A->pseg[x] = f.pseg;
+  }
   uint32_t qmax = 0;
   HSACHK(hsa_agent_get_info(A->agent, HSA_AGENT_INFO_QUEUE_MAX_SIZE, &qmax));
   HSACHK(hsa_queue_create(A->agent, std::min<uint32_t>(qmax, 16384), HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
@@ -1315,9 +1321,10 @@ static void aql_flush(AqlQueue& A, double* ms) {
     pk->grid_size_x = A.pending[i].grid * kThreads;
     pk->grid_size_y = 1;
     pk->grid_size_z = 1;
-    pk->private_segment_size = A.pseg;
-    pk->group_segment_size = A.gseg;
-    pk->kernel_object = A.kobj;
+    const int x = A.pending[i].ext;
+    pk->private_segment_size = A.pseg[x];
+    pk->group_segment_size = A.gseg[x];
+    pk->kernel_object = A.kobj[x];
     pk->kernarg_address = const_cast<void*>(A.pending[i].ka);
     pk->reserved2 = 0;
     const bool last = i + 1 == n;
@@ -1401,6 +1408,9 @@ struct Engine {
   rle_config cfg;
   rle_plan plan = plan_defaults();  // (resolved: no field left "default")
   // Defaults of the fields left at "default" for this engine's algorithm (rle.h rle_plan).
+  // The extended kernel instance runs this engine's programs when its plan uses what only that
+  // instance compiles: register-blocked weight-gradient tiles, the fused priority sampler.
+  bool ext_kernels() const { return plan.rb || (plan.fuse_on & RLE_FUSE_PRIOSAMPLE); }
   void resolve_plan() {
     if (plan.steps_per_graph < 0) plan.steps_per_graph = algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 6;
     if (plan.pre_tn == 0) plan.pre_tn = algo == RLE_TD3 ? 64 : 32;
@@ -3613,7 +3623,7 @@ struct Engine {
       const size_t ln = l + 1 < levels.size() ? l + 1 : 0;
       hipError_t e = launch_level(G.d_ops + G.off[l], levels[l].data(), G.nops[l], G.nwg[l], stream,
                                   G.trace ? G.trace + tr_off * trace_stride() : nullptr, G.d_ops + G.off[ln],
-                                  dpf ? G.nops[ln] : 0);
+                                  dpf ? G.nops[ln] : 0, ext_kernels());
       tr_off += G.nwg[l];
       if (e != hipSuccess) {
         g_level_rec = nullptr;
@@ -3816,10 +3826,13 @@ struct Engine {
   long long launches = 0;  // rle_level dispatches enqueued by step graphs (rle_launch_count)
   std::unique_ptr<AqlQueue> aql;  // (RLE_AQL=1) direct dispatch of the step graphs
   bool aql_active = false;        // inside step(): graphs go to the AQL queue
+  // Direct AQL dispatch of the step graphs (synchronous rle_step / rle_step_timed; rle_step_async keeps
+  // hipGraph replays, which order themselves on the engine's stream).  RLE_AQL=0: hipGraph everywhere
+  // (A/B; the launch path does not change any result).
   static bool aql_mode() {
     static const bool on = [] {
       const char* e = std::getenv("RLE_AQL");
-      return e && e[0] == '1';
+      return !(e && e[0] == '0');
     }();
     return on;
   }
@@ -3829,13 +3842,14 @@ struct Engine {
       return e && e[0] == '1';
     }();
     if (aql_active && !G.aql.empty()) {
-      for (size_t i = 0; i < G.aql.size(); ++i) aql->pending.push_back({G.aql_ka + i * 128, G.aql[i].grid});
+      for (size_t i = 0; i < G.aql.size(); ++i) aql->pending.push_back({G.aql_ka + i * 128, G.aql[i].grid, G.aql[i].ext});
       launches += G.nlaunch;
       return;
     }
     if (eager && !G.trace) {
       for (size_t l = 0; l < G.host_levels.size(); ++l)
-        HIPCHK(launch_level(G.d_ops + G.off[l], G.host_levels[l].data(), G.nops[l], G.nwg[l], stream));
+        HIPCHK(launch_level(G.d_ops + G.off[l], G.host_levels[l].data(), G.nops[l], G.nwg[l], stream, nullptr,
+                            nullptr, 0, ext_kernels()));
     } else {
       HIPCHK(hipGraphLaunch(G.x, stream));
     }

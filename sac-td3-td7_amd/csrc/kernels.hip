@@ -526,7 +526,13 @@ __device__ __forceinline__ void chunk_loop2(__amdgpu_buffer_rsrc_t ra, int va, _
 // tile's blocks lie in one X segment: engine.cpp rb_eligible); blocks cb >= nb are outside the tile
 // (no load, no MFMA).  tabb: B scaled per reduction row from an LDS table (deferred AvgL1Norm of X);
 // NBX: A = g * ti + sgn(x) * tg per reduction row (kDwNb), x from (rx, vx).
-constexpr int kRbOff = 3200;  // LDS floats: [4 waves][NB][64 lanes][4] partials (after the tables)
+// LDS floats: [4 waves][NB][64 lanes][4] partials, over the tables (rb_exchange waits for every
+// wave's loop first)
+#ifdef RLE_RB_OWN_LDS
+constexpr int kRbOff = 3200;
+#else
+constexpr int kRbOff = 2048;
+#endif
 template <int NB, int RG>
 struct RbRing {
   float4 a[RG], x[RG], b[RG][NB];
@@ -587,6 +593,9 @@ template <int NB>
 __device__ __forceinline__ f32x4 rb_exchange(const f32x4 (&acc)[NB], float* smem, int cg, bool lead) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* xr = smem + kRbOff;
+#ifndef RLE_RB_OWN_LDS
+  __syncthreads();  // (every wave is done with the tables this region overlaps)
+#endif
 #pragma unroll
   for (int cb = 0; cb < NB; ++cb) *(f32x4*)(xr + ((wave * NB + cb) * 64 + lane) * 4) = acc[cb];
   __syncthreads();
@@ -979,8 +988,10 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
   return acc + acc1;
 }
 
-template <int MODE, int EPI, int ACT, bool NORM, int PK = 0>  // PK: 1 pre-GEMM, 2 fused loss head, 3 pre-layer
-__device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr, unsigned hpf) {
+// EXT: the extended instance of rle_level (register-blocked weight-gradient tiles, 32-row tiles); the
+// production instance compiles without them, so their registers do not shape its allocation
+template <int MODE, int EPI, int ACT, bool NORM, int PK = 0, bool EXT = false>  // PK: 1 pre-GEMM, 2 fused loss head, 3 pre-layer
+__device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
   FINE_MARK(10);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -990,8 +1001,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   // The same batch also touches (one dword each) every other 64-byte line of the descriptor
   // this variant reads later (segments, epilogue, Adam, pre-GEMM fields), so those loads hit
   // the scalar cache instead of each paying a dependent L2/MALL round trip (+2% steps/s).
-  // Early-clobber outputs: the base must not share SGPRs with a load still being issued.  (hpf: the
-  // hot lines' touch loads rle_level issued before the variant dispatch, kept live until this wait)
+  // Early-clobber outputs: the base must not share SGPRs with a load still being issued.
   u32x16 h0, h1;
   unsigned dsink;
 #define RLE_HOT_ASM(TOUCH)                                  \
@@ -999,7 +1009,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
                "s_load_dwordx16 %1, %3, 0x40\n\t" TOUCH     \
                "s_waitcnt lgkmcnt(0)"                       \
                : "=&s"(h0), "=&s"(h1), "=&s"(dsink)         \
-               : "s"(&g.hot), "s"(hpf))
+               : "s"(&g.hot))
 #define TL(off) "s_load_dword %2, %3, " #off "\n\t"
 #define TL_A TL(0xb0) TL(0xf0) TL(0x130) TL(0x170)
 #define TL_B TL(0x1b0) TL(0x1f0) TL(0x230) TL(0x270)
@@ -1049,7 +1059,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   const float* biasp = ptr(h1[2], h1[3]);
   const int cg = wave >> ksl, kp = wave & ((1 << ksl) - 1);
   // register-blocked wide weight-gradient tile (GemmHot::rb; the host sets it only for tn 32 / 64)
-  constexpr bool RBOK = PK == 0 && MODE == GEMM_DW;
+  constexpr bool RBOK = EXT && PK == 0 && MODE == GEMM_DW;
   const bool rbm = RBOK && h1[10] != 0;
   int it, jt;
   if (h1[4]) {  // XCD-aware order (GemmHot::xb): residue class t % 8 -> a contiguous run p
@@ -1358,47 +1368,50 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
 
   // ---- epilogue
   if constexpr (EPI == EPI_STORE || EPI == EPI_QDOT) {
-    float rowabs[4] = {0.f, 0.f, 0.f, 0.f};
-    if (jok) {
-      float y[4];
+    auto epi_store = [&](const f32x4 acc, const int i0, const int ib, const float4 ds, float* red) {
+      float rowabs[4] = {0.f, 0.f, 0.f, 0.f};
+      if (jok) {
+        float y[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) y[q] = acc[q] + pre_b;
-      if constexpr (MODE == GEMM_FWD) {
-        if (g.pre.t) mat_st4(g.pre, ib, j, make_float4(y[0], y[1], y[2], y[3]));
+        for (int q = 0; q < 4; ++q) y[q] = acc[q] + pre_b;
+        if constexpr (MODE == GEMM_FWD) {
+          if (g.pre.t) mat_st4(g.pre, ib, j, make_float4(y[0], y[1], y[2], y[3]));
 #pragma unroll
-        for (int q = 0; q < 4; ++q) y[q] = act_f<ACT>(y[q]);
-        if constexpr (ACT == ACT_TANH) {
-          if (g.noise.t && ib >= g.noise_row0) {  // target policy smoothing (td7.py:188-194)
-            const float4 e = mat_ld4(g.noise, ib - g.noise_row0, j);
-            const float ev[4] = {e.x, e.y, e.z, e.w};
+          for (int q = 0; q < 4; ++q) y[q] = act_f<ACT>(y[q]);
+          if constexpr (ACT == ACT_TANH) {
+            if (g.noise.t && ib >= g.noise_row0) {  // target policy smoothing (td7.py:188-194)
+              const float4 e = mat_ld4(g.noise, ib - g.noise_row0, j);
+              const float ev[4] = {e.x, e.y, e.z, e.w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float nz = fminf(fmaxf(ev[q] * g.noise_sigma, -g.noise_clip), g.noise_clip);
-              y[q] = fminf(fmaxf(y[q] + nz, -1.f), 1.f);
+              for (int q = 0; q < 4; ++q) {
+                const float nz = fminf(fmaxf(ev[q] * g.noise_sigma, -g.noise_clip), g.noise_clip);
+                y[q] = fminf(fmaxf(y[q] + nz, -1.f), 1.f);
+              }
             }
           }
+        } else {  // DX: derivative mask
+          const float dv[4] = {ds.x, ds.y, ds.z, ds.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) y[q] *= act_b<ACT>(dv[q]);
         }
-      } else {  // DX: derivative mask
-        const float dv[4] = {ds.x, ds.y, ds.z, ds.w};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) y[q] *= act_b<ACT>(dv[q]);
+        for (int q = 0; q < 4; ++q) rowabs[q] = EPI == EPI_QDOT ? y[q] * qwj : fabsf(y[q]);
+        mat_st4(g.out, ib, j, make_float4(y[0], y[1], y[2], y[3]));
       }
+      if constexpr (MODE == GEMM_FWD) {
+        if (EPI == EPI_QDOT || g.norm_out) {  // |y| (EPI_QDOT: y w) summed over the tile's tn columns, per row
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rowabs[q] = EPI == EPI_QDOT ? y[q] * qwj : fabsf(y[q]);
-      mat_st4(g.out, ib, j, make_float4(y[0], y[1], y[2], y[3]));
-    }
-    if constexpr (MODE == GEMM_FWD) {
-      if (EPI == EPI_QDOT || g.norm_out) {  // |y| (EPI_QDOT: y w) summed over the tile's tn columns, per row
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rowabs[q] = row16_sum(rowabs[q]);
-        if ((lane & 15) == 0) *(float4*)(red + wave * 16 + ((lane >> 4) << 2)) =
-            make_float4(rowabs[0], rowabs[1], rowabs[2], rowabs[3]);
-        __syncthreads();
-        if (tid < 16)
-          GW(g.norm_out)[(size_t)jt * g.norm_ld + i0 + tid] =
-              (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
+          for (int q = 0; q < 4; ++q) rowabs[q] = row16_sum(rowabs[q]);
+          if ((lane & 15) == 0) *(float4*)(red + wave * 16 + ((lane >> 4) << 2)) =
+              make_float4(rowabs[0], rowabs[1], rowabs[2], rowabs[3]);
+          __syncthreads();
+          if (tid < 16)
+            GW(g.norm_out)[(size_t)jt * g.norm_ld + i0 + tid] =
+                (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
+        }
       }
-    }
+    };
+    epi_store(acc, i0, ib, ds, red);
   } else if constexpr (EPI == EPI_SACFWD) {  // op_sac_actor for the tile's 16 rows (sac.py:132-152)
     const CAS SacFwdArgs& s = g.sf;
     float y[4];
@@ -1489,19 +1502,22 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     ls = wg_sum(ls, red);
     if (tid == 0) GW(g.loss_part)[t] = t == 0 ? ls + (float)g.M * sload(g.qb) : ls;
   } else if constexpr (EPI == EPI_NBDOT) {  // sale.py:11-13 backward, first half (the rest: kDwNb)
-    float rd[4] = {0.f, 0.f, 0.f, 0.f};
-    if (jok) {
-      const float xq[4] = {nbxv.x, nbxv.y, nbxv.z, nbxv.w};
+    auto epi_nbdot = [&](const f32x4 acc, const int i0, const int ib, const float4 nbxv, float* red) {
+      float rd[4] = {0.f, 0.f, 0.f, 0.f};
+      if (jok) {
+        const float xq[4] = {nbxv.x, nbxv.y, nbxv.z, nbxv.w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rd[q] = acc[q] * xq[q];
-      mat_st4(g.out, ib, j, make_float4(acc[0], acc[1], acc[2], acc[3]));
-    }
+        for (int q = 0; q < 4; ++q) rd[q] = acc[q] * xq[q];
+        mat_st4(g.out, ib, j, make_float4(acc[0], acc[1], acc[2], acc[3]));
+      }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) rd[q] = row16_sum(rd[q]);
-    if ((lane & 15) == 0) *(float4*)(red + wave * 16 + ((lane >> 4) << 2)) = make_float4(rd[0], rd[1], rd[2], rd[3]);
-    __syncthreads();
-    if (tid < 16)
-      GW(g.norm_out)[(size_t)jt * g.norm_ld + i0 + tid] = (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
+      for (int q = 0; q < 4; ++q) rd[q] = row16_sum(rd[q]);
+      if ((lane & 15) == 0) *(float4*)(red + wave * 16 + ((lane >> 4) << 2)) = make_float4(rd[0], rd[1], rd[2], rd[3]);
+      __syncthreads();
+      if (tid < 16)
+        GW(g.norm_out)[(size_t)jt * g.norm_ld + i0 + tid] = (red[tid] + red[16 + tid]) + (red[32 + tid] + red[48 + tid]);
+    };
+    epi_nbdot(acc, i0, ib, nbxv, red);
   } else if constexpr (EPI == EPI_ACT) {  // td7.py:141-156 / td3.py:114-129: env action of the act graph
     if (jok) {
       const CAS ActArgs& ao = g.ao;
@@ -1630,27 +1646,27 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   }
 }
 
-__device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, float* smem, unsigned long long* tr,
-                                        unsigned hpf) {
+template <bool EXT>
+__device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, float* smem, unsigned long long* tr) {
 #define RLE_V(mode, epi, act, norm)                      \
   case gemm_vid(mode, epi, act, norm):                   \
     asm volatile("; gemm variant " #mode #epi #act #norm ::); \
-    gemm_v<mode, epi, act, norm>(g, t, smem, tr, hpf);   \
+    gemm_v<mode, epi, act, norm, 0, EXT>(g, t, smem, tr); \
     break;
 #define RLE_VP(mode, epi, act, norm)                                  \
   case gemm_vid(mode, epi, act, norm, 1):                            \
     asm volatile("; gemm variant pre " #mode #epi #act #norm ::);    \
-    gemm_v<mode, epi, act, norm, 1>(g, t, smem, tr, hpf);            \
+    gemm_v<mode, epi, act, norm, 1, EXT>(g, t, smem, tr);            \
     break;
 #define RLE_VL(mode, epi, act, norm)                                  \
   case gemm_vid(mode, epi, act, norm, 3):                            \
     asm volatile("; gemm variant prelayer " #mode #epi #act #norm ::); \
-    gemm_v<mode, epi, act, norm, 3>(g, t, smem, tr, hpf);            \
+    gemm_v<mode, epi, act, norm, 3, EXT>(g, t, smem, tr);            \
     break;
 #define RLE_VH(mode, epi, act, norm)                                  \
   case gemm_vid(mode, epi, act, norm, 2):                            \
     asm volatile("; gemm variant head " #mode #epi #act #norm ::);   \
-    gemm_v<mode, epi, act, norm, 2>(g, t, smem, tr, hpf);            \
+    gemm_v<mode, epi, act, norm, 2, EXT>(g, t, smem, tr);            \
     break;
   switch (vid) {
     RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, false)
@@ -2078,12 +2094,13 @@ __device__ __forceinline__ PendTab pend_prepare(const CAS SampleArgs& s, float* 
   return PendTab{wkey, wnext, wnew, wdel, bdel, bhead};
 }
 
+template <bool EXT>  // (EXT: the fused priority update, SampleArgs::pend_n)
 __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t, float* smem, unsigned long long* tr) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = t * 4 + wave;  // query (wave-uniform)
   const int tape = sload(s.tape_mode);
   // (uniform over the workgroup: every wave takes part in the fused update's LDS phases)
-  const bool pend = s.pend_n > 0 && s.lap && !(tape & kTapeInd);
+  const bool pend = EXT && s.pend_n > 0 && s.lap && !(tape & kTapeInd);
   if (!pend && b >= s.B) return;
   const bool live = b < s.B;  // (wave-uniform; a wave past the batch only helps with the update)
   const long long size = sload(s.size);
@@ -2567,12 +2584,8 @@ __device__ __forceinline__ void op_foldbias(const CAS FoldBiasArgs& f) {
 // (-mllvm -amdgpu-kernarg-preload-count=14, Makefile): a workgroup knows its op without
 // a kernel-argument load; its first memory access is its op's descriptor.
 static_assert(kLevelOps == 12, "rle_level takes the op table as 12 scalar arguments");
-#ifndef RLE_NO_HOT_EARLY
-#define HOT_EARLY 1
-#else
-#define HOT_EARLY 0
-#endif
-template <bool TRACE>
+
+template <bool TRACE, bool EXT>
 #ifndef RLE_WAVES
 #define RLE_WAVES 4  // waves per SIMD the register allocation must allow (4 workgroups per CU)
 #endif
@@ -2581,7 +2594,7 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
                                                                   unsigned e8, unsigned e9, unsigned e10, unsigned e11,
                                                                   const Op* ops_arg, unsigned long long* trace_arg,
                                                                   const Op* next_arg, unsigned next_lines) {
-  __shared__ __attribute__((aligned(16))) float smem[kRbOff + 4096];  // 28.5 KB
+  __shared__ __attribute__((aligned(16))) float smem[kRbOff + 4096 > 6144 ? kRbOff + 4096 : 6144];  // 24 KB
   // op of this workgroup from the (preloaded) entry table: straight-line selects over SGPRs
   const unsigned long long t_in = TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;  // before any load
   // Entry 0 bit 31: the launch leads with 8 workgroups that only load the next launch's
@@ -2638,17 +2651,6 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
         : "s"(&op));
     (void)dsink;
   }
-  // GEMM: the descriptor lines of the hot header (GemmHot: op + 0x10 .. 0x8f) requested before the
-  // variant dispatch (a compare tree of far branches, instruction-cache misses at each): gemm_v's hot
-  // batch then finds them in flight or in the scalar cache.  hpf stays live until that batch's wait.
-  unsigned hpf = 0;
-  if (kind == OP_GEMM && HOT_EARLY)
-    asm volatile(
-        "s_load_dword %0, %1, 0x10\n\t"
-        "s_load_dword %0, %1, 0x50\n\t"
-        "s_load_dword %0, %1, 0x80"
-        : "=&s"(hpf)
-        : "s"(&op));
   FINE_MARK(7);
   switch (kind) {
 #define RLE_OP(K, call)                       \
@@ -2657,18 +2659,18 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     call;                                     \
     break;
 #ifdef RLE_EXP_TWICE_GEMM  // diagnostics: the stamps of a second, cache-warm pass overwrite the first
-    RLE_OP(OP_GEMM, op_gemm(op.gemm, vid, t, smem, tr, hpf); __syncthreads(); op_gemm(op.gemm, vid, t, smem, tr, hpf))
+    RLE_OP(OP_GEMM, op_gemm<EXT>(op.gemm, vid, t, smem, tr); __syncthreads(); op_gemm<EXT>(op.gemm, vid, t, smem, tr))
 #else
-    RLE_OP(OP_GEMM, op_gemm(op.gemm, vid, t, smem, tr, hpf))
+    RLE_OP(OP_GEMM, op_gemm<EXT>(op.gemm, vid, t, smem, tr))
 #endif
 #ifndef RLE_EXP_GEMM_ONLY
     RLE_OP(OP_NORMBWD, op_normbwd(op.nb, t))
     RLE_OP(OP_SAMPLE_REDUCE, op_sample_reduce(op.sample, t, smem))
 #ifdef RLE_EXP_TWICE  // diagnostics: the stamps of a second, cache-warm pass overwrite the first
-    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather(op.sample, t, smem, tr); __syncthreads();
-           op_sample_gather(op.sample, t, smem, tr))
+    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather<EXT>(op.sample, t, smem, tr); __syncthreads();
+           op_sample_gather<EXT>(op.sample, t, smem, tr))
 #else
-    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather(op.sample, t, smem, tr))
+    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather<EXT>(op.sample, t, smem, tr))
 #endif
     RLE_OP(OP_HEAD, op_head(op.head, t, smem, tr))
     RLE_OP(OP_PRIORITY, op_priority(op.prio, smem))
@@ -2959,7 +2961,7 @@ int trace_stride() { return kTraceStride; }
 int level_capacity() {
   int per_cu = 0, cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false>, kThreads, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false, false>, kThreads, 0) != hipSuccess)
     return 1024;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
   return per_cu * cus;
@@ -2969,10 +2971,13 @@ int level_capacity() {
 // AQL launch lists; traced launches are never recorded)
 std::vector<LevelLaunch>* g_level_rec = nullptr;
 // the production kernel's HSA symbol name (AQL dispatch)
-const char* level_kernel_symbol() { return "_ZN3rle9rle_levelILb0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"; }
+const char* level_kernel_symbol(bool ext) {
+  return ext ? "_ZN3rle9rle_levelILb0ELb1EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"
+             : "_ZN3rle9rle_levelILb0ELb0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd";
+}
 
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
-                        unsigned long long* trace, const Op* next_ops, int next_nops) {
+                        unsigned long long* trace, const Op* next_ops, int next_nops, bool ext) {
   // a level of more than kLevelOps ops: consecutive launches of kLevelOps (its ops are
   // independent, so any split is correct)
   for (int q0 = 0; q0 < nops; q0 += kLevelOps) {
@@ -3008,13 +3013,17 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
       std::memcpy(L.ka + 64, &next, 8);
       std::memcpy(L.ka + 72, &next_lines, 4);
       L.grid = (unsigned)(w1 - w0 + npf);
+      L.ext = ext ? 1 : 0;
       g_level_rec->push_back(L);
     }
 #define RLE_LEVEL_ARGS                                                                                         \
   la.entry[0], la.entry[1], la.entry[2], la.entry[3], la.entry[4], la.entry[5], la.entry[6], la.entry[7], \
       la.entry[8], la.entry[9], la.entry[10], la.entry[11], la.ops, la.trace, next, next_lines
-    if (trace) hipLaunchKernelGGL((rle_level<true>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
-    else hipLaunchKernelGGL((rle_level<false>), dim3(w1 - w0 + npf), dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    const dim3 grid(w1 - w0 + npf);
+    if (trace && ext) hipLaunchKernelGGL((rle_level<true, true>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    else if (trace) hipLaunchKernelGGL((rle_level<true, false>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    else if (ext) hipLaunchKernelGGL((rle_level<false, true>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    else hipLaunchKernelGGL((rle_level<false, false>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
 #undef RLE_LEVEL_ARGS
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -531,6 +531,7 @@ constexpr int kMaxLevelWG = 0xfffe;  // workgroups per launch (16-bit entry fiel
 struct LevelLaunch {
   unsigned char ka[80];
   unsigned grid;  // workgroups
+  int ext;        // the extended kernel instance (rle_level<false, true>)
 };
 
 // Device control block.

@@ -389,7 +389,7 @@ def test_train_ops_on_a_host_batch_dict():
 def test_lap_agent_host_batch_needs_its_lap_replay():
     """A LAP agent's train_ops on a host BATCH dict with no LAP replay to send the priorities to fails
     as the reference's assert does (td7.py:310, td3.py:221), instead of skipping the update."""
-    ag = TD7("Tiny-v0", hidden=32, batch_size=32, seed=3)
+    ag = TD7("Tiny-v0", use_lap=True, hidden=32, batch_size=32, seed=3)
     t = _transitions(32, 9)
     batch = {k: np.array([r[i] for r in t], np.float32) for i, k in enumerate(("state", "action", "reward",
                                                                                "next_state", "done"))}

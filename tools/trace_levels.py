@@ -21,6 +21,7 @@ from rl.nn.layout import init_agent  # noqa: E402
 # RLE_TRACE_ALGO=td3 / sac: the secondary configs (TD3 HalfCheetah, SAC Humanoid; uniform replay)
 ALGO = os.environ.get("RLE_TRACE_ALGO", "td7")
 S, A, H, B = (17, 6, 256, 256) if ALGO == "td3" else (376, 17, 256, 256)
+B = int(os.environ.get("RLE_TRACE_BATCH", B))  # (BASELINE config 4: 1024)
 LAP = ALGO == "td7"
 eng = E.Engine(E.make_config({"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[ALGO], S, A, H, B, use_lap=LAP),
                E.parse_plan(os.environ.get("RLE_PLAN", "")))  # (RLE_PLAN: the plan to trace, bench.py --plan syntax)
