@@ -70,6 +70,10 @@ typedef struct rle_config {
                                         fuse_on): one level fewer per step pair, but the heavy critic
                                         weight-gradient ops then share a level with the next batch's
                                         first layers (TD7 Humanoid A/B: -4.5%)                        */
+#define RLE_FUSE_TWOSTAGE (1u << 11) /* TD3 target critics' first layer (behind the pre-GEMM target
+                                        action) recomputed in-tile by their second layer             */
+#define RLE_FUSE_SACPRE   (1u << 12) /* SAC raw head + target rsample recomputed in-tile by the target
+                                        critics' first layer                                         */
 #define RLE_FUSE_OPT_IN RLE_FUSE_PRIOSAMPLE  /* fusions off unless set in fuse_on                      */
 typedef struct rle_plan {
   int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity, TD3 3/4) */

@@ -348,7 +348,7 @@ static void gemm_finalize(GemmArgs& g) {
                                    g.sb.eps2.t && (g.sb.dout.n || g.sb.dout.t) && g.sb.log_alpha &&
                                    g.sb.ls_off >= g.sb.mean_off + g.N),
           "gemm: SAC actor backward epilogue operands");
-  REQUIRE(g.has_pre != 3 || (((g.mode == GEMM_FWD && (g.epi == EPI_STORE || g.epi == EPI_QDOT) && g.prea.bias) ||
+  REQUIRE((g.has_pre != 3 && g.has_pre != 4) || (((g.mode == GEMM_FWD && (g.epi == EPI_STORE || g.epi == EPI_QDOT) && g.prea.bias) ||
                                 (g.mode == GEMM_DX && g.epi == EPI_STORE && g.prea.dsrc.t)) &&
                                act == ACT_RELU && !norm && g.A.nseg == 1 && g.prea.seg == 0 && g.prea.mode == g.mode &&
                                g.prea.act == ACT_RELU && g.prea.N == g.A.seg[0].r1 - g.A.seg[0].r0 && g.prea.N <= 256 &&
@@ -356,8 +356,33 @@ static void gemm_finalize(GemmArgs& g) {
                                g.R == g.prea.N &&  // (<= 16 chunks per wave: kernels.hip PK 3 holds them all)
                                !g.pre.t && g.B.nseg == 1),
           "gemm: pre-layer layout");
-  REQUIRE(g.has_pre >= 0 && g.has_pre <= 3, "gemm: pre kind");
-  g.vid = gemm_vid(g.mode, g.epi, act, norm, g.has_pre);
+  {  // has_pre 4: the pre-layer's input segment prea2.seg from the pre-GEMM prea2 (kernels.hip PK 4: its
+     // output, at most 2 column blocks, in LDS; FWD with target smoothing, as pre_actor_fwd builds it)
+    const PreArgs& q = g.prea2;
+    REQUIRE(g.has_pre != 4 || (g.mode == GEMM_FWD && g.epi == EPI_QDOT && q.mode == GEMM_FWD && q.N <= 32 &&
+                               q.R % 16 == 0 && q.R <= 16 * 1024 && q.A.nseg == 1 && q.B.nseg == 1 &&
+                               q.seg == 1 && g.prea.A.nseg == 2 && g.prea.A.seg[0].r0 == 0 &&
+                               g.prea.A.seg[q.seg].r1 - g.prea.A.seg[q.seg].r0 <= 16 &&
+                               g.prea.A.seg[q.seg].r0 % 16 == 0),
+            "gemm: two-stage pre-layer layout");
+  }
+  {  // has_pre 5: SAC's raw head + rsample (kernels.hip sacraw_*, PK 5) as segment prea.seg of a ReLU forward
+    const PreArgs& q = g.prea;
+    REQUIRE(g.has_pre != 5 || (g.mode == GEMM_FWD && g.epi == EPI_STORE && act == ACT_RELU && !norm &&
+                               q.mode == GEMM_FWD && q.A.nseg == 1 && q.B.nseg == 1 && q.sac_a >= 1 &&
+                               q.N == 2 * q.sac_a && q.N <= 48 && q.R % 16 == 0 && q.R <= 256 && q.bias &&
+                               q.noise.t && q.seg < g.A.nseg && g.A.seg[q.seg].r1 - g.A.seg[q.seg].r0 <= 32 &&
+                               g.A.seg[q.seg].r1 - g.A.seg[q.seg].r0 >= q.sac_a),
+            "gemm: SAC pre-GEMM layout");
+  }
+  REQUIRE(g.epi != EPI_SACFWD || (g.R <= 256 && g.N <= 48 && g.A.nseg == 1 && g.B.nseg == 1),
+          "gemm: SAC raw head (kernels.hip sacraw_*: three column blocks, R <= 256)");
+  REQUIRE(g.has_pre >= 0 && g.has_pre <= 5, "gemm: pre kind");
+  // (has_pre 4 takes the pre-layer's id with the norm bit, which no pre-layer variant uses; has_pre 5 a
+  // pre-GEMM id with the norm bit on a ReLU forward, which no pre-GEMM consumer has)
+  g.vid = g.has_pre == 4   ? gemm_vid(g.mode, g.epi, act, 1, 3)
+          : g.has_pre == 5 ? gemm_vid(g.mode, g.epi, act, 1, 1)
+                           : gemm_vid(g.mode, g.epi, act, norm, g.has_pre);
   REQUIRE(g.tn == 16 || g.tn == 32 || g.tn == 64, "gemm: tile width");
   g.ks_log = g.tn == 16 ? 2 : (g.tn == 32 ? 1 : 0);
   REQUIRE(g.R % 16 == 0, "gemm: reduction length must be a multiple of 16");
@@ -511,7 +536,7 @@ static void audit_gemm(const GemmArgs& g) {
           if (k0 >= k1) continue;
           const int kb = wabs ? k0 : k0 - s0;
           if (!mine[0] && !mine[1] && !mine[2] && !mine[3]) continue;  // inactive wave: no loads
-          if (!((g.has_pre == 1 || g.has_pre == 3) && q == g.prea.seg)) {
+          if (!((g.has_pre == 1 || g.has_pre >= 3) && q == g.prea.seg)) {
             audit_range(sa.p, ((long long)(i0 / 16) * sa.xs + (k0 - s0)) * 1024, (long long)(k1 - k0) * 1024, "A", g);
             if (sa.norm.part) audit_norm(sa.norm, i0, 16, g);
           }
@@ -521,14 +546,16 @@ static void audit_gemm(const GemmArgs& g) {
         }
         // pre-GEMM operands (pre_issue / pre_finish): 16 rows at i0, both column blocks (has_pre 2,
         // the fused loss head, keeps HeadArgs in the same union: its reads are not audited here)
-        if (g.has_pre == 3) {  // pre-layer (prelayer_fwd): every A chunk, the wave's 4 W column blocks, bias
+        if (g.has_pre == 3 || g.has_pre == 4) {  // pre-layer (prelayer_*): every A chunk, the wave's 4 W column
+                                                 // blocks, bias (has_pre 4: segment prea2.seg from LDS)
           const PreArgs& p = g.prea;
           for (int k = 0; k < p.R / 16; ++k) {
             int q = 0;
             for (int u = 1; u < p.A.nseg; ++u)
               if (k >= p.A.seg[u].r0 / 16) q = u;
             const Seg& sa = p.A.seg[q];
-            audit_range(sa.p, ((long long)(i0 / 16) * sa.xs + (k - sa.r0 / 16)) * 1024, 1024, "prelayer A", g);
+            if (!(g.has_pre == 4 && q == g.prea2.seg))
+              audit_range(sa.p, ((long long)(i0 / 16) * sa.xs + (k - sa.r0 / 16)) * 1024, 1024, "prelayer A", g);
             for (int c = 0; c < 4; ++c)
               if ((w * 4 + c) * 16 < p.N)
                 audit_range(p.B.seg[0].p, ((long long)(w * 4 + c) * p.B.seg[0].xs + k) * 1024, 1024, "prelayer W", g);
@@ -542,8 +569,21 @@ static void audit_gemm(const GemmArgs& g) {
                 audit_range(p.dsrc.t, h_tblk(p.dsrc.rbs, i0, (w * 4 + c) * 16), 1024, "prelayer dsrc", g);
             }
         }
-        if (g.has_pre == 1) {
+        if (g.has_pre == 5) {  // sacraw_issue: the wave's 4 chunks of A and of the 3 W column blocks; bias, noise
           const PreArgs& p = g.prea;
+          const int nchp = p.R / 16, k0 = std::min(nchp, w * 4), k1 = std::min(nchp, w * 4 + 4);
+          if (k1 > k0) {
+            const Seg& sa = p.A.seg[0];
+            audit_range(sa.p, ((long long)(i0 / 16) * sa.xs + k0) * 1024, (long long)(k1 - k0) * 1024, "sacpre A", g);
+            for (int c = 0; c < 3; ++c)
+              audit_range(p.B.seg[0].p, ((long long)c * p.B.seg[0].xs + k0) * 1024, (long long)(k1 - k0) * 1024,
+                          "sacpre W", g);
+          }
+          audit_range(p.bias, 0, (long long)p.N * 4, "sacpre bias", g);
+          for (int c = 0; c < p.sac_a; c += 16) audit_range(p.noise.t, h_tblk(p.noise.rbs, i0, c), 1024, "sacpre eps", g);
+        }
+        if (g.has_pre == 1 || g.has_pre == 4) {
+          const PreArgs& p = g.has_pre == 4 ? g.prea2 : g.prea;
           const int nchp = p.R / 16, perp = (nchp + 3) / 4;
           const int c0p = w * perp, c1p = std::min(nchp, c0p + perp);
           const bool wp = p.mode == GEMM_FWD && p.B.nseg == 1;
@@ -1840,7 +1880,8 @@ struct Engine {
   struct PreUse {
     PreArgs a;
     std::vector<int> rd;
-    int kind = 1;  // GemmArgs::has_pre: 1 pre-GEMM (actor output layer), 3 pre-layer
+    int kind = 1;  // GemmArgs::has_pre: 1 pre-GEMM (actor output layer), 3 pre-layer, 4 pre-layer behind a2
+    PreArgs a2{};  // (kind 4) the pre-GEMM computing the pre-layer's input segment a2.seg
   };
   // The critic loss head fused into the DX of critic n's last hidden layer (GemmArgs::has_pre 2)
   struct HeadUse {
@@ -1887,6 +1928,38 @@ struct Engine {
     }
     return u;
   }
+  // SAC's raw head L over rows x, then the target rsample a' = tanh(mean + exp(clamp(log_std)) eps)
+  // (sac.py:132-152), as a pre-GEMM of the target critics' first layer (GemmArgs::has_pre 5): the target
+  // branch does not wait a level for the standalone EPI_SACFWD op, which still runs for the policy rows,
+  // log pi and the backward.  Both reduce the raw head in one order (kernels.hip sacraw_*).
+  PreUse pre_sac_fwd(const Layer& L, const View& x, const View& eps, int seg) {
+    REQUIRE(L.out == 2 * A && L.out <= 48 && L.K <= 256 && L.seg_p.size() == 1 && x.m.n && !x.norm && eps.m.t,
+            "pre: SAC raw head operands");
+    PreUse u{};
+    u.kind = 5;
+    PreArgs& p = u.a;
+    p.mode = GEMM_FWD;
+    p.A.seg[0] = seg_n(x, 0, L.K);
+    p.A.nseg = 1;
+    Seg w{};
+    w.p = P + L.wn_off;
+    w.xs = L.cb;
+    w.x1 = L.out;
+    w.r1 = L.K;
+    p.B.seg[0] = w;
+    p.B.nseg = 1;
+    p.N = L.out;
+    p.R = L.K;
+    p.seg = seg;
+    p.sac_a = A;
+    p.bias = bias(L);
+    p.noise = eps.m;
+    p.noise_sigma = cfg.min_log_std;
+    p.noise_clip = cfg.max_log_std;
+    u.rd = {x.id, L.res, eps.id};
+    return u;
+  }
+  bool sac_pre() const { return fused(RLE_FUSE_SACPRE) && sac_fwd_fused() && 2 * A <= 48 && H <= 256; }
   // A small-K first layer L0 (ReLU, K <= 48: TD3 / SAC on low-dimensional observations) over the
   // input segments xs, recomputed in-tile by the layer after it (prelayer_fwd): one level fewer on
   // the critic and actor chains.  The standalone L0 output stays for its other readers (the
@@ -1900,15 +1973,18 @@ struct Engine {
   bool fused(unsigned bit) const {
     return (bit & RLE_FUSE_OPT_IN) ? (plan.fuse_on & bit) != 0 : !(plan.fuse_off & bit);
   }
+  bool prelayer_shape(const Layer& L0, const Layer& L1) const {
+    return L0.K <= 48 && L0.out <= 256 && L0.out % 16 == 0 && L1.seg_p.size() == 1 && L1.seg_p[0] == L0.out;
+  }
   bool prelayer_ok(const Layer& L0, const Layer& L1) const {
-    return fused(RLE_FUSE_PRELAYER) && L0.K <= 48 && L0.out <= 256 && L0.out % 16 == 0 && L1.seg_p.size() == 1 &&
-           L1.seg_p[0] == L0.out;
+    return fused(RLE_FUSE_PRELAYER) && prelayer_shape(L0, L1);
   }
   bool prelayer_ok_dx(const Layer& L, const Layer& Lprev) const {
     return fused(RLE_FUSE_PRELAYER) && r16(L.out) <= 48 && L.K <= 256 && L.K % 16 == 0 && Lprev.out == L.K &&
            Lprev.out <= 256;
   }
-  PreUse pre_layer(const Layer& L0, const std::vector<View>& xs) {
+  // (lds_seg >= 0: input segment lds_seg is computed in-tile by a pre-GEMM -- its view gives the layout)
+  PreUse pre_layer(const Layer& L0, const std::vector<View>& xs, int lds_seg = -1) {
     REQUIRE(xs.size() == L0.seg_p.size() && L0.K <= 48, "pre-layer: operands");
     PreUse u{};
     u.kind = 3;
@@ -1919,7 +1995,7 @@ struct Engine {
       REQUIRE(xs[q].m.n && xs[q].cols == L0.seg_p[q] && !xs[q].norm, "pre-layer: input segment");
       p.A.seg[q] = seg_n(xs[q], koff, koff + L0.seg_p[q]);
       koff += L0.seg_p[q];
-      u.rd.push_back(xs[q].id);
+      if ((int)q != lds_seg) u.rd.push_back(xs[q].id);
     }
     p.A.nseg = (int)xs.size();
     Seg w{};
@@ -2033,9 +2109,11 @@ struct Engine {
     // (pl_src: this layer is also recomputed in-tile by a pre-layer consumer -- at most 32-wide tiles
     // keep its reduction split, so the stored output (the ReLU mask of the input gradient, the weight
     // gradient's operand) is the same floats as the consumer's copy, whatever the planner widens)
+    // (a pre-GEMM consumer that is also a pre-layer source: at most 32 wide, as any pl_src)
     const int tn = sfu ? 64
-                       : (pre && pre->kind == 3 ? std::max(tq.first, pl_tn())
-                          : pre && pre->kind == 1 ? std::max(tq.first, pre_tn())
+                       : (pre && pre->kind >= 3 ? std::max(tq.first, pl_tn())
+                          : pre && (pre->kind == 1 || pre->kind == 5)
+                              ? (pl_src ? std::min(std::max(tq.first, pre_tn()), 32) : std::max(tq.first, pre_tn()))
                                                   : (pl_src ? std::min(tq.first, 32) : tq.first));
     const int tiles_n = cdiv(L.out, tn);
     View out = buf(M, L.out, true, out_t);
@@ -2156,6 +2234,7 @@ struct Engine {
       if (pre) {
         g.has_pre = pre->kind;
         g.prea = pre->a;
+        if (pre->kind == 4) g.prea2 = pre->a2;
       }
       op.wg_count = g.tiles_m * g.tiles_n;
       op.seq = tq.second;
@@ -3135,17 +3214,33 @@ struct Engine {
 
   // MLP critic stack forward: returns (h0, h1)
   // qd: the last hidden layer also emits EPI_QDOT row partials of q (a fused head reads them)
+  // Behind a pre-GEMM (TD3's target critics: a' computed in-tile from the actor's last hidden layer),
+  // the first layer is recomputed in-tile by the second too, its a' segment first (two-stage prologue,
+  // GemmArgs::has_pre 4): the target branch's first layer costs no level of its own.  Without the
+  // fusion it is its own level, in at most 32-wide tiles (pl_src), so both give the same floats.
   void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, View& h0, View& h1,
                       const PreUse* pre = nullptr, bool h1_t = true, bool qd = false) {
+    const bool shape = prelayer_shape(Q.layers[0], Q.layers[1]);
+    const bool two = pre && pre->kind == 1 && pre->a.mode == GEMM_FWD && qd && prelayer_ok(Q.layers[0], Q.layers[1]) &&
+                     fused(RLE_FUSE_TWOSTAGE);
     // (not behind a pre-GEMM: the first layer's own a segment is recomputed in-tile already)
     const bool use_pl = !pre && prelayer_ok(Q.layers[0], Q.layers[1]);
-    pl_src = use_pl;
-    h0 = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pre);
-    pl_src = false;
+    if (two) {
+      h0 = buf(B, Q.layers[0].out, true, false);  // (layout of the consumer's A operand only: never stored)
+    } else {
+      pl_src = use_pl || (pre && shape);
+      h0 = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pre);
+      pl_src = false;
+    }
     const bool keep = out_t;
     out_t = keep && h1_t;  // (h1_t = false: only the head reads h1, in the N image)
-    const PreUse pl = use_pl ? pre_layer(Q.layers[0], {sv, av}) : PreUse{};
-    h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pl.kind == 3 ? &pl : nullptr,
+    PreUse pl = use_pl || two ? pre_layer(Q.layers[0], {sv, av}, two ? pre->a.seg : -1) : PreUse{};
+    if (two) {
+      pl.kind = 4;
+      pl.a2 = pre->a;
+      pl.rd.insert(pl.rd.end(), pre->rd.begin(), pre->rd.end());
+    }
+    h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pl.kind >= 3 ? &pl : nullptr,
              qd ? &Q.layers[2] : nullptr);
     out_t = keep;
   }
@@ -3256,11 +3351,14 @@ struct Engine {
       pg.add(op, {raw.id, eps.id, eps2.id}, {actv.id, logpi.id});
     }
     View a_pi = actv.sub(0, B), a_next = prea ? a_pi : actv.sub(B, B);  // (pre: layout only)
+    // SAC: the target critics' first layer recomputes a' in-tile from the raw head (pre-GEMM, has_pre 5)
+    const PreUse psac = sac && sac_pre() ? pre_sac_fwd(pi.layers[2], h1n, eps, 1) : PreUse{};
+    const PreUse* tpre = prea ? &pn1 : (psac.kind == 5 ? &psac : nullptr);
     // target critics + y
     View th0[2], th1[2];
     out_t = false;  // (forward only)
     const bool hdx = mlp_headdx();
-    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n], prea ? &pn1 : nullptr, true, hdx);
+    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n], tpre, true, hdx);
     out_t = true;
     // online critics
     View c0[2], c1[2];
@@ -3592,6 +3690,8 @@ struct Engine {
           const char* ep = op.gemm.mode == GEMM_DW && op.gemm.act == kDwNb ? "adam+nb"
                            : op.gemm.has_pre == 2                         ? "head+dx"
                            : op.gemm.has_pre == 3                         ? (op.gemm.epi == EPI_QDOT ? "qdot+pl" : "st+pl")
+                           : op.gemm.has_pre == 4                         ? "qdot+pl2"
+                           : op.gemm.has_pre == 5                         ? "st+sacpre"
                                                                            : kepi[op.gemm.epi];
           G.desc += "[" + std::to_string(op.gemm.M) + "x" + std::to_string(op.gemm.N) + "x" +
                     std::to_string(op.gemm.R) + " " + ep + "]";

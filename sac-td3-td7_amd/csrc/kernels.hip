@@ -614,6 +614,20 @@ __device__ __forceinline__ f32x4 chunk_loop_lds(const float* la, __amdgpu_buffer
   return acc;
 }
 
+// ... with the chunks on two accumulators by parity, as ring_run sums a segment read from memory (the
+// consumer's floats equal those of reading the standalone op's output)
+__device__ __forceinline__ f32x4 chunk_loop_lds_par(const float* la, __amdgpu_buffer_rsrc_t rb, int vb, int n,
+                                                    f32x4 acc) {
+  const int lane = threadIdx.x & 63;
+  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < n; ++c) {
+    const float4 x = *(const float4*)(la + c * 256 + lane * 4);
+    if (c & 1) acc1 = mfma4(x, bload(rb, vb + c * 1024), acc1);
+    else acc = mfma4(x, bload(rb, vb + c * 1024), acc);
+  }
+  return acc + acc1;
+}
+
 // Pre-GEMM (PreArgs): the actor's tanh output layer for the 16 rows at i0 into pimg[2][256]
 // (N-image fragment blocks, columns >= N zero).  Each wave reduces a quarter of the chunks
 // for both column blocks; the quarters are summed in fixed wave order by wave 0, which
@@ -634,21 +648,23 @@ struct PreRing {
   int c0, c1, cp;
 };
 
-template <int MODE>
+// (LITE: the host guarantees N <= 16 and one A and one B segment -- one column block, no registers
+// for a second, no segment lookup; GemmArgs::has_pre 4)
+template <int MODE, bool LITE = false>
 __device__ __forceinline__ void pre_issue(const CAS PreArgs& p, int i0, PreRing& R) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nch = p.R >> 4, per = (nch + 3) >> 2;
   R.c0 = wave * per;
   R.c1 = min(nch, R.c0 + per);
   R.cp = min(R.c1, R.c0 + kPreRing);
-  const bool wabs = MODE == GEMM_FWD && p.B.nseg == 1;
+  const bool wabs = MODE == GEMM_FWD && (LITE || p.B.nseg == 1);
   const int lb = lane * 16;
 #pragma unroll
   for (int r = 0; r < kPreRing; ++r) {
     const int k = R.c0 + r;
     int q = 0;  // segment of chunk k (wave-uniform)
 #pragma unroll
-    for (int u = 1; u < kMaxSeg; ++u)
+    for (int u = 1; u < (LITE ? 1 : kMaxSeg); ++u)
       if (u < p.A.nseg && k >= (p.A.seg[u].r0 >> 4)) q = u;
     const CAS Seg& sa = p.A.seg[q];
     const CAS Seg& sb = p.B.seg[wabs ? 0 : q];
@@ -656,14 +672,14 @@ __device__ __forceinline__ void pre_issue(const CAS PreArgs& p, int i0, PreRing&
     if (k >= R.cp) break;  // (uniform)
     R.a[r] = bload(rsrc(sa.p), ((i0 >> 4) * sa.xs + (k - s0)) * 1024 + lb);
     R.b0[r] = bload(rsrc(sb.p), kb * 1024 + lb);
-    if (p.N > 16) R.b1[r] = bload(rsrc(sb.p), (sb.xs + kb) * 1024 + lb);
+    if (!LITE && p.N > 16) R.b1[r] = bload(rsrc(sb.p), (sb.xs + kb) * 1024 + lb);
   }
   // (buffer loads at an out-of-range offset return 0: no branch, so no register merge that would
   // wait for every load in flight)
   const int rb = (lane >> 4) << 2;
   if (wave != 0) return;  // (wave 0 runs the epilogue: no loads for the others)
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
+  for (int cb = 0; cb < (LITE ? 1 : 2); ++cb) {
     const int j = cb * 16 + (lane & 15);
     const bool jok = j < p.N;
     if constexpr (MODE == GEMM_FWD) {
@@ -676,12 +692,12 @@ __device__ __forceinline__ void pre_issue(const CAS PreArgs& p, int i0, PreRing&
   }
 }
 
-template <int MODE>
+template <int MODE, bool LITE = false>
 __device__ __forceinline__ void pre_finish(const CAS PreArgs& p, int i0, PreRing& R, float* part, float* part2,
                                            float* pimg) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool two = p.N > 16, wabs = MODE == GEMM_FWD && p.B.nseg == 1;
+  const bool two = !LITE && p.N > 16, wabs = MODE == GEMM_FWD && (LITE || p.B.nseg == 1);
   const int lb = lane * 16;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
 #pragma unroll
@@ -690,7 +706,7 @@ __device__ __forceinline__ void pre_finish(const CAS PreArgs& p, int i0, PreRing
     acc0 = mfma4(R.a[r], R.b0[r], acc0);
     if (two) acc1 = mfma4(R.a[r], R.b1[r], acc1);
   }
-  for (int q = 0; q < p.A.nseg; ++q) {  // the rest of the wave's chunks
+  for (int q = 0; q < (LITE ? 1 : p.A.nseg); ++q) {  // the rest of the wave's chunks
     const CAS Seg& sa = p.A.seg[q];
     const CAS Seg& sb = p.B.seg[wabs ? 0 : q];
     const int s0 = sa.r0 >> 4;
@@ -703,17 +719,17 @@ __device__ __forceinline__ void pre_finish(const CAS PreArgs& p, int i0, PreRing
   }
   if (wave) {
     *(f32x4*)(part + (wave * 64 + lane) * 4) = acc0;
-    *(f32x4*)(part2 + (wave * 64 + lane) * 4) = acc1;
+    if (!LITE) *(f32x4*)(part2 + (wave * 64 + lane) * 4) = acc1;
   }
   __syncthreads();
   if (wave == 0) {
     for (int w = 1; w < 4; ++w) {
       acc0 += *(const f32x4*)(part + (w * 64 + lane) * 4);
-      acc1 += *(const f32x4*)(part2 + (w * 64 + lane) * 4);
+      if (!LITE) acc1 += *(const f32x4*)(part2 + (w * 64 + lane) * 4);
     }
     const int rb = (lane >> 4) << 2;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
+    for (int cb = 0; cb < (LITE ? 1 : 2); ++cb) {
       const f32x4 acc = cb ? acc1 : acc0;
       const int j = cb * 16 + (lane & 15);
       const bool jok = j < p.N;
@@ -750,42 +766,66 @@ __device__ __forceinline__ void pre_finish(const CAS PreArgs& p, int i0, PreRing
 // reduces them split-K over its waves (tn 16 / 32): the same floats.
 // (GEMM_DX: the same over dZ (N image) and W's T image, no bias, the output scaled by act'(saved)
 // (p.dsrc, T image) -- SAC's gradient through the actor's raw head, K = 2 x action dims.)
-template <int MODE, int ACT>
-__device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float* pimg) {
+// (prelayer_issue puts every operand in flight; prelayer_finish reduces and publishes pimg.  TWO: the
+// input has two segments and the chunks of segment 1 come from lds_a, an LDS fragment image --
+// GemmArgs::has_pre 4, whose pre-GEMM computed them -- instead of memory)
+struct PlRing {
+  float4 a[3], b[3][4];
+  float bj[4];
+  float4 ev[4];  // (DX) act'(saved) sources: 4 rows of column j per lane
+};
+template <int MODE, bool TWO = false>
+__device__ __forceinline__ void prelayer_issue(const CAS PreArgs& p, int i0, PlRing& R) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nch = p.R >> 4;
   const int lb = lane * 16;
   const CAS Seg& sb = p.B.seg[0];
   const auto rw = rsrc(sb.p);
-  float4 a[3], b[3][4];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     if (k >= nch) break;  // (uniform)
-    int q = 0;
+    if constexpr (TWO) {  // (segment 0 starts at chunk 0)
+      const CAS Seg& sa = p.A.seg[0];
+      if (k < (p.A.seg[1].r0 >> 4)) R.a[k] = bload(rsrc(sa.p), ((i0 >> 4) * sa.xs + k) * 1024 + lb);
+    } else {
+      int q = 0;
 #pragma unroll
-    for (int u = 1; u < kMaxSeg; ++u)
-      if (u < p.A.nseg && k >= (p.A.seg[u].r0 >> 4)) q = u;
-    const CAS Seg& sa = p.A.seg[q];
-    a[k] = bload(rsrc(sa.p), ((i0 >> 4) * sa.xs + (k - (sa.r0 >> 4))) * 1024 + lb);
+      for (int u = 1; u < kMaxSeg; ++u)
+        if (u < p.A.nseg && k >= (p.A.seg[u].r0 >> 4)) q = u;
+      const CAS Seg& sa = p.A.seg[q];
+      R.a[k] = bload(rsrc(sa.p), ((i0 >> 4) * sa.xs + (k - (sa.r0 >> 4))) * 1024 + lb);
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c)  // (column blocks past N: no load, zeros)
-      b[k][c] = (wave * 4 + c) * 16 < p.N ? bload(rw, ((wave * 4 + c) * sb.xs + k) * 1024 + lb)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      R.b[k][c] = (wave * 4 + c) * 16 < p.N ? bload(rw, ((wave * 4 + c) * sb.xs + k) * 1024 + lb)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  float bj[4];
-  float4 ev[4];  // (DX) act'(saved) sources: 4 rows of column j per lane
   const int rb = (lane >> 4) << 2;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int j = (wave * 4 + c) * 16 + (lane & 15);
     if constexpr (MODE == GEMM_FWD) {
-      bj[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(p.bias), j < p.N ? j * 4 : kOOB, 0, 0));
-      ev[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      R.bj[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(p.bias), j < p.N ? j * 4 : kOOB, 0, 0));
+      R.ev[c] = make_float4(0.f, 0.f, 0.f, 0.f);
     } else {
-      bj[c] = 0.f;
-      ev[c] = bload(rsrc(p.dsrc.t), j < p.N ? (int)tidx(p.dsrc.rbs, i0 + rb, j) * 4 : kOOB);
+      R.bj[c] = 0.f;
+      R.ev[c] = bload(rsrc(p.dsrc.t), j < p.N ? (int)tidx(p.dsrc.rbs, i0 + rb, j) * 4 : kOOB);
     }
   }
+}
+template <int MODE, int ACT, bool TWO = false>
+__device__ __forceinline__ void prelayer_finish(const CAS PreArgs& p, PlRing& R, float* pimg, const float* lds_a) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nch = p.R >> 4;
+  if constexpr (TWO) {
+    const int s1 = p.A.seg[1].r0 >> 4;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (k >= nch) break;
+      if (k >= s1) R.a[k] = *(const float4*)(lds_a + (k - s1) * 256 + lane * 4);
+    }
+  }
+  const int rb = (lane >> 4) << 2;
   f32x4 s[4];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -793,7 +833,7 @@ __device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 pk = mfma4(a[k], b[k][c], z);
+      const f32x4 pk = mfma4(R.a[k], R.b[k][c], z);
       s[c] = k ? s[c] + pk : pk;
     }
   }
@@ -802,16 +842,67 @@ __device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float
     const int cb = wave * 4 + c;
     float* dst = pimg + cb * 256 + ((lane & 15) >> 2) * 64 + rb * 4 + (lane & 3);
     const bool jok = cb * 16 + (lane & 15) < p.N;
-    const float e4[4] = {ev[c].x, ev[c].y, ev[c].z, ev[c].w};
+    const float e4[4] = {R.ev[c].x, R.ev[c].y, R.ev[c].z, R.ev[c].w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float y;
-      if constexpr (MODE == GEMM_FWD) y = act_f<ACT>(s[c][q] + bj[c]);
+      if constexpr (MODE == GEMM_FWD) y = act_f<ACT>(s[c][q] + R.bj[c]);
       else y = s[c][q] * act_b<ACT>(e4[q]);
       dst[q * 4] = jok ? y : 0.f;
     }
   }
   __syncthreads();
+}
+template <int MODE, int ACT>
+__device__ __forceinline__ void prelayer_fwd(const CAS PreArgs& p, int i0, float* pimg) {
+  PlRing R;
+  prelayer_issue<MODE>(p, i0, R);
+  prelayer_finish<MODE, ACT>(p, R, pimg, nullptr);
+}
+
+// SAC's raw head [mean | log_std] (sac.py:132-152; N = 2A <= 48, three column blocks, R <= 256) for the
+// 16 rows at i0: wave w reduces chunks 4w .. 4w + 3 for every column block, and wave 0 sums the partials
+// in wave order.  Both the standalone EPI_SACFWD op and the target critics' in-tile copy (GemmArgs::has_pre
+// 5) reduce this way, so their floats agree.  sacraw_issue puts the operands in flight; sacraw_finish
+// returns the sums in wave 0 (part: [3 blocks][4 waves][256] floats of LDS).
+struct SacRing {
+  float4 a[4], b[3][4];
+};
+__device__ __forceinline__ void sacraw_issue(const float* ap, int axs, const float* bp, int bxs, int nch, int i0,
+                                             SacRing& R) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lb = lane * 16;
+  const auto ra = rsrc(ap), rb = rsrc(bp);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k = wave * 4 + r;
+    if (k >= nch) break;  // (uniform)
+    R.a[r] = bload(ra, ((i0 >> 4) * axs + k) * 1024 + lb);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) R.b[c][r] = bload(rb, (c * bxs + k) * 1024 + lb);
+  }
+}
+__device__ __forceinline__ void sacraw_finish(const SacRing& R, int nch, float* part, f32x4 (&s)[3]) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) s[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (wave * 4 + r >= nch) break;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s[c] = mfma4(R.a[r], R.b[c][r], s[c]);
+  }
+  if (wave) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) *(f32x4*)(part + (c * 4 + wave) * 256 + lane * 4) = s[c];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    for (int w = 1; w < 4; ++w) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) s[c] += *(const f32x4*)(part + (c * 4 + w) * 256 + lane * 4);
+    }
+  }
 }
 
 // max(|td|, 1)^0.4 rounded from double (torch's float pow is correctly rounded).  The double pow
@@ -990,7 +1081,7 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
 
 // EXT: the extended instance of rle_level (register-blocked weight-gradient tiles, 32-row tiles); the
 // production instance compiles without them, so their registers do not shape its allocation
-template <int MODE, int EPI, int ACT, bool NORM, int PK = 0, bool EXT = false>  // PK: 1 pre-GEMM, 2 fused loss head, 3 pre-layer
+template <int MODE, int EPI, int ACT, bool NORM, int PK = 0, bool EXT = false>  // PK: 1 pre-GEMM, 2 fused loss head, 3 pre-layer, 4 pre-layer behind a pre-GEMM, 5 SAC raw head + rsample pre-GEMM
 __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
   FINE_MARK(10);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1019,12 +1110,15 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
 #define TL_P TL(0x3b0) TL(0x3f0) TL(0x430) TL(0x470) TL(0x4b0) TL(0x4f0) TL(0x530) TL(0x570) TL(0x5b0) TL(0x5f0)
 #define TL_D TL(0x5f0) TL(0x630)
 #define TL_O TL(0x670)
+#define TL_Q TL(0x6b0) TL(0x770) TL(0x7b0) TL(0x870) TL(0x8b0)
 #ifdef RLE_NO_TOUCH
   RLE_HOT_ASM("");
 #else
   if constexpr (MODE == GEMM_DW) {
     if constexpr (ACT == kDwNb) RLE_HOT_ASM(TL_B TL_D TL_X);
     else RLE_HOT_ASM(TL_B TL_D);
+  } else if constexpr (PK == 4) {
+    RLE_HOT_ASM(TL_A TL_B TL_S TL_N TL_P TL_Q);
   } else if constexpr (PK != 0) {
     if constexpr (MODE == GEMM_FWD && (ACT == ACT_TANH || EPI == EPI_QDOT)) RLE_HOT_ASM(TL_A TL_B TL_S TL_N TL_P);
     else RLE_HOT_ASM(TL_A TL_B TL_S TL_P);
@@ -1048,6 +1142,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
 #undef TL_P
 #undef TL_D
 #undef TL_O
+#undef TL_Q
   (void)dsink;
   auto ptr = [](unsigned lo, unsigned hi) { return (const float*)(((unsigned long long)hi << 32) | lo); };
   const int ksl = (int)h0[0], tiles_n = (int)h0[1], tn = (int)h0[2], gN = (int)h0[3], gR = (int)h0[4];
@@ -1158,6 +1253,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
 
   // ---- reduction
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 sac1 = acc, sac2 = acc;  // (EPI_SACFWD: column blocks 1, 2 of the raw tile, wave 0)
   const int lb = lane * 16;
   if constexpr (MODE != GEMM_DW) {
     // A: N image, segments along the reduction; B: W (FWD: N image, one segment over
@@ -1189,18 +1285,35 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     if constexpr (PK == 2) {  // fused loss head: one A segment, dZ of the critic's last hidden layer
       acc = headdx_reduce<ACT>(g, i0, j0, active, jt == 0, jt == 0 && cg == 0, c0, c1, nch, a0p, a0xs, b0p, b0xs,
                                smem, acc);
-    } else if constexpr (PK == 3) {  // the whole A operand from the pre-layer in LDS (prelayer_fwd)
+    } else if constexpr (PK == 3 || PK == 4) {  // the whole A operand from the pre-layer in LDS (prelayer_*)
       float* pimg = smem + 64 + 1024;
       const int nrun = active && c0 < c1 ? c1 - c0 : 0;
       const int vb = ((j0 >> 4) * b0xs + c0) * 1024 + lb;
       const auto rbw = rsrc(b0p);
       float4 rbq[4];  // the wave's first W chunks in flight with the pre-layer's operands
+      auto issue_rbq = [&]() {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (r < nrun) rbq[r] = bload(rbw, vb + r * 1024);
+        for (int r = 0; r < 4; ++r)
+          if (r < nrun) rbq[r] = bload(rbw, vb + r * 1024);
+      };
+      if constexpr (PK == 3) issue_rbq();
       // (A/B, TD3: issuing 8 more chunks once the pre-layer's MFMAs free their registers measured
       // -1.2% against this one-group-ahead loop)
-      prelayer_fwd<MODE, ACT>(g.prea, i0, pimg);
+      if constexpr (PK == 4) {
+        // two-stage prologue: the pre-GEMM (target action, N <= 16) and the pre-layer's memory operands in
+        // flight together; the pre-GEMM's output (pimg2, after the pre-layer image) is the pre-layer's input
+        // segment 1 (host-checked: prea2.seg == 1 of 2)
+        float* pimg2 = smem + 64 + 1024 + 4096;
+        PreRing pr;
+        PlRing pl;
+        pre_issue<GEMM_FWD, true>(g.prea2, i0, pr);
+        prelayer_issue<MODE, true>(g.prea, i0, pl);
+        pre_finish<GEMM_FWD, true>(g.prea2, i0, pr, part, nullptr, pimg2);
+        issue_rbq();  // (in the pre-GEMM ring's registers, in flight through the pre-layer's MFMAs)
+        prelayer_finish<MODE, ACT, true>(g.prea, pl, pimg, pimg2);
+      } else {
+        prelayer_fwd<MODE, ACT>(g.prea, i0, pimg);
+      }
       f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};  // (chunks on two accumulators by parity, as ring_run)
 #pragma unroll 1
       for (int c = 0; c < nrun; c += 4) {
@@ -1219,6 +1332,75 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         for (int r = 0; r < 4; ++r) rbq[r] = nx[r];
       }
       acc = acc + acc1;
+    } else if constexpr (PK == 5) {
+      // segment g.prea.seg is SAC's target action a' = tanh(mean + exp(clamp(log_std)) eps) of the tile's
+      // rows, from the raw head recomputed in-tile (sacraw_*, the standalone EPI_SACFWD's order and
+      // arithmetic); its operands are in flight with the consumer's own segments
+      const CAS PreArgs& p = g.prea;
+      float* pimg = smem + 64 + 3072;  // a' (N-image fragment blocks, columns >= A zero)
+      float* rt = pimg + 512;          // [16][48] raw rows
+      const int nchp = p.R >> 4, A = p.sac_a;
+      SacRing sr;
+      sacraw_issue(p.A.seg[0].p, p.A.seg[0].xs, p.B.seg[0].p, p.B.seg[0].xs, nchp, i0, sr);
+      float bj[3], ev[2];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int jj = c * 16 + (lane & 15);
+        bj[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(p.bias), jj < p.N ? jj * 4 : kOOB, 0, 0));
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int it = tid + k * kThreads, r = it >> 5, jj = it & 31;
+        ev[k] = jj < A ? mat_ld(p.noise, i0 + r, jj) : 0.f;
+      }
+      const int pseg = p.seg;
+      if (pseg != 0) seg(a0p, a0xs, a0r0, a0r1, b0p, b0xs, 0);
+      for (int q = 1; q < nseg_a; ++q) {
+        if (q == pseg) continue;
+        const CAS Seg& sa = g.A.seg[q];
+        const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
+        seg(sa.p, sa.xs, sa.r0, sa.r1, sb.p, sb.xs, q);
+      }
+      f32x4 sv[3];
+      sacraw_finish(sr, nchp, part, sv);
+      if (wave == 0) {
+        const int rb = (lane >> 4) << 2;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rt[(rb + q) * 48 + c * 16 + (lane & 15)] = sv[c][q] + bj[c];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {  // (as the standalone epilogue's rsample)
+        const int it = tid + k * kThreads, r = it >> 5, jj = it & 31;
+        float v = 0.f;
+        if (jj < A) {
+          const float mu = rt[r * 48 + jj];
+          const float ls = fminf(fmaxf(rt[r * 48 + A + jj], p.noise_sigma), p.noise_clip);
+          const float sd = expf(ls);
+          v = tanhf(mu + ev[k] * sd);
+        }
+        pimg[(jj >> 4) * 256 + ((jj & 15) >> 2) * 64 + r * 4 + (jj & 3)] = v;
+      }
+      __syncthreads();
+      const CAS Seg& sa = g.A.seg[pseg];
+      const CAS Seg& sb = g.B.seg[wabs ? 0 : pseg];
+      const int s0 = sa.r0 >> 4;
+      const int k0 = max(c0, s0), k1 = min(c1, (sa.r1 + 15) >> 4);
+      if (active && k0 < k1)
+        acc = chunk_loop_lds_par(pimg + (k0 - s0) * 256, rsrc(sb.p),
+                                 ((j0 >> 4) * sb.xs + (wabs ? k0 : k0 - s0)) * 1024 + lb, k1 - k0, acc);
+    } else if constexpr (EPI == EPI_SACFWD) {  // the raw head in sacraw order (see PK 5), whole rows per tile
+      SacRing sr;
+      sacraw_issue(a0p, a0xs, b0p, b0xs, nch, i0, sr);
+      f32x4 sv[3];
+      sacraw_finish(sr, nch, part, sv);
+      if (wave == 0) {
+        acc = sv[0];
+        sac1 = sv[1];
+        sac2 = sv[2];
+      }
     } else if constexpr (PK == 1) {  // segment g.prea.seg comes from the pre-GEMM in LDS
       float* pimg = smem + 64 + 2048;
       PreRing pr;
@@ -1414,17 +1596,23 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     epi_store(acc, i0, ib, ds, red);
   } else if constexpr (EPI == EPI_SACFWD) {  // op_sac_actor for the tile's 16 rows (sac.py:132-152)
     const CAS SacFwdArgs& s = g.sf;
-    float y[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) y[q] = acc[q] + pre_b;
-    if (jok) mat_st4(g.out, ib, j, make_float4(y[0], y[1], y[2], y[3]));  // raw (the backward reads it)
-    __syncthreads();  // (the split-K scratch is free)
     float* rt = smem;                // [16][64] the tile's raw rows
     float* lpt = smem + 1024;        // [16][32] log-density terms
     float* crt = lpt + 512;          // [16][32] tanh corrections
-    if (active && lead) {
+    __syncthreads();  // (the reduction scratch is free)
+    if (wave == 0) {  // (sacraw_finish: every column block's sums in wave 0)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rt[(ib - i0 + q) * 64 + (j - jt * 64)] = jok ? y[q] : 0.f;
+      for (int c = 0; c < 3; ++c) {
+        const f32x4 a4 = c == 0 ? acc : (c == 1 ? sac1 : sac2);
+        const int jc = c * 16 + (lane & 15);
+        const float bc = jc < gN && biasp ? G(biasp)[jc] : 0.f;
+        float y[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] = a4[q] + bc;
+        if (jc < gN) mat_st4(g.out, ib, jc, make_float4(y[0], y[1], y[2], y[3]));  // raw (the backward reads it)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rt[(ib - i0 + q) * 64 + jc] = jc < gN ? y[q] : 0.f;
+      }
     }
     __syncthreads();
     const float c = (float)0.9189385332046727;  // log(sqrt(2*pi))
@@ -1702,6 +1890,16 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
     RLE_VL(GEMM_FWD, EPI_STORE, ACT_RELU, false)
     RLE_VL(GEMM_FWD, EPI_QDOT, ACT_RELU, false)
     RLE_VL(GEMM_DX, EPI_STORE, ACT_RELU, false)
+    case gemm_vid(GEMM_FWD, EPI_STORE, ACT_RELU, 1, 1):  // (has_pre 5: a pre-GEMM id with the norm bit)
+      asm volatile("; gemm variant sacpre GEMM_FWD EPI_STORE ACT_RELU" ::);
+      gemm_v<GEMM_FWD, EPI_STORE, ACT_RELU, false, 5, EXT>(g, t, smem, tr);
+      break;
+#ifndef RLE_NO_PK4
+    case gemm_vid(GEMM_FWD, EPI_QDOT, ACT_RELU, 1, 3):  // (has_pre 4: the pre-layer id with the norm bit)
+      asm volatile("; gemm variant prelayer2 GEMM_FWD EPI_QDOT ACT_RELU" ::);
+      gemm_v<GEMM_FWD, EPI_QDOT, ACT_RELU, false, 4, EXT>(g, t, smem, tr);
+      break;
+#endif
     default: break;
   }
 #undef RLE_VL

@@ -202,8 +202,11 @@ struct PreArgs {
   int N, R;            // output columns (<= 32), reduction length
   int seg;             // consumer A segment produced
   int act;             // (pre-layer, has_pre 3) the layer's activation
+  int sac_a;           // (has_pre 5) action dims A: the output is SAC's raw head [mean | log_std], 2A wide
   const float* bias;   // FWD
-  Mat noise; float noise_sigma, noise_clip;  // FWD: smoothing noise (T image, consumer rows)
+  // FWD: smoothing noise (T image, consumer rows), sigma, clip; has_pre 5: the rsample noise and the
+  // log-std clamp (noise_sigma = min, noise_clip = max)
+  Mat noise; float noise_sigma, noise_clip;
   Mat dsrc;            // DX: saved tanh output (T image, consumer rows)
 };
 
@@ -301,7 +304,11 @@ struct GemmArgs {
   Mat nbx; int nbx_xs;             // EPI_NBDOT / kDwNb: x of the AvgL1Norm (T image; DW: its x-block step)
   NormRef nbm;                     // kDwNb: m of x's rows (producer |x| partials)
   const float* nbdot; int nbdot_ld, nbdot_n;  // kDwNb: the EPI_NBDOT producer's row partials of sum g x
-  int has_pre;                     // 1: pre-GEMM (prea) in use; 2: loss head fused into this DX (hd)
+  int has_pre;                     // 1: pre-GEMM (prea) in use; 2: loss head fused into this DX (hd);
+                                   // 3: pre-layer (prea); 4: pre-layer behind a pre-GEMM (prea, prea2;
+                                   // variant id: pre 3 with the norm bit, which a pre-layer never sets);
+                                   // 5: SAC's raw head + rsample as the pre-GEMM (prea; variant id: pre 1
+                                   // with the norm bit on a ReLU forward, which no pre-GEMM consumer has)
   union {
     PreArgs prea;
     // has_pre 2 (TD7 critic backward, engine.cpp build_td7): the HEAD_TD7_LOSS head (target
@@ -316,6 +323,11 @@ struct GemmArgs {
   int head_n;
   AdamArgs adam;
   ActArgs ao;                      // EPI_ACT
+  // has_pre 4 (TD3 target critics, engine.cpp mlp_critic_fwd): the pre-layer prea's input segment
+  // prea2.seg is itself computed in-tile first, by the pre-GEMM prea2 (the target action), so the
+  // first layer behind the target action costs no level of its own
+  PreArgs prea2;
+  int pad_tail_[2];                // (Op: whole 64-byte lines)
 };
 
 // AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise);
@@ -468,7 +480,7 @@ static_assert(16 + sizeof(HeadArgs) <= 8 * 64 && 16 + sizeof(StepEndArgs) <= 8 *
 static_assert(offsetof(GemmArgs, A) == 0xb0 && offsetof(GemmArgs, B) == 0x1a0 && offsetof(GemmArgs, out) == 0x290 &&
                   offsetof(GemmArgs, noise) == 0x2f0 && offsetof(GemmArgs, nbx) == 0x370 &&
                   offsetof(GemmArgs, prea) == 0x3c0 && offsetof(GemmArgs, adam) == 0x600 &&
-                  offsetof(GemmArgs, ao) == 0x670,
+                  offsetof(GemmArgs, ao) == 0x670 && offsetof(GemmArgs, prea2) == 0x6b0,
               "GemmArgs layout (descriptor line touches)");
 
 // ---- B = 1 act chain (rle_act_sample, one observation): ONE launch of nwg workgroups

@@ -367,6 +367,48 @@ def test_prelayer_bitwise(name):
             np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
 
 
+@pytest.mark.parametrize("name", ["td3_tiny", "td3_tiny_lap", "td3_halfcheetah"])
+def test_td3_twostage_bitwise(name):
+    """TD3's target critics: their first layer, behind the pre-GEMM target action, recomputed in-tile by
+    their second layer with the action segment computed in-tile first (GemmArgs::has_pre 4, kernels.hip
+    PK 4), gives the floats of the standalone first layer (plan fuse_off twostage: a level of its own, in
+    at most 32-wide tiles so that its split-K order is the pre-layer's chunk order).  Tile widening off
+    in both and the consumers 16 wide (pl_tn 16), as test_prelayer_bitwise."""
+    g = load_golden(name)
+    n = 20
+    e1, r1, _ = engine_from_golden(g, plan=E.make_plan(level_cap=100000, pl_tn=16))
+    info1 = e1.step(n)
+    e2, r2, _ = engine_from_golden(g, plan=E.make_plan(["twostage"], level_cap=100000, pl_tn=16))
+    info2 = e2.step(n)
+    assert "qdot+pl2" in e1.describe() and "qdot+pl2" not in e2.describe()
+    np.testing.assert_array_equal(info1, info2)
+    np.testing.assert_array_equal(r1.get_priority(), r2.get_priority())
+    alg, env, H = parse(g)[:3]
+    for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
+        for pname in params:
+            np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
+
+
+@pytest.mark.parametrize("name", ["sac_tiny", "sac_tiny_fixed", "sac_humanoid"])
+def test_sac_target_pre_bitwise(name):
+    """SAC's target critics: their first layer recomputes the raw head and the target rsample a' for
+    its rows in-tile (GemmArgs::has_pre 5, kernels.hip PK 5), in the standalone EPI_SACFWD op's reduction
+    order (sacraw_*) and arithmetic, and sums a' on ring_run's two accumulators: the floats of reading
+    the standalone op's output (plan fuse_off sacpre).  Equal tile widths in both (level_cap, pre_tn 16)."""
+    g = load_golden(name)
+    n = 20
+    e1, r1, _ = engine_from_golden(g, plan=E.make_plan(level_cap=100000, pre_tn=16))
+    info1 = e1.step(n)
+    e2, r2, _ = engine_from_golden(g, plan=E.make_plan(["sacpre"], level_cap=100000, pre_tn=16))
+    info2 = e2.step(n)
+    assert "st+sacpre" in e1.describe() and "st+sacpre" not in e2.describe()
+    np.testing.assert_array_equal(info1, info2)
+    alg, env, H = parse(g)[:3]
+    for net, params in spec.agent_params(alg, *spec.TASKS[env][:2], H, 0).items():
+        for pname in params:
+            np.testing.assert_array_equal(e1.get_param(net, pname), e2.get_param(net, pname))
+
+
 # (TD7 with policy_freq 2 starts a 6-step graph at every odd step count n_runs whose window holds no
 # hard update: n_runs = 1 -> steps 2..7 as one graph.  Humanoid 13: 1 + 6 + 6 steps, the headline
 # program (B = 256, default planner, LAP over 4096 rows); B = 1024: 1 + 6 + 1, BASELINE config 4;
