@@ -35,11 +35,11 @@ namespace rle {
 // ext: the extended kernel instance (register-blocked / 32-row tiles, fused priority sampler)
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
                         unsigned long long* trace = nullptr, const Op* next_ops = nullptr, int next_nops = 0,
-                        bool ext = false);
+                        int ks = KS_EXT);
 int level_capacity();
 int trace_stride();
 extern std::vector<LevelLaunch>* g_level_rec;
-const char* level_kernel_symbol(bool ext);
+const char* level_kernel_symbol(int ks);
 hipError_t launch_append(float* state, float* next_state, float* action, float* reward, float* notdone,
                          float* priority, const float* st_s, const float* st_ns, const float* st_a,
                          const float* st_r, const float* st_d, long long ptr, long long cap, int count,
@@ -306,6 +306,14 @@ static void check_gemm(const GemmArgs& g) {
 
 static void xcd_plan(GemmArgs& g);
 
+// (ks < 0: in any kernel set)
+static bool gemm_variant_compiled(int vid, int ks = -1) {
+#define RLE_VID(mode, epi, act, norm, pre, pk, sets) \
+  (vid == gemm_vid(mode, epi, act, norm, pre) && (ks < 0 || ks == KS_EXT || (((sets) >> ks) & 1))) ||
+  return RLE_GEMM_VARIANTS(RLE_VID) false;
+#undef RLE_VID
+}
+
 // Device-side dispatch fields of a GEMM op: compiled variant, split count, tile-row
 // reciprocal (kernels.hip gemm_v).
 static void gemm_finalize(GemmArgs& g) {
@@ -383,6 +391,8 @@ static void gemm_finalize(GemmArgs& g) {
   g.vid = g.has_pre == 4   ? gemm_vid(g.mode, g.epi, act, 1, 3)
           : g.has_pre == 5 ? gemm_vid(g.mode, g.epi, act, 1, 1)
                            : gemm_vid(g.mode, g.epi, act, norm, g.has_pre);
+  REQUIRE(gemm_variant_compiled(g.vid), "gemm: no compiled variant for this mode / epilogue / activation / norm / pre "
+                                        "(ops.h RLE_GEMM_VARIANTS)");
   REQUIRE(g.tn == 16 || g.tn == 32 || g.tn == 64, "gemm: tile width");
   g.ks_log = g.tn == 16 ? 2 : (g.tn == 32 ? 1 : 0);
   REQUIRE(g.R % 16 == 0, "gemm: reduction length must be a multiple of 16");
@@ -1257,13 +1267,13 @@ struct AqlQueue {
   hsa_agent_t agent{};
   hsa_queue_t* q = nullptr;
   hsa_signal_t sig{};
-  uint64_t kobj[2] = {0, 0};  // rle_level<false, ext>
-  uint32_t gseg[2] = {0, 0}, pseg[2] = {0, 0};
+  uint64_t kobj[KS_COUNT] = {};  // rle_level<false, ks>
+  uint32_t gseg[KS_COUNT] = {}, pseg[KS_COUNT] = {};
   int acq = HSA_FENCE_SCOPE_AGENT, rel = HSA_FENCE_SCOPE_AGENT;
   struct Pending {
     const void* ka;
     unsigned grid;
-    int ext;
+    int ks;
   };
   std::vector<Pending> pending;
   ~AqlQueue() {
@@ -1320,8 +1330,8 @@ static std::unique_ptr<AqlQueue> aql_open(int dev) {
   A->agent = want.second;
   hsa_ven_amd_loader_1_03_pfn_t tbl;
   HSACHK(hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof(tbl), &tbl));
-  for (int x = 0; x < 2; ++x) {
-    AqlFind f{A->agent, level_kernel_symbol(x != 0), 0, 0, 0};
+  for (int x = 0; x < KS_COUNT; ++x) {
+    AqlFind f{A->agent, level_kernel_symbol(x), 0, 0, 0};
     tbl.hsa_ven_amd_loader_iterate_executables(aql_find_kernel, &f);
     REQUIRE(f.kobj, "aql: rle_level's kernel object is not loaded");
     A->kobj[x] = f.kobj;
@@ -1361,7 +1371,7 @@ static void aql_flush(AqlQueue& A, double* ms) {
     pk->grid_size_x = A.pending[i].grid * kThreads;
     pk->grid_size_y = 1;
     pk->grid_size_z = 1;
-    const int x = A.pending[i].ext;
+    const int x = A.pending[i].ks;
     pk->private_segment_size = A.pseg[x];
     pk->group_segment_size = A.gseg[x];
     pk->kernel_object = A.kobj[x];
@@ -1450,7 +1460,12 @@ struct Engine {
   // Defaults of the fields left at "default" for this engine's algorithm (rle.h rle_plan).
   // The extended kernel instance runs this engine's programs when its plan uses what only that
   // instance compiles: register-blocked weight-gradient tiles, the fused priority sampler.
-  bool ext_kernels() const { return plan.rb || (plan.fuse_on & RLE_FUSE_PRIOSAMPLE); }
+  // the rle_level instance this engine's programs run on (ops.h KernelSet): the agent's own set, or the
+  // extended instance when the plan asks for its opt-in paths
+  int kernel_set() const {
+    if (plan.rb || (plan.fuse_on & RLE_FUSE_PRIOSAMPLE)) return KS_EXT;
+    return algo == RLE_TD7 ? KS_TD7 : KS_MLP;
+  }
   void resolve_plan() {
     if (plan.steps_per_graph < 0) plan.steps_per_graph = algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 6;
     if (plan.pre_tn == 0) plan.pre_tn = algo == RLE_TD3 ? 64 : 32;
@@ -3703,7 +3718,11 @@ struct Engine {
     std::vector<Op> flat_ops;
     flat_ops.reserve(total);
     for (auto& lv : levels)
-      for (auto& op : lv) flat_ops.push_back(op);
+      for (auto& op : lv) {
+        REQUIRE(op.kind != OP_GEMM || gemm_variant_compiled(op.gemm.vid, kernel_set()),
+                "capture: a GEMM variant outside the engine's rle_level instance (ops.h RLE_GEMM_VARIANTS sets)");
+        flat_ops.push_back(op);
+      }
     G.d_ops = mem.make<Op>(total);
     HIPCHK(hipMemcpy(G.d_ops, flat_ops.data(), total * sizeof(Op), hipMemcpyHostToDevice));
     const char* tr_env = std::getenv("RLE_TRACE");
@@ -3723,7 +3742,7 @@ struct Engine {
       const size_t ln = l + 1 < levels.size() ? l + 1 : 0;
       hipError_t e = launch_level(G.d_ops + G.off[l], levels[l].data(), G.nops[l], G.nwg[l], stream,
                                   G.trace ? G.trace + tr_off * trace_stride() : nullptr, G.d_ops + G.off[ln],
-                                  dpf ? G.nops[ln] : 0, ext_kernels());
+                                  dpf ? G.nops[ln] : 0, kernel_set());
       tr_off += G.nwg[l];
       if (e != hipSuccess) {
         g_level_rec = nullptr;
@@ -3942,14 +3961,14 @@ struct Engine {
       return e && e[0] == '1';
     }();
     if (aql_active && !G.aql.empty()) {
-      for (size_t i = 0; i < G.aql.size(); ++i) aql->pending.push_back({G.aql_ka + i * 128, G.aql[i].grid, G.aql[i].ext});
+      for (size_t i = 0; i < G.aql.size(); ++i) aql->pending.push_back({G.aql_ka + i * 128, G.aql[i].grid, G.aql[i].ks});
       launches += G.nlaunch;
       return;
     }
     if (eager && !G.trace) {
       for (size_t l = 0; l < G.host_levels.size(); ++l)
         HIPCHK(launch_level(G.d_ops + G.off[l], G.host_levels[l].data(), G.nops[l], G.nwg[l], stream, nullptr,
-                            nullptr, 0, ext_kernels()));
+                            nullptr, 0, kernel_set()));
     } else {
       HIPCHK(hipGraphLaunch(G.x, stream));
     }

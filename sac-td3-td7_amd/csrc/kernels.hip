@@ -1834,78 +1834,22 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   }
 }
 
-template <bool EXT>
+template <int KS>
 __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, float* smem, unsigned long long* tr) {
-#define RLE_V(mode, epi, act, norm)                      \
-  case gemm_vid(mode, epi, act, norm):                   \
-    asm volatile("; gemm variant " #mode #epi #act #norm ::); \
-    gemm_v<mode, epi, act, norm, 0, EXT>(g, t, smem, tr); \
-    break;
-#define RLE_VP(mode, epi, act, norm)                                  \
-  case gemm_vid(mode, epi, act, norm, 1):                            \
-    asm volatile("; gemm variant pre " #mode #epi #act #norm ::);    \
-    gemm_v<mode, epi, act, norm, 1, EXT>(g, t, smem, tr);            \
-    break;
-#define RLE_VL(mode, epi, act, norm)                                  \
-  case gemm_vid(mode, epi, act, norm, 3):                            \
-    asm volatile("; gemm variant prelayer " #mode #epi #act #norm ::); \
-    gemm_v<mode, epi, act, norm, 3, EXT>(g, t, smem, tr);            \
-    break;
-#define RLE_VH(mode, epi, act, norm)                                  \
-  case gemm_vid(mode, epi, act, norm, 2):                            \
-    asm volatile("; gemm variant head " #mode #epi #act #norm ::);   \
-    gemm_v<mode, epi, act, norm, 2, EXT>(g, t, smem, tr);            \
+  // (ops.h RLE_GEMM_VARIANTS, those of kernel set KS; the host refuses any other id.  PK 4 / 5 take an id
+  // with the norm bit their consumers never set, so their NORM is false)
+#define RLE_VX(mode, epi, act, norm, pre, pk, sets)                                              \
+  case gemm_vid(mode, epi, act, norm, pre):                                                      \
+    if constexpr (KS == KS_EXT || (((sets) >> KS) & 1)) {                                       \
+      asm volatile("; gemm variant " #mode " " #epi " " #act " norm " #norm " pk " #pk ::);      \
+      gemm_v<mode, epi, act, (norm) != 0 && (pk) <= 3, pk, KS == KS_EXT>(g, t, smem, tr);        \
+    }                                                                                            \
     break;
   switch (vid) {
-    RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, false)
-    RLE_V(GEMM_FWD, EPI_STORE, ACT_NONE, true)
-    RLE_V(GEMM_FWD, EPI_STORE, ACT_RELU, false)
-    RLE_V(GEMM_FWD, EPI_STORE, ACT_RELU, true)
-    RLE_V(GEMM_FWD, EPI_STORE, ACT_ELU, false)
-    RLE_V(GEMM_FWD, EPI_STORE, ACT_ELU, true)
-    RLE_V(GEMM_FWD, EPI_STORE, ACT_TANH, false)
-    RLE_V(GEMM_FWD, EPI_STORE, ACT_TANH, true)
-    RLE_V(GEMM_FWD, EPI_QHEAD, ACT_ELU, false)
-    RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, false)
-    RLE_V(GEMM_FWD, EPI_MSE, ACT_NONE, true)
-    RLE_V(GEMM_FWD, EPI_ACT, ACT_TANH, false)
-    RLE_V(GEMM_FWD, EPI_QDOT, ACT_ELU, false)
-    RLE_V(GEMM_FWD, EPI_QDOT, ACT_RELU, false)
-    RLE_V(GEMM_DX, EPI_STORE, ACT_NONE, false)
-    RLE_V(GEMM_DX, EPI_STORE, ACT_RELU, false)
-    RLE_V(GEMM_DX, EPI_STORE, ACT_ELU, false)
-    RLE_V(GEMM_DX, EPI_STORE, ACT_TANH, false)
-    RLE_V(GEMM_DX, EPI_NBDOT, ACT_NONE, false)
-    RLE_V(GEMM_DW, EPI_ADAM, ACT_NONE, false)
-    RLE_V(GEMM_DW, EPI_ADAM, ACT_NONE, true)
-    RLE_V(GEMM_DW, EPI_ADAM, kDwNb, false)
-    RLE_VP(GEMM_FWD, EPI_STORE, ACT_NONE, false)
-    RLE_VP(GEMM_FWD, EPI_STORE, ACT_RELU, false)
-    RLE_VP(GEMM_FWD, EPI_STORE, ACT_ELU, true)
-    RLE_VP(GEMM_DX, EPI_STORE, ACT_RELU, false)
-    RLE_V(GEMM_DX, EPI_SACBWD, ACT_NONE, false)
-    RLE_V(GEMM_FWD, EPI_SACFWD, ACT_NONE, false)
-    RLE_VH(GEMM_DX, EPI_STORE, ACT_ELU, false)
-    RLE_VH(GEMM_DX, EPI_STORE, ACT_RELU, false)
-    RLE_VL(GEMM_FWD, EPI_STORE, ACT_RELU, false)
-    RLE_VL(GEMM_FWD, EPI_QDOT, ACT_RELU, false)
-    RLE_VL(GEMM_DX, EPI_STORE, ACT_RELU, false)
-    case gemm_vid(GEMM_FWD, EPI_STORE, ACT_RELU, 1, 1):  // (has_pre 5: a pre-GEMM id with the norm bit)
-      asm volatile("; gemm variant sacpre GEMM_FWD EPI_STORE ACT_RELU" ::);
-      gemm_v<GEMM_FWD, EPI_STORE, ACT_RELU, false, 5, EXT>(g, t, smem, tr);
-      break;
-#ifndef RLE_NO_PK4
-    case gemm_vid(GEMM_FWD, EPI_QDOT, ACT_RELU, 1, 3):  // (has_pre 4: the pre-layer id with the norm bit)
-      asm volatile("; gemm variant prelayer2 GEMM_FWD EPI_QDOT ACT_RELU" ::);
-      gemm_v<GEMM_FWD, EPI_QDOT, ACT_RELU, false, 4, EXT>(g, t, smem, tr);
-      break;
-#endif
+    RLE_GEMM_VARIANTS(RLE_VX)
     default: break;
   }
-#undef RLE_VL
-#undef RLE_V
-#undef RLE_VP
-#undef RLE_VH
+#undef RLE_VX
 }
 
 // ---------------------------------------------------------------- AvgL1Norm backward
@@ -2783,7 +2727,7 @@ __device__ __forceinline__ void op_foldbias(const CAS FoldBiasArgs& f) {
 // a kernel-argument load; its first memory access is its op's descriptor.
 static_assert(kLevelOps == 12, "rle_level takes the op table as 12 scalar arguments");
 
-template <bool TRACE, bool EXT>
+template <bool TRACE, int KS>  // KS: KernelSet (ops.h)
 #ifndef RLE_WAVES
 #define RLE_WAVES 4  // waves per SIMD the register allocation must allow (4 workgroups per CU)
 #endif
@@ -2857,18 +2801,18 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     call;                                     \
     break;
 #ifdef RLE_EXP_TWICE_GEMM  // diagnostics: the stamps of a second, cache-warm pass overwrite the first
-    RLE_OP(OP_GEMM, op_gemm<EXT>(op.gemm, vid, t, smem, tr); __syncthreads(); op_gemm<EXT>(op.gemm, vid, t, smem, tr))
+    RLE_OP(OP_GEMM, op_gemm<KS>(op.gemm, vid, t, smem, tr); __syncthreads(); op_gemm<KS>(op.gemm, vid, t, smem, tr))
 #else
-    RLE_OP(OP_GEMM, op_gemm<EXT>(op.gemm, vid, t, smem, tr))
+    RLE_OP(OP_GEMM, op_gemm<KS>(op.gemm, vid, t, smem, tr))
 #endif
 #ifndef RLE_EXP_GEMM_ONLY
     RLE_OP(OP_NORMBWD, op_normbwd(op.nb, t))
     RLE_OP(OP_SAMPLE_REDUCE, op_sample_reduce(op.sample, t, smem))
 #ifdef RLE_EXP_TWICE  // diagnostics: the stamps of a second, cache-warm pass overwrite the first
-    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather<EXT>(op.sample, t, smem, tr); __syncthreads();
-           op_sample_gather<EXT>(op.sample, t, smem, tr))
+    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather<KS == KS_EXT>(op.sample, t, smem, tr); __syncthreads();
+           op_sample_gather<KS == KS_EXT>(op.sample, t, smem, tr))
 #else
-    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather<EXT>(op.sample, t, smem, tr))
+    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather<KS == KS_EXT>(op.sample, t, smem, tr))
 #endif
     RLE_OP(OP_HEAD, op_head(op.head, t, smem, tr))
     RLE_OP(OP_PRIORITY, op_priority(op.prio, smem))
@@ -3159,8 +3103,13 @@ int trace_stride() { return kTraceStride; }
 int level_capacity() {
   int per_cu = 0, cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false, false>, kThreads, 0) != hipSuccess)
+  int p1 = 0, p2 = 0;  // (every instance: the planner's capacity must hold for the one an engine runs)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false, KS_TD7>, kThreads, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p1, rle_level<false, KS_MLP>, kThreads, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p2, rle_level<false, KS_EXT>, kThreads, 0) != hipSuccess)
     return 1024;
+  per_cu = per_cu < p1 ? per_cu : p1;
+  per_cu = per_cu < p2 ? per_cu : p2;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
   return per_cu * cus;
 }
@@ -3169,13 +3118,14 @@ int level_capacity() {
 // AQL launch lists; traced launches are never recorded)
 std::vector<LevelLaunch>* g_level_rec = nullptr;
 // the production kernel's HSA symbol name (AQL dispatch)
-const char* level_kernel_symbol(bool ext) {
-  return ext ? "_ZN3rle9rle_levelILb0ELb1EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"
-             : "_ZN3rle9rle_levelILb0ELb0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd";
+const char* level_kernel_symbol(int ks) {
+  return ks == KS_EXT   ? "_ZN3rle9rle_levelILb0ELi2EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"
+         : ks == KS_MLP ? "_ZN3rle9rle_levelILb0ELi1EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"
+                        : "_ZN3rle9rle_levelILb0ELi0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd";
 }
 
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
-                        unsigned long long* trace, const Op* next_ops, int next_nops, bool ext) {
+                        unsigned long long* trace, const Op* next_ops, int next_nops, int ks) {
   // a level of more than kLevelOps ops: consecutive launches of kLevelOps (its ops are
   // independent, so any split is correct)
   for (int q0 = 0; q0 < nops; q0 += kLevelOps) {
@@ -3211,17 +3161,22 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
       std::memcpy(L.ka + 64, &next, 8);
       std::memcpy(L.ka + 72, &next_lines, 4);
       L.grid = (unsigned)(w1 - w0 + npf);
-      L.ext = ext ? 1 : 0;
+      L.ks = ks;
       g_level_rec->push_back(L);
     }
 #define RLE_LEVEL_ARGS                                                                                         \
   la.entry[0], la.entry[1], la.entry[2], la.entry[3], la.entry[4], la.entry[5], la.entry[6], la.entry[7], \
       la.entry[8], la.entry[9], la.entry[10], la.entry[11], la.ops, la.trace, next, next_lines
     const dim3 grid(w1 - w0 + npf);
-    if (trace && ext) hipLaunchKernelGGL((rle_level<true, true>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
-    else if (trace) hipLaunchKernelGGL((rle_level<true, false>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
-    else if (ext) hipLaunchKernelGGL((rle_level<false, true>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
-    else hipLaunchKernelGGL((rle_level<false, false>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    if (trace) {
+      if (ks == KS_TD7) hipLaunchKernelGGL((rle_level<true, KS_TD7>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+      else if (ks == KS_MLP) hipLaunchKernelGGL((rle_level<true, KS_MLP>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+      else hipLaunchKernelGGL((rle_level<true, KS_EXT>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    } else {
+      if (ks == KS_TD7) hipLaunchKernelGGL((rle_level<false, KS_TD7>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+      else if (ks == KS_MLP) hipLaunchKernelGGL((rle_level<false, KS_MLP>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+      else hipLaunchKernelGGL((rle_level<false, KS_EXT>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+    }
 #undef RLE_LEVEL_ARGS
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -143,6 +143,51 @@ constexpr int gemm_vid(int mode, int epi, int act, int norm, int pre = 0) {
 // (the level-launch entry keeps it in bits 20-30: bit 31 of entry 0 is the descriptor-prefetch flag)
 static_assert(gemm_vid(2, 8, 15, 1, 3) < 2048, "GEMM variant ids fit 11 bits");
 
+// The compiled GEMM variants: X(mode, epilogue, activation, norm, pre, PK, sets) -- the variant id's fields
+// (gemm_vid), gemm_v's path (PK: 0 plain, 1 pre-GEMM, 2 fused loss head, 3 pre-layer, 4 pre-layer behind a
+// pre-GEMM, 5 SAC raw head pre-GEMM) and the kernel sets that hold it (bit 0: TD7, bit 1: TD3 / SAC; the
+// extended instance holds all).  kernels.hip op_gemm dispatches exactly these, and the engine refuses a
+// program with an op whose id is not in its kernel set.
+#define RLE_GEMM_VARIANTS(X)                        \
+  X(GEMM_FWD, EPI_STORE, ACT_NONE, 0, 0, 0, 3)      \
+  X(GEMM_FWD, EPI_STORE, ACT_NONE, 1, 0, 0, 1)      \
+  X(GEMM_FWD, EPI_STORE, ACT_RELU, 0, 0, 0, 3)      \
+  X(GEMM_FWD, EPI_STORE, ACT_RELU, 1, 0, 0, 1)      \
+  X(GEMM_FWD, EPI_STORE, ACT_ELU, 0, 0, 0, 3)       \
+  X(GEMM_FWD, EPI_STORE, ACT_ELU, 1, 0, 0, 1)       \
+  X(GEMM_FWD, EPI_STORE, ACT_TANH, 0, 0, 0, 3)      \
+  X(GEMM_FWD, EPI_STORE, ACT_TANH, 1, 0, 0, 1)      \
+  X(GEMM_FWD, EPI_QHEAD, ACT_ELU, 0, 0, 0, 1)       \
+  X(GEMM_FWD, EPI_MSE, ACT_NONE, 0, 0, 0, 1)        \
+  X(GEMM_FWD, EPI_MSE, ACT_NONE, 1, 0, 0, 1)        \
+  X(GEMM_FWD, EPI_ACT, ACT_TANH, 0, 0, 0, 3)        \
+  X(GEMM_FWD, EPI_QDOT, ACT_ELU, 0, 0, 0, 1)        \
+  X(GEMM_FWD, EPI_QDOT, ACT_RELU, 0, 0, 0, 2)       \
+  X(GEMM_DX, EPI_STORE, ACT_NONE, 0, 0, 0, 3)       \
+  X(GEMM_DX, EPI_STORE, ACT_RELU, 0, 0, 0, 3)       \
+  X(GEMM_DX, EPI_STORE, ACT_ELU, 0, 0, 0, 3)        \
+  X(GEMM_DX, EPI_STORE, ACT_TANH, 0, 0, 0, 3)       \
+  X(GEMM_DX, EPI_NBDOT, ACT_NONE, 0, 0, 0, 1)       \
+  X(GEMM_DW, EPI_ADAM, ACT_NONE, 0, 0, 0, 3)        \
+  X(GEMM_DW, EPI_ADAM, ACT_NONE, 1, 0, 0, 1)        \
+  X(GEMM_DW, EPI_ADAM, kDwNb, 0, 0, 0, 1)           \
+  X(GEMM_FWD, EPI_STORE, ACT_NONE, 0, 1, 1, 1)      \
+  X(GEMM_FWD, EPI_STORE, ACT_RELU, 0, 1, 1, 3)      \
+  X(GEMM_FWD, EPI_STORE, ACT_ELU, 1, 1, 1, 1)       \
+  X(GEMM_DX, EPI_STORE, ACT_RELU, 0, 1, 1, 3)       \
+  X(GEMM_DX, EPI_SACBWD, ACT_NONE, 0, 0, 0, 2)      \
+  X(GEMM_FWD, EPI_SACFWD, ACT_NONE, 0, 0, 0, 2)     \
+  X(GEMM_DX, EPI_STORE, ACT_ELU, 0, 2, 2, 1)        \
+  X(GEMM_DX, EPI_STORE, ACT_RELU, 0, 2, 2, 2)       \
+  X(GEMM_FWD, EPI_STORE, ACT_RELU, 0, 3, 3, 2)      \
+  X(GEMM_FWD, EPI_QDOT, ACT_RELU, 0, 3, 3, 2)       \
+  X(GEMM_DX, EPI_STORE, ACT_RELU, 0, 3, 3, 2)       \
+  X(GEMM_FWD, EPI_QDOT, ACT_RELU, 1, 3, 4, 2)       \
+  X(GEMM_FWD, EPI_STORE, ACT_RELU, 1, 1, 5, 2)
+// kernel sets (rle_level's KS): TD7, TD3 / SAC, and the extended instance (every variant, plus the opt-in
+// register-blocked weight-gradient tiles and the fused priority sampler)
+enum KernelSet : int { KS_TD7 = 0, KS_MLP = 1, KS_EXT = 2, KS_COUNT = 3 };
+
 enum GemmMode : int {
   GEMM_FWD = 0,   // A contiguous (activations), B contiguous (W rows):  Y = X W^T
   GEMM_DX = 1,    // A contiguous (dZ), B strided (W columns):            dX = dZ W
@@ -543,7 +588,7 @@ constexpr int kMaxLevelWG = 0xfffe;  // workgroups per launch (16-bit entry fiel
 struct LevelLaunch {
   unsigned char ka[80];
   unsigned grid;  // workgroups
-  int ext;        // the extended kernel instance (rle_level<false, true>)
+  int ks;         // the rle_level instance (KernelSet)
 };
 
 // Device control block.

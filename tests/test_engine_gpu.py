@@ -394,12 +394,14 @@ def test_sac_target_pre_bitwise(name):
     """SAC's target critics: their first layer recomputes the raw head and the target rsample a' for
     its rows in-tile (GemmArgs::has_pre 5, kernels.hip PK 5), in the standalone EPI_SACFWD op's reduction
     order (sacraw_*) and arithmetic, and sums a' on ring_run's two accumulators: the floats of reading
-    the standalone op's output (plan fuse_off sacpre).  Equal tile widths in both (level_cap, pre_tn 16)."""
+    the standalone op's output (plan fuse_off sacpre).  Equal tile widths in both (level_cap; pre_tn and
+    pl_tn 16: on the tiny shapes, K <= 48, the unfused target critics take the pre-layer instead, whose
+    consumer must keep the q partials' 16-wide tiles)."""
     g = load_golden(name)
     n = 20
-    e1, r1, _ = engine_from_golden(g, plan=E.make_plan(level_cap=100000, pre_tn=16))
+    e1, r1, _ = engine_from_golden(g, plan=E.make_plan(level_cap=100000, pre_tn=16, pl_tn=16))
     info1 = e1.step(n)
-    e2, r2, _ = engine_from_golden(g, plan=E.make_plan(["sacpre"], level_cap=100000, pre_tn=16))
+    e2, r2, _ = engine_from_golden(g, plan=E.make_plan(["sacpre"], level_cap=100000, pre_tn=16, pl_tn=16))
     info2 = e2.step(n)
     assert "st+sacpre" in e1.describe() and "st+sacpre" not in e2.describe()
     np.testing.assert_array_equal(info1, info2)
