@@ -76,7 +76,7 @@ typedef struct rle_config {
                                         critics' first layer                                         */
 #define RLE_FUSE_OPT_IN RLE_FUSE_PRIOSAMPLE  /* fusions off unless set in fuse_on                      */
 typedef struct rle_plan {
-  int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity, TD3 3/4) */
+  int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity; TD3 7/8, TD7 at B >= 1024 3/2) */
   int steps_per_graph;  /* steps per multi-step graph (-1: TD7 6, SAC 8, TD3 16; 0: single-step only)  */
   int pre_tn;           /* tile width of pre-GEMM consumers (0: TD3 64, else 32)                         */
   int pl_tn;            /* tile width of pre-layer consumers (0: 64)                                     */

@@ -3811,10 +3811,15 @@ struct Engine {
       for (auto& op : lv)
         if (op.kind == OP_GEMM) at(op.seq) = std::max(op.gemm.tn, plan.tn_min);
     int cap = std::max(256, level_capacity());  // (plan.level_cap 0)
-    // TD3 (its first layers folded into 64-wide pre-layer consumers) plans its levels for 3/4 of the
+    // TD3 (its first layers folded into 64-wide pre-layer consumers) plans its levels for 7/8 of the
     // resident workgroups: A/B on HalfCheetah, capacity 1024 / 832 / 768 / 640 -> 23.18k / 23.47k /
-    // 23.47k / 23.37k steps/s (TD7: 1024 best, 896 -1.2%; SAC: 1024 best, 768 -0.8%)
-    if (algo == RLE_TD3) cap = cap * 3 / 4;
+    // 23.47k / 23.37k steps/s in round 3; with the two-stage prologue and its own kernel instance
+    // (round 4, 2 pairs) 1024 / 896 / 768 / 640 -> 25.22k / 25.33k / 25.23k / 24.94k.  TD7 at
+    // B >= 1024 plans for 3/2 of them (its levels are over capacity anyway; 2 pairs at B = 1024:
+    // 1024 / 1536 / 2048 -> 3564 / 3598 / 3529).  (TD7 B = 256: 1024 best, 896 -1.2%; SAC: 1024 best,
+    // 768 -0.8%.)
+    if (algo == RLE_TD3) cap = cap * 7 / 8;
+    if (algo == RLE_TD7 && B >= 1024) cap = cap * 3 / 2;
     // (plan.level_cap: tuning experiments, and seeds per GPU on streams -- bench.py)
     if (plan.level_cap > 0) cap = plan.level_cap;
     // elementwise ops (Polyak, copies) are short: they free their slots long before the level's
