@@ -1468,7 +1468,7 @@ struct Engine {
   }
   void resolve_plan() {
     if (plan.steps_per_graph < 0) plan.steps_per_graph = algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 6;
-    if (plan.pre_tn == 0) plan.pre_tn = algo == RLE_TD3 ? 64 : 32;
+    if (plan.pre_tn == 0) plan.pre_tn = algo == RLE_TD7 ? 32 : 64;  // (SAC: its target critics' raw-head pre-GEMM)
     plan.pre_tn = plan.pre_tn == 32 || plan.pre_tn == 64 ? plan.pre_tn : 16;
     if (plan.pl_tn == 0) plan.pl_tn = 64;
     plan.pl_tn = plan.pl_tn == 16 || plan.pl_tn == 32 ? plan.pl_tn : 64;
@@ -2126,7 +2126,7 @@ struct Engine {
     // gradient's operand) is the same floats as the consumer's copy, whatever the planner widens)
     // (a pre-GEMM consumer that is also a pre-layer source: at most 32 wide, as any pl_src)
     const int tn = sfu ? 64
-                       : (pre && pre->kind >= 3 ? std::max(tq.first, pl_tn())
+                       : (pre && (pre->kind == 3 || pre->kind == 4) ? std::max(tq.first, pl_tn())
                           : pre && (pre->kind == 1 || pre->kind == 5)
                               ? (pl_src ? std::min(std::max(tq.first, pre_tn()), 32) : std::max(tq.first, pre_tn()))
                                                   : (pl_src ? std::min(tq.first, 32) : tq.first));
