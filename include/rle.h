@@ -78,7 +78,7 @@ typedef struct rle_config {
 typedef struct rle_plan {
   int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity; TD3 7/8, TD7 at B >= 1024 3/2) */
   int steps_per_graph;  /* steps per multi-step graph (-1: TD7 6, SAC 8, TD3 16; 0: single-step only)  */
-  int pre_tn;           /* tile width of pre-GEMM consumers (0: TD7 32, else 64)                         */
+  int pre_tn;           /* tile width of pre-GEMM consumers (0: TD3 64, else 32)                         */
   int pl_tn;            /* tile width of pre-layer consumers (0: 64)                                     */
   int tn_min;           /* narrowest GEMM tile (0: 16)                                                   */
   int flat_div;         /* Polyak / copy workgroups count 1 / flat_div in the planner (0: 4)            */

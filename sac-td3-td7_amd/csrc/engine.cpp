@@ -1468,7 +1468,8 @@ struct Engine {
   }
   void resolve_plan() {
     if (plan.steps_per_graph < 0) plan.steps_per_graph = algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 6;
-    if (plan.pre_tn == 0) plan.pre_tn = algo == RLE_TD7 ? 32 : 64;  // (SAC: its target critics' raw-head pre-GEMM)
+    // (SAC's target critics' raw-head pre-GEMM consumers: 32 measured +1.0% over 64, 2 pairs)
+    if (plan.pre_tn == 0) plan.pre_tn = algo == RLE_TD3 ? 64 : 32;
     plan.pre_tn = plan.pre_tn == 32 || plan.pre_tn == 64 ? plan.pre_tn : 16;
     if (plan.pl_tn == 0) plan.pl_tn = 64;
     plan.pl_tn = plan.pl_tn == 16 || plan.pl_tn == 32 ? plan.pl_tn : 64;
