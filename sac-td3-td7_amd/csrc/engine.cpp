@@ -927,8 +927,9 @@ static void op_accesses(const Op& op, std::vector<Access>& v) {
         acc_bytes(v, c.vt, 8, 1, "vt");
       } else {
         acc_bytes(v, c.counters, 3 * 8, 0, "counters");
-        acc_bytes(v, c.adam_step, 3 * 4, 1, "adam step");
-        acc_bytes(v, c.adam_bc2s, 3 * 4, 1, "adam bc2s");
+        acc_bytes(v, c.adam_step, (c.la_t ? 4 : 3) * 4, 1, "adam step");
+        acc_bytes(v, c.adam_bc2s, (c.la_t ? 4 : 3) * 4, 1, "adam bc2s");
+        if (c.la_t) acc_bytes(v, c.la_t, 8, 0, "la_t");
       }
       break;
     }
@@ -3633,6 +3634,9 @@ struct Engine {
       a.la_v = P + 2 * nP + (nP - 4);
       a.la_t = &ctrl->la_t;
       a.la_lr = cfg.policy_lr;
+      a.adam_step = adam_step_of(asc_set);  // (slot 3: the temperature's bias corrections, this step's ctrl)
+      a.adam_bc2s = adam_bc2s_of(asc_set);
+      rd.push_back(asc_set ? R_ADAMSC1 : R_ADAMSC);
       a.target_entropy = -(float)A;
       a.logpi_part = ploss_part;
       a.nlogpi = hw;
@@ -3919,7 +3923,14 @@ struct Engine {
 
   // Adam bias-correction scalars of this step from the completed-step counters; the
   // op has no producers, so it runs in level 0 beside the LAP block sums.
-  void add_adam_scalars(Prog& pg) { pg.add(adam_scalars_op(asc_set), {R_CNT}, {asc_set ? R_ADAMSC1 : R_ADAMSC}); }
+  // (SAC autotune: also the temperature optimizer's bias corrections, from la_t, which the previous
+  // step end wrote: R_LA)
+  bool sac_tmp_auto() const { return algo == RLE_SAC && cfg.tmp < 0.f; }
+  void add_adam_scalars(Prog& pg) {
+    std::vector<int> rd{R_CNT};
+    if (sac_tmp_auto()) rd.push_back(R_LA);
+    pg.add(adam_scalars_op(asc_set), rd, {asc_set ? R_ADAMSC1 : R_ADAMSC});
+  }
   Op adam_scalars_op(int set) {
     Op op{};
     op.kind = OP_CTRL;
@@ -3932,6 +3943,10 @@ struct Engine {
     c.adam_lr[CNT_ADAM_Q] = cfg.critic_lr;
     c.adam_lr[CNT_ADAM_PI] = cfg.policy_lr;
     c.adam_lr[CNT_ADAM_ENC] = cfg.policy_lr;
+    if (sac_tmp_auto()) {
+      c.la_t = &ctrl->la_t;
+      c.la_lr = cfg.policy_lr;
+    }
     return op;
   }
 

@@ -2566,6 +2566,8 @@ __device__ __forceinline__ void adam_scalars(long long t, float lr, GAS float* s
 // All partial-sum reductions of the step end in one pass: every thread loads its
 // elements of every sum (independent loads, one memory round trip), parks its
 // per-sum partials in LDS, then wave w reduces sums w, w+4, ... (fixed order).
+// (SAC: the temperature terms, compiled into the TD3 / SAC and extended instances only)
+template <bool SAC>
 __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* smem, unsigned long long* tr) {
   constexpr int kSums = kInfoMax + 1 + 9;  // info sums, logpi, grad-norm tensors
   float* res = smem + kSums * kThreads;    // [kSums]
@@ -2577,11 +2579,14 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
   const long long cnt = (w0 && tid < 16 && a.mode != 2) ? G(a.counters)[tid] : 0;
   const int slot0 = (w0 && a.info_slot && a.mode != 1) ? G(a.info_slot)[0] : 0;
   const int mode = a.mode;
-  const bool scr = mode == 2 && a.sac_scratch;  // (alpha and the logpi sum from the counters op)
-  const bool sac_tmp = a.log_alpha && a.la_lr > 0.f && mode != 2;
-  const float la = a.log_alpha && !scr ? G(a.log_alpha)[0] : 0.f;
+  const bool scr = SAC && mode == 2 && a.sac_scratch;  // (alpha and the logpi sum from the counters op)
+  const bool sac_tmp = SAC && a.log_alpha && a.la_lr > 0.f && mode != 2;
+  const float la = SAC && a.log_alpha && !scr ? G(a.log_alpha)[0] : 0.f;
   const float la_m = sac_tmp ? G(a.la_m)[0] : 0.f, la_v = sac_tmp ? G(a.la_v)[0] : 0.f;
   const long long la_t = sac_tmp ? G(a.la_t)[0] : 0;
+  // (the temperature's bias corrections: from the step's control op when it computed them, slot 3)
+  const bool la_pre = sac_tmp && a.adam_step;
+  const float la_bx = la_pre ? G(a.adam_step)[3] : 0.f, la_by = la_pre ? G(a.adam_bc2s)[3] : 0.f;
   const float scr_alpha = scr ? G(a.sac_scratch)[0] : 0.f, scr_slp = scr ? G(a.sac_scratch)[1] : 0.f;
   FINE_MARK(0);
   // sum list: j < ninfo -> info k (if summed); kInfoMax -> logpi; kInfoMax+1+q -> gsq tensor q
@@ -2683,7 +2688,7 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
   FINE_MARK(4);
   if (sac_tmp && tid == 0) {  // optim_tmp.step (sac.py:283)
     const float g = tmp_obj;
-    const float2 bc = adam_bias(la_t, a.la_lr);
+    const float2 bc = la_pre ? make_float2(la_bx, la_by) : adam_bias(la_t, a.la_lr);
     float m = la_m, v2 = la_v;
     m = m + (float)(1.0 - 0.9) * (g - m);
     v2 = v2 * 0.999f + ((float)(1.0 - 0.999) * g) * g;
@@ -2739,6 +2744,7 @@ __device__ __forceinline__ void op_maxred(const CAS FlatArgs& f, int t, float* s
   }
 }
 
+template <bool SAC>  // (SAC: the temperature's bias corrections; not compiled into the TD7 instance)
 __device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
   if (threadIdx.x != 0) return;
   if (c.mode == 0) {
@@ -2746,6 +2752,7 @@ __device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
     GW(c.vt)[1] = unkey(G(c.vmin_key)[0]);
   } else {
     for (int k = 0; k < 3; ++k) adam_scalars(G(c.counters)[k], c.adam_lr[k], GW(c.adam_step) + k, GW(c.adam_bc2s) + k);
+    if (SAC && c.la_t) adam_scalars(G(c.la_t)[0], c.la_lr, GW(c.adam_step) + 3, GW(c.adam_bc2s) + 3);
   }
 }
 
@@ -2860,11 +2867,11 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     RLE_OP(OP_PRIORITY, op_priority(op.prio, smem))
     RLE_OP(OP_SAC_ACTOR, op_sac_actor(op.sac, t))
     RLE_OP(OP_SAC_ACTOR_BWD, op_sac_actor_bwd(op.sac, t))
-    RLE_OP(OP_STEP_END, op_step_end(op.end, smem, tr))
+    RLE_OP(OP_STEP_END, op_step_end<KS != KS_TD7>(op.end, smem, tr))
     RLE_OP(OP_POLYAK, op_polyak(op.flat, t))
     RLE_OP(OP_COPY, op_copy(op.flat, t))
     RLE_OP(OP_MAXRED, op_maxred(op.flat, t, smem))
-    RLE_OP(OP_CTRL, op_ctrl(op.ctrl))
+    RLE_OP(OP_CTRL, op_ctrl<KS != KS_TD7>(op.ctrl))
     RLE_OP(OP_NOISE, op_noise(op.sample, t))
     RLE_OP(OP_FOLDBIAS, op_foldbias(op.fb))
 #endif

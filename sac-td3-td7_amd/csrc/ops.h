@@ -452,7 +452,7 @@ struct StepEndArgs {
   int kind[kInfoMax]; int ninfo;
   // SAC temperature
   float* log_alpha; float* la_m; float* la_v; long long* la_t; float la_lr; float target_entropy;
-  float* adam_step; float* adam_bc2s; float adam_lr[4];  // next-step Adam scalars of counters 0..2
+  float* adam_step; float* adam_bc2s; float adam_lr[4];  // (SAC autotune) slot 3: the temperature optimizer's bias corrections from this step's control op
   const float* logpi_part; int nlogpi; float inv_b;
   const float* gsq; int gsq_off[9]; int ngsq_t;      // TD3 grad norm: tensor t = tiles [off[t], off[t+1])
   // 0: the whole step end; 1: counters (+ the SAC temperature update, which needs the logpi sum)
@@ -496,6 +496,9 @@ struct CtrlArgs {   // small control-plane writes
   int mode;          // 0: value bounds copy at the hard update; 1: Adam scalars from the counters
   const int* vmax_key; const int* vmin_key; float* vt;
   const long long* counters; float* adam_step; float* adam_bc2s; float adam_lr[4];
+  // (mode 1, SAC with an autotuned temperature: the temperature optimizer's bias corrections from its step
+  // count into adam_step[3] / adam_bc2s[3], so the step end does not compute them on the chain)
+  const long long* la_t; float la_lr;
 };
 
 struct Op {
