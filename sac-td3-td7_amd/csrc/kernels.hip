@@ -2746,13 +2746,15 @@ __device__ __forceinline__ void op_maxred(const CAS FlatArgs& f, int t, float* s
 
 template <bool SAC>  // (SAC: the temperature's bias corrections; not compiled into the TD7 instance)
 __device__ __forceinline__ void op_ctrl(const CAS CtrlArgs& c) {
-  if (threadIdx.x != 0) return;
+  const int k = threadIdx.x;
   if (c.mode == 0) {
+    if (k != 0) return;
     GW(c.vt)[0] = unkey(G(c.vmax_key)[0]);
     GW(c.vt)[1] = unkey(G(c.vmin_key)[0]);
-  } else {
-    for (int k = 0; k < 3; ++k) adam_scalars(G(c.counters)[k], c.adam_lr[k], GW(c.adam_step) + k, GW(c.adam_bc2s) + k);
-    if (SAC && c.la_t) adam_scalars(G(c.la_t)[0], c.la_lr, GW(c.adam_step) + 3, GW(c.adam_bc2s) + 3);
+  } else if (k < 3) {  // (one lane per optimizer: the fp64 pow pairs side by side, not one after another)
+    adam_scalars(G(c.counters)[k], c.adam_lr[k], GW(c.adam_step) + k, GW(c.adam_bc2s) + k);
+  } else if (SAC && k == 3 && c.la_t) {
+    adam_scalars(G(c.la_t)[0], c.la_lr, GW(c.adam_step) + 3, GW(c.adam_bc2s) + 3);
   }
 }
 
