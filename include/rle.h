@@ -89,6 +89,8 @@ typedef struct rle_plan {
   unsigned fuse_on;     /* RLE_FUSE_OPT_IN bits switched on                                             */
   int rb;               /* 1: 32 / 64-wide weight-gradient tiles register-blocked (the 4 waves split the batch
                            rows, each accumulates every column block; -1: default)                       */
+  int pl_w;             /* rebalance weight added to GEMMs with an in-tile prologue (pre-layer, two-stage,
+                           SAC raw head; -1: default, SAC 24, else 0)                                     */
 } rle_plan;
 
 /* ---- replay memory: rl/replay_memory/{lap,simple}.py ---------------------- */

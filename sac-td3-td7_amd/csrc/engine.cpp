@@ -1100,6 +1100,7 @@ struct Prog {
   // (rle_plan tiny_w / uni_w / tiny_wg; A/B tiny_w 0 / 20 / 30: TD7 8021 / 8050 / 8054, SAC 12249 /
   // 12235 / 12328; uni_w 60 as the LAP sampler, 12 with tiny_wg 64: SAC +-0, TD3 -0.5%)
   int tiny_w = 30, uni_w = 60, tiny_wg = 2;
+  int pl_w = 0;  // (rle_plan pl_w) added to GEMMs whose workgroups run an in-tile prologue (has_pre 3-5)
   int tiny_weight() const { return tiny_w ? tiny_w : 8; }
   int uniform_weight() const { return uni_w; }
   bool tiny_moves() const { return tiny_w != 0; }
@@ -1107,7 +1108,8 @@ struct Prog {
     int w = 0;
     for (const Op& op : it.ops) {
       int x = 8;
-      if (op.kind == OP_GEMM) x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? 8 : 0);
+      if (op.kind == OP_GEMM)
+        x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? 8 : 0) + (op.gemm.has_pre >= 3 ? pl_w : 0);
       else if (op.kind == OP_HEAD) x = 60;
       else if (op.kind == OP_SAMPLE_GATHER) x = op.sample.lap ? 60 : uniform_weight();  // (uniform: a
                                                                                          // ~6 us gather)
@@ -1452,6 +1454,7 @@ static rle_plan plan_defaults() {
   p.balance = -1;
   p.tiny_w = p.uni_w = p.tiny_wg = -1;
   p.rb = -1;
+  p.pl_w = -1;
   return p;
 }
 
@@ -1482,6 +1485,9 @@ struct Engine {
     if (plan.tiny_wg < 0) plan.tiny_wg = 2;
     plan.sched_cap = plan.sched_cap ? 1 : 0;
     plan.rb = plan.rb < 0 ? 0 : (plan.rb ? 1 : 0);
+    // (A/B, 2 pairs: SAC Humanoid pl_w 0 / 8 / 16 / 24 -> 14.09k / 14.09k / 14.11k / 14.15k; TD3 HalfCheetah
+    // 25.37k / 25.33k / 25.38k / 25.36k)
+    if (plan.pl_w < 0) plan.pl_w = algo == RLE_SAC ? 24 : 0;
     if (plan.level_cap < 0) plan.level_cap = 0;
   }
   int S, Sp, A, Ap, H, Hp, B;
@@ -3672,6 +3678,7 @@ struct Engine {
     pg.tiny_w = plan.tiny_w;
     pg.uni_w = plan.uni_w;
     pg.tiny_wg = plan.tiny_wg;
+    pg.pl_w = plan.pl_w;
     auto levels = pg.schedule(sched_cap());
     Graph G;
     size_t total = 0;
