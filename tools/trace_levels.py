@@ -38,6 +38,12 @@ JSON = sys.argv[3] if len(sys.argv) > 3 else None  # per-op-kind spans (bench.py
 opspans = {}
 for which in graphs:
     tr = eng.trace(which).astype(np.int64)
+    if which == 3 and tr.size and not tr.any():
+        # (rle_graph_trace(3) reads the multi-step graph of the last single policy step's batch set;
+        # SAC's trailing singles can leave it on the set whose multi-step graph did not run: one
+        # more single step flips it)
+        eng.step_timed(1)
+        tr = eng.trace(which).astype(np.int64)
     if tr.size == 0:
         continue
     tot_t = 0.0
