@@ -79,11 +79,12 @@ typedef struct rle_plan {
   int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity; TD3 7/8, TD7 at B >= 1024 3/2) */
   int steps_per_graph;  /* steps per multi-step graph (-1: TD7 6, SAC 8, TD3 16; 0: single-step only)  */
   int pre_tn;           /* tile width of pre-GEMM consumers (0: TD3 64, else 32)                         */
-  int pl_tn;            /* tile width of pre-layer consumers (0: 64)                                     */
+  int pl_tn;            /* tile width of pre-layer consumers (0: SAC 32, else 64)                        */
   int tn_min;           /* narrowest GEMM tile (0: 16)                                                   */
   int flat_div;         /* Polyak / copy workgroups count 1 / flat_div in the planner (0: 4)            */
   int balance;          /* rebalance pass (-1: 1 = on; 0 off)                                            */
-  int tiny_w, uni_w, tiny_wg;  /* rebalance weights: step end, uniform sampler, tiny-op bound (-1: 30, 60, 2) */
+  int tiny_w, uni_w, tiny_wg;  /* rebalance weights: step end, uniform sampler, tiny-op bound (-1: 30,
+                                  SAC 30 / TD3 8 / TD7 60, 2) */
   int sched_cap;        /* 1: the scheduler defers ops past level_cap workgroups to a later level       */
   unsigned fuse_off;    /* RLE_FUSE_* bits switched off (A/B, tests); 0 = every default fusion on       */
   unsigned fuse_on;     /* RLE_FUSE_OPT_IN bits switched on                                             */

@@ -1475,13 +1475,18 @@ struct Engine {
     // (SAC's target critics' raw-head pre-GEMM consumers: 32 measured +1.0% over 64, 2 pairs)
     if (plan.pre_tn == 0) plan.pre_tn = algo == RLE_TD3 ? 64 : 32;
     plan.pre_tn = plan.pre_tn == 32 || plan.pre_tn == 64 ? plan.pre_tn : 16;
-    if (plan.pl_tn == 0) plan.pl_tn = 64;
+    // (SAC pl_tn 32: its 64-workgroup actor-DX pre-layer level; with uni_w 30, A/B 2 pairs: 14.40k -> 14.55k;
+    // TD3 32: -5%)
+    if (plan.pl_tn == 0) plan.pl_tn = algo == RLE_SAC ? 32 : 64;
     plan.pl_tn = plan.pl_tn == 16 || plan.pl_tn == 32 ? plan.pl_tn : 64;
     plan.tn_min = plan.tn_min == 32 || plan.tn_min == 64 ? plan.tn_min : 16;
     if (plan.flat_div <= 0) plan.flat_div = 4;
     if (plan.balance < 0) plan.balance = 1;
     if (plan.tiny_w < 0) plan.tiny_w = 30;
-    if (plan.uni_w < 0) plan.uni_w = 60;
+    // (uniform sampler weight, A/B 2 pairs, SAC Humanoid uni_w 60 / 45 / 30 / 15 -> 14.10k / 14.13k / 14.40k /
+    // 14.39k; TD3 HalfCheetah 60 / 30 / 20 / 15 / 8 / 1 -> 25.40k / 25.42k / 25.30k / 25.81k / 25.84k / 25.76k: a
+    // lighter sampler is moved off the level it would bound)
+    if (plan.uni_w < 0) plan.uni_w = algo == RLE_SAC ? 30 : algo == RLE_TD3 ? 8 : 60;
     if (plan.tiny_wg < 0) plan.tiny_wg = 2;
     plan.sched_cap = plan.sched_cap ? 1 : 0;
     plan.rb = plan.rb < 0 ? 0 : (plan.rb ? 1 : 0);

@@ -1,4 +1,4 @@
 set -o pipefail
-export RLE_LIB=$PWD/sac-td3-td7_amd/lib/librle_exp8.so
-AB_TAG=_td3w BENCH_ARGS="--algo td3 --env HalfCheetah-v4" bash tools/abplan.sh 2 6000 "-" "pl_w=8" "pl_w=16" "pl_w=24" || exit 1
-AB_TAG=_sacw BENCH_ARGS="--algo sac" bash tools/abplan.sh 2 3000 "-" "pl_w=8" "pl_w=16" "pl_w=24" || exit 1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > gpurun_out/r04_gpu_tests.txt 2>&1 || { tail -40 gpurun_out/r04_gpu_tests.txt; exit 1; }
+tail -2 gpurun_out/r04_gpu_tests.txt
+bash tools/r04_final2.sh || exit 1
