@@ -1101,6 +1101,7 @@ struct Prog {
   // 12235 / 12328; uni_w 60 as the LAP sampler, 12 with tiny_wg 64: SAC +-0, TD3 -0.5%)
   int tiny_w = 30, uni_w = 60, tiny_wg = 2;
   int pl_w = 0;  // (rle_plan pl_w) added to GEMMs whose workgroups run an in-tile prologue (has_pre 3-5)
+  int lap_w = 60, head_w = 60, adam_w = 8;  // (rle_plan lap_w / head_w / adam_w)
   int tiny_weight() const { return tiny_w ? tiny_w : 8; }
   int uniform_weight() const { return uni_w; }
   bool tiny_moves() const { return tiny_w != 0; }
@@ -1109,9 +1110,9 @@ struct Prog {
     for (const Op& op : it.ops) {
       int x = 8;
       if (op.kind == OP_GEMM)
-        x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? 8 : 0) + (op.gemm.has_pre >= 3 ? pl_w : 0);
-      else if (op.kind == OP_HEAD) x = 60;
-      else if (op.kind == OP_SAMPLE_GATHER) x = op.sample.lap ? 60 : uniform_weight();  // (uniform: a
+        x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? adam_w : 0) + (op.gemm.has_pre >= 3 ? pl_w : 0);
+      else if (op.kind == OP_HEAD) x = head_w;
+      else if (op.kind == OP_SAMPLE_GATHER) x = op.sample.lap ? lap_w : uniform_weight();  // (uniform: a
                                                                                          // ~6 us gather)
       else if (op.kind == OP_STEP_END && op.end.mode != 1) x = tiny_weight();  // (one workgroup, ~4 KB of straight-line
                                                            // code fetched at L2 latency: 7-8 us)
@@ -1455,6 +1456,7 @@ static rle_plan plan_defaults() {
   p.tiny_w = p.uni_w = p.tiny_wg = -1;
   p.rb = -1;
   p.pl_w = -1;
+  p.lap_w = p.head_w = p.adam_w = -1;
   return p;
 }
 
@@ -1493,6 +1495,9 @@ struct Engine {
     // (A/B, 2 pairs: SAC Humanoid pl_w 0 / 8 / 16 / 24 -> 14.09k / 14.09k / 14.11k / 14.15k; TD3 HalfCheetah
     // 25.37k / 25.33k / 25.38k / 25.36k)
     if (plan.pl_w < 0) plan.pl_w = algo == RLE_SAC ? 24 : 0;
+    if (plan.lap_w < 0) plan.lap_w = 60;
+    if (plan.head_w < 0) plan.head_w = 60;
+    if (plan.adam_w < 0) plan.adam_w = 8;
     if (plan.level_cap < 0) plan.level_cap = 0;
   }
   int S, Sp, A, Ap, H, Hp, B;
@@ -3684,6 +3689,9 @@ struct Engine {
     pg.uni_w = plan.uni_w;
     pg.tiny_wg = plan.tiny_wg;
     pg.pl_w = plan.pl_w;
+    pg.lap_w = plan.lap_w;
+    pg.head_w = plan.head_w;
+    pg.adam_w = plan.adam_w;
     auto levels = pg.schedule(sched_cap());
     Graph G;
     size_t total = 0;
