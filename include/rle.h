@@ -93,7 +93,7 @@ typedef struct rle_plan {
   int pl_w;             /* rebalance weight added to GEMMs with an in-tile prologue (pre-layer, two-stage,
                            SAC raw head; -1: default, SAC 24, else 0)                                     */
   int lap_w, head_w, adam_w; /* rebalance weights: LAP sampler, loss head, added to Adam-epilogue GEMMs
-                                (-1: 60, 60, 8)                                                           */
+                                (-1: 60, 60, SAC 16 / else 8)                                             */
 } rle_plan;
 
 /* ---- replay memory: rl/replay_memory/{lap,simple}.py ---------------------- */

@@ -1497,7 +1497,10 @@ struct Engine {
     if (plan.pl_w < 0) plan.pl_w = algo == RLE_SAC ? 24 : 0;
     if (plan.lap_w < 0) plan.lap_w = 60;
     if (plan.head_w < 0) plan.head_w = 60;
-    if (plan.adam_w < 0) plan.adam_w = 8;
+    // (A/B 2 pairs, SAC Humanoid adam_w 0 / 8 / 12 / 16 / 24 / 32 -> 14.38k / 14.56k / 14.67k / 14.67k / 14.64k /
+    // 14.67k; TD3 HalfCheetah 0 / 8 / 16 -> 25.81k / 25.84k / 25.00k; TD7 Humanoid 0 / 8 / 16 -> 8.17k / 8.25k /
+    // 8.24k, B = 1024 flat: profiles/r04_ab_weights.txt)
+    if (plan.adam_w < 0) plan.adam_w = algo == RLE_SAC ? 16 : 8;
     if (plan.level_cap < 0) plan.level_cap = 0;
   }
   int S, Sp, A, Ap, H, Hp, B;

@@ -1,4 +1,4 @@
 set -o pipefail
-AB_TAG=_td7w BENCH_ARGS="" bash tools/abplan.sh 2 4000 "-" "lap_w=20" "lap_w=40" "head_w=30" "head_w=90" "adam_w=0" "adam_w=16" || exit 1
-AB_TAG=_sacw2 BENCH_ARGS="--algo sac" bash tools/abplan.sh 2 3000 "-" "head_w=30" "adam_w=0" "adam_w=16" || exit 1
-AB_TAG=_td3w2 BENCH_ARGS="--algo td3 --env HalfCheetah-v4" bash tools/abplan.sh 2 6000 "-" "head_w=30" "adam_w=0" "adam_w=16" || exit 1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > gpurun_out/r04_gpu_tests.txt 2>&1 || { tail -40 gpurun_out/r04_gpu_tests.txt; exit 1; }
+tail -2 gpurun_out/r04_gpu_tests.txt
+bash tools/r04_final2.sh || exit 1
