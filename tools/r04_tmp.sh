@@ -1,4 +1,4 @@
 set -o pipefail
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > gpurun_out/r04_gpu_tests.txt 2>&1 || { tail -40 gpurun_out/r04_gpu_tests.txt; exit 1; }
-tail -2 gpurun_out/r04_gpu_tests.txt
-bash tools/r04_final2.sh || exit 1
+AB_TAG=_td7w2 BENCH_ARGS="" bash tools/abplan.sh 2 4000 "-" "adam_w=4" "adam_w=6" "adam_w=10" "adam_w=12" || exit 1
+AB_TAG=_td3w3 BENCH_ARGS="--algo td3 --env HalfCheetah-v4" bash tools/abplan.sh 2 6000 "-" "tiny_w=15" "tiny_w=60" "pl_w=8" "adam_w=4" || exit 1
+AB_TAG=_sacw4 BENCH_ARGS="--algo sac" bash tools/abplan.sh 2 3000 "-" "tiny_w=15" "tiny_w=60" "head_w=30" || exit 1
