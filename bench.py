@@ -192,6 +192,9 @@ def _cpu_run(seconds, algo, env, batch, lap, s_dim, a_dim, hi, agents, replay, s
                       f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads} pinned one per physical core "
                       f"of socket {pinning['socket']} ({pinning['physical_cores_socket']} physical cores; the box's "
                       f"share is 16 CPUs)",
+            # the GPU boxes share their host with other jobs: the same oracle run measured 34.5-53.9 steps/s
+            # (TD7 Humanoid B=256) on different boxes in rounds 3-4, i.e. about 1.5x box to box
+            "box_to_box_spread": "about 1.5x (TD7 Humanoid B=256: 34.5-53.9 steps/s across GPU boxes, rounds 3-4)",
             "host": hc}
 
 
@@ -374,7 +377,12 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
                    "replay": N_REPLAY, "lap": lap, "policy_freq": 2, "target_update_rate": 250,
                    "parallelism": f"replicas x{n_gpus} (one seed per GPU, no collective)"},
         "roofline": roofline,
-        "gpu_event_s": round(gpu_s, 6),
+        # the engine's own elapsed time over the timed steps: under the default direct AQL dispatch it is host
+        # wall time from the first doorbell to the last packet's completion signal (rle_step_timed, rle.h);
+        # with RLE_AQL=0 HIP event time on the engine's stream
+        "engine_s": round(gpu_s, 6),
+        "engine_timer": ("host wall, first AQL doorbell to completion signal" if os.environ.get("RLE_AQL", "1") != "0"
+                         else "HIP events on the engine stream"),
     }
 
 
@@ -581,7 +589,9 @@ def main():
     cuda_sync(local)
     n_l0 = eng.launch_count()
     t0 = time.perf_counter()
+    c0 = time.thread_time()  # (CPU time of this thread: rle_step_timed waits in it, ctypes releases the GIL)
     gpu_ms = eng.step_timed(args.steps)
+    c1 = time.thread_time()
     cuda_sync(local)
     t1 = time.perf_counter()
     launches = (eng.launch_count() - n_l0) / args.steps
@@ -595,6 +605,9 @@ def main():
     out = summarize(world, args.steps, args.warmup, wall, gpu_s, lv_policy, lv_plain, args.algo, args.env,
                     args.batch, lap, launches)
     out["config"]["plan"] = eng.plan()
+    # share of the timed region the stepping thread spent on a host core (the AQL wait sleeps: engine.cpp
+    # aql_wait_step), i.e. what is left for MuJoCo stepping beside the engine (north_star)
+    out["host_thread_busy_frac"] = round((c1 - c0) / max(wall, 1e-9), 4)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.algo, args.env, args.batch, lap)
     print(json.dumps(out), flush=True)

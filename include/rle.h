@@ -164,8 +164,13 @@ int rle_set_value_bounds(rle_engine* e, const float* in4);
  * device incl. sampling and LAP priority update.  info_out: [n_steps][RLE_INFO_MAX] (per-agent
  * key order; NaN = None).  One host sync per call. */
 int rle_step(rle_engine* e, int n_steps, float* info_out);
-/* Benchmark form of rle_step: n_steps without info readback, bracketed by HIP events recorded
- * on the engine's own stream; *gpu_ms = elapsed event time.  Syncs once at the end. */
+/* Benchmark form of rle_step: n_steps without info readback; *gpu_ms = the engine's elapsed time.
+ * Under the default direct AQL dispatch (RLE_AQL unset or 1; the levels go to the engine's own HSA
+ * queue, opened at its first synchronous step) that is HOST WALL time from the first doorbell to the
+ * last packet's completion signal; with RLE_AQL=0 (hipGraph replays) it is HIP event time on the
+ * engine's stream.  The host thread sleeps while the expected remainder of the burst exceeds 150 us
+ * and spins only for the tail (rle_aql_wait_plan); a burst that does not complete within 60 s closes
+ * the engine's queue (every later step fails).  Syncs once at the end. */
 int rle_step_timed(rle_engine* e, int n_steps, float* gpu_ms);
 /* Enqueue n_steps as rle_step does, without any host sync or info readback (the device info
  * ring keeps the last rows); rle_synchronize waits.  Lets one host thread drive several
@@ -241,6 +246,10 @@ int rle_graph_trace(rle_engine* e, int which, unsigned long long* out, long long
 /* Timestamps per workgroup in rle_graph_trace rows: 4, or 16 in diagnostics builds
  * (-DRLE_TRACE_FINE: slots 4.. are finer in-op stamps). */
 int rle_trace_stride(void);
+/* The AQL wait policy of rle_step / rle_step_timed (no GPU): given the expected duration of what is
+ * outstanding and the time waited so far, returns 0 spin on the completion signal, 1 sleep *sleep_us
+ * then check again, 2 time out (the engine's queue is then closed). */
+int rle_aql_wait_plan(double expected_us, double elapsed_us, double timeout_s, double* sleep_us);
 /* Copy all weights/optimizer state/counters of src into dst (checkpoint agent,
  * ckpt_agent.load_state_dict(agent), run_w_checkpoint.py:140). Same config required. */
 int rle_copy_state(rle_engine* dst, rle_engine* src);

@@ -24,6 +24,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ops.h"
@@ -1280,6 +1281,8 @@ struct AqlQueue {
     int ks;
   };
   std::vector<Pending> pending;
+  double us_per_launch = 10.0;  // measured mean dispatch-to-completion time per packet (EWMA over flushes)
+  bool failed = false;          // a flush timed out: its packets may still be queued, the queue takes no more
   ~AqlQueue() {
     if (q) (void)hsa_queue_destroy(q);
     if (sig.handle) (void)hsa_signal_destroy(sig);
@@ -1353,11 +1356,47 @@ static std::unique_ptr<AqlQueue> aql_open(int dev) {
   return A;
 }
 
+// How the host waits for a flush without holding its core (MuJoCo stepping runs on the host cores beside
+// the engine, north_star): while more than kAqlSpinUs of the expected duration remain it sleeps (slices of
+// at most kAqlSliceUs, the signal checked between them), then spins on the signal; past timeout_s it gives
+// up.  expected_us = packets still to retire x the queue's measured time per packet.
+constexpr double kAqlSpinUs = 150.0, kAqlSliceUs = 2000.0, kAqlTimeoutS = 60.0;
+enum AqlWaitAct : int { AQL_SPIN = 0, AQL_SLEEP = 1, AQL_TIMEOUT = 2 };
+static int aql_wait_step(double expected_us, double elapsed_us, double timeout_s, double* sleep_us) {
+  *sleep_us = 0.0;
+  if (elapsed_us > timeout_s * 1e6) return AQL_TIMEOUT;
+  const double left = expected_us - elapsed_us - kAqlSpinUs;
+  if (left < 20.0) return AQL_SPIN;
+  *sleep_us = std::min(left, kAqlSliceUs);
+  return AQL_SLEEP;
+}
+// Waits until pred() holds, by aql_wait_step's policy; on timeout the queue is marked failed.
+template <class Pred>
+static void aql_wait(AqlQueue& A, Pred pred, double expected_us, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!pred()) {
+    const double el = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    double sl = 0.0;
+    const int act = aql_wait_step(expected_us, el, kAqlTimeoutS, &sl);
+    if (act == AQL_TIMEOUT) {
+      A.failed = true;
+      A.pending.clear();
+      throw Error{RLE_EHIP, std::string("aql: ") + what + " did not complete within 60 s; the engine's queue is "
+                            "closed (every later step fails; destroy the engine)"};
+    }
+    if (act == AQL_SLEEP) std::this_thread::sleep_for(std::chrono::duration<double, std::micro>(sl));
+  }
+}
+
 // Writes every pending packet, rings the doorbell and waits for the last (host-side wall time
 // from the first doorbell to completion into *ms when given).
 static void aql_flush(AqlQueue& A, double* ms) {
   const size_t n = A.pending.size();
   if (!n) return;
+  if (A.failed) {
+    A.pending.clear();
+    throw Error{RLE_EHIP, "aql: the engine's queue is closed after a timed-out dispatch"};
+  }
   hsa_signal_store_relaxed(A.sig, 1);
   hsa_queue_t* q = A.q;
   const uint64_t mask = q->size - 1;
@@ -1365,7 +1404,10 @@ static void aql_flush(AqlQueue& A, double* ms) {
   bool rung = false;
   for (size_t i = 0; i < n; ++i) {
     const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
-    while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+    if (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {  // (bursts of > q->size packets)
+      const double ahead = (double)(idx - hsa_queue_load_read_index_scacquire(q) - q->size + 1);
+      aql_wait(A, [&] { return idx - hsa_queue_load_read_index_scacquire(q) < q->size; }, ahead * A.us_per_launch,
+               "a queue slot");
     }
     auto* pk = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx & mask);
     pk->workgroup_size_x = kThreads;
@@ -1396,11 +1438,12 @@ static void aql_flush(AqlQueue& A, double* ms) {
     }
   }
   A.pending.clear();
-  while (hsa_signal_wait_scacquire(A.sig, HSA_SIGNAL_CONDITION_LT, 1, 1000000000ull, HSA_WAIT_STATE_ACTIVE) >= 1) {
-    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 60)
-      throw Error{RLE_EHIP, "aql: dispatch did not complete within 60 s"};
-  }
-  if (ms) *ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  // (the packets not yet retired when the last one was written: those behind the read index)
+  const double left = (double)(hsa_queue_load_write_index_relaxed(q) - hsa_queue_load_read_index_scacquire(q));
+  aql_wait(A, [&] { return hsa_signal_load_scacquire(A.sig) < 1; }, left * A.us_per_launch, "a dispatch");
+  const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (n >= 8) A.us_per_launch = 0.5 * A.us_per_launch + 0.5 * (wall_ms * 1e3 / (double)n);
+  if (ms) *ms += wall_ms;
 }
 
 struct Graph {
@@ -3257,8 +3300,9 @@ struct Engine {
   void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, View& h0, View& h1,
                       const PreUse* pre = nullptr, bool h1_t = true, bool qd = false) {
     const bool shape = prelayer_shape(Q.layers[0], Q.layers[1]);
-    const bool two = pre && pre->kind == 1 && pre->a.mode == GEMM_FWD && qd && prelayer_ok(Q.layers[0], Q.layers[1]) &&
-                     fused(RLE_FUSE_TWOSTAGE);
+    // (the pre-GEMM's a' segment is one column block, kernels.hip PK 4 / gemm_finalize's two-stage REQUIRE)
+    const bool two = pre && pre->kind == 1 && pre->a.mode == GEMM_FWD && pre->a.N <= 32 && r16(A) <= 16 && qd &&
+                     prelayer_ok(Q.layers[0], Q.layers[1]) && fused(RLE_FUSE_TWOSTAGE);
     // (not behind a pre-GEMM: the first layer's own a segment is recomputed in-tile already)
     const bool use_pl = !pre && prelayer_ok(Q.layers[0], Q.layers[1]);
     if (two) {
@@ -3284,7 +3328,9 @@ struct Engine {
   // critic's last hidden layer (GemmArgs::has_pre 2; one level fewer on the critic chain and on
   // the policy chain).  without RLE_FUSE_HEADDX: the standalone heads (tests, A/B).
   // SAC: the rsample as the epilogue of the actor's raw head (without RLE_FUSE_SACFWD: OP_SAC_ACTOR, A/B)
-  bool sac_fwd_fused() const { return fused(RLE_FUSE_SACFWD) && 2 * A <= 64 && A <= 32; }
+  // (kernels.hip sacraw_*: three column blocks over R <= 256, gemm_finalize's REQUIRE; wider heads or larger
+  // hidden layers take OP_SAC_ACTOR)
+  bool sac_fwd_fused() const { return fused(RLE_FUSE_SACFWD) && 2 * A <= 48 && H <= 256; }
   // SAC: the actor backward as the epilogue of the da DX (without RLE_FUSE_SACBWD: OP_SAC_ACTOR_BWD, A/B)
   bool sac_bwd_fused() const { return fused(RLE_FUSE_SACBWD); }
   bool mlp_headdx() const { return fused(RLE_FUSE_HEADDX) && B % 16 == 0 && H <= 256 && H % 4 == 0; }
@@ -5085,6 +5131,13 @@ int rle_graph_trace(rle_engine* h, int which, unsigned long long* out, long long
 }
 
 int rle_trace_stride(void) { return rle::trace_stride(); }
+
+int rle_aql_wait_plan(double expected_us, double elapsed_us, double timeout_s, double* sleep_us) {
+  double sl = 0.0;
+  const int act = rle::aql_wait_step(expected_us, elapsed_us, timeout_s, &sl);
+  if (sleep_us) *sleep_us = sl;
+  return act;
+}
 
 int rle_copy_state(rle_engine* dst, rle_engine* src) {
   return guard([&] {

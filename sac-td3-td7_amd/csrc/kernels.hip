@@ -254,20 +254,6 @@ __device__ __forceinline__ float4 mat_ld4(const CAS Mat& m, int r, int c) {
   return ld4g(G(m.t) + tidx(m.rbs, r, c));
 }
 __device__ __forceinline__ void mat_st4(const CAS Mat& m, int r, int c, float4 v) {
-#ifdef RLE_EXP_ACT_NT  // experiment: activation / gradient tile stores as streaming stores
-  if (m.t) {
-    f32x4 w;
-    w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
-    __builtin_nontemporal_store(w, (GAS f32x4*)(GW(m.t) + tidx(m.rbs, r, c)));
-  }
-  if (m.n) {
-    GAS float* q = GW(m.n) + nidx(m.cbn, r, c);
-    __builtin_nontemporal_store(v.x, q);
-    __builtin_nontemporal_store(v.y, q + 4);
-    __builtin_nontemporal_store(v.z, q + 8);
-    __builtin_nontemporal_store(v.w, q + 12);
-  }
-#else
   if (m.t) st4g(GW(m.t) + tidx(m.rbs, r, c), v);
   if (m.n) {
     GAS float* q = GW(m.n) + nidx(m.cbn, r, c);  // rows r..r+3 are 4 floats apart in the N image
@@ -276,7 +262,6 @@ __device__ __forceinline__ void mat_st4(const CAS Mat& m, int r, int c, float4 v
     q[8] = v.z;
     q[12] = v.w;
   }
-#endif
 }
 
 // Phase timestamps of one workgroup (wave 0, lane 0): [0] entry, [1] main loop
@@ -344,10 +329,6 @@ __device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int off) {
   return as_f4(__builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 __device__ __forceinline__ f32x4 mfma4(const float4& a, const float4& b, f32x4 acc) {
-#ifdef RLE_EXP_NOMFMA  // timing experiment only: operands consumed by one VALU op instead of 4 MFMAs
-  acc.x += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
-  return acc;
-#endif
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
@@ -434,9 +415,6 @@ template <int SA, int SB>
 __device__ __forceinline__ f32x4 chunk_loop(__amdgpu_buffer_rsrc_t ra, int va, __amdgpu_buffer_rsrc_t rb, int vb,
                                             int n, f32x4 acc, float inva, const float* taba, const float* tabb,
                                             bool bias_ones) {
-#ifdef RLE_EXP_NOLOOP  // timing experiment only: no main-loop loads / MFMAs
-  n = 0;
-#endif
   float4 a[kRing], b[kRing];
   ring_issue(a, b, ra, va, rb, vb, n, bias_ones);
   return ring_run<SA, SB>(a, b, ra, va, rb, vb, n, acc, inva, taba, tabb, bias_ones);
@@ -528,11 +506,7 @@ __device__ __forceinline__ void chunk_loop2(__amdgpu_buffer_rsrc_t ra, int va, _
 // NBX: A = g * ti + sgn(x) * tg per reduction row (kDwNb), x from (rx, vx).
 // LDS floats: [4 waves][NB][64 lanes][4] partials, over the tables (rb_exchange waits for every
 // wave's loop first)
-#ifdef RLE_RB_OWN_LDS
-constexpr int kRbOff = 3200;
-#else
 constexpr int kRbOff = 2048;
-#endif
 template <int NB, int RG>
 struct RbRing {
   float4 a[RG], x[RG], b[RG][NB];
@@ -593,9 +567,7 @@ template <int NB>
 __device__ __forceinline__ f32x4 rb_exchange(const f32x4 (&acc)[NB], float* smem, int cg, bool lead) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* xr = smem + kRbOff;
-#ifndef RLE_RB_OWN_LDS
   __syncthreads();  // (every wave is done with the tables this region overlaps)
-#endif
 #pragma unroll
   for (int cb = 0; cb < NB; ++cb) *(f32x4*)(xr + ((wave * NB + cb) * 64 + lane) * 4) = acc[cb];
   __syncthreads();
@@ -1111,9 +1083,6 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
 #define TL_D TL(0x5f0) TL(0x630)
 #define TL_O TL(0x670)
 #define TL_Q TL(0x6b0) TL(0x770) TL(0x7b0) TL(0x870) TL(0x8b0)
-#ifdef RLE_NO_TOUCH
-  RLE_HOT_ASM("");
-#else
   if constexpr (MODE == GEMM_DW) {
     if constexpr (ACT == kDwNb) RLE_HOT_ASM(TL_B TL_D TL_X);
     else RLE_HOT_ASM(TL_B TL_D);
@@ -1131,7 +1100,6 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   } else {
     RLE_HOT_ASM(TL_A TL_B TL_S);
   }
-#endif
 #undef RLE_HOT_ASM
 #undef TL
 #undef TL_A
@@ -1169,9 +1137,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   // instruction arbitration over the shorter ops sharing a CU (A/B: +0.2-0.3%; also raising the
   // pre-GEMM and fused-head consumers: no further gain)
   if constexpr (MODE == GEMM_DW) {
-#ifndef RLE_EXP_NO_SETPRIO
     if (tn == 64) __builtin_amdgcn_s_setprio(3);
-#endif
   }
   const bool bias_tile = EPI == EPI_ADAM && jt * tn >= bias_col;
   const bool lead = kp == 0;
@@ -1189,9 +1155,6 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   // ---- epilogue operands fetched ahead of the main loop
   float pre_b = 0.f;
   float4 ds = make_float4(1.f, 1.f, 1.f, 1.f), pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
-#ifdef RLE_EXP_EARLY_ADAM
-  float early_step = 0.f, early_bc2s = 1.f;
-#endif
   size_t wt = 0;
   float qwj = 0.f;
   if constexpr (EPI == EPI_QHEAD || EPI == EPI_QDOT) {
@@ -1229,11 +1192,6 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       if (jok) ds = mat_ld4(g.dsrc, ib, j);
     }
   } else {
-#ifdef RLE_EXP_EARLY_ADAM  // diagnostics build (tools/bitcmp.py): Adam scalars read before the main loop
-    early_step = sload(g.adam.step);
-    early_bc2s = sload(g.adam.bc2s);
-#endif
-#ifndef RLE_EXP_ADAM_LATE  // (experiment: p / m / v loaded after the main loop, registers for a deeper ring)
     if (jok) {
       const CAS AdamArgs& ad = g.adam;
       if (bias_tile) {
@@ -1247,7 +1205,6 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         vv = ld4g(G(ad.w.t) + wt + ad.vo);
       }
     }
-#endif
   }
   trace_mark(tr, 1);
 
@@ -1495,11 +1452,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
     const int va = ((i0 >> 4) * a0xs + c0) * 1024 + lb;
     const int vb = (((j0 - sb.x0) >> 4) * sb.xs + c0) * 1024 + lb;
     const int vx = ACT == kDwNb ? ((i0 >> 4) * g.nbx_xs + c0) * 1024 + lb : 0;
-#ifdef RLE_EXP_DW_NOLOOP  // timing experiment only: no DW main loop
-    const int nrun = 0;
-#else
     const int nrun = run ? c1 - c0 : 0;
-#endif
     constexpr int RGD = ACT == kDwNb ? kRing : kRingDW;  // (the kDwNb ring carries a third operand)
     float4 ra[RGD], rb[RGD], rx[RGD];
     ring_issue<RGD>(ra, rb, rsrc(a0p), va, rsrc(sb.p), vb, nrun, bias_tile);
@@ -1757,26 +1710,8 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   } else {  // EPI_ADAM (torch.optim.Adam single-tensor law, see oracle/agents.py)
     const CAS AdamArgs& ad = g.adam;
     float gg = 0.f;
-#ifdef RLE_EXP_ADAM_LATE
     if (jok) {
-      if (bias_tile) {
-        pp = ld4g(G(ad.b) + ib);
-        mm = ld4g(G(ad.b) + ib + ad.mo);
-        vv = ld4g(G(ad.b) + ib + ad.vo);
-      } else {
-        wt = tidx(ad.w.rbs, ib, j);
-        pp = ld4g(G(ad.w.t) + wt);
-        mm = ld4g(G(ad.w.t) + wt + ad.mo);
-        vv = ld4g(G(ad.w.t) + wt + ad.vo);
-      }
-    }
-#endif
-    if (jok) {
-#ifdef RLE_EXP_EARLY_ADAM
-      const float step_size = early_step, bc2s = early_bc2s;
-#else
       const float step_size = sload(ad.step), bc2s = sload(ad.bc2s);  // this step's (level-0 CTRL op)
-#endif
       const float p4[4] = {pp.x, pp.y, pp.z, pp.w}, m4[4] = {mm.x, mm.y, mm.z, mm.w}, v4[4] = {vv.x, vv.y, vv.z, vv.w};
       float po[4], mo[4], vo[4];
 #pragma unroll
@@ -1812,11 +1747,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         w.x = vo[0]; w.y = vo[1]; w.z = vo[2]; w.w = vo[3];
         __builtin_nontemporal_store(w, (GAS f32x4*)(pw + ad.vo));
       }
-#ifdef RLE_EXP_NO_NSTORE  // timing experiment only: no N-image weight store
-      if (false) {
-#else
       if (!bias_tile) {
-#endif
         GAS float* qn = GW(ad.w.n) + nidx(ad.w.cbn, ib, j);
         qn[0] = po[0];
         qn[4] = po[1];
@@ -2851,20 +2782,10 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     asm volatile("; op case " #K ::);         \
     call;                                     \
     break;
-#ifdef RLE_EXP_TWICE_GEMM  // diagnostics: the stamps of a second, cache-warm pass overwrite the first
-    RLE_OP(OP_GEMM, op_gemm<KS>(op.gemm, vid, t, smem, tr); __syncthreads(); op_gemm<KS>(op.gemm, vid, t, smem, tr))
-#else
     RLE_OP(OP_GEMM, op_gemm<KS>(op.gemm, vid, t, smem, tr))
-#endif
-#ifndef RLE_EXP_GEMM_ONLY
     RLE_OP(OP_NORMBWD, op_normbwd(op.nb, t))
     RLE_OP(OP_SAMPLE_REDUCE, op_sample_reduce(op.sample, t, smem))
-#ifdef RLE_EXP_TWICE  // diagnostics: the stamps of a second, cache-warm pass overwrite the first
-    RLE_OP(OP_SAMPLE_GATHER, op_sample_gather<KS == KS_EXT>(op.sample, t, smem, tr); __syncthreads();
-           op_sample_gather<KS == KS_EXT>(op.sample, t, smem, tr))
-#else
     RLE_OP(OP_SAMPLE_GATHER, op_sample_gather<KS == KS_EXT>(op.sample, t, smem, tr))
-#endif
     RLE_OP(OP_HEAD, op_head(op.head, t, smem, tr))
     RLE_OP(OP_PRIORITY, op_priority(op.prio, smem))
     RLE_OP(OP_SAC_ACTOR, op_sac_actor(op.sac, t))
@@ -2876,7 +2797,6 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     RLE_OP(OP_CTRL, op_ctrl<KS != KS_TD7>(op.ctrl))
     RLE_OP(OP_NOISE, op_noise(op.sample, t))
     RLE_OP(OP_FOLDBIAS, op_foldbias(op.fb))
-#endif
 #undef RLE_OP
     default: break;
   }

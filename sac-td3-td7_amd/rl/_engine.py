@@ -146,6 +146,7 @@ SIGNATURES = {
     "rle_graph_describe": (_int, [_vp, _int, ctypes.c_char_p, _int]),
     "rle_graph_trace": (_int, [_vp, _int, ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)]),
     "rle_trace_stride": (_int, []),
+    "rle_aql_wait_plan": (_int, [ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
     "rle_eval": (_int, [_vp, _int, _cs, _cs, _f32p, _f32p, _int, _f32p]),
     "rle_sac_rsample": (_int, [_vp, _f32p, _f32p, _f32p, _int, _f32p, _f32p]),
     "rle_get_info": (_int, [_vp, _int, _f32p]),

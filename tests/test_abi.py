@@ -43,3 +43,27 @@ def test_errors_are_reported_not_raised_across_abi():
     rc = lib.rle_replay_create(0, -5, 3, 2, 0, ctypes.byref(out))
     assert rc == -1
     assert b"bad args" in lib.rle_last_error()
+
+
+def test_aql_wait_policy_releases_the_host_core():
+    """rle_step's AQL wait (engine.cpp aql_wait_step): sleep while more than the 150 us spin tail of the
+    expected duration remains (slices <= 2 ms), spin for the tail, time out past the limit (the engine's
+    queue is then closed: aql_flush refuses every later packet).  No GPU: the policy alone."""
+    import ctypes
+
+    from rl import _engine
+
+    lib = _engine.lib()
+    sl = ctypes.c_double()
+
+    def plan(expected, elapsed, timeout=60.0):
+        return lib.rle_aql_wait_plan(expected, elapsed, timeout, ctypes.byref(sl)), sl.value
+
+    assert plan(250_000.0, 0.0) == (1, 2000.0)          # a 2000-step burst: sleep in 2 ms slices
+    act, us = plan(250_000.0, 249_000.0)
+    assert act == 1 and abs(us - 850.0) < 1e-6          # ... up to 150 us before the expected end
+    assert plan(250_000.0, 249_900.0)[0] == 0           # then spin
+    assert plan(100.0, 0.0)[0] == 0                     # short flushes never sleep
+    assert plan(250_000.0, 400_000.0)[0] == 0           # overran the estimate: spin, no more sleeping
+    assert plan(250_000.0, 61e6)[0] == 2                # past 60 s: time out
+    assert plan(250_000.0, 1.5e6, timeout=1.0)[0] == 2

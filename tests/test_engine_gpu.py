@@ -418,7 +418,8 @@ def test_sac_target_pre_bitwise(name):
 # 6-step graphs run on either side of a hard update)
 BURSTS = [("td3", "HalfCheetah-v4", 18, 256, {}), ("sac", "Humanoid-v4", 9, 256, {}),
           ("td7", "Ant-v4", 8, 256, {}), ("td7", "Humanoid-v4", 13, 256, {}),
-          ("td7", "Humanoid-v4", 8, 1024, {}), ("td7", "Humanoid-v4", 16, 256, {"target_update_rate": 8})]
+          ("td7", "Humanoid-v4", 8, 1024, {}), ("td7", "Humanoid-v4", 16, 256, {"target_update_rate": 8}),
+          ("td7", "Humanoid-v4", 8, 512, {})]
 
 
 @pytest.mark.parametrize("alg,env,n,B,extra", BURSTS,
@@ -453,12 +454,20 @@ def test_fused_priority_sampler_matches_reference(name, burst):
     _trajectory(name, burst, E.make_plan(fuse_on=["priosample"]))
 
 
-def _burst_vs_oracle(alg, env, n, B, extra, plan=None):
+@pytest.mark.parametrize("alg,env,n,H", [("sac", "Humanoid-v4", 3, 512), ("td3", "HalfCheetah-v4", 3, 512)])
+def test_wide_hidden_burst_matches_oracle(alg, env, n, H):
+    """Hidden width 512 (rle_create accepts H <= 512): the fusions whose kernels bound H (SAC's raw head
+    + rsample in one GEMM epilogue, kernels.hip sacraw_*, R <= 256) fall back to their standalone ops
+    instead of failing the program build, and the steps agree with the oracle."""
+    _burst_vs_oracle(alg, env, n, 256, {}, H=H)
+
+
+def _burst_vs_oracle(alg, env, n, B, extra, plan=None, H=256):
     from oracle import agents
     from test_oracle import build_from_golden
 
     ncap = 8192 if B > 256 else 4096
-    g = _synthetic_golden(alg, env, 256, B, ncap, ncap, n, alg == "td7", 91, **extra)
+    g = _synthetic_golden(alg, env, H, B, ncap, ncap, n, alg == "td7", 91, **extra)
     _, orc, orep, tp, n_steps, B = build_from_golden(g)
     eng, rep, tp2 = engine_from_golden(g, plan=plan)
     launches0 = eng.launch_count()
@@ -528,3 +537,76 @@ def test_plan_is_explicit_and_env_free(name, monkeypatch):
 def _alg_dims(g):
     alg, env, H = parse(g)[:3]
     return (alg, *spec.TASKS[env][:2], H, 0)
+
+
+def test_bench_program_1m_lap_replay_matches_oracle():
+    """The exact bench program (bench.py's default line): TD7 Humanoid B=256, LAP over a 1,000,000-row
+    replay (245 priority blocks of 4096 in the sampler's block-sum scan), 13 steps = 1 single step + two
+    6-step graphs with the default plan, against the oracle stepped one taped step at a time on the same
+    draws.  Rows are a 4096-row pattern repeated over the replay (bench.py's fill shape, small host
+    memory); the priorities are distinct over all 1M rows.  Indices bit-exact, every priority of the 1M
+    rows (which records every index drawn) at rtol 1e-4, parameters at the module's bulk criterion."""
+    from oracle import agents, replay
+
+    S, A, hi = spec.TASKS["Humanoid-v4"]
+    N, blk, n, B, H, seed = 1_000_000, 4096, 13, 256, 256, 93
+    data = spec.replay_data(S, A, blk, seed + 1, hi)
+    scale = np.full(A, hi, np.float32)
+    scale = (scale - (-scale)) / 2.0
+    pat = {"state": data["state"].astype(np.float32), "next_state": data["next_state"].astype(np.float32),
+           "action": (np.asarray(data["action"]) / scale - np.zeros(A, np.float32)).astype(np.float32),
+           "reward": data["reward"].astype(np.float32), "done": data["done"].astype(np.float32)}
+    p0 = spec.init_priorities(N, seed + 2)
+    # engine side: the pattern appended in 64K-row chunks (the replay stores the normalised action)
+    cfg = E.make_config(E.RLE_TD7, S, A, H, B, use_lap=True, seed=seed)
+    eng = E.Engine(cfg)
+    nets = spec.agent_params("td7", S, A, H, seed)
+    for net, params in nets.items():
+        for name, v in params.items():
+            eng.set_param(net, name, v)
+    rep = E.Replay(N, S, A, True)
+    chunk = 16 * blk
+    tiled = {k: np.tile(v, (16,) + (1,) * (v.ndim - 1)) for k, v in pat.items()}
+    for i in range(0, N, chunk):
+        m = min(chunk, N - i)
+        rep.append(tiled["state"][:m], tiled["action"][:m], tiled["reward"][:m], tiled["next_state"][:m],
+                   tiled["done"][:m])
+    del tiled
+    rep.set_priority(p0, float(p0.max()))
+    eng.bind(rep)
+    # oracle side: the same rows written in place (Replay.append row by row would take minutes)
+    orc = agents.make_oracle("td7", nets, A, True)
+    orep = replay.Replay(N, S, A, scale, np.zeros(A, np.float32), True)
+    for i in range(0, N, blk):
+        m = min(blk, N - i)
+        orep.state[i:i + m] = pat["state"][:m]
+        orep.next_state[i:i + m] = pat["next_state"][:m]
+        orep.action[i:i + m] = pat["action"][:m]
+        orep.reward[i:i + m, 0] = pat["reward"][:m]
+        orep.done[i:i + m, 0] = pat["done"][:m]
+    orep.priority[:] = p0
+    orep.max_priority = float(p0.max())
+    orep.size, orep.ptr = N, 0
+    tp = spec.tapes("td7", B, A, n, seed + 3)
+    infos_ref, inds = [], []
+    for t in range(n):
+        i1, n1 = agents.run_steps(orc, "td7", orep, {k: v[t:t + 1] for k, v in tp.items()}, 1, B)
+        infos_ref += i1
+        inds += n1
+    launches0 = eng.launch_count()
+    eng.set_tapes(u=tp["u"], eps=tp["eps"])
+    infos = np.array(eng.step(n))
+    eng.set_tapes()
+    lp, lpl = eng.graph_stats()
+    assert eng.launch_count() - launches0 < (n // 2) * (lp + lpl), "no multi-step graph ran"
+    np.testing.assert_array_equal(eng.last_indices(), inds[-1])
+    keys = ["train/encoder", "train/q_fn", "train/policy"]
+    ref = np.array([[np.nan if i[k] is None else i[k] for k in keys] for i in infos_ref], np.float64)
+    np.testing.assert_allclose(infos[:, :3], ref, rtol=2e-3, atol=1e-4, equal_nan=True)
+    np.testing.assert_allclose(rep.get_priority(N), orep.priority, rtol=1e-4, atol=1e-5)
+    vb = np.array([orc.value_max, orc.value_min, orc.vt_max, orc.vt_min], np.float32)
+    np.testing.assert_allclose(eng.value_bounds(), vb, rtol=1e-4, atol=1e-4)
+    tol = 2 * 3e-4 * n + 1e-4
+    for net, d in orc.nets().items():
+        for name, v in d.items():
+            assert_params_close(eng.get_param(net, name, tuple(v.shape)), v.detach().numpy(), tol, (net, name))
