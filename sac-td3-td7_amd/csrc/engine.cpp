@@ -310,7 +310,7 @@ static void xcd_plan(GemmArgs& g);
 // (ks < 0: in any kernel set)
 static bool gemm_variant_compiled(int vid, int ks = -1) {
 #define RLE_VID(mode, epi, act, norm, pre, pk, sets) \
-  (vid == gemm_vid(mode, epi, act, norm, pre) && (ks < 0 || ks == KS_EXT || (((sets) >> ks) & 1))) ||
+  (vid == gemm_vid(mode, epi, act, norm, pre) && (ks < 0 || ks == KS_EXT || (((sets) >> ks_family(ks)) & 1))) ||
   return RLE_GEMM_VARIANTS(RLE_VID) false;
 #undef RLE_VID
 }
@@ -398,6 +398,11 @@ static void gemm_finalize(GemmArgs& g) {
   g.ks_log = g.tn == 16 ? 2 : (g.tn == 32 ? 1 : 0);
   REQUIRE(g.R % 16 == 0, "gemm: reduction length must be a multiple of 16");
   REQUIRE((long long)g.tiles_m * g.tiles_n < 65536, "gemm: too many tiles");
+  // 64-row LDS-staged tiles (kernels.hip gemm_wide): one of its variants, 64-wide tiles over whole 64-row blocks,
+  // no in-tile prologue, no target smoothing; tiles_m stays the 16-row block count (loss partial slots)
+  REQUIRE(!g.hot.wide || (wide_variant(g.mode, g.epi, g.has_pre) && g.tn == 64 && g.M % 64 == 0 &&
+                          g.tiles_m * 16 == g.M && !g.noise.t && g.N % 64 == 0),
+          "gemm: wide tile layout");
   g.inv_tiles_n = 1.f / (float)g.tiles_n;
   GemmHot& h = g.hot;
   h.ks_log = g.ks_log;
@@ -416,7 +421,7 @@ static void gemm_finalize(GemmArgs& g) {
   h.a0p = g.A.seg[0].p;
   h.b0p = g.B.seg[0].p;
   h.bias = g.epi == EPI_ADAM ? nullptr : g.bias;
-  h.tiles = g.tiles_m * g.tiles_n;
+  h.tiles = (g.hot.wide ? g.tiles_m / 4 : g.tiles_m) * g.tiles_n;
   xcd_plan(g);
 }
 
@@ -429,21 +434,22 @@ static void xcd_plan(GemmArgs& g) {
   h.xb = 0;
   const char* e = std::getenv("RLE_XCD");
   if (e && e[0] == '0') return;
-  const int T = g.tiles_m * g.tiles_n;
+  const int tm = g.hot.wide ? g.tiles_m / 4 : g.tiles_m, rh = g.hot.wide ? 64 : 16;  // tile rows, rows per tile
+  const int T = tm * g.tiles_n;
   if (T < 16 || g.tiles_n < 2) return;
   const int share = (T + 7) / 8;
   int best = g.tiles_n;
   long long bc = -1;
   for (int b = 1; b <= g.tiles_n; ++b) {
-    const long long rows = std::min<long long>(g.tiles_m, (share + b - 1) / b + 1);  // a run may straddle a row
-    const long long cost = rows * 16 + (long long)std::min(b, share) * g.tn;
+    const long long rows = std::min<long long>(tm, (share + b - 1) / b + 1);  // a run may straddle a row
+    const long long cost = rows * rh + (long long)std::min(b, share) * g.tn;
     if (bc < 0 || cost < bc) {
       bc = cost;
       best = b;
     }
   }
   h.xb = best;
-  h.tmb = g.tiles_m * best;
+  h.tmb = tm * best;
   h.nfull = g.tiles_n / best;
   h.inv_tmb = 1.f / (float)h.tmb;
   h.inv_xb = 1.f / (float)best;
@@ -453,7 +459,7 @@ static void xcd_plan(GemmArgs& g) {
   for (int t = 0; t < T; ++t) {
     int it, jt;
     xcd_tile(t, T, g.tiles_n, h.xb, h.tmb, h.nfull, h.inv_tmb, h.inv_xb, h.inv_blast, it, jt);
-    const bool ok = it >= 0 && it < g.tiles_m && jt >= 0 && jt < g.tiles_n && !seen[(size_t)it * g.tiles_n + jt];
+    const bool ok = it >= 0 && it < tm && jt >= 0 && jt < g.tiles_n && !seen[(size_t)it * g.tiles_n + jt];
     if (!ok) {
       h.xb = 0;
       return;
@@ -516,7 +522,18 @@ static void audit_norm(const NormRef& nr, int row, int nrows, const GemmArgs& g)
     audit_range(nr.part, ((long long)p * nr.ld + nr.row0 + row) * 4, (long long)nrows * 4, "norm partials", g);
 }
 
-static void audit_gemm(const GemmArgs& g) {
+static void audit_gemm(const GemmArgs& g0) {
+  // (a 64-row tile, kernels.hip gemm_wide: the byte ranges of the four 16-row tn-64 tiles it covers, in row-major
+  // order -- its loss partial slots are theirs)
+  GemmArgs gw;
+  if (g0.hot.wide) {
+    gw = g0;
+    gw.hot.wide = 0;
+    gw.hot.xb = 0;
+    gw.hot.tiles = gw.tiles_m * gw.tiles_n;
+    gw.ks_log = 0;
+  }
+  const GemmArgs& g = g0.hot.wide ? gw : g0;
   const GemmHot& h = g.hot;
   // wave w of a 16 x tn tile: column group w >> ks_log, reduction split w & (2^ks_log - 1)
   const int NB = g.tn / 16, T = g.tiles_m * g.tiles_n, ks = 1 << g.ks_log;
@@ -1404,9 +1421,12 @@ static void aql_flush(AqlQueue& A, double* ms) {
   bool rung = false;
   for (size_t i = 0; i < n; ++i) {
     const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
-    if (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {  // (bursts of > q->size packets)
-      const double ahead = (double)(idx - hsa_queue_load_read_index_scacquire(q) - q->size + 1);
-      aql_wait(A, [&] { return idx - hsa_queue_load_read_index_scacquire(q) < q->size; }, ahead * A.us_per_launch,
+    if (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+      // (bursts of > q->size packets) wait until half the queue has drained, then write on: the host
+      // sleeps through most of it instead of tracking the device one retired packet at a time
+      const uint64_t half = q->size / 2;
+      const double ahead = (double)(idx - hsa_queue_load_read_index_scacquire(q) - half + 1);
+      aql_wait(A, [&] { return idx - hsa_queue_load_read_index_scacquire(q) < half; }, ahead * A.us_per_launch,
                "a queue slot");
     }
     auto* pk = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx & mask);
@@ -1500,6 +1520,7 @@ static rle_plan plan_defaults() {
   p.rb = -1;
   p.pl_w = -1;
   p.lap_w = p.head_w = p.adam_w = -1;
+  p.wide = -1;
   return p;
 }
 
@@ -1512,8 +1533,8 @@ struct Engine {
   // the rle_level instance this engine's programs run on (ops.h KernelSet): the agent's own set, or the
   // extended instance when the plan asks for its opt-in paths
   int kernel_set() const {
-    if (plan.rb || (plan.fuse_on & RLE_FUSE_PRIOSAMPLE)) return KS_EXT;
-    return algo == RLE_TD7 ? KS_TD7 : KS_MLP;
+    if (plan.rb || (plan.fuse_on & RLE_FUSE_PRIOSAMPLE) || (plan.wide && algo != RLE_TD7)) return KS_EXT;
+    return algo == RLE_TD7 ? (plan.wide ? KS_TD7W : KS_TD7) : KS_MLP;
   }
   void resolve_plan() {
     if (plan.steps_per_graph < 0) plan.steps_per_graph = algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 6;
@@ -1545,6 +1566,10 @@ struct Engine {
     // 8.24k, B = 1024 flat: profiles/r04_ab_weights.txt)
     if (plan.adam_w < 0) plan.adam_w = algo == RLE_SAC ? 16 : 8;
     if (plan.level_cap < 0) plan.level_cap = 0;
+    // (64-row LDS-staged tiles: the 16-row tiles' per-workgroup fixed cost and 2 KB of operand loads per 4
+    // MFMAs bound the B >= 512 levels, DESIGN round 5)
+    if (plan.wide < 0) plan.wide = algo == RLE_TD7 && cfg.batch >= 512 ? 1 : 0;
+    plan.wide = plan.wide ? 1 : 0;
   }
   int S, Sp, A, Ap, H, Hp, B;
   int algo;
@@ -2194,7 +2219,11 @@ struct Engine {
                           : pre && (pre->kind == 1 || pre->kind == 5)
                               ? (pl_src ? std::min(std::max(tq.first, pre_tn()), 32) : std::max(tq.first, pre_tn()))
                                                   : (pl_src ? std::min(tq.first, 32) : tq.first));
-    const int tiles_n = cdiv(L.out, tn);
+    // 64-row LDS-staged tiles (rle_plan wide): every row piece whole 64-row blocks, 64-column blocks
+    bool wide = plan.wide && !sfu && !pre && !noise && L.out % 64 == 0;
+    for (size_t ci = 0; wide && ci + 1 < cuts.size(); ++ci) wide = (cuts[ci + 1] - cuts[ci]) % 64 == 0;
+    const int tn_w = wide ? 64 : tn;
+    const int tiles_n = cdiv(L.out, tn_w);
     View out = buf(M, L.out, true, out_t);
     if (sfu) {
       REQUIRE(!pre && !qdot && !normed && !noise && act == ACT_NONE && L.out <= 64, "fwd: SAC forward epilogue");
@@ -2279,7 +2308,8 @@ struct Engine {
       g.M = m;
       g.N = L.out;
       g.R = L.K;
-      g.tn = tn;
+      g.tn = tn_w;
+      g.hot.wide = wide;
       g.tiles_m = cdiv(m, kTileM);
       g.tiles_n = tiles_n;
       g.epi = EPI_STORE;
@@ -2315,7 +2345,7 @@ struct Engine {
         g.prea = pre->a;
         if (pre->kind == 4) g.prea2 = pre->a2;
       }
-      op.wg_count = g.tiles_m * g.tiles_n;
+      op.wg_count = (wide ? g.tiles_m / 4 : g.tiles_m) * g.tiles_n;
       op.seq = tq.second;
       ops.push_back(op);
     }
@@ -2366,6 +2396,10 @@ struct Engine {
            : pre && pre->kind == 1 ? std::max(tq.first, pre_tn())
                                    : (pl_src ? std::min(tq.first, 32) : tq.first);
     op.seq = tq.second;
+    // 64-row LDS-staged tiles (rle_plan wide): a plain or EPI_NBDOT input gradient over whole 64-row blocks
+    const bool wide = plan.wide && !pre && !head && !sbu && M % 64 == 0 && ncols % 64 == 0;
+    if (wide) g.tn = 64;
+    g.hot.wide = wide;
     g.tiles_m = cdiv(M, kTileM);
     g.tiles_n = cdiv(ncols, g.tn);
     g.epi = EPI_STORE;
@@ -2415,7 +2449,7 @@ struct Engine {
       rd.insert(rd.end(), sbu->rd.begin(), sbu->rd.end());
       wr.insert(wr.end(), sbu->wr.begin(), sbu->wr.end());
     }
-    op.wg_count = g.tiles_m * g.tiles_n;
+    op.wg_count = (wide ? g.tiles_m / 4 : g.tiles_m) * g.tiles_n;
     pg.add(op, rd, wr);
     return out;
   }
@@ -2878,7 +2912,9 @@ struct Engine {
       g.N = L.out;
       g.R = L.K;
       const auto tq = choose_tn(B, L.out);
-      g.tn = tq.first;
+      const bool wide = plan.wide && B % 64 == 0 && L.out % 64 == 0;
+      g.tn = wide ? 64 : tq.first;
+      g.hot.wide = wide;
       op.seq = tq.second;
       g.tiles_m = cdiv(B, kTileM);
       g.tiles_n = cdiv(L.out, g.tn);
@@ -2892,7 +2928,7 @@ struct Engine {
       enc_loss = mem.make<float>(enc_tiles);
       g.loss_part = enc_loss;
       g.mse_scale = 1.f / (float)((long long)B * H);
-      op.wg_count = enc_tiles;
+      op.wg_count = (wide ? g.tiles_m / 4 : g.tiles_m) * g.tiles_n;
       pg.add(op, {ea2.id, L.res, ezs2.id, ezs2.norm_id}, {ed3.id, loss_id_enc = next_id++});
     }
     // encoder backward + Adam (optim_encoder, lr = policy_lr)
@@ -3175,11 +3211,13 @@ struct Engine {
     g.N = L.out;
     g.R = L.K;
     const auto tq = choose_tn(M, L.out);
-    g.tn = tq.first;
+    const bool wide = plan.wide && M % 64 == 0 && L.out % 64 == 0;
+    g.tn = wide ? 64 : tq.first;
+    g.hot.wide = wide;
     op.seq = tq.second;
     g.tiles_m = cdiv(M, kTileM);
     g.tiles_n = cdiv(L.out, g.tn);
-    *ntiles = g.tiles_m * g.tiles_n;
+    *ntiles = g.tiles_m * g.tiles_n;  // (wide: one loss partial per 16-row block too)
     g.epi = EPI_QHEAD;
     g.act = ACT_ELU;
     g.bias = bias(L);
@@ -3190,7 +3228,7 @@ struct Engine {
     g.qw_cbn = Lq.cb;
     g.qb = bias(Lq);
     g.qscale = dq;
-    op.wg_count = g.tiles_m * g.tiles_n;
+    op.wg_count = (wide ? g.tiles_m / 4 : g.tiles_m) * g.tiles_n;
     pg.add(op, {x.id, L.res, Lq.res}, {dz.id, loss_id});
     return dz;
   }
@@ -3783,7 +3821,7 @@ struct Engine {
                            : op.gemm.has_pre == 5                         ? "st+sacpre"
                                                                            : kepi[op.gemm.epi];
           G.desc += "[" + std::to_string(op.gemm.M) + "x" + std::to_string(op.gemm.N) + "x" +
-                    std::to_string(op.gemm.R) + " " + ep + "]";
+                    std::to_string(op.gemm.R) + " " + ep + (op.gemm.hot.wide ? ".w" : "") + "]";
         }
         if (std::getenv("RLE_DESC_WG")) G.desc += "/" + std::to_string(op.wg_count);  // trace tools
       }
@@ -3903,6 +3941,7 @@ struct Engine {
       if (op.kind == OP_POLYAK || op.kind == OP_COPY) return op.wg_count / flat_div;
       if (op.kind != OP_GEMM) return op.wg_count;
       const GemmArgs& g = op.gemm;
+      if (g.hot.wide) return op.wg_count;  // (64-row tiles: never widened)
       return g.tiles_m * (cdiv(g.N, at(op.seq)) + (g.epi == EPI_ADAM ? 1 : 0));
     };
     for (auto& lv : levels) {
@@ -3912,7 +3951,7 @@ struct Engine {
         if (total <= cap) break;
         int best = -1, best_wg = 0;
         for (auto& op : lv)
-          if (op.kind == OP_GEMM && at(op.seq) < 64 && wg_of(op) > best_wg) {
+          if (op.kind == OP_GEMM && !op.gemm.hot.wide && at(op.seq) < 64 && wg_of(op) > best_wg) {
             best = op.seq;
             best_wg = wg_of(op);
           }

@@ -1051,9 +1051,282 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
   return acc + acc1;
 }
 
+// ---------------------------------------------------------------- 64-row LDS-staged tiles (GemmHot::wide)
+//
+// One workgroup = a 64 x 64 output tile of a FWD / DX GEMM over >= 512 batch rows (rle_plan wide, the KS_TD7W
+// instance): wave w owns rows 16w .. 16w + 15 and all 4 column blocks.  Each 16-wide reduction chunk's operands
+// -- the tile's 4 A row blocks and its 4 W column blocks, 8 KB -- are copied into one slot of an LDS ring by
+// LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction: wave w copies its own A block and W column
+// block w), so each W block is fetched once per workgroup and feeds all four row blocks, and the ring holds no
+// VGPRs: kWideRing - 1 chunks are in flight while one is reduced.  Every wave keeps 4 independent accumulator
+// chains (one per column block), each split by chunk parity exactly as ring_run sums a segment, and the
+// epilogues combine column blocks in the 16-row tile's wave order: the floats of the 16-row tn-64 tile.
+// Protocol per chunk k: wait for this wave's DMAs of chunk k (counted vmcnt: the DMAs are inline asm, outside
+// the compiler's wait bookkeeping), s_barrier (every wave's DMAs of chunk k landed; every wave is done reading
+// chunk k - 1's slot), issue chunk k + kWideRing - 1 into that freed slot, read chunk k's fragments, MFMA.
+constexpr int kWideRing = 4;
+constexpr int kWideSlot = 2048;                  // floats per ring slot: A [4 waves][256], W [4 column blocks][256]
+constexpr int kWideSmem = kWideRing * kWideSlot;  // 32 KB
+
+__device__ __forceinline__ unsigned lds_off(const float* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+// one 1 KB fragment block (this lane's 16 bytes at src) -> LDS bytes [lds, lds + 1 KB), lane l at lds + 16 l
+__device__ __forceinline__ void glds_block(const float* src, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+// this wave's DMAs of a chunk landed, with `ahead` younger chunks (2 DMAs each) still in flight
+__device__ __forceinline__ void wide_wait(int ahead) {
+  static_assert(kWideRing == 4, "wide_wait's counts assume 2 chunks ahead at most");
+  if (ahead >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void wide_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int MODE, int EPI, int ACT, bool NORM>
+__device__ __forceinline__ void gemm_wide(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr,
+                                                    int tiles_n, int gN, int gR, float inv_tn, int nseg_a, int nseg_b,
+                                                    int tiles, int xb, int tmb, int nfull, float inv_tmb, float inv_xb,
+                                                    float inv_blast, const float* biasp) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int it, jt;
+  if (xb) {
+    xcd_tile(t, tiles, tiles_n, xb, tmb, nfull, inv_tmb, inv_xb, inv_blast, it, jt);
+  } else {
+    it = (int)(((float)t + 0.5f) * inv_tn);
+    jt = t - it * tiles_n;
+  }
+  const int i0 = (it << 6) + (wave << 4);  // this wave's 16 rows
+  const int jc0 = jt << 6;                 // the tile's first column
+  const int ib = i0 + ((lane >> 4) << 2);
+  const int nch = gR >> 4;
+  const bool wabs = MODE == GEMM_FWD && nseg_b == 1;
+  const int nbv = min(4, (gN - jc0 + 15) >> 4);  // column blocks of this tile inside the output
+  // ---- epilogue operands, issued before any LDS-DMA (ordinary loads older than the ring)
+  float pb[4] = {0.f, 0.f, 0.f, 0.f}, qwj[4] = {0.f, 0.f, 0.f, 0.f};
+  float4 ev[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int j = jc0 + c * 16 + (lane & 15);
+    const bool jok = j < gN;
+    ev[c] = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (jok && biasp) pb[c] = G(biasp)[j];
+    if constexpr (EPI == EPI_QHEAD || EPI == EPI_QDOT) {
+      if (jok) qwj[c] = G(g.qw)[nidx(g.qw_cbn, 0, j)];
+    }
+    if constexpr (MODE == GEMM_DX && ACT != ACT_NONE && EPI == EPI_STORE) {
+      if (jok) ev[c] = mat_ld4(g.dsrc, ib, j);
+    }
+    if constexpr (EPI == EPI_MSE) {
+      if (jok) ev[c] = mat_ld4(g.tgt, ib, j);
+    }
+    if constexpr (EPI == EPI_NBDOT) {
+      if (jok) ev[c] = mat_ld4(g.nbx, ib, j);
+    }
+  }
+  // EPI_MSE: |zs'| partials of the wave's 16 rows, partial p = lane / 16 + 4 m (<= 16 partials: a row table)
+  float tnv[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_MSE) {
+    const CAS NormRef& nr = g.tgt_norm;
+    if (nr.part && nr.nparts <= 16) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int p = (lane >> 4) + 4 * m;
+        if (p < nr.nparts) tnv[m] = G(nr.part)[(size_t)p * nr.ld + nr.row0 + i0 + (lane & 15)];
+      }
+    }
+  }
+  // deferred AvgL1Norm of each A segment: 1 / m of this lane's row (as inv_of in gemm_v)
+  float inv[kMaxSeg] = {1.f, 1.f, 1.f, 1.f};
+  if constexpr (NORM) {
+#pragma unroll
+    for (int q = 0; q < kMaxSeg; ++q)
+      if (q < nseg_a && g.A.seg[q].norm.part) inv[q] = norm_inv_i(g.A.seg[q].norm, i0 + (lane & 15));
+  }
+  trace_mark(tr, 1);
+  // ---- the chunk loop over the LDS ring
+  const unsigned ring = lds_off(smem);
+  auto seg_of = [&](int k) {
+    int q = 0;
+#pragma unroll
+    for (int u = 1; u < kMaxSeg; ++u)
+      if (u < nseg_a && k >= (g.A.seg[u].r0 >> 4)) q = u;
+    return q;
+  };
+  const int bcol = (jc0 >> 4) + min(wave, nbv - 1);  // (blocks past the output: a valid block, never used)
+  auto issue = [&](int k) {
+    const int q = seg_of(k);
+    const CAS Seg& sa = g.A.seg[q];
+    const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
+    const int s0 = sa.r0 >> 4, kb = wabs ? k : k - s0;
+    const unsigned slot = ring + (unsigned)((k & (kWideRing - 1)) * kWideSlot * 4);
+    glds_block(sa.p + ((size_t)((i0 >> 4) * sa.xs + (k - s0)) * 256 + lane * 4), slot + wave * 1024);
+    glds_block(sb.p + ((size_t)(bcol * sb.xs + kb) * 256 + lane * 4), slot + 4096 + wave * 1024);
+  };
+#pragma unroll
+  for (int k = 0; k < kWideRing - 1; ++k)
+    if (k < nch) issue(k);
+  f32x4 ac[4], ac1[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) ac[c] = ac1[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int q = 0, kseg = 0;
+  int qnext = nseg_a > 1 ? (g.A.seg[1].r0 >> 4) : nch;
+  float sinv = inv[0];
+#pragma unroll 1
+  for (int k = 0; k < nch; ++k) {
+    wide_wait(min(kWideRing - 2, nch - 1 - k));
+    wide_barrier();
+    if (k + kWideRing - 1 < nch) issue(k + kWideRing - 1);
+    if (k == qnext) {  // segment boundary: ring_run's "return acc + acc1", then the next segment
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        ac[c] = ac[c] + ac1[c];
+        ac1[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      ++q;
+      kseg = k;
+      qnext = q + 1 < nseg_a ? (g.A.seg[q + 1].r0 >> 4) : nch;
+      if constexpr (NORM) sinv = q == 1 ? inv[1] : (q == 2 ? inv[2] : inv[3]);
+    }
+    const float* slot = smem + (k & (kWideRing - 1)) * kWideSlot;
+    float4 a = *(const float4*)(slot + wave * 256 + lane * 4);
+    if constexpr (NORM) a = scale4(a, sinv);
+    float4 b[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) b[c] = *(const float4*)(slot + 1024 + c * 256 + lane * 4);
+    if ((k - kseg) & 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ac1[c] = mfma4(a, b[c], ac1[c]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ac[c] = mfma4(a, b[c], ac[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) ac[c] = ac[c] + ac1[c];
+  trace_mark(tr, 2);
+  __syncthreads();  // (every wave is done with the ring: the epilogue reuses the LDS)
+  // ---- epilogue, column block by column block; the tile's row sums in the 16-row tile's wave order
+  // ((s0 + s1) + (s2 + s3), s_c the row16_sum of column block c), loss partials one per 16-row block
+  // (wave_sum per column block, then the same order) at the 16-row tile's row-major index
+  float rs01[4] = {0.f, 0.f, 0.f, 0.f}, rs23[4] = {0.f, 0.f, 0.f, 0.f};
+  float ls01 = 0.f, ls23 = 0.f;
+  float* tabw = smem + wave * 256;  // (EPI_MSE: this wave's row table of norm partials)
+  if constexpr (EPI == EPI_MSE) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) tabw[((lane >> 4) + 4 * m) * 16 + (lane & 15)] = tnv[m];
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int j = jc0 + c * 16 + (lane & 15);
+    const bool jok = j < gN;
+    const f32x4 acc = ac[c];
+    const float e4[4] = {ev[c].x, ev[c].y, ev[c].z, ev[c].w};
+    float rv[4] = {0.f, 0.f, 0.f, 0.f};
+    float lv = 0.f;
+    if constexpr (EPI == EPI_STORE || EPI == EPI_QDOT) {
+      if (jok) {
+        float y[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) y[qq] = acc[qq] + pb[c];
+        if constexpr (MODE == GEMM_FWD) {
+          if (g.pre.t) mat_st4(g.pre, ib, j, make_float4(y[0], y[1], y[2], y[3]));
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) y[qq] = act_f<ACT>(y[qq]);
+        } else {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) y[qq] *= act_b<ACT>(e4[qq]);
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) rv[qq] = EPI == EPI_QDOT ? y[qq] * qwj[c] : fabsf(y[qq]);
+        mat_st4(g.out, ib, j, make_float4(y[0], y[1], y[2], y[3]));
+      }
+    } else if constexpr (EPI == EPI_NBDOT) {
+      if (jok) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) rv[qq] = acc[qq] * e4[qq];
+        mat_st4(g.out, ib, j, make_float4(acc[0], acc[1], acc[2], acc[3]));
+      }
+    } else if constexpr (EPI == EPI_QHEAD) {  // td7.py:268-275
+      if (jok) {
+        float dz[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const float z = acc[qq] + pb[c], y = act_f<ACT>(z);
+          lv += y * qwj[c];
+          dz[qq] = (g.qscale * qwj[c]) * act_b<ACT>(ACT == ACT_RELU ? y : z);
+        }
+        mat_st4(g.out, ib, j, make_float4(dz[0], dz[1], dz[2], dz[3]));
+      }
+    } else if constexpr (EPI == EPI_MSE) {  // td7.py:256
+      const CAS NormRef& nr = g.tgt_norm;
+      if (jok) {
+        float gr[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          float iv;
+          if (nr.part && nr.nparts <= 16) {  // the sum order, clamp and reciprocal of norm_inv
+            float sm = 0.f;
+            for (int p = 0; p < nr.nparts; ++p) sm += tabw[p * 16 + (ib - i0) + qq];
+            const float m = sm / (float)nr.width;
+            iv = 1.f / (m < 1e-8f ? 1e-8f : m);
+          } else {
+            iv = norm_inv(nr, ib + qq);
+          }
+          const float d = (acc[qq] + pb[c]) - e4[qq] * iv;
+          gr[qq] = (2.f * d) * g.mse_scale;
+          lv += d * d;
+        }
+        mat_st4(g.out, ib, j, make_float4(gr[0], gr[1], gr[2], gr[3]));
+      }
+    }
+    if constexpr (EPI == EPI_QDOT || EPI == EPI_NBDOT || (EPI == EPI_STORE && MODE == GEMM_FWD)) {
+      if (EPI != EPI_STORE || g.norm_out) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const float s = row16_sum(rv[qq]);
+          if (c == 0) rs01[qq] = s;
+          else if (c == 1) rs01[qq] += s;
+          else if (c == 2) rs23[qq] = s;
+          else rs23[qq] += s;
+        }
+      }
+    }
+    if constexpr (EPI == EPI_QHEAD || EPI == EPI_MSE) {
+      const float s = wave_sum(lv);
+      if (c == 0) ls01 = s;
+      else if (c == 1) ls01 += s;
+      else if (c == 2) ls23 = s;
+      else ls23 += s;
+    }
+  }
+  if constexpr (EPI == EPI_QDOT || EPI == EPI_NBDOT || (EPI == EPI_STORE && MODE == GEMM_FWD)) {
+    if ((EPI != EPI_STORE || g.norm_out) && (lane & 15) == 0) {
+      GAS float* dst = GW(g.norm_out) + (size_t)jt * g.norm_ld + ib;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) dst[qq] = rs01[qq] + rs23[qq];
+    }
+  }
+  if constexpr (EPI == EPI_QHEAD || EPI == EPI_MSE) {
+    if (lane == 0) {
+      const int t16 = (i0 >> 4) * tiles_n + jt;  // (the 16-row tile's row-major index: the partial count is unchanged)
+      float v = ls01 + ls23;
+      if constexpr (EPI == EPI_QHEAD) v = t16 == 0 ? v + (float)g.M * sload(g.qb) : v;
+      GW(g.loss_part)[t16] = v;
+    }
+  }
+}
+
 // EXT: the extended instance of rle_level (register-blocked weight-gradient tiles, 32-row tiles); the
 // production instance compiles without them, so their registers do not shape its allocation
-template <int MODE, int EPI, int ACT, bool NORM, int PK = 0, bool EXT = false>  // PK: 1 pre-GEMM, 2 fused loss head, 3 pre-layer, 4 pre-layer behind a pre-GEMM, 5 SAC raw head + rsample pre-GEMM
+// WIDE: the variant also runs 64-row LDS-staged tiles (GemmHot::wide, gemm_wide; the KS_TD7W and extended instances)
+template <int MODE, int EPI, int ACT, bool NORM, int PK = 0, bool EXT = false, bool WIDE = false>  // PK: 1 pre-GEMM, 2 fused loss head, 3 pre-layer, 4 pre-layer behind a pre-GEMM, 5 SAC raw head + rsample pre-GEMM
 __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
   FINE_MARK(10);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1120,6 +1393,14 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   const float* a0p = ptr(h0[14], h0[15]);
   const float* b0p = ptr(h1[0], h1[1]);
   const float* biasp = ptr(h1[2], h1[3]);
+  if constexpr (WIDE) {
+    if (h1[11]) {
+      gemm_wide<MODE, EPI, ACT, NORM>(g, t, smem, tr, tiles_n, gN, gR, inv_tn, nseg_a, nseg_b, (int)h0[13], (int)h1[4],
+                                      (int)h1[5], (int)h1[9], __uint_as_float(h1[6]), __uint_as_float(h1[7]),
+                                      __uint_as_float(h1[8]), biasp);
+      return;
+    }
+  }
   const int cg = wave >> ksl, kp = wave & ((1 << ksl) - 1);
   // register-blocked wide weight-gradient tile (GemmHot::rb; the host sets it only for tn 32 / 64)
   constexpr bool RBOK = EXT && PK == 0 && MODE == GEMM_DW;
@@ -1461,6 +1742,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       for (int r = 0; r < RGD; ++r)
         if (r < nrun) rx[r] = bload(rsrc(g.nbx.t), vx + r * 1024);
     }
+    FINE_MARK(0);
     const float* tb = nullptr;
     if constexpr (NORM) {
       // 1/m of every reduction row of every normed B segment, segment by segment
@@ -1481,6 +1763,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       build_nb_tab(g, gR, tabs, tabs + tgo);
       __syncthreads();
     }
+    FINE_MARK(1);
     if (run) {
       if constexpr (ACT == kDwNb) {
         acc = ring_run_nb<RGD>(ra, rx, rb, rsrc(a0p), va, rsrc(g.nbx.t), vx, rsrc(sb.p), vb, nrun, acc,
@@ -1769,12 +2052,13 @@ template <int KS>
 __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, float* smem, unsigned long long* tr) {
   // (ops.h RLE_GEMM_VARIANTS, those of kernel set KS; the host refuses any other id.  PK 4 / 5 take an id
   // with the norm bit their consumers never set, so their NORM is false)
-#define RLE_VX(mode, epi, act, norm, pre, pk, sets)                                              \
-  case gemm_vid(mode, epi, act, norm, pre):                                                      \
-    if constexpr (KS == KS_EXT || (((sets) >> KS) & 1)) {                                       \
-      asm volatile("; gemm variant " #mode " " #epi " " #act " norm " #norm " pk " #pk ::);      \
-      gemm_v<mode, epi, act, (norm) != 0 && (pk) <= 3, pk, KS == KS_EXT>(g, t, smem, tr);        \
-    }                                                                                            \
+#define RLE_VX(mode, epi, act, norm, pre, pk, sets)                                                       \
+  case gemm_vid(mode, epi, act, norm, pre):                                                               \
+    if constexpr (KS == KS_EXT || (((sets) >> ks_family(KS)) & 1)) {                                     \
+      asm volatile("; gemm variant " #mode " " #epi " " #act " norm " #norm " pk " #pk ::);               \
+      gemm_v<mode, epi, act, (norm) != 0 && (pk) <= 3, pk, KS == KS_EXT,                                  \
+             (KS == KS_TD7W || KS == KS_EXT) && wide_variant(mode, epi, pk)>(g, t, smem, tr);             \
+    }                                                                                                     \
     break;
   switch (vid) {
     RLE_GEMM_VARIANTS(RLE_VX)
@@ -2718,7 +3002,10 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
                                                                   unsigned e8, unsigned e9, unsigned e10, unsigned e11,
                                                                   const Op* ops_arg, unsigned long long* trace_arg,
                                                                   const Op* next_arg, unsigned next_lines) {
-  __shared__ __attribute__((aligned(16))) float smem[kRbOff + 4096 > 6144 ? kRbOff + 4096 : 6144];  // 24 KB
+  // 24 KB (the wide instances: the 32 KB LDS ring of gemm_wide)
+  constexpr int kSmemF = (KS == KS_TD7W || KS == KS_EXT) && kWideSmem > 6144 ? kWideSmem : 6144;
+  static_assert(kSmemF >= kRbOff + 4096, "LDS for the register-blocked exchange");
+  __shared__ __attribute__((aligned(16))) float smem[kSmemF];
   // op of this workgroup from the (preloaded) entry table: straight-line selects over SGPRs
   const unsigned long long t_in = TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;  // before any load
   // Entry 0 bit 31: the launch leads with 8 workgroups that only load the next launch's
@@ -2790,11 +3077,11 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
     RLE_OP(OP_PRIORITY, op_priority(op.prio, smem))
     RLE_OP(OP_SAC_ACTOR, op_sac_actor(op.sac, t))
     RLE_OP(OP_SAC_ACTOR_BWD, op_sac_actor_bwd(op.sac, t))
-    RLE_OP(OP_STEP_END, op_step_end<KS != KS_TD7>(op.end, smem, tr))
+    RLE_OP(OP_STEP_END, op_step_end<ks_family(KS) != KS_TD7>(op.end, smem, tr))
     RLE_OP(OP_POLYAK, op_polyak(op.flat, t))
     RLE_OP(OP_COPY, op_copy(op.flat, t))
     RLE_OP(OP_MAXRED, op_maxred(op.flat, t, smem))
-    RLE_OP(OP_CTRL, op_ctrl<KS != KS_TD7>(op.ctrl))
+    RLE_OP(OP_CTRL, op_ctrl<ks_family(KS) != KS_TD7>(op.ctrl))
     RLE_OP(OP_NOISE, op_noise(op.sample, t))
     RLE_OP(OP_FOLDBIAS, op_foldbias(op.fb))
 #undef RLE_OP
@@ -3074,13 +3361,15 @@ int trace_stride() { return kTraceStride; }
 int level_capacity() {
   int per_cu = 0, cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
-  int p1 = 0, p2 = 0;  // (every instance: the planner's capacity must hold for the one an engine runs)
+  int p1 = 0, p2 = 0, p3 = 0;  // (every instance: the planner's capacity must hold for the one an engine runs)
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rle_level<false, KS_TD7>, kThreads, 0) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&p1, rle_level<false, KS_MLP>, kThreads, 0) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p2, rle_level<false, KS_EXT>, kThreads, 0) != hipSuccess)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p2, rle_level<false, KS_EXT>, kThreads, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p3, rle_level<false, KS_TD7W>, kThreads, 0) != hipSuccess)
     return 1024;
   per_cu = per_cu < p1 ? per_cu : p1;
   per_cu = per_cu < p2 ? per_cu : p2;
+  per_cu = per_cu < p3 ? per_cu : p3;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
   return per_cu * cus;
 }
@@ -3090,9 +3379,10 @@ int level_capacity() {
 std::vector<LevelLaunch>* g_level_rec = nullptr;
 // the production kernel's HSA symbol name (AQL dispatch)
 const char* level_kernel_symbol(int ks) {
-  return ks == KS_EXT   ? "_ZN3rle9rle_levelILb0ELi2EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"
-         : ks == KS_MLP ? "_ZN3rle9rle_levelILb0ELi1EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"
-                        : "_ZN3rle9rle_levelILb0ELi0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd";
+  return ks == KS_EXT    ? "_ZN3rle9rle_levelILb0ELi2EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"
+         : ks == KS_MLP  ? "_ZN3rle9rle_levelILb0ELi1EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"
+         : ks == KS_TD7W ? "_ZN3rle9rle_levelILb0ELi3EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd"
+                         : "_ZN3rle9rle_levelILb0ELi0EEEvjjjjjjjjjjjjPKNS_2OpEPyS3_j.kd";
 }
 
 hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hipStream_t st,
@@ -3142,10 +3432,12 @@ hipError_t launch_level(const Op* d_ops, const Op* h_ops, int nops, int nwg, hip
     if (trace) {
       if (ks == KS_TD7) hipLaunchKernelGGL((rle_level<true, KS_TD7>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
       else if (ks == KS_MLP) hipLaunchKernelGGL((rle_level<true, KS_MLP>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+      else if (ks == KS_TD7W) hipLaunchKernelGGL((rle_level<true, KS_TD7W>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
       else hipLaunchKernelGGL((rle_level<true, KS_EXT>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
     } else {
       if (ks == KS_TD7) hipLaunchKernelGGL((rle_level<false, KS_TD7>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
       else if (ks == KS_MLP) hipLaunchKernelGGL((rle_level<false, KS_MLP>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
+      else if (ks == KS_TD7W) hipLaunchKernelGGL((rle_level<false, KS_TD7W>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
       else hipLaunchKernelGGL((rle_level<false, KS_EXT>), grid, dim3(kThreads), 0, st, RLE_LEVEL_ARGS);
     }
 #undef RLE_LEVEL_ARGS

@@ -184,9 +184,19 @@ static_assert(gemm_vid(2, 8, 15, 1, 3) < 2048, "GEMM variant ids fit 11 bits");
   X(GEMM_DX, EPI_STORE, ACT_RELU, 0, 3, 3, 2)       \
   X(GEMM_FWD, EPI_QDOT, ACT_RELU, 1, 3, 4, 2)       \
   X(GEMM_FWD, EPI_STORE, ACT_RELU, 1, 1, 5, 2)
+// the variants kernels.hip gemm_wide implements (64-row LDS-staged tiles, GemmHot::wide): forward and input-gradient
+// GEMMs with a plain, q-dot, MSE, q-head or AvgL1Norm-dot epilogue and no in-tile prologue
+constexpr bool wide_variant(int mode, int epi, int pk) {
+  return pk == 0 && mode != 2 /* GEMM_DW */ &&
+         (epi == EPI_STORE || epi == EPI_QDOT || epi == EPI_MSE || epi == EPI_QHEAD || epi == EPI_NBDOT);
+}
 // kernel sets (rle_level's KS): TD7, TD3 / SAC, and the extended instance (every variant, plus the opt-in
 // register-blocked weight-gradient tiles and the fused priority sampler)
-enum KernelSet : int { KS_TD7 = 0, KS_MLP = 1, KS_EXT = 2, KS_COUNT = 3 };
+// KS_TD7W: the TD7 set with the 64-row LDS-staged tiles (GemmHot::wide) and a larger LDS allocation, for
+// batches >= 512 (rle_plan wide)
+enum KernelSet : int { KS_TD7 = 0, KS_MLP = 1, KS_EXT = 2, KS_TD7W = 3, KS_COUNT = 4 };
+// the agent family whose variants (RLE_GEMM_VARIANTS sets bit) and ops an instance compiles
+constexpr int ks_family(int ks) { return ks == KS_TD7W ? KS_TD7 : ks; }
 
 enum GemmMode : int {
   GEMM_FWD = 0,   // A contiguous (activations), B contiguous (W rows):  Y = X W^T
@@ -216,7 +226,11 @@ struct GemmHot {
   // quarters and each accumulates every column block of the tile (kernels.hip rb_run); 0: column
   // groups x splits
   int rb;
-  int pad_[5];
+  // 64-row LDS-staged tile (rle_plan wide; the TD7 instance at B >= 512, kernels.hip gemm_wide): the
+  // workgroup's 4 waves own 16 rows each of a 64 x 64 output tile, every W chunk staged once in LDS for all
+  // four; tiles counts 64-row tiles, GemmArgs::tiles_m 16-row blocks
+  int wide;
+  int pad_[4];
 };
 static_assert(sizeof(GemmHot) == 128, "GemmHot is loaded as 2 x 16 dwords");
 

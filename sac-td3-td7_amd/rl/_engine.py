@@ -51,7 +51,7 @@ class Plan(ctypes.Structure):
         ("level_cap", _int), ("steps_per_graph", _int), ("pre_tn", _int), ("pl_tn", _int), ("tn_min", _int),
         ("flat_div", _int), ("balance", _int), ("tiny_w", _int), ("uni_w", _int), ("tiny_wg", _int),
         ("sched_cap", _int), ("fuse_off", ctypes.c_uint), ("fuse_on", ctypes.c_uint), ("rb", _int),
-        ("pl_w", _int), ("lap_w", _int), ("head_w", _int), ("adam_w", _int),
+        ("pl_w", _int), ("lap_w", _int), ("head_w", _int), ("adam_w", _int), ("wide", _int),
     ]
 
 

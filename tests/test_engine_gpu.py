@@ -454,12 +454,47 @@ def test_fused_priority_sampler_matches_reference(name, burst):
     _trajectory(name, burst, E.make_plan(fuse_on=["priosample"]))
 
 
-@pytest.mark.parametrize("alg,env,n,H", [("sac", "Humanoid-v4", 3, 512), ("td3", "HalfCheetah-v4", 3, 512)])
-def test_wide_hidden_burst_matches_oracle(alg, env, n, H):
+@pytest.mark.parametrize("alg,env,H", [("sac", "Humanoid-v4", 512), ("td3", "HalfCheetah-v4", 512)])
+def test_wide_hidden_steps_match_oracle(alg, env, H):
     """Hidden width 512 (rle_create accepts H <= 512): the fusions whose kernels bound H (SAC's raw head
     + rsample in one GEMM epilogue, kernels.hip sacraw_*, R <= 256) fall back to their standalone ops
-    instead of failing the program build, and the steps agree with the oracle."""
-    _burst_vs_oracle(alg, env, n, 256, {}, H=H)
+    instead of failing the program build.  Step 1's gradients (the Adam first moments) agree with the
+    oracle's at 1e-5 of each tensor's max |g| (measured <= 5e-7), then 3 more steps' losses and parameters.
+    (The parameters' bulk criterion is 0.98 here: at H = 512 SAC's critic input layers carry more
+    near-zero gradients whose sign the fp32 summation order decides, and Adam's first steps move those
+    elements by ~2 lr: measured 0.989 for q2.mlp.0 after 3 steps while step 1's gradients agree to 4.8e-7
+    of the tensor max, tools/diag_wide.py.)"""
+    from oracle import agents
+    from test_oracle import build_from_golden
+
+    n, B, ncap = 4, 256, 4096
+    g = _synthetic_golden(alg, env, H, B, ncap, ncap, n, False, 91)
+    _, orc, orep, tp, n_steps, B = build_from_golden(g)
+    eng, rep, tp2 = engine_from_golden(g)
+    eng.set_tapes(u=tp2["u"][:n], eps=tp2["eps"][:n], eps_pi=tp2.get("eps_pi", None))
+    infos = [eng.step(1)[0]]
+    i1, _ = agents.run_steps(orc, alg, orep, {k: v[0:1] for k, v in tp.items()}, 1, B)
+    infos_ref = list(i1)
+    for key, ref in agents.moments(orc).items():
+        if not key.endswith(":m") or key.startswith("tmp."):
+            continue
+        net, pname = key[:-2].split(".", 1)
+        got = eng.get_adam(net, pname, 0, ref.shape)
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5 * float(np.abs(ref).max()), err_msg=key)
+    infos += list(eng.step(n - 1))
+    eng.set_tapes()
+    for t in range(1, n):
+        i1, _ = agents.run_steps(orc, alg, orep, {k: v[t:t + 1] for k, v in tp.items()}, 1, B)
+        infos_ref += i1
+    keys = {"td3": ["train/q_fn", "train/policy", "norm/policy"],
+            "sac": ["train/q_fn", "tmp", "norm/tmp", "train/policy", "train/tmp", "entropy"]}[alg]
+    ref = np.array([[np.nan if i[k] is None else i[k] for k in keys] for i in infos_ref], np.float64)
+    np.testing.assert_allclose(np.array(infos)[:, :len(keys)], ref, rtol=2e-3, atol=1e-4, equal_nan=True)
+    tol = 2 * 3e-4 * n + 1e-4
+    for net, d in orc.nets().items():
+        for name, v in d.items():
+            assert_params_close(eng.get_param(net, name, tuple(v.shape)), v.detach().numpy(), tol, (net, name),
+                                bulk=0.98)
 
 
 def _burst_vs_oracle(alg, env, n, B, extra, plan=None, H=256):
@@ -610,3 +645,42 @@ def test_bench_program_1m_lap_replay_matches_oracle():
     for net, d in orc.nets().items():
         for name, v in d.items():
             assert_params_close(eng.get_param(net, name, tuple(v.shape)), v.detach().numpy(), tol, (net, name))
+
+
+def _wide_run(B, n, plan, env="Humanoid-v4"):
+    g = _synthetic_golden("td7", env, 256, B, 8192, 8192, n, True, 95)
+    eng, rep, tp = engine_from_golden(g, plan=plan)
+    eng.set_tapes(u=tp["u"][:n], eps=tp["eps"][:n])
+    info = np.array(eng.step(n))
+    eng.set_tapes()
+    S, A, _ = spec.TASKS[env]
+    params = {(net, p): eng.get_param(net, p) for net, ps in spec.agent_params("td7", S, A, 256, 0).items() for p in ps}
+    return eng, rep, info, params
+
+
+@pytest.mark.parametrize("B", [512, 1024])
+def test_wide_tiles_bitwise_equal_16_row_tiles(B):
+    """The 64-row LDS-staged tiles (rle_plan wide, kernels.hip gemm_wide) against the 16-row tiles at the same tile
+    width (tn_min 64: every 16-row tile reduces all of K in one wave, on ring_run's two parity accumulators, as
+    each wave of a wide tile does for each of its 4 column blocks): 8 TD7 Humanoid steps (single step + a 6-step
+    graph + 1) end with bit-identical parameters, indices and priorities.  (The loss values may differ in the
+    last bits: the 16-row tiles write their MSE / q-head loss partials in XCD tile order, the wide tiles in row
+    order, and only the info row sums them.)"""
+    e1, r1, i1, p1 = _wide_run(B, 8, E.make_plan(tn_min=64, wide=1))
+    e0, r0, i0, p0 = _wide_run(B, 8, E.make_plan(tn_min=64, wide=0))
+    assert ".w]" in e1.describe(0) and ".w]" not in e0.describe(0)
+    np.testing.assert_array_equal(e1.last_indices(), e0.last_indices())
+    np.testing.assert_array_equal(r1.get_priority(), r0.get_priority())
+    for k in p1:
+        np.testing.assert_array_equal(p1[k], p0[k], err_msg=str(k))
+    np.testing.assert_allclose(i1, i0, rtol=1e-5, atol=1e-7, equal_nan=True)
+
+
+@pytest.mark.parametrize("check", ["RLE_AUDIT", "RLE_HAZARD"])
+def test_wide_tiles_audit_and_hazards(check, monkeypatch):
+    """RLE_AUDIT / RLE_HAZARD over every program of a B = 512 TD7 engine with the 64-row tiles (the address replay
+    covers a wide tile as the four 16-row tn-64 tiles it computes), then steps run."""
+    monkeypatch.setenv(check, "1")
+    e, r, info, _ = _wide_run(512, 3, E.make_plan(wide=1))
+    assert ".w]" in e.describe(0)
+    assert np.isfinite(info[:, :2]).all()

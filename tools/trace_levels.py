@@ -96,6 +96,8 @@ for which in graphs:
                     if tr.shape[1] == 16 and "gemm" in name and (tt[:, 11] > 0).all() and (tt[:, 12] > 0).all():
                         extra = (f" [dec {f(ph(0, 11))} desc {f(ph(11, 12))} pf {f(ph(12, 1))}"
                                  f" splitK {f(ph(2, 13))} epi {f(ph(13, 3))}]")
+                        if "adam" in name and (tt[:, 4] > 0).all() and (tt[:, 5] > 0).all():  # DW: AvgL1Norm tables
+                            extra += f" [ring {f(ph(1, 4))} tables {f(ph(4, 5))} run {f(ph(5, 2))}]"
                         if (tt[:, 4] > 0).all() and (tt[:, 6] > 0).all():  # pre-GEMM consumer phases
                             extra += (f" [pre issue {f(ph(1, 4))} segs {f(ph(4, 5))} finish {f(ph(5, 6))}"
                                       f" lds {f(ph(6, 2))}]")
