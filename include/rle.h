@@ -94,9 +94,9 @@ typedef struct rle_plan {
                            SAC raw head; -1: default, SAC 24, else 0)                                     */
   int lap_w, head_w, adam_w; /* rebalance weights: LAP sampler, loss head, added to Adam-epilogue GEMMs
                                 (-1: 60, 60, SAC 16 / else 8)                                             */
-  int wide;             /* 1: forward / input-gradient GEMMs over >= 64 rows as 64 x 64 tiles with every W chunk
-                           staged once in LDS for the tile's four 16-row blocks (kernels.hip gemm_wide;
-                           -1: default, TD7 at batch >= 512)                                              */
+  int wide;             /* 64 / 32: forward / input-gradient GEMMs over >= 64 rows as 64 x 64 / 64 x 32 tiles with
+                           every W chunk staged once in LDS for the tile's four 16-row blocks (kernels.hip
+                           gemm_wide; 1 = 64; 0 off; -1: default, TD7 at batch >= 512)                     */
 } rle_plan;
 
 /* ---- replay memory: rl/replay_memory/{lap,simple}.py ---------------------- */

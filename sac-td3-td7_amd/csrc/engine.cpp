@@ -400,8 +400,9 @@ static void gemm_finalize(GemmArgs& g) {
   REQUIRE((long long)g.tiles_m * g.tiles_n < 65536, "gemm: too many tiles");
   // 64-row LDS-staged tiles (kernels.hip gemm_wide): one of its variants, 64-wide tiles over whole 64-row blocks,
   // no in-tile prologue, no target smoothing; tiles_m stays the 16-row block count (loss partial slots)
-  REQUIRE(!g.hot.wide || (wide_variant(g.mode, g.epi, g.has_pre) && g.tn == 64 && g.M % 64 == 0 &&
-                          g.tiles_m * 16 == g.M && !g.noise.t && g.N % 64 == 0),
+  REQUIRE(!g.hot.wide || (wide_variant(g.mode, g.epi, g.has_pre) && (g.tn == 64 || g.tn == 32) &&
+                          g.hot.wide == g.tn && g.M % 64 == 0 && g.tiles_m * 16 == g.M && !g.noise.t &&
+                          g.N % g.tn == 0),
           "gemm: wide tile layout");
   g.inv_tiles_n = 1.f / (float)g.tiles_n;
   GemmHot& h = g.hot;
@@ -1533,8 +1534,9 @@ struct Engine {
   // the rle_level instance this engine's programs run on (ops.h KernelSet): the agent's own set, or the
   // extended instance when the plan asks for its opt-in paths
   int kernel_set() const {
-    if (plan.rb || (plan.fuse_on & RLE_FUSE_PRIOSAMPLE) || (plan.wide && algo != RLE_TD7)) return KS_EXT;
-    return algo == RLE_TD7 ? (plan.wide ? KS_TD7W : KS_TD7) : KS_MLP;
+    if (algo == RLE_TD7 && plan.wide && !(plan.fuse_on & RLE_FUSE_PRIOSAMPLE)) return KS_TD7W;  // (rb compiled in)
+    if (plan.rb || (plan.fuse_on & RLE_FUSE_PRIOSAMPLE) || plan.wide) return KS_EXT;
+    return algo == RLE_TD7 ? KS_TD7 : KS_MLP;
   }
   void resolve_plan() {
     if (plan.steps_per_graph < 0) plan.steps_per_graph = algo == RLE_TD3 ? 16 : algo == RLE_SAC ? 8 : 6;
@@ -1555,7 +1557,11 @@ struct Engine {
     if (plan.uni_w < 0) plan.uni_w = algo == RLE_SAC ? 30 : algo == RLE_TD3 ? 8 : 60;
     if (plan.tiny_wg < 0) plan.tiny_wg = 2;
     plan.sched_cap = plan.sched_cap ? 1 : 0;
-    plan.rb = plan.rb < 0 ? 0 : (plan.rb ? 1 : 0);
+    // (64-row LDS-staged tiles: the 16-row tiles' per-workgroup fixed cost and 2 KB of operand loads per 4
+    // MFMAs bound the B >= 512 levels, DESIGN round 5; with them the register-blocked weight-gradient tiles, the
+    // batch split over the 4 waves, where a 16 x 64 weight-gradient tile's waves would each reduce all B rows)
+    if (plan.wide < 0) plan.wide = 0;  // (opt-in: slower at B = 1024 than the 16-row tiles, DESIGN round 5)
+    plan.rb = plan.rb < 0 ? (plan.wide ? 1 : 0) : (plan.rb ? 1 : 0);
     // (A/B, 2 pairs: SAC Humanoid pl_w 0 / 8 / 16 / 24 -> 14.09k / 14.09k / 14.11k / 14.15k; TD3 HalfCheetah
     // 25.37k / 25.33k / 25.38k / 25.36k)
     if (plan.pl_w < 0) plan.pl_w = algo == RLE_SAC ? 24 : 0;
@@ -1566,10 +1572,7 @@ struct Engine {
     // 8.24k, B = 1024 flat: profiles/r04_ab_weights.txt)
     if (plan.adam_w < 0) plan.adam_w = algo == RLE_SAC ? 16 : 8;
     if (plan.level_cap < 0) plan.level_cap = 0;
-    // (64-row LDS-staged tiles: the 16-row tiles' per-workgroup fixed cost and 2 KB of operand loads per 4
-    // MFMAs bound the B >= 512 levels, DESIGN round 5)
-    if (plan.wide < 0) plan.wide = algo == RLE_TD7 && cfg.batch >= 512 ? 1 : 0;
-    plan.wide = plan.wide ? 1 : 0;
+    plan.wide = plan.wide == 32 || plan.wide == 0 ? plan.wide : 64;  // (the tile width; 1 = 64)
   }
   int S, Sp, A, Ap, H, Hp, B;
   int algo;
@@ -2220,9 +2223,9 @@ struct Engine {
                               ? (pl_src ? std::min(std::max(tq.first, pre_tn()), 32) : std::max(tq.first, pre_tn()))
                                                   : (pl_src ? std::min(tq.first, 32) : tq.first));
     // 64-row LDS-staged tiles (rle_plan wide): every row piece whole 64-row blocks, 64-column blocks
-    bool wide = plan.wide && !sfu && !pre && !noise && L.out % 64 == 0;
+    bool wide = plan.wide && !sfu && !pre && !noise && L.out % plan.wide == 0;
     for (size_t ci = 0; wide && ci + 1 < cuts.size(); ++ci) wide = (cuts[ci + 1] - cuts[ci]) % 64 == 0;
-    const int tn_w = wide ? 64 : tn;
+    const int tn_w = wide ? plan.wide : tn;
     const int tiles_n = cdiv(L.out, tn_w);
     View out = buf(M, L.out, true, out_t);
     if (sfu) {
@@ -2309,7 +2312,7 @@ struct Engine {
       g.N = L.out;
       g.R = L.K;
       g.tn = tn_w;
-      g.hot.wide = wide;
+      g.hot.wide = wide ? plan.wide : 0;
       g.tiles_m = cdiv(m, kTileM);
       g.tiles_n = tiles_n;
       g.epi = EPI_STORE;
@@ -2397,9 +2400,9 @@ struct Engine {
                                    : (pl_src ? std::min(tq.first, 32) : tq.first);
     op.seq = tq.second;
     // 64-row LDS-staged tiles (rle_plan wide): a plain or EPI_NBDOT input gradient over whole 64-row blocks
-    const bool wide = plan.wide && !pre && !head && !sbu && M % 64 == 0 && ncols % 64 == 0;
-    if (wide) g.tn = 64;
-    g.hot.wide = wide;
+    const bool wide = plan.wide && !pre && !head && !sbu && M % 64 == 0 && ncols % plan.wide == 0;
+    if (wide) g.tn = plan.wide;
+    g.hot.wide = wide ? plan.wide : 0;
     g.tiles_m = cdiv(M, kTileM);
     g.tiles_n = cdiv(ncols, g.tn);
     g.epi = EPI_STORE;
@@ -2912,9 +2915,9 @@ struct Engine {
       g.N = L.out;
       g.R = L.K;
       const auto tq = choose_tn(B, L.out);
-      const bool wide = plan.wide && B % 64 == 0 && L.out % 64 == 0;
-      g.tn = wide ? 64 : tq.first;
-      g.hot.wide = wide;
+      const bool wide = plan.wide && B % 64 == 0 && L.out % plan.wide == 0;
+      g.tn = wide ? plan.wide : tq.first;
+      g.hot.wide = wide ? plan.wide : 0;
       op.seq = tq.second;
       g.tiles_m = cdiv(B, kTileM);
       g.tiles_n = cdiv(L.out, g.tn);
@@ -3211,9 +3214,9 @@ struct Engine {
     g.N = L.out;
     g.R = L.K;
     const auto tq = choose_tn(M, L.out);
-    const bool wide = plan.wide && M % 64 == 0 && L.out % 64 == 0;
-    g.tn = wide ? 64 : tq.first;
-    g.hot.wide = wide;
+    const bool wide = plan.wide && M % 64 == 0 && L.out % plan.wide == 0;
+    g.tn = wide ? plan.wide : tq.first;
+    g.hot.wide = wide ? plan.wide : 0;
     op.seq = tq.second;
     g.tiles_m = cdiv(M, kTileM);
     g.tiles_n = cdiv(L.out, g.tn);

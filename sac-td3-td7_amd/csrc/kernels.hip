@@ -213,10 +213,52 @@ __device__ __forceinline__ float norm_inv_i(const CAS NormRef& nr, int row) {
   return 1.f / (m < 1e-8f ? 1e-8f : m);
 }
 
+// Sums of the first nparts (<= PMAX) row partials, in partial order as norm_mean adds them, of rows
+// tid + kThreads r (r < RPT, clamped to n - 1) of a partial array: every load issued together, clamped instead
+// of branched, so a thread pays one memory round trip for all its rows.  (The weight gradients' AvgL1Norm
+// tables cover the whole batch: 4 rows per thread at B = 1024, where one round trip per row cost 7-12 us per
+// workgroup, DESIGN round 5.)
+template <int RPT, int PMAX>
+__device__ __forceinline__ void row_sums(const float* part, int ld, int row0, int nparts, int n, float (&s)[RPT]) {
+  const GAS float* p = G(part) + row0;
+  float v[RPT][PMAX];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int i = min((int)threadIdx.x + r * kThreads, n - 1);
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) v[r][q] = p[(size_t)min(q, nparts - 1) * ld + i];
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q)
+      if (q < nparts) a += v[r][q];
+    s[r] = a;
+  }
+}
+
 // LDS table of 1/m for n consecutive rows of a normed tensor (16-padded with 0).
+template <int RPT, int PMAX>
+__device__ __forceinline__ void norm_tab_batched(const CAS NormRef& nr, int n, float* dst) {
+  float sm[RPT];
+  row_sums<RPT, PMAX>(nr.part, nr.ld, nr.row0, nr.nparts, n, sm);
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int i = threadIdx.x + r * kThreads;
+    const float m = sm[r] / (float)nr.width;
+    if (i < n) dst[i] = 1.f / (m < 1e-8f ? 1e-8f : m);  // (norm_inv_i's floats)
+  }
+}
 __device__ __forceinline__ void build_norm_tab(const CAS NormRef& nr, int n, float* dst) {
+  if (n <= kThreads && nr.nparts <= 16) {
+    norm_tab_batched<1, 16>(nr, n, dst);
+  } else if (n <= 4 * kThreads && nr.nparts <= 8) {
+    norm_tab_batched<4, 8>(nr, n, dst);
+  } else {
 #pragma unroll 1
-  for (int i = threadIdx.x; i < n; i += kThreads) dst[i] = norm_inv_i(nr, i);
+    for (int i = threadIdx.x; i < n; i += kThreads) dst[i] = norm_inv_i(nr, i);
+  }
 #pragma unroll 1
   for (int i = n + threadIdx.x; i < ((n + 15) & ~15); i += kThreads) dst[i] = 0.f;
 }
@@ -457,7 +499,32 @@ __device__ __forceinline__ f32x4 ring_run_nb(float4 (&a)[RG], float4 (&x)[RG], f
 
 // kDwNb tables for the n reduction rows: 1/m and the sign coefficient
 // gm = -(sum_j g x) / (n_x m^2) (0 when m is clamped), exactly as op_normbwd.
+template <int RPT, int PMAX>
+__device__ __forceinline__ void nb_tab_batched(const CAS GemmArgs& g, int n, float* ti, float* tg) {
+  float sm[RPT], sd[RPT];
+  row_sums<RPT, PMAX>(g.nbm.part, g.nbm.ld, g.nbm.row0, g.nbm.nparts, n, sm);
+  row_sums<RPT, PMAX>(g.nbdot, g.nbdot_ld, 0, g.nbdot_n, n, sd);
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int i = threadIdx.x + r * kThreads;
+    const float mean = sm[r] / (float)g.nbm.width, dot = sd[r] / 1.f;  // (norm_mean_i's floats)
+    const bool clamped = mean < 1e-8f;
+    const float inv = 1.f / (clamped ? 1e-8f : mean);
+    if (i < n) {
+      ti[i] = inv;
+      tg[i] = clamped ? 0.f : (-dot * inv * inv) / (float)g.nbm.width;
+    }
+  }
+}
 __device__ __forceinline__ void build_nb_tab(const CAS GemmArgs& g, int n, float* ti, float* tg) {
+  if (n <= kThreads && g.nbm.nparts <= 16 && g.nbdot_n <= 16) {
+    nb_tab_batched<1, 16>(g, n, ti, tg);
+    return;
+  }
+  if (n <= 4 * kThreads && g.nbm.nparts <= 4 && g.nbdot_n <= 4) {
+    nb_tab_batched<4, 4>(g, n, ti, tg);
+    return;
+  }
 #pragma unroll 1
   for (int i = threadIdx.x; i < n; i += kThreads) {
     const float mean = norm_mean_i(g.nbm.part, g.nbm.ld, i + g.nbm.row0, g.nbm.nparts, g.nbm.width);
@@ -1053,20 +1120,28 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
 
 // ---------------------------------------------------------------- 64-row LDS-staged tiles (GemmHot::wide)
 //
-// One workgroup = a 64 x 64 output tile of a FWD / DX GEMM over >= 512 batch rows (rle_plan wide, the KS_TD7W
-// instance): wave w owns rows 16w .. 16w + 15 and all 4 column blocks.  Each 16-wide reduction chunk's operands
-// -- the tile's 4 A row blocks and its 4 W column blocks, 8 KB -- are copied into one slot of an LDS ring by
-// LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction: wave w copies its own A block and W column
-// block w), so each W block is fetched once per workgroup and feeds all four row blocks, and the ring holds no
-// VGPRs: kWideRing - 1 chunks are in flight while one is reduced.  Every wave keeps 4 independent accumulator
-// chains (one per column block), each split by chunk parity exactly as ring_run sums a segment, and the
-// epilogues combine column blocks in the 16-row tile's wave order: the floats of the 16-row tn-64 tile.
+// One workgroup = a 64 x (16 NBW) output tile of a FWD / DX GEMM over >= 512 batch rows (rle_plan wide, the
+// KS_TD7W instance): wave w owns rows 16w .. 16w + 15 and the tile's NBW column blocks (NBW = 4: 64 columns, 2:
+// 32).  Each 16-wide reduction chunk's operands -- the tile's 4 A row blocks and its NBW W column blocks -- are
+// copied into one slot of an LDS ring by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction: wave w
+// copies its own A block and, w < NBW, W column block w), so each W block is fetched once per workgroup and
+// feeds all four row blocks, and the ring holds no VGPRs: R - 1 chunks are in flight while one is reduced
+// (R = wide_ring<NBW>, 40 KB of LDS).  Every wave keeps NBW independent accumulator chains, each split by chunk
+// parity relative to its segment exactly as ring_run sums a segment, so at NBW = 4 the sums are the floats of
+// the 16-row tn-64 tile; the epilogues combine column blocks in that tile's wave order.
 // Protocol per chunk k: wait for this wave's DMAs of chunk k (counted vmcnt: the DMAs are inline asm, outside
-// the compiler's wait bookkeeping), s_barrier (every wave's DMAs of chunk k landed; every wave is done reading
-// chunk k - 1's slot), issue chunk k + kWideRing - 1 into that freed slot, read chunk k's fragments, MFMA.
-constexpr int kWideRing = 4;
-constexpr int kWideSlot = 2048;                  // floats per ring slot: A [4 waves][256], W [4 column blocks][256]
-constexpr int kWideSmem = kWideRing * kWideSlot;  // 32 KB
+// the compiler's wait bookkeeping, and no other vector-memory instruction is issued inside the loop), s_barrier
+// (every wave's DMAs of chunk k landed; every wave is done reading chunk k - 1's slot), issue chunk k + R - 1
+// into that freed slot, read chunk k's fragments, MFMA.
+constexpr int kWideSmem = 10240;  // floats (40 KB: 4 workgroups per CU, as the 127 VGPRs allow)
+template <int NBW>
+constexpr int wide_slot() {
+  return (4 + NBW) * 256;
+}
+template <int NBW>
+constexpr int wide_ring() {
+  return kWideSmem / wide_slot<NBW>() > 6 ? 6 : kWideSmem / wide_slot<NBW>();
+}
 
 __device__ __forceinline__ unsigned lds_off(const float* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
@@ -1079,20 +1154,31 @@ __device__ __forceinline__ void glds_block(const float* src, unsigned lds) {
                : "v"(src), "s"(lds)
                : "memory");
 }
-// this wave's DMAs of a chunk landed, with `ahead` younger chunks (2 DMAs each) still in flight
-__device__ __forceinline__ void wide_wait(int ahead) {
-  static_assert(kWideRing == 4, "wide_wait's counts assume 2 chunks ahead at most");
-  if (ahead >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// this wave's DMAs of a chunk landed, with n younger DMAs still in flight (n <= 10)
+__device__ __forceinline__ void wide_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+  }
 }
 __device__ __forceinline__ void wide_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-template <int MODE, int EPI, int ACT, bool NORM>
+template <int MODE, int EPI, int ACT, bool NORM, int NBW>
 __device__ __forceinline__ void gemm_wide(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr,
-                                                    int tiles_n, int gN, int gR, float inv_tn, int nseg_a, int nseg_b,
-                                                    int tiles, int xb, int tmb, int nfull, float inv_tmb, float inv_xb,
-                                                    float inv_blast, const float* biasp) {
+                                          int tiles_n, int gN, int gR, float inv_tn, int nseg_a, int nseg_b,
+                                          int tiles, int xb, int tmb, int nfull, float inv_tmb, float inv_xb,
+                                          float inv_blast, const float* biasp) {
+  constexpr int R = wide_ring<NBW>(), SLOT = wide_slot<NBW>();
+  static_assert(R >= 3 && R * SLOT <= kWideSmem, "wide ring");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int it, jt;
@@ -1103,18 +1189,20 @@ __device__ __forceinline__ void gemm_wide(const CAS GemmArgs& g, int t, float* s
     jt = t - it * tiles_n;
   }
   const int i0 = (it << 6) + (wave << 4);  // this wave's 16 rows
-  const int jc0 = jt << 6;                 // the tile's first column
+  const int jc0 = jt * (16 * NBW);         // the tile's first column
   const int ib = i0 + ((lane >> 4) << 2);
   const int nch = gR >> 4;
   const bool wabs = MODE == GEMM_FWD && nseg_b == 1;
-  const int nbv = min(4, (gN - jc0 + 15) >> 4);  // column blocks of this tile inside the output
+  const int nbv = min(NBW, (gN - jc0 + 15) >> 4);  // column blocks of this tile inside the output
+  const int per = wave < NBW ? 2 : 1;              // DMAs this wave issues per chunk
   // ---- epilogue operands, issued before any LDS-DMA (ordinary loads older than the ring)
-  float pb[4] = {0.f, 0.f, 0.f, 0.f}, qwj[4] = {0.f, 0.f, 0.f, 0.f};
-  float4 ev[4];
+  float pb[NBW], qwj[NBW];
+  float4 ev[NBW];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < NBW; ++c) {
     const int j = jc0 + c * 16 + (lane & 15);
     const bool jok = j < gN;
+    pb[c] = qwj[c] = 0.f;
     ev[c] = make_float4(1.f, 1.f, 1.f, 1.f);
     if (jok && biasp) pb[c] = G(biasp)[j];
     if constexpr (EPI == EPI_QHEAD || EPI == EPI_QDOT) {
@@ -1150,80 +1238,82 @@ __device__ __forceinline__ void gemm_wide(const CAS GemmArgs& g, int t, float* s
       if (q < nseg_a && g.A.seg[q].norm.part) inv[q] = norm_inv_i(g.A.seg[q].norm, i0 + (lane & 15));
   }
   trace_mark(tr, 1);
-  // ---- the chunk loop over the LDS ring
+  // ---- DMA issue: chunk by chunk in reduction order, the segment pointers advanced at segment starts
   const unsigned ring = lds_off(smem);
-  auto seg_of = [&](int k) {
-    int q = 0;
-#pragma unroll
-    for (int u = 1; u < kMaxSeg; ++u)
-      if (u < nseg_a && k >= (g.A.seg[u].r0 >> 4)) q = u;
-    return q;
-  };
   const int bcol = (jc0 >> 4) + min(wave, nbv - 1);  // (blocks past the output: a valid block, never used)
-  auto issue = [&](int k) {
-    const int q = seg_of(k);
-    const CAS Seg& sa = g.A.seg[q];
-    const CAS Seg& sb = g.B.seg[wabs ? 0 : q];
-    const int s0 = sa.r0 >> 4, kb = wabs ? k : k - s0;
-    const unsigned slot = ring + (unsigned)((k & (kWideRing - 1)) * kWideSlot * 4);
-    glds_block(sa.p + ((size_t)((i0 >> 4) * sa.xs + (k - s0)) * 256 + lane * 4), slot + wave * 1024);
-    glds_block(sb.p + ((size_t)(bcol * sb.xs + kb) * 256 + lane * 4), slot + 4096 + wave * 1024);
+  int iq = 0, inext = nseg_a > 1 ? (g.A.seg[1].r0 >> 4) : nch;
+  const float* ia = g.A.seg[0].p + ((size_t)((i0 >> 4) * g.A.seg[0].xs) * 256 + lane * 4);
+  const float* ibp = g.B.seg[0].p + ((size_t)(bcol * g.B.seg[0].xs) * 256 + lane * 4);
+  int ik = 0;  // the next chunk to issue
+  auto issue_next = [&]() {
+    if (ik == inext) {  // (uniform) the next A segment; W: its own segment (DX / folded), or the same (wabs)
+      ++iq;
+      const CAS Seg& sa = g.A.seg[iq];
+      ia = sa.p + ((size_t)((i0 >> 4) * sa.xs) * 256 + lane * 4);
+      if (!wabs) {
+        const CAS Seg& sb = g.B.seg[iq];
+        ibp = sb.p + ((size_t)(bcol * sb.xs) * 256 + lane * 4);
+      }
+      inext = iq + 1 < nseg_a ? (g.A.seg[iq + 1].r0 >> 4) : nch;
+    }
+    const unsigned slot = ring + (unsigned)((ik % R) * SLOT * 4);
+    glds_block(ia, slot + wave * 1024);
+    if (wave < NBW) glds_block(ibp, slot + 4096 + wave * 1024);
+    ia += 256;
+    ibp += 256;
+    ++ik;
   };
 #pragma unroll
-  for (int k = 0; k < kWideRing - 1; ++k)
-    if (k < nch) issue(k);
-  f32x4 ac[4], ac1[4];
+  for (int k = 0; k < R - 1; ++k)
+    if (k < nch) issue_next();
+  // ---- the chunk loop, segment by segment, chunks in pairs (even / odd accumulators, as ring_run); one wait,
+  // barrier and issue round per pair, so the per-step synchronisation is paid once per 32 reduction rows
+  f32x4 ac[NBW], ac1[NBW];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) ac[c] = ac1[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int q = 0, kseg = 0;
-  int qnext = nseg_a > 1 ? (g.A.seg[1].r0 >> 4) : nch;
-  float sinv = inv[0];
-#pragma unroll 1
-  for (int k = 0; k < nch; ++k) {
-    wide_wait(min(kWideRing - 2, nch - 1 - k));
-    wide_barrier();
-    if (k + kWideRing - 1 < nch) issue(k + kWideRing - 1);
-    if (k == qnext) {  // segment boundary: ring_run's "return acc + acc1", then the next segment
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        ac[c] = ac[c] + ac1[c];
-        ac1[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      ++q;
-      kseg = k;
-      qnext = q + 1 < nseg_a ? (g.A.seg[q + 1].r0 >> 4) : nch;
-      if constexpr (NORM) sinv = q == 1 ? inv[1] : (q == 2 ? inv[2] : inv[3]);
-    }
-    const float* slot = smem + (k & (kWideRing - 1)) * kWideSlot;
+  for (int c = 0; c < NBW; ++c) ac[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int k, f32x4(&acc)[NBW], float sinv) {
+    const float* slot = smem + (k % R) * SLOT;
     float4 a = *(const float4*)(slot + wave * 256 + lane * 4);
     if constexpr (NORM) a = scale4(a, sinv);
-    float4 b[4];
+    float4 b[NBW];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) b[c] = *(const float4*)(slot + 1024 + c * 256 + lane * 4);
-    if ((k - kseg) & 1) {
+    for (int c = 0; c < NBW; ++c) b[c] = *(const float4*)(slot + 1024 + c * 256 + lane * 4);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) ac1[c] = mfma4(a, b[c], ac1[c]);
-    } else {
+    for (int c = 0; c < NBW; ++c) acc[c] = mfma4(a, b[c], acc[c]);
+  };
+#pragma unroll 1
+  for (int q = 0; q < nseg_a; ++q) {
+    const int k0 = g.A.seg[q].r0 >> 4, k1 = q + 1 < nseg_a ? (g.A.seg[q + 1].r0 >> 4) : nch;
+    const float sinv = NORM ? (q == 0 ? inv[0] : q == 1 ? inv[1] : q == 2 ? inv[2] : inv[3]) : 1.f;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) ac[c] = mfma4(a, b[c], ac[c]);
+    for (int c = 0; c < NBW; ++c) ac1[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int k = k0; k < k1; k += 2) {
+      const bool two = k + 1 < k1;
+      wide_wait(per * (ik - k - (two ? 2 : 1)));  // (chunks k, k + 1 landed: ik - k - n younger ones in flight)
+      wide_barrier();
+      if (ik < nch && ik < k + R) issue_next();  // (the slots of chunks < k are free: up to chunk k + R - 1)
+      if (ik < nch && ik < k + R) issue_next();
+      mma(k, ac, sinv);
+      if (two) mma(k + 1, ac1, sinv);
     }
-  }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) ac[c] = ac[c] + ac1[c];
+    for (int c = 0; c < NBW; ++c) ac[c] = ac[c] + ac1[c];  // (ring_run's "return acc + acc1")
+  }
   trace_mark(tr, 2);
   __syncthreads();  // (every wave is done with the ring: the epilogue reuses the LDS)
   // ---- epilogue, column block by column block; the tile's row sums in the 16-row tile's wave order
-  // ((s0 + s1) + (s2 + s3), s_c the row16_sum of column block c), loss partials one per 16-row block
-  // (wave_sum per column block, then the same order) at the 16-row tile's row-major index
-  float rs01[4] = {0.f, 0.f, 0.f, 0.f}, rs23[4] = {0.f, 0.f, 0.f, 0.f};
-  float ls01 = 0.f, ls23 = 0.f;
+  // (NBW 4: (s0 + s1) + (s2 + s3), s_c the row16_sum of column block c; NBW 2: s0 + s1), loss partials one per
+  // 16-row block (wave_sum per column block, the same order) at the 16-row tile's row-major index
+  float rsa[4] = {0.f, 0.f, 0.f, 0.f}, rsb[4] = {0.f, 0.f, 0.f, 0.f};
+  float lsa = 0.f, lsb = 0.f;
   float* tabw = smem + wave * 256;  // (EPI_MSE: this wave's row table of norm partials)
   if constexpr (EPI == EPI_MSE) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) tabw[((lane >> 4) + 4 * m) * 16 + (lane & 15)] = tnv[m];
   }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < NBW; ++c) {
     const int j = jc0 + c * 16 + (lane & 15);
     const bool jok = j < gN;
     const f32x4 acc = ac[c];
@@ -1291,40 +1381,40 @@ __device__ __forceinline__ void gemm_wide(const CAS GemmArgs& g, int t, float* s
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           const float s = row16_sum(rv[qq]);
-          if (c == 0) rs01[qq] = s;
-          else if (c == 1) rs01[qq] += s;
-          else if (c == 2) rs23[qq] = s;
-          else rs23[qq] += s;
+          if (c == 0) rsa[qq] = s;
+          else if (c == 1) rsa[qq] += s;
+          else if (c == 2) rsb[qq] = s;
+          else rsb[qq] += s;
         }
       }
     }
     if constexpr (EPI == EPI_QHEAD || EPI == EPI_MSE) {
       const float s = wave_sum(lv);
-      if (c == 0) ls01 = s;
-      else if (c == 1) ls01 += s;
-      else if (c == 2) ls23 = s;
-      else ls23 += s;
+      if (c == 0) lsa = s;
+      else if (c == 1) lsa += s;
+      else if (c == 2) lsb = s;
+      else lsb += s;
     }
   }
   if constexpr (EPI == EPI_QDOT || EPI == EPI_NBDOT || (EPI == EPI_STORE && MODE == GEMM_FWD)) {
     if ((EPI != EPI_STORE || g.norm_out) && (lane & 15) == 0) {
       GAS float* dst = GW(g.norm_out) + (size_t)jt * g.norm_ld + ib;
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) dst[qq] = rs01[qq] + rs23[qq];
+      for (int qq = 0; qq < 4; ++qq) dst[qq] = NBW == 4 ? rsa[qq] + rsb[qq] : rsa[qq];
     }
   }
   if constexpr (EPI == EPI_QHEAD || EPI == EPI_MSE) {
     if (lane == 0) {
       const int t16 = (i0 >> 4) * tiles_n + jt;  // (the 16-row tile's row-major index: the partial count is unchanged)
-      float v = ls01 + ls23;
+      float v = NBW == 4 ? lsa + lsb : lsa;
       if constexpr (EPI == EPI_QHEAD) v = t16 == 0 ? v + (float)g.M * sload(g.qb) : v;
       GW(g.loss_part)[t16] = v;
     }
   }
 }
 
-// EXT: the extended instance of rle_level (register-blocked weight-gradient tiles, 32-row tiles); the
-// production instance compiles without them, so their registers do not shape its allocation
+// EXT: the register-blocked weight-gradient tiles are compiled in (the extended and the KS_TD7W instances); the
+// production instances compile without them, so their registers do not shape their allocation
 // WIDE: the variant also runs 64-row LDS-staged tiles (GemmHot::wide, gemm_wide; the KS_TD7W and extended instances)
 template <int MODE, int EPI, int ACT, bool NORM, int PK = 0, bool EXT = false, bool WIDE = false>  // PK: 1 pre-GEMM, 2 fused loss head, 3 pre-layer, 4 pre-layer behind a pre-GEMM, 5 SAC raw head + rsample pre-GEMM
 __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem, unsigned long long* tr) {
@@ -1394,10 +1484,15 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
   const float* b0p = ptr(h1[0], h1[1]);
   const float* biasp = ptr(h1[2], h1[3]);
   if constexpr (WIDE) {
-    if (h1[11]) {
-      gemm_wide<MODE, EPI, ACT, NORM>(g, t, smem, tr, tiles_n, gN, gR, inv_tn, nseg_a, nseg_b, (int)h0[13], (int)h1[4],
-                                      (int)h1[5], (int)h1[9], __uint_as_float(h1[6]), __uint_as_float(h1[7]),
-                                      __uint_as_float(h1[8]), biasp);
+    if (h1[11]) {  // (GemmHot::wide: 64 -> 64-column tiles, 32 -> 32-column tiles)
+      if (h1[11] == 64)
+        gemm_wide<MODE, EPI, ACT, NORM, 4>(g, t, smem, tr, tiles_n, gN, gR, inv_tn, nseg_a, nseg_b, (int)h0[13],
+                                           (int)h1[4], (int)h1[5], (int)h1[9], __uint_as_float(h1[6]),
+                                           __uint_as_float(h1[7]), __uint_as_float(h1[8]), biasp);
+      else
+        gemm_wide<MODE, EPI, ACT, NORM, 2>(g, t, smem, tr, tiles_n, gN, gR, inv_tn, nseg_a, nseg_b, (int)h0[13],
+                                           (int)h1[4], (int)h1[5], (int)h1[9], __uint_as_float(h1[6]),
+                                           __uint_as_float(h1[7]), __uint_as_float(h1[8]), biasp);
       return;
     }
   }
@@ -2056,7 +2151,7 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
   case gemm_vid(mode, epi, act, norm, pre):                                                               \
     if constexpr (KS == KS_EXT || (((sets) >> ks_family(KS)) & 1)) {                                     \
       asm volatile("; gemm variant " #mode " " #epi " " #act " norm " #norm " pk " #pk ::);               \
-      gemm_v<mode, epi, act, (norm) != 0 && (pk) <= 3, pk, KS == KS_EXT,                                  \
+      gemm_v<mode, epi, act, (norm) != 0 && (pk) <= 3, pk, KS == KS_EXT || KS == KS_TD7W,                 \
              (KS == KS_TD7W || KS == KS_EXT) && wide_variant(mode, epi, pk)>(g, t, smem, tr);             \
     }                                                                                                     \
     break;
@@ -3002,8 +3097,8 @@ __global__ __launch_bounds__(kThreads, RLE_WAVES) void rle_level(unsigned e0, un
                                                                   unsigned e8, unsigned e9, unsigned e10, unsigned e11,
                                                                   const Op* ops_arg, unsigned long long* trace_arg,
                                                                   const Op* next_arg, unsigned next_lines) {
-  // 24 KB (the wide instances: the 32 KB LDS ring of gemm_wide)
-  constexpr int kSmemF = (KS == KS_TD7W || KS == KS_EXT) && kWideSmem > 6144 ? kWideSmem : 6144;
+  // 24 KB (the wide instances: the 40 KB LDS ring of gemm_wide)
+  constexpr int kSmemF = (KS == KS_TD7W || KS == KS_EXT) && kWideSmem > 6144 ? kWideSmem : 6144;  // (40 KB)
   static_assert(kSmemF >= kRbOff + 4096, "LDS for the register-blocked exchange");
   __shared__ __attribute__((aligned(16))) float smem[kSmemF];
   // op of this workgroup from the (preloaded) entry table: straight-line selects over SGPRs

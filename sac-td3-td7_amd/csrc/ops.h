@@ -227,8 +227,8 @@ struct GemmHot {
   // groups x splits
   int rb;
   // 64-row LDS-staged tile (rle_plan wide; the TD7 instance at B >= 512, kernels.hip gemm_wide): the
-  // workgroup's 4 waves own 16 rows each of a 64 x 64 output tile, every W chunk staged once in LDS for all
-  // four; tiles counts 64-row tiles, GemmArgs::tiles_m 16-row blocks
+  // workgroup's 4 waves own 16 rows each of a 64 x wide output tile (wide = tn: 64 or 32), every W chunk staged
+  // once in LDS for all four; tiles counts 64-row tiles, GemmArgs::tiles_m 16-row blocks; 0: 16-row tiles
   int wide;
   int pad_[4];
 };

@@ -666,8 +666,8 @@ def test_wide_tiles_bitwise_equal_16_row_tiles(B):
     graph + 1) end with bit-identical parameters, indices and priorities.  (The loss values may differ in the
     last bits: the 16-row tiles write their MSE / q-head loss partials in XCD tile order, the wide tiles in row
     order, and only the info row sums them.)"""
-    e1, r1, i1, p1 = _wide_run(B, 8, E.make_plan(tn_min=64, wide=1))
-    e0, r0, i0, p0 = _wide_run(B, 8, E.make_plan(tn_min=64, wide=0))
+    e1, r1, i1, p1 = _wide_run(B, 8, E.make_plan(tn_min=64, wide=1, rb=1))
+    e0, r0, i0, p0 = _wide_run(B, 8, E.make_plan(tn_min=64, wide=0, rb=1))
     assert ".w]" in e1.describe(0) and ".w]" not in e0.describe(0)
     np.testing.assert_array_equal(e1.last_indices(), e0.last_indices())
     np.testing.assert_array_equal(r1.get_priority(), r0.get_priority())
