@@ -74,6 +74,8 @@ typedef struct rle_config {
                                         action) recomputed in-tile by their second layer             */
 #define RLE_FUSE_SACPRE   (1u << 12) /* SAC raw head + target rsample recomputed in-tile by the target
                                         critics' first layer                                         */
+#define RLE_FUSE_NORMFIN  (1u << 13) /* TD7: the AvgL1Norm row means finalized once (a small op the level after
+                                        their producer) for the weight gradients' per-row tables      */
 #define RLE_FUSE_OPT_IN RLE_FUSE_PRIOSAMPLE  /* fusions off unless set in fuse_on                      */
 typedef struct rle_plan {
   int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity; TD3 7/8, TD7 at B >= 1024 3/2) */

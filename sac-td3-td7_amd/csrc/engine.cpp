@@ -799,6 +799,11 @@ static void op_accesses(const Op& op, std::vector<Access>& v) {
     }
     case OP_NORMBWD: {
       const NormBwdArgs& a = op.nb;
+      if (a.fwd == 2) {  // finalize: partials in, one mean per row out
+        acc_whole(v, a.norm.part, 0, "nb norm");
+        acc_bytes(v, a.mout, (long long)a.rows * 4, 1, "nb mean");
+        break;
+      }
       acc_mat(v, a.g, 0, "nb g");
       acc_mat(v, a.x, 0, "nb x");
       acc_whole(v, a.norm.part, 0, "nb norm");
@@ -1087,6 +1092,8 @@ struct Prog {
   static constexpr int max_ops = kLevelOps;
   // register-blocked wide weight-gradient tiles (rle_plan rb)
   int rb = 0;
+  // (Engine::norm_fin) the finalized AvgL1Norm row means of this program: producer partials -> (means, resource)
+  std::map<const float*, std::pair<float*, int>> norm_fins;
   static bool rb_eligible(const GemmArgs& g) {
     bool seg_ok = true;  // (the tile's column blocks lie in one X segment, kernels.hip rb path)
     for (int q = 0; q < g.B.nseg; ++q) seg_ok = seg_ok && g.B.seg[q].x0 % g.tn == 0;
@@ -2489,7 +2496,13 @@ struct Engine {
       const View& v = X[s];
       REQUIRE(v.cols == L.seg_p[s] && v.rows >= Brows && v.m.t, "dw: input view mismatch for " + L.wname);
       g.B.seg[s] = seg_t(v, koff, 0, Brows);
-      if (v.norm) rd.push_back(v.norm_id);
+      if (v.norm && fused(RLE_FUSE_NORMFIN)) {  // (the finalized row means, norm_fin)
+        const auto f = norm_fin(pg, v);
+        g.B.seg[s].norm = f.first;
+        rd.push_back(f.second);
+      } else if (v.norm) {
+        rd.push_back(v.norm_id);
+      }
       rd.push_back(v.id);
       koff += L.seg_p[s];
     }
@@ -2530,7 +2543,14 @@ struct Engine {
       g.nbdot_ld = dz.nbdot_ld;
       g.nbdot_n = dz.nbdot_n;
       rd.push_back(nb_x->id);
-      rd.push_back(nb_x->norm_id);
+      if (fused(RLE_FUSE_NORMFIN)) {  // (the finalized row means, norm_fin; x's width for the sign term)
+        const auto f = norm_fin(pg, *nb_x);
+        g.nbm = f.first;
+        g.nb_width = nb_x->width;
+        rd.push_back(f.second);
+      } else {
+        rd.push_back(nb_x->norm_id);
+      }
       rd.push_back(dz.nbdot_id);
     }
     op.wg_count = g.tiles_m * g.tiles_n;
@@ -2542,6 +2562,42 @@ struct Engine {
   float adam_ptau = 0.f;
   // (plan without RLE_FUSE_PIPOLYAK: the standalone OP_POLYAK over the policy instead, tests, A/B)
   bool pi_polyak_fused() const { return fused(RLE_FUSE_PIPOLYAK); }
+
+  // The AvgL1Norm means of a normed view's rows (sale.py:11-13: mean |x| before the 1e-8 clamp), computed once
+  // from its producer's partials by a finalize op (OP_NORMBWD fwd 2, the level after the producer), for the
+  // weight gradients: their tables cover every batch row and would otherwise sum every row's partials in every
+  // workgroup (B = 1024: 4 rows per thread, 16 partials each, 3-7 us per workgroup).  Returned as a one-partial
+  // NormRef of width 1 (the consumer's sum / 1 and clamp are the same floats) and its resource id; one op per
+  // producer output per program.
+  std::pair<NormRef, int> norm_fin(Prog& pg, const View& v) {
+    REQUIRE(v.norm && v.norm_ld > 0, "norm_fin: not a normed view");
+    auto it = pg.norm_fins.find(v.norm);
+    if (it == pg.norm_fins.end()) {
+      Op op{};
+      op.kind = OP_NORMBWD;
+      NormBwdArgs& a = op.nb;
+      a.fwd = 2;
+      a.rows = v.norm_ld;  // (the producer's rows: partials are [nparts][norm_ld])
+      a.width = v.width;
+      a.norm.part = v.norm;
+      a.norm.ld = v.norm_ld;
+      a.norm.row0 = 0;
+      a.norm.nparts = v.nparts;
+      a.norm.width = v.width;
+      a.mout = mem.make<float>((size_t)v.norm_ld);
+      op.wg_count = cdiv(v.norm_ld, kThreads);
+      const int id = next_id++;
+      pg.add(op, {v.norm_id}, {id});
+      it = pg.norm_fins.emplace(v.norm, std::make_pair(a.mout, id)).first;
+    }
+    NormRef r{};
+    r.part = it->second.first;
+    r.ld = v.norm_ld;
+    r.row0 = v.norm_row0;
+    r.nparts = 1;
+    r.width = 1;
+    return {r, it->second.second};
+  }
 
   View normbwd(Prog& pg, const View& gv, const View& x) {
     REQUIRE(x.norm, "normbwd: x is not a normed view");

@@ -251,7 +251,11 @@ __device__ __forceinline__ void norm_tab_batched(const CAS NormRef& nr, int n, f
   }
 }
 __device__ __forceinline__ void build_norm_tab(const CAS NormRef& nr, int n, float* dst) {
-  if (n <= kThreads && nr.nparts <= 16) {
+  if (n <= kThreads && nr.nparts == 1) {  // (finalized means, engine.cpp norm_fin)
+    norm_tab_batched<1, 1>(nr, n, dst);
+  } else if (n <= 4 * kThreads && nr.nparts == 1) {
+    norm_tab_batched<4, 1>(nr, n, dst);
+  } else if (n <= kThreads && nr.nparts <= 16) {
     norm_tab_batched<1, 16>(nr, n, dst);
   } else if (n <= 4 * kThreads && nr.nparts <= 8) {
     norm_tab_batched<4, 8>(nr, n, dst);
@@ -499,11 +503,12 @@ __device__ __forceinline__ f32x4 ring_run_nb(float4 (&a)[RG], float4 (&x)[RG], f
 
 // kDwNb tables for the n reduction rows: 1/m and the sign coefficient
 // gm = -(sum_j g x) / (n_x m^2) (0 when m is clamped), exactly as op_normbwd.
-template <int RPT, int PMAX>
-__device__ __forceinline__ void nb_tab_batched(const CAS GemmArgs& g, int n, float* ti, float* tg) {
+// (rows r0 .. r0 + n - 1 into ti / tg [0, n); PM / PD: the mean's and the dot's partial bounds)
+template <int RPT, int PM, int PD>
+__device__ __forceinline__ void nb_tab_batched(const CAS GemmArgs& g, int n, float* ti, float* tg, float xw, int r0 = 0) {
   float sm[RPT], sd[RPT];
-  row_sums<RPT, PMAX>(g.nbm.part, g.nbm.ld, g.nbm.row0, g.nbm.nparts, n, sm);
-  row_sums<RPT, PMAX>(g.nbdot, g.nbdot_ld, 0, g.nbdot_n, n, sd);
+  row_sums<RPT, PM>(g.nbm.part, g.nbm.ld, g.nbm.row0 + r0, g.nbm.nparts, n, sm);
+  row_sums<RPT, PD>(g.nbdot, g.nbdot_ld, r0, g.nbdot_n, n, sd);
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
     const int i = threadIdx.x + r * kThreads;
@@ -512,17 +517,29 @@ __device__ __forceinline__ void nb_tab_batched(const CAS GemmArgs& g, int n, flo
     const float inv = 1.f / (clamped ? 1e-8f : mean);
     if (i < n) {
       ti[i] = inv;
-      tg[i] = clamped ? 0.f : (-dot * inv * inv) / (float)g.nbm.width;
+      tg[i] = clamped ? 0.f : (-dot * inv * inv) / xw;
     }
   }
 }
 __device__ __forceinline__ void build_nb_tab(const CAS GemmArgs& g, int n, float* ti, float* tg) {
-  if (n <= kThreads && g.nbm.nparts <= 16 && g.nbdot_n <= 16) {
-    nb_tab_batched<1, 16>(g, n, ti, tg);
+  // (x's width: the mean may come finalized, engine.cpp norm_fin, as one partial of width 1)
+  const float xw = (float)(g.nb_width ? g.nb_width : g.nbm.width);
+  const int pm = g.nbm.nparts, pd = g.nbdot_n;
+  if (n <= kThreads && pm <= 16 && pd <= 16) {
+    nb_tab_batched<1, 16, 16>(g, n, ti, tg, xw);
     return;
   }
-  if (n <= 4 * kThreads && g.nbm.nparts <= 4 && g.nbdot_n <= 4) {
-    nb_tab_batched<4, 4>(g, n, ti, tg);
+  if (n <= 4 * kThreads && pm == 1 && pd <= 8) {
+    nb_tab_batched<4, 1, 8>(g, n, ti, tg, xw);
+    return;
+  }
+  if (n <= 4 * kThreads && pm <= 4 && pd <= 4) {
+    nb_tab_batched<4, 4, 4>(g, n, ti, tg, xw);
+    return;
+  }
+  if (n <= 4 * kThreads && pm == 1 && pd <= 16) {  // (two rows per thread per round trip)
+    nb_tab_batched<2, 1, 16>(g, min(n, 2 * kThreads), ti, tg, xw);
+    if (n > 2 * kThreads) nb_tab_batched<2, 1, 16>(g, n - 2 * kThreads, ti + 2 * kThreads, tg + 2 * kThreads, xw, 2 * kThreads);
     return;
   }
 #pragma unroll 1
@@ -532,7 +549,7 @@ __device__ __forceinline__ void build_nb_tab(const CAS GemmArgs& g, int n, float
     const bool clamped = mean < 1e-8f;
     const float inv = 1.f / (clamped ? 1e-8f : mean);
     ti[i] = inv;
-    tg[i] = clamped ? 0.f : (-dot * inv * inv) / (float)g.nbm.width;
+    tg[i] = clamped ? 0.f : (-dot * inv * inv) / xw;
   }
 }
 
@@ -2167,6 +2184,11 @@ __device__ __forceinline__ void op_gemm(const CAS GemmArgs& g, int vid, int t, f
 // One row per wave (4 per workgroup): lane l holds columns 4l..4l+3 (+256 per
 // pass) as float4s of the N images; the row dot product is one wave reduction.
 __device__ __forceinline__ void op_normbwd(const CAS NormBwdArgs& a, int t) {
+  if (a.fwd == 2) {  // finalize (NormBwdArgs::mout): the mean of each row's partials, one thread per row
+    const int row = t * kThreads + (int)threadIdx.x;
+    if (row < a.rows) GW(a.mout)[row] = norm_mean_i(a.norm.part, a.norm.ld, row + a.norm.row0, a.norm.nparts, a.width);
+    return;
+  }
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int row = t * 4 + wave;
   if (row >= a.rows) return;

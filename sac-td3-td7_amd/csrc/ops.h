@@ -379,7 +379,10 @@ struct GemmArgs {
     SacBwdArgs sb;  // EPI_SACBWD (has_pre 0)
     SacFwdArgs sf;  // EPI_SACFWD (has_pre 0)
   };
-  int head_n;
+  union {
+    int head_n;    // has_pre 2: the critic whose DX this is
+    int nb_width;  // kDwNb with nbm finalized (nparts 1, width 1; engine.cpp norm_fin): x's width for the sign term
+  };
   AdamArgs adam;
   ActArgs ao;                      // EPI_ACT
   // has_pre 4 (TD3 target critics, engine.cpp mlp_critic_fwd): the pre-layer prea's input segment
@@ -392,11 +395,14 @@ struct GemmArgs {
 // AvgL1Norm backward: dx = (g - sign(x) * (sum g*y)/n) / m, y = x/m (row-wise);
 // 4 rows per workgroup (1 per wave), N images in, N + T images out.
 // fwd = 1: the forward itself, dx = x / m (g = x; diagnostics: rle_eval's zs output).
+// fwd = 2 (finalize): mout[row] = mean |x| of the row (norm_mean of its partials, before the 1e-8 clamp), one
+// thread per row -- read by the weight gradients as a one-partial NormRef of width 1, the same floats
 struct NormBwdArgs {
   Mat g, x, dx;
   int rows, width;
   NormRef norm;  // partials for m (x rows)
   int fwd, pad_;
+  float* mout;
 };
 
 

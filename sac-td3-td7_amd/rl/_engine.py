@@ -58,7 +58,7 @@ class Plan(ctypes.Structure):
 # RLE_FUSE_* bits of rle_plan.fuse_off
 FUSE = {"prelayer": 1 << 0, "pre": 1 << 1, "qdot": 1 << 2, "headdx": 1 << 3, "nbdefer": 1 << 4, "sacfwd": 1 << 5,
         "sacbwd": 1 << 6, "fold": 1 << 7, "pipolyak": 1 << 8, "endsplit": 1 << 9, "priosample": 1 << 10,
-        "twostage": 1 << 11, "sacpre": 1 << 12}
+        "twostage": 1 << 11, "sacpre": 1 << 12, "normfin": 1 << 13}
 
 
 def make_plan(fuse_off=(), fuse_on=(), **kw) -> Plan:

@@ -574,17 +574,13 @@ def _alg_dims(g):
     return (alg, *spec.TASKS[env][:2], H, 0)
 
 
-def test_bench_program_1m_lap_replay_matches_oracle():
-    """The exact bench program (bench.py's default line): TD7 Humanoid B=256, LAP over a 1,000,000-row
-    replay (245 priority blocks of 4096 in the sampler's block-sum scan), 13 steps = 1 single step + two
-    6-step graphs with the default plan, against the oracle stepped one taped step at a time on the same
-    draws.  Rows are a 4096-row pattern repeated over the replay (bench.py's fill shape, small host
-    memory); the priorities are distinct over all 1M rows.  Indices bit-exact, every priority of the 1M
-    rows (which records every index drawn) at rtol 1e-4, parameters at the module's bulk criterion."""
+def _bench_program_run(n=13, plan=None):
+    """TD7 Humanoid B=256, LAP over a 1,000,000-row replay, n taped steps on the engine (one burst, default plan)
+    and on the oracle: (eng, rep, infos, orc, orep, infos_ref, inds, launches)."""
     from oracle import agents, replay
 
     S, A, hi = spec.TASKS["Humanoid-v4"]
-    N, blk, n, B, H, seed = 1_000_000, 4096, 13, 256, 256, 93
+    N, blk, B, H, seed = 1_000_000, 4096, 256, 256, 93
     data = spec.replay_data(S, A, blk, seed + 1, hi)
     scale = np.full(A, hi, np.float32)
     scale = (scale - (-scale)) / 2.0
@@ -594,7 +590,7 @@ def test_bench_program_1m_lap_replay_matches_oracle():
     p0 = spec.init_priorities(N, seed + 2)
     # engine side: the pattern appended in 64K-row chunks (the replay stores the normalised action)
     cfg = E.make_config(E.RLE_TD7, S, A, H, B, use_lap=True, seed=seed)
-    eng = E.Engine(cfg)
+    eng = E.Engine(cfg, plan)
     nets = spec.agent_params("td7", S, A, H, seed)
     for net, params in nets.items():
         for name, v in params.items():
@@ -624,7 +620,14 @@ def test_bench_program_1m_lap_replay_matches_oracle():
     orep.size, orep.ptr = N, 0
     tp = spec.tapes("td7", B, A, n, seed + 3)
     infos_ref, inds = [], []
+    amb = {"q1": set(), "q2": set()}  # q01 outputs whose sign fp32 rounding decides (see the test)
     for t in range(n):
+        ind = orep.sample_indices(tp["u"][t][:B])
+        sa = np.concatenate([orep.state[ind], orep.action[ind]], 1).astype(np.float64)
+        for qn, qp in (("q1", orc.q1), ("q2", orc.q2)):
+            w, b = qp["q01.weight"].detach().numpy(), qp["q01.bias"].detach().numpy()
+            x = sa @ w.T.astype(np.float64) + b
+            amb[qn].update(np.nonzero((np.abs(x) < 1e-5).any(0))[0].tolist())
         i1, n1 = agents.run_steps(orc, "td7", orep, {k: v[t:t + 1] for k, v in tp.items()}, 1, B)
         infos_ref += i1
         inds += n1
@@ -632,8 +635,25 @@ def test_bench_program_1m_lap_replay_matches_oracle():
     eng.set_tapes(u=tp["u"], eps=tp["eps"])
     infos = np.array(eng.step(n))
     eng.set_tapes()
+    return eng, rep, infos, orc, orep, infos_ref, inds, eng.launch_count() - launches0, amb
+
+
+def test_bench_program_1m_lap_replay_matches_oracle():
+    """The exact bench program (bench.py's default line): TD7 Humanoid B=256, LAP over a 1,000,000-row
+    replay (245 priority blocks of 4096 in the sampler's block-sum scan), 13 steps = 1 single step + two
+    6-step graphs with the default plan, against the oracle stepped one taped step at a time on the same
+    draws.  Rows are a 4096-row pattern repeated over the replay (bench.py's fill shape, small host
+    memory); the priorities are distinct over all 1M rows.  Indices bit-exact, every priority of the 1M
+    rows (which records every index drawn) at rtol 1e-4, parameters at the module's bulk criterion.
+    One exclusion, measured (tools/diag_bench1m.py): a critic's first-layer output x = q01([s, a]) that lies
+    within fp32 rounding of zero (|x| < 1e-5; step 1 here has x = 2.0e-7 in q1's unit 55) gets its sign --
+    which the AvgL1Norm backward's d|x|/dx = sign(x) uses -- from the summation order, so that unit's row of
+    the q01 weight gradient differs from torch's (step-1 gradients elsewhere agree to < 1e-6 of each tensor's
+    max), and the rows of such units are left out of the q01 bulk fraction (their max bound still holds)."""
+    n, N = 13, 1_000_000
+    eng, rep, infos, orc, orep, infos_ref, inds, launches, amb = _bench_program_run(n)
     lp, lpl = eng.graph_stats()
-    assert eng.launch_count() - launches0 < (n // 2) * (lp + lpl), "no multi-step graph ran"
+    assert launches < (n // 2) * (lp + lpl), "no multi-step graph ran"
     np.testing.assert_array_equal(eng.last_indices(), inds[-1])
     keys = ["train/encoder", "train/q_fn", "train/policy"]
     ref = np.array([[np.nan if i[k] is None else i[k] for k in keys] for i in infos_ref], np.float64)
@@ -644,7 +664,12 @@ def test_bench_program_1m_lap_replay_matches_oracle():
     tol = 2 * 3e-4 * n + 1e-4
     for net, d in orc.nets().items():
         for name, v in d.items():
-            assert_params_close(eng.get_param(net, name, tuple(v.shape)), v.detach().numpy(), tol, (net, name))
+            got, ref = eng.get_param(net, name, tuple(v.shape)), v.detach().numpy()
+            if net in amb and name.startswith("q01.") and amb[net]:
+                keep = np.setdiff1d(np.arange(ref.shape[0]), sorted(amb[net]))
+                assert_params_close(got, ref, tol, (net, name), bulk=0.0)
+                got, ref = got[keep], ref[keep]
+            assert_params_close(got, ref, tol, (net, name))
 
 
 def _wide_run(B, n, plan, env="Humanoid-v4"):
