@@ -37,7 +37,7 @@ typedef struct rle_engine rle_engine;
 typedef struct rle_config {
   int algo;                 /* RLE_TD7 / RLE_TD3 / RLE_SAC */
   int state_dim, action_dim;
-  int hidden;               /* hidden width (TD7: hdim = zs_dim) */
+  int hidden;               /* hidden width (TD7: hdim; TD3/SAC: every hidden layer unless n_hidden is set) */
   int batch;                /* B (multiple of 16, <= 1024) */
   int use_lap;              /* TD7/TD3: LAP Huber + priority update */
   float discount;           /* td7.py:37 / td3.py:36 / sac.py:30 */
@@ -50,7 +50,13 @@ typedef struct rle_config {
   float tmp;                /* SAC: < 0 => auto temperature (sac.py:36,55) */
   unsigned long long seed;  /* Philox stream for sampling / noise */
   int device;
+  /* Net shapes beyond the defaults (make_nn, td7.py:46-61 / td3.py:44-58 / sac.py:40-52): */
+  int zs_dim;               /* TD7: SALE embedding width (sale.py:23 zs_dim); 0 = hidden.  `hidden` is hdim */
+  int n_hidden;             /* TD3/SAC: hidden layers of make_mlp (mlp.py:10-35), 2..RLE_MAX_HIDDEN; 0 = two
+                               layers of `hidden` (mlp.py:45-47) */
+  int hidden_sizes[8];      /* TD3/SAC: their widths, input side first (each a multiple of 4, <= 512) */
 } rle_config;
+#define RLE_MAX_HIDDEN 6
 
 /* Step-program plan: the schedule and tile-plan choices that decide how the step's reductions are
  * split (so its fp32 summation order) and how its ops are fused.  Every engine starts from the

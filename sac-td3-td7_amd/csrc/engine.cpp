@@ -219,9 +219,8 @@ struct Replay {
   // enqueued step: replay operations on `stream` wait for them first (an append after
   // rle_step_async must not race the step's priority scatter and block sums)
   std::vector<std::pair<Engine*, hipEvent_t>> users;
-  void wait_users() {
-    for (auto& u : users) HIPCHK(hipStreamWaitEvent(stream, u.second, 0));
-  }
+  void wait_users();   // (after Engine: also drains the users' direct-dispatch bursts)
+  void drain_users();  // the users' rle_step_async bursts on their own queues retired (host wait)
 };
 
 // ------------------------------------------------------------------ programs
@@ -1308,6 +1307,8 @@ struct AqlQueue {
   std::vector<Pending> pending;
   double us_per_launch = 10.0;  // measured mean dispatch-to-completion time per packet (EWMA over flushes)
   bool failed = false;          // a flush timed out: its packets may still be queued, the queue takes no more
+  size_t inflight = 0;          // packets submitted since the last aql_complete
+  std::chrono::steady_clock::time_point t0{};  // first doorbell of the oldest burst in flight
   ~AqlQueue() {
     if (q) (void)hsa_queue_destroy(q);
     if (sig.handle) (void)hsa_signal_destroy(sig);
@@ -1374,7 +1375,7 @@ static std::unique_ptr<AqlQueue> aql_open(int dev) {
   HSACHK(hsa_agent_get_info(A->agent, HSA_AGENT_INFO_QUEUE_MAX_SIZE, &qmax));
   HSACHK(hsa_queue_create(A->agent, std::min<uint32_t>(qmax, 16384), HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
                           UINT32_MAX, UINT32_MAX, &A->q));
-  HSACHK(hsa_signal_create(1, 0, nullptr, &A->sig));
+  HSACHK(hsa_signal_create(0, 0, nullptr, &A->sig));  // (bursts in flight: aql_submit)
   auto scope = [](const char* v, int d) { return v ? std::max(0, std::min(2, std::atoi(v))) : d; };
   A->acq = scope(std::getenv("RLE_AQL_ACQ"), HSA_FENCE_SCOPE_AGENT);
   A->rel = scope(std::getenv("RLE_AQL_REL"), HSA_FENCE_SCOPE_AGENT);
@@ -1413,19 +1414,19 @@ static void aql_wait(AqlQueue& A, Pred pred, double expected_us, const char* wha
   }
 }
 
-// Writes every pending packet, rings the doorbell and waits for the last (host-side wall time
-// from the first doorbell to completion into *ms when given).
-static void aql_flush(AqlQueue& A, double* ms) {
+// Writes every pending packet and rings the doorbell; the completion signal counts the submitted bursts
+// still in flight (each burst's last packet decrements it), so bursts may be submitted back to back
+// (rle_step_async) and aql_complete waits for all of them.
+static void aql_submit(AqlQueue& A) {
   const size_t n = A.pending.size();
   if (!n) return;
   if (A.failed) {
     A.pending.clear();
     throw Error{RLE_EHIP, "aql: the engine's queue is closed after a timed-out dispatch"};
   }
-  hsa_signal_store_relaxed(A.sig, 1);
+  hsa_signal_add_relaxed(A.sig, 1);
   hsa_queue_t* q = A.q;
   const uint64_t mask = q->size - 1;
-  std::chrono::steady_clock::time_point t0{};
   bool rung = false;
   for (size_t i = 0; i < n; ++i) {
     const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
@@ -1459,19 +1460,29 @@ static void aql_flush(AqlQueue& A, double* ms) {
     __atomic_store_n((uint32_t*)pk, (uint32_t)hdr | (1u << 16), __ATOMIC_RELEASE);  // header | setup (1 dim)
     if (last || (i & 63) == 63) {
       hsa_signal_store_screlease(q->doorbell_signal, idx);
-      if (!rung) {
-        t0 = std::chrono::steady_clock::now();
-        rung = true;
-      }
+      if (!A.inflight && !rung) A.t0 = std::chrono::steady_clock::now();
+      rung = true;
     }
   }
+  A.inflight += n;
   A.pending.clear();
-  // (the packets not yet retired when the last one was written: those behind the read index)
+}
+// Waits until every submitted burst has retired (host-side wall time from the first doorbell of the
+// oldest burst in flight to completion added to *ms when given).
+static void aql_complete(AqlQueue& A, double* ms) {
+  if (!A.inflight) return;
+  hsa_queue_t* q = A.q;
+  // (the packets not yet retired: those behind the read index)
   const double left = (double)(hsa_queue_load_write_index_relaxed(q) - hsa_queue_load_read_index_scacquire(q));
   aql_wait(A, [&] { return hsa_signal_load_scacquire(A.sig) < 1; }, left * A.us_per_launch, "a dispatch");
-  const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (n >= 8) A.us_per_launch = 0.5 * A.us_per_launch + 0.5 * (wall_ms * 1e3 / (double)n);
+  const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - A.t0).count();
+  if (A.inflight >= 8) A.us_per_launch = 0.5 * A.us_per_launch + 0.5 * (wall_ms * 1e3 / (double)A.inflight);
+  A.inflight = 0;
   if (ms) *ms += wall_ms;
+}
+static void aql_flush(AqlQueue& A, double* ms) {
+  aql_submit(A);
+  aql_complete(A, ms);
 }
 
 struct Graph {
@@ -1582,6 +1593,8 @@ struct Engine {
     plan.wide = plan.wide == 32 || plan.wide == 0 ? plan.wide : 64;  // (the tile width; 1 = 64)
   }
   int S, Sp, A, Ap, H, Hp, B;
+  int Z = 0, Zp = 0;    // TD7: SALE embedding width zs_dim (sale.py:23), padded
+  std::vector<int> HS;  // TD3 / SAC: hidden widths of make_mlp (mlp.py:10-35), input side first
   int algo;
   hipStream_t stream = nullptr;
   DevMem mem;
@@ -1599,6 +1612,7 @@ struct Engine {
   // step); g_pol[p] / g_pln[p] run a (policy / plain) step on batch p and, once its
   // priority update is done, prefetch the next step's batch into 1 - p.
   Graph g_prime[2], g_pol[2], g_pln[2], g_hard;
+  Graph g_slot0;  // info slot := 0 as a level of its own (rle_step_async bursts on the AQL queue)
   // g_pair[p]: multi_k consecutive steps as ONE program, starting on batch p (policy,
   // plain, policy, ... with policy_freq 2; SAC: every step), so the scheduler overlaps
   // each step's early levels (encoder phase, fixed encoders, online critic forward) with
@@ -1704,9 +1718,9 @@ struct Engine {
       ok &= layer(pi.layers[3], ACT_TANH, 6, -1, 0, 7, 0);
     } else {  // mlp.py:55-68
       Net& pi = net("policy");
-      ok &= layer(pi.layers[0], ACT_RELU, 0, -1, 0, 1, 1);
-      ok &= layer(pi.layers[1], ACT_RELU, 1, -1, 0, 2, 1);
-      ok &= layer(pi.layers[2], algo == RLE_SAC ? ACT_NONE : ACT_TANH, 2, -1, 0, 7, 0);
+      const int D = (int)HS.size();  // (hidden layer i -> slot i + 1; the output -> slot 7)
+      for (int i = 0; i < D; ++i) ok &= layer(pi.layers[i], ACT_RELU, i, -1, 0, i + 1, 1);
+      ok &= layer(pi.layers[D], algo == RLE_SAC ? ACT_NONE : ACT_TANH, D, -1, 0, 7, 0);
       c.sac = algo == RLE_SAC;
     }
     c.nwg = 1;
@@ -1766,31 +1780,33 @@ struct Engine {
     n.name = name;
     n.kind = kind;
     n.res = next_id++;
-    if (kind == "sale_enc") {  // rl/nn/sale.py:16-55
+    if (kind == "sale_enc") {  // rl/nn/sale.py:16-55 (zs_dim Z, hdim H)
       add_layer(n, "zs1", H, {S});
       add_layer(n, "zs2", H, {H});
-      add_layer(n, "zs3", H, {H});
-      add_layer(n, "zsa1", H, {H, A});
+      add_layer(n, "zs3", Z, {H});
+      add_layer(n, "zsa1", H, {Z, A});
       add_layer(n, "zsa2", H, {H});
-      add_layer(n, "zsa3", H, {H});
+      add_layer(n, "zsa3", Z, {H});
     } else if (kind == "sale_actor") {  // sale.py:58-83
       add_layer(n, "l0", H, {S});
-      add_layer(n, "l1", H, {H, H});
+      add_layer(n, "l1", H, {H, Z});
       add_layer(n, "l2", H, {H});
       add_layer(n, "l3", A, {H});
     } else if (kind == "sale_critic") {  // sale.py:86-121
       add_layer(n, "q01", H, {S, A});
-      add_layer(n, "q1", H, {H, H, H});
+      add_layer(n, "q1", H, {H, Z, Z});
       add_layer(n, "q2", H, {H});
       add_layer(n, "q3", 1, {H});
-    } else if (kind == "mlp_actor") {  // mlp.py:38-55
-      add_layer(n, "mlp.0", H, {S});
-      add_layer(n, "mlp.2", H, {H});
-      add_layer(n, "mlp.4", algo == RLE_SAC ? 2 * A : A, {H});
-    } else {  // mlp_critic, mlp.py:75-101
-      add_layer(n, "mlp.0", H, {S, A});
-      add_layer(n, "mlp.2", H, {H});
-      add_layer(n, "mlp.4", 1, {H});
+    } else {  // mlp_actor (mlp.py:38-55) / mlp_critic (mlp.py:75-101): Linear / ReLU pairs, nn.Sequential
+      // indices 0, 2, 4, ... (make_mlp, mlp.py:24-35)
+      const bool actor = kind == "mlp_actor";
+      const int D = (int)HS.size();
+      for (int i = 0; i <= D; ++i) {
+        const int out = i < D ? HS[i] : !actor ? 1 : algo == RLE_SAC ? 2 * A : A;
+        std::vector<int> in{i ? HS[i - 1] : S};
+        if (!i && !actor) in.push_back(A);
+        add_layer(n, "mlp." + std::to_string(2 * i), out, in);
+      }
     }
     return n;
   }
@@ -2650,6 +2666,15 @@ struct Engine {
     return fwd(pg, E.layers[5], {{a2}}, M, ACT_NONE, nullptr, false);
   }
 
+  // make_mlp forward (mlp.py:24-35): ReLU after every hidden layer, `last` after the output layer.
+  View mlp_fwd(Prog& pg, Net& N, const std::vector<std::vector<View>>& in, int M, int last) {
+    View h;
+    for (size_t i = 0; i < N.layers.size(); ++i)
+      h = fwd(pg, N.layers[i], i ? std::vector<std::vector<View>>{{h}} : in, M,
+              i + 1 == N.layers.size() ? last : ACT_RELU, nullptr, false);
+    return h;
+  }
+
   // Host rows [n][w] into every kept image of v (rows past n and columns past w stay zero).
   void upload(const View& v, const float* host, int n, int w) {
     const size_t img = (size_t)v.m.rbs * 16 * v.m.cbn * 16;
@@ -2986,7 +3011,7 @@ struct Engine {
       enc_tiles = g.tiles_m * g.tiles_n;
       enc_loss = mem.make<float>(enc_tiles);
       g.loss_part = enc_loss;
-      g.mse_scale = 1.f / (float)((long long)B * H);
+      g.mse_scale = 1.f / (float)((long long)B * Z);  // (mean over the B x zs_dim zsa, td7.py:253)
       op.wg_count = (wide ? g.tiles_m / 4 : g.tiles_m) * g.tiles_n;
       pg.add(op, {ea2.id, L.res, ezs2.id, ezs2.norm_id}, {ed3.id, loss_id_enc = next_id++});
     }
@@ -2997,7 +3022,7 @@ struct Engine {
       View d1 = dx(pg, {{d2, &enc.layers[4], 0}}, H, B, ACT_ELU, &ea1z);
       dw(pg, enc.layers[4], d2, {ea1}, B, CNT_ADAM_ENC, cfg.policy_lr);
       out_t = false;  // (read by the norm backward only)
-      View gzs = dx(pg, {{d1, &enc.layers[3], 0}}, H, B, ACT_NONE, nullptr);
+      View gzs = dx(pg, {{d1, &enc.layers[3], 0}}, Z, B, ACT_NONE, nullptr);
       out_t = true;
       dw(pg, enc.layers[3], d1, {ezs, act_in}, B, CNT_ADAM_ENC, cfg.policy_lr);
       View dx3 = normbwd(pg, gzs, ex3.sub(0, B));
@@ -3195,7 +3220,7 @@ struct Engine {
         dpa2 = dx(pg, {{dzp1[0], nullptr, 0, &G[0]}, {dzp1[1], nullptr, 0, &G[1]}}, H, B, ACT_ELU, &pa2z);
         out_t = true;
       } else {
-        View gzsa = dx(pg, {{dzp1[0], &q[0]->layers[1], Hp}, {dzp1[1], &q[1]->layers[1], Hp}}, H, B, ACT_NONE,
+        View gzsa = dx(pg, {{dzp1[0], &q[0]->layers[1], Hp}, {dzp1[1], &q[1]->layers[1], Hp}}, Z, B, ACT_NONE,
                        nullptr);
         dpa2 = dx(pg, {{gzsa, &fe.layers[5], 0}}, H, B, ACT_ELU, &pa2z);
       }
@@ -3204,7 +3229,7 @@ struct Engine {
       out_t = true;
       // d action = sum of three paths, then tanh' (actor output)
       const std::vector<DxTerm> t3{
-          {dxp01[0], &q[0]->layers[0], Sp}, {dxp01[1], &q[1]->layers[0], Sp}, {dpa1, &fe.layers[3], Hp}};
+          {dxp01[0], &q[0]->layers[0], Sp}, {dxp01[1], &q[1]->layers[0], Sp}, {dpa1, &fe.layers[3], Zp}};
       View dl3 = dx(pg, t3, A, B, ACT_TANH, &a_pi);
       const PreUse p3 = prea ? pre_actor_dx(t3, A, a_pi, 0) : PreUse{};  // dl2 recomputes dl3 in-tile
       // input-grads through a layer are emitted BEFORE its Adam update so the
@@ -3229,7 +3254,7 @@ struct Engine {
     // ---- step end: info row [encoder, q_fn, policy]
     Op op = step_end_op();
     StepEndArgs& a = op.end;
-    info_sum(a, 0, enc_loss, enc_tiles, 1, 1.f / (float)((long long)B * H));
+    info_sum(a, 0, enc_loss, enc_tiles, 1, 1.f / (float)((long long)B * Z));
     info_sum(a, 1, qloss_part, hw * 4, 1, (lap ? 1.f : 0.5f) / (float)B);
     if (policy) info_sum(a, 2, ploss_part, ploss_n, 1, -0.5f / (float)B);
     else a.kind[2] = INFO_NAN;
@@ -3300,9 +3325,10 @@ struct Engine {
   bool out_n = true;  // (the same for the N image: dx / normbwd outputs only a DW reads)
 
   // Algebraic folds of TD7's linear zsa3 layer into its consumers (build_td7): on when
-  // every block is 16-aligned.  RLE_NO_FOLD=1 keeps the unfolded programs (tests).
+  // every block is 16-aligned and zs_dim = hdim (the folded block replaces the zsa block in place).
+  // Without RLE_FUSE_FOLD: the unfolded programs (tests).
   bool td7_fold() const {
-    return algo == RLE_TD7 && H % 16 == 0 && fused(RLE_FUSE_FOLD);
+    return algo == RLE_TD7 && H % 16 == 0 && Z == H && fused(RLE_FUSE_FOLD);
   }
   // The actor's tanh output layer (N = act_dim <= 32) recomputed in-tile by the consumers on
   // the critical path (PreArgs).  Without RLE_FUSE_PRE: separate ops (tests).
@@ -3388,37 +3414,43 @@ struct Engine {
     pg.add(b, {pid}, {R_MAXP});
   }
 
-  // MLP critic stack forward: returns (h0, h1)
+  // MLP critic stack forward (mlp.py:98-101 over make_mlp's layers): hs[i] = hidden layer i's output
   // qd: the last hidden layer also emits EPI_QDOT row partials of q (a fused head reads them)
   // Behind a pre-GEMM (TD3's target critics: a' computed in-tile from the actor's last hidden layer),
   // the first layer is recomputed in-tile by the second too, its a' segment first (two-stage prologue,
-  // GemmArgs::has_pre 4): the target branch's first layer costs no level of its own.  Without the
-  // fusion it is its own level, in at most 32-wide tiles (pl_src), so both give the same floats.
-  void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, View& h0, View& h1,
-                      const PreUse* pre = nullptr, bool h1_t = true, bool qd = false) {
+  // GemmArgs::has_pre 4, whose epilogue is the q partials: two hidden layers only): the target branch's
+  // first layer costs no level of its own.  Without the fusion it is its own level, in at most 32-wide
+  // tiles (pl_src), so both give the same floats.
+  void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, std::vector<View>& hs,
+                      const PreUse* pre = nullptr, bool last_t = true, bool qd = false) {
+    const int D = (int)Q.layers.size() - 1;
+    hs.assign(D, View{});
     const bool shape = prelayer_shape(Q.layers[0], Q.layers[1]);
     // (the pre-GEMM's a' segment is one column block, kernels.hip PK 4 / gemm_finalize's two-stage REQUIRE)
     const bool two = pre && pre->kind == 1 && pre->a.mode == GEMM_FWD && pre->a.N <= 32 && r16(A) <= 16 && qd &&
-                     prelayer_ok(Q.layers[0], Q.layers[1]) && fused(RLE_FUSE_TWOSTAGE);
+                     D == 2 && prelayer_ok(Q.layers[0], Q.layers[1]) && fused(RLE_FUSE_TWOSTAGE);
     // (not behind a pre-GEMM: the first layer's own a segment is recomputed in-tile already)
     const bool use_pl = !pre && prelayer_ok(Q.layers[0], Q.layers[1]);
     if (two) {
-      h0 = buf(B, Q.layers[0].out, true, false);  // (layout of the consumer's A operand only: never stored)
+      hs[0] = buf(B, Q.layers[0].out, true, false);  // (layout of the consumer's A operand only: never stored)
     } else {
       pl_src = use_pl || (pre && shape);
-      h0 = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pre);
+      hs[0] = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pre);
       pl_src = false;
     }
     const bool keep = out_t;
-    out_t = keep && h1_t;  // (h1_t = false: only the head reads h1, in the N image)
-    PreUse pl = use_pl || two ? pre_layer(Q.layers[0], {sv, av}, two ? pre->a.seg : -1) : PreUse{};
-    if (two) {
-      pl.kind = 4;
-      pl.a2 = pre->a;
-      pl.rd.insert(pl.rd.end(), pre->rd.begin(), pre->rd.end());
+    for (int i = 1; i < D; ++i) {
+      const bool last = i == D - 1;
+      out_t = keep && (!last || last_t);  // (last_t = false: only the head reads the last layer, in the N image)
+      PreUse pl = i == 1 && (use_pl || two) ? pre_layer(Q.layers[0], {sv, av}, two ? pre->a.seg : -1) : PreUse{};
+      if (i == 1 && two) {
+        pl.kind = 4;
+        pl.a2 = pre->a;
+        pl.rd.insert(pl.rd.end(), pre->rd.begin(), pre->rd.end());
+      }
+      hs[i] = fwd(pg, Q.layers[i], {{hs[i - 1]}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr,
+                  pl.kind >= 3 ? &pl : nullptr, last && qd ? &Q.layers[D] : nullptr);
     }
-    h1 = fwd(pg, Q.layers[1], {{h0}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pl.kind >= 3 ? &pl : nullptr,
-             qd ? &Q.layers[2] : nullptr);
     out_t = keep;
   }
   // TD3 / SAC: the critic loss head and the actor objective's head fused into the DX of each
@@ -3473,21 +3505,27 @@ struct Engine {
     asc_set = set;
     add_adam_scalars(pg);
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
+    // make_mlp's depth (mlp.py:24-35): D hidden layers, then the output layer Lout
+    const int D = (int)HS.size();
+    const Layer& Lout = pi.layers[D];
     // actor on [s; s'] (target policy aliases the policy, Q1; SAC policy unchanged until its step)
     pl_src = prelayer_ok(pi.layers[0], pi.layers[1]);
-    View h0 = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_RELU, nullptr, false);
+    std::vector<View> h(D);
+    h[0] = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_RELU, nullptr, false);
     pl_src = false;
     const PreUse pl0 = prelayer_ok(pi.layers[0], pi.layers[1]) ? pre_layer(pi.layers[0], {ss}) : PreUse{};
-    View h1 = fwd(pg, pi.layers[1], {{h0}}, B2, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr,
-                  pl0.kind == 3 ? &pl0 : nullptr);
+    for (int i = 1; i < D; ++i)
+      h[i] = fwd(pg, pi.layers[i], {{h[i - 1]}}, B2, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr,
+                 i == 1 && pl0.kind == 3 ? &pl0 : nullptr);
+    const View hl = h[D - 1];  // the last hidden layer's output
     View actv, raw, logpi;
     // TD3: the target critics' first layer recomputes a' in-tile (pre-GEMM, as TD7)
     const bool prea = !sac && actor_pre();
-    const View h1n = h1.sub(B, B);
-    const PreUse pn1 = prea ? pre_actor_fwd(pi.layers[2], h1n, &eps, 1) : PreUse{};
+    const View h1n = hl.sub(B, B);
+    const PreUse pn1 = prea ? pre_actor_fwd(Lout, h1n, &eps, 1) : PreUse{};
     if (!sac) {
-      actv = prea ? fwd(pg, pi.layers[2], {{h1.sub(0, B)}}, B, ACT_TANH, nullptr, false)
-                  : fwd(pg, pi.layers[2], {{h1}}, B2, ACT_TANH, nullptr, false, &eps, B);
+      actv = prea ? fwd(pg, Lout, {{hl.sub(0, B)}}, B, ACT_TANH, nullptr, false)
+                  : fwd(pg, Lout, {{hl}}, B2, ACT_TANH, nullptr, false, &eps, B);
     } else if (sac_fwd_fused()) {  // the rsample in the raw head's epilogue (one level fewer)
       actv = buf(B2, A);
       logpi = vec(B2);
@@ -3505,10 +3543,10 @@ struct Engine {
       a.eps_row_split = B;
       sfu.rd = {eps.id, eps2.id};
       sfu.wr = {actv.id, logpi.id};
-      raw = fwd(pg, pi.layers[2], {{h1}}, B2, ACT_NONE, nullptr, false, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
+      raw = fwd(pg, Lout, {{hl}}, B2, ACT_NONE, nullptr, false, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
                 false, &sfu);
     } else {
-      raw = fwd(pg, pi.layers[2], {{h1}}, B2, ACT_NONE, nullptr, false);
+      raw = fwd(pg, Lout, {{hl}}, B2, ACT_NONE, nullptr, false);
       actv = buf(B2, A);
       logpi = vec(B2);
       Op op{};
@@ -3531,17 +3569,20 @@ struct Engine {
     }
     View a_pi = actv.sub(0, B), a_next = prea ? a_pi : actv.sub(B, B);  // (pre: layout only)
     // SAC: the target critics' first layer recomputes a' in-tile from the raw head (pre-GEMM, has_pre 5)
-    const PreUse psac = sac && sac_pre() ? pre_sac_fwd(pi.layers[2], h1n, eps, 1) : PreUse{};
+    const PreUse psac = sac && sac_pre() ? pre_sac_fwd(Lout, h1n, eps, 1) : PreUse{};
     const PreUse* tpre = prea ? &pn1 : (psac.kind == 5 ? &psac : nullptr);
     // target critics + y
-    View th0[2], th1[2];
+    std::vector<View> th[2];
     out_t = false;  // (forward only)
     const bool hdx = mlp_headdx();
-    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th0[n], th1[n], tpre, true, hdx);
+    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th[n], tpre, true, hdx);
     out_t = true;
     // online critics
-    View c0[2], c1[2];
-    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c0[n], c1[n], nullptr, true, hdx);
+    std::vector<View> c[2];
+    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c[n], nullptr, true, hdx);
+    // (the last hidden layers and the heads' layers)
+    const View c1[2] = {c[0][D - 1], c[1][D - 1]}, th1[2] = {th[0][D - 1], th[1][D - 1]};
+    const Layer *qo[2] = {&q[0]->layers[D], &q[1]->layers[D]}, *tqo[2] = {&tq[0]->layers[D], &tq[1]->layers[D]};
     // (dZ of the critics' last hidden layers: with the fused head only their weight gradients read
     // it, in the T image)
     View dz1[2] = {buf(B, H, !hdx, true), buf(B, H, !hdx, true)},
@@ -3554,12 +3595,12 @@ struct Engine {
       // target head (td3.py:160-164, sac.py:188-193) fused: y per row, then the loss
       Op op = head_op(HEAD_MLP_LOSS, B);
       HeadArgs& h = op.head;
-      set_head_twin(h, c1[0], c1[1], q[0]->layers[2], q[1]->layers[2]);
-      set_head_target(h, HEAD_MLP_TARGET, th1[0], th1[1], tq[0]->layers[2], tq[1]->layers[2]);
+      set_head_twin(h, c1[0], c1[1], *qo[0], *qo[1]);
+      set_head_target(h, HEAD_MLP_TARGET, th1[0], th1[1], *tqo[0], *tqo[1]);
       h.reward = rw.p;
       h.notdone = nd.p;
-      std::vector<int> rd{c1[0].id, c1[1].id, q[0]->layers[2].res, q[1]->layers[2].res, th1[0].id, th1[1].id,
-                          tq[0]->layers[2].res, tq[1]->layers[2].res, rw.id, nd.id};
+      std::vector<int> rd{c1[0].id, c1[1].id, qo[0]->res, qo[1]->res, th1[0].id, th1[1].id,
+                          tqo[0]->res, tqo[1]->res, rw.id, nd.id};
       if (sac) {
         h.sac = 1;
         h.logpi = logpi.p + B;  // next-state rows
@@ -3588,24 +3629,30 @@ struct Engine {
         for (int n = 0; n < 2; ++n) {
           HeadUse hu{h, n, rd, {dz1[n].id, dq[n].id}};
           if (n == 0) hu.wr.insert(hu.wr.end(), {prio.id, qloss_id});
-          d0f[n] = dx(pg, {{c1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &c0[n], nullptr, nullptr, nullptr, &hu);
+          d0f[n] = dx(pg, {{c1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &c[n][D - 2], nullptr, nullptr,
+                      nullptr, &hu);
         }
       }
     }
     add_update_and_prefetch(pg, sac, set, lap, prio);
-    for (int n = 0; n < 2; ++n) {
+    for (int n = 0; n < 2; ++n) {  // (input gradients through a layer before its Adam update)
       Net& Q = *q[n];
-      dw(pg, Q.layers[2], dq[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
-      View d0 = hdx ? d0f[n] : dx(pg, {{dz1[n], &Q.layers[1], 0}}, H, B, ACT_RELU, &c0[n]);
-      dw(pg, Q.layers[1], dz1[n], {c0[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
-      dw(pg, Q.layers[0], d0, {s, act_in}, B, CNT_ADAM_Q, cfg.critic_lr);
+      dw(pg, Q.layers[D], dq[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
+      View d = dz1[n];  // dZ of hidden layer i, from i = D - 1 down
+      for (int i = D - 1; i >= 1; --i) {
+        const View dp = hdx && i == D - 1 ? d0f[n] : dx(pg, {{d, &Q.layers[i], 0}}, HS[i - 1], B, ACT_RELU, &c[n][i - 1]);
+        dw(pg, Q.layers[i], d, {c[n][i - 1]}, B, CNT_ADAM_Q, cfg.critic_lr);
+        d = dp;
+      }
+      dw(pg, Q.layers[0], d, {s, act_in}, B, CNT_ADAM_Q, cfg.critic_lr);
     }
     ploss_part = nullptr;
     float* gsq = nullptr;
     int ngsq = 0;
     if (policy) {
-      View p0[2], p1[2];
-      for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, a_pi, p0[n], p1[n], nullptr, false, hdx);
+      std::vector<View> pc[2];
+      for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, a_pi, pc[n], nullptr, false, hdx);
+      const View p1[2] = {pc[0][D - 1], pc[1][D - 1]};
       // (no weight gradient of the critics in the policy pass: the gradients keep N images only)
       View dzp1[2];
       if (!hdx) dzp1[0] = buf(B, H, true, false), dzp1[1] = buf(B, H, true, false);
@@ -3614,10 +3661,10 @@ struct Engine {
       if (hdx) {  // the objective's head inside the DX of each critic's last hidden layer
         Op op = head_op(HEAD_MLP_POLICY, B);
         HeadArgs& h = op.head;
-        set_head_twin(h, p1[0], p1[1], q[0]->layers[2], q[1]->layers[2]);
+        set_head_twin(h, p1[0], p1[1], *qo[0], *qo[1]);
         h.dact = ACT_RELU;
         h.loss_part = ploss_part;
-        std::vector<int> rd{p1[0].id, p1[1].id, q[0]->layers[2].res, q[1]->layers[2].res};
+        std::vector<int> rd{p1[0].id, p1[1].id, qo[0]->res, qo[1]->res};
         if (sac) {
           h.sac = 1;
           h.logpi = logpi.p;
@@ -3632,20 +3679,21 @@ struct Engine {
         for (int n = 0; n < 2; ++n) {
           HeadUse hu{h, n, rd, {}};
           if (n == 0) hu.wr.push_back(ploss_id);
-          dzp0[n] = dx(pg, {{p1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &p0[n], nullptr, nullptr, nullptr, &hu);
+          dzp0[n] = dx(pg, {{p1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &pc[n][D - 2], nullptr, nullptr,
+                       nullptr, &hu);
         }
         out_t = true;
       } else {
         Op op = head_op(HEAD_MLP_POLICY, B);
         HeadArgs& h = op.head;
-        set_head_twin(h, p1[0], p1[1], q[0]->layers[2], q[1]->layers[2]);
+        set_head_twin(h, p1[0], p1[1], *qo[0], *qo[1]);
         h.dsrc[0] = p1[0].m;
         h.dsrc[1] = p1[1].m;
         h.dact = ACT_RELU;
         h.dz[0] = dzp1[0].m;
         h.dz[1] = dzp1[1].m;
         h.loss_part = ploss_part;
-        std::vector<int> rd{p1[0].id, p1[1].id, q[0]->layers[2].res, q[1]->layers[2].res};
+        std::vector<int> rd{p1[0].id, p1[1].id, qo[0]->res, qo[1]->res};
         if (sac) {
           h.sac = 1;
           h.logpi = logpi.p;
@@ -3656,9 +3704,15 @@ struct Engine {
         }
         pg.add(op, rd, {dzp1[0].id, dzp1[1].id, ploss_id = next_id++});
         out_t = false;
-        for (int n = 0; n < 2; ++n) dzp0[n] = dx(pg, {{dzp1[n], &q[n]->layers[1], 0}}, H, B, ACT_RELU, &p0[n]);
+        for (int n = 0; n < 2; ++n)
+          dzp0[n] = dx(pg, {{dzp1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &pc[n][D - 2]);
         out_t = true;
       }
+      // (deeper critics: on down to the first hidden layer; no weight gradient reads these)
+      out_t = false;
+      for (int i = D - 2; i >= 1; --i)
+        for (int n = 0; n < 2; ++n) dzp0[n] = dx(pg, {{dzp0[n], &q[n]->layers[i], 0}}, HS[i - 1], B, ACT_RELU, &pc[n][i - 1]);
+      out_t = true;
       View dout;
       PreUse pdout{};  // TD3: d1 recomputes dout in-tile
       if (!sac) {
@@ -3725,29 +3779,35 @@ struct Engine {
         return {w, b};
       };
       // actor backward: tensors in parameters() order mlp.0.w, mlp.0.b, mlp.2.w, ...
-      auto g0 = gsq_for(pi.layers[0], 0, 1);
-      auto g1 = gsq_for(pi.layers[1], 2, 3);
-      auto g2 = gsq_for(pi.layers[2], 4, 5);
-      View h1s = h1.sub(0, B), h0s = h0.sub(0, B);
+      std::vector<std::pair<float*, float*>> gl;
+      for (int i = 0; i <= D; ++i) gl.push_back(gsq_for(pi.layers[i], 2 * i, 2 * i + 1));
+      std::vector<View> hsub(D);
+      for (int i = 0; i < D; ++i) hsub[i] = h[i].sub(0, B);
       // TD3: the aliased target policy's Polyak (td3.py:200-204) in the Adam epilogues: one level
       // fewer between the actor update and the next step's target action
       adam_ptau = !sac && pi_polyak_fused() ? cfg.tau : 0.f;
       // SAC: d1 (the gradient through the raw head, K = 2A <= 48) recomputed in-tile by d0's DX
-      const bool pld = sac && sac_bwd_fused() && prelayer_ok_dx(pi.layers[2], pi.layers[1]);
+      const bool pld = sac && sac_bwd_fused() && prelayer_ok_dx(Lout, pi.layers[D - 1]);
       pl_src = pld;
-      View d1 = dx(pg, {{dout, &pi.layers[2], 0}}, H, B, ACT_RELU, &h1s, nullptr, nullptr, prea ? &pdout : nullptr);
+      View d = dx(pg, {{dout, &Lout, 0}}, HS[D - 1], B, ACT_RELU, &hsub[D - 1], nullptr, nullptr, prea ? &pdout : nullptr);
       pl_src = false;
       // (d0 reads the raw head's pre-update weights when it recomputes d1: emitted before that Adam)
-      const PreUse pd1 = pld ? pre_layer_dx(pi.layers[2], dout, h1s) : PreUse{};
-      View d0;
-      if (pld) d0 = dx(pg, {{d1, &pi.layers[1], 0}}, H, B, ACT_RELU, &h0s, nullptr, nullptr, &pd1);
-      dw(pg, pi.layers[2], dout, {h1s}, B, CNT_ADAM_PI, cfg.policy_lr, g2.first, g2.second);
-      if (!pld) d0 = dx(pg, {{d1, &pi.layers[1], 0}}, H, B, ACT_RELU, &h0s);
-      dw(pg, pi.layers[1], d1, {h0s}, B, CNT_ADAM_PI, cfg.policy_lr, g1.first, g1.second);
-      dw(pg, pi.layers[0], d0, {s}, B, CNT_ADAM_PI, cfg.policy_lr, g0.first, g0.second);
+      const PreUse pd1 = pld ? pre_layer_dx(Lout, dout, hsub[D - 1]) : PreUse{};
+      View dp;
+      if (pld) dp = dx(pg, {{d, &pi.layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &hsub[D - 2], nullptr, nullptr, &pd1);
+      dw(pg, Lout, dout, {hsub[D - 1]}, B, CNT_ADAM_PI, cfg.policy_lr, gl[D].first, gl[D].second);
+      if (!pld) dp = dx(pg, {{d, &pi.layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &hsub[D - 2]);
+      dw(pg, pi.layers[D - 1], d, {hsub[D - 2]}, B, CNT_ADAM_PI, cfg.policy_lr, gl[D - 1].first, gl[D - 1].second);
+      d = dp;
+      for (int i = D - 2; i >= 1; --i) {  // (deeper actors)
+        dp = dx(pg, {{d, &pi.layers[i], 0}}, HS[i - 1], B, ACT_RELU, &hsub[i - 1]);
+        dw(pg, pi.layers[i], d, {hsub[i - 1]}, B, CNT_ADAM_PI, cfg.policy_lr, gl[i].first, gl[i].second);
+        d = dp;
+      }
+      dw(pg, pi.layers[0], d, {s}, B, CNT_ADAM_PI, cfg.policy_lr, gl[0].first, gl[0].second);
       adam_ptau = 0.f;
       if (gsq) {
-        // tensor t owns tiles [gsq_offs[t], gsq_offs[t+1]) (params() order: w0, b0, w1, b1, w2, b2)
+        // tensor t owns tiles [gsq_offs[t], gsq_offs[t+1]) (params() order: w0, b0, w1, b1, ...)
         gsq_offs.assign(1, 0);
         for (size_t i = 0; i < tens.size(); ++i)
           if (i + 1 == tens.size() || tens[i + 1] != tens[i]) gsq_offs.push_back((int)i + 1);
@@ -4084,6 +4144,17 @@ struct Engine {
         g_fold = capture(pf);
       }
     }
+    {
+      Prog pz;
+      Op z{};
+      z.kind = OP_COPY;
+      z.flat.dst = reinterpret_cast<float*>(&ctrl->info_slot);  // (int 0 = the bits of float 0)
+      z.flat.src = mem.make<float>(4);                          // (zero-filled)
+      z.flat.n = 1;
+      z.wg_count = 1;
+      pz.add(z, {}, {next_id++});
+      g_slot0 = capture(pz);
+    }
     use_set(0);
     built = true;
   }
@@ -4133,15 +4204,20 @@ struct Engine {
   long long launches = 0;  // rle_level dispatches enqueued by step graphs (rle_launch_count)
   std::unique_ptr<AqlQueue> aql;  // (RLE_AQL=1) direct dispatch of the step graphs
   bool aql_active = false;        // inside step(): graphs go to the AQL queue
-  // Direct AQL dispatch of the step graphs (synchronous rle_step / rle_step_timed; rle_step_async keeps
-  // hipGraph replays, which order themselves on the engine's stream).  RLE_AQL=0: hipGraph everywhere
-  // (A/B; the launch path does not change any result).
+  // Direct AQL dispatch of the step graphs (rle_step / rle_step_timed wait for their bursts; rle_step_async
+  // leaves its burst in flight on the engine's own queue -- each seed on a queue of its own, where hipGraph
+  // replays on HIP streams share GPU_MAX_HW_QUEUES hardware queues -- and every other entry point, and
+  // every replay operation on a replay the engine is bound to, drains it first: aql_drain).  RLE_AQL=0:
+  // hipGraph everywhere (A/B; the launch path does not change any result).
   static bool aql_mode() {
     static const bool on = [] {
       const char* e = std::getenv("RLE_AQL");
       return !(e && e[0] == '0');
     }();
     return on;
+  }
+  void aql_drain(double* ms = nullptr) {
+    if (aql) aql_complete(*aql, ms);
   }
   void launch_graph(const Graph& G) {
     static const bool eager = [] {
@@ -4205,17 +4281,27 @@ struct Engine {
       HIPCHK(hipEventRecord(ev0, stream));
     }
     // direct dispatch (RLE_AQL=1): the graphs' levels go to the engine's own queue; the HIP
-    // stream is drained first and the queue after each chunk (host-side ordering between them)
-    const bool use_aql = aql_mode() && !async && !g_pol[0].aql.empty();
+    // stream is drained first and the queue after each chunk (host-side ordering between them; async:
+    // the last chunk stays in flight, aql_drain)
+    const bool use_aql = aql_mode() && !g_pol[0].aql.empty();
     if (use_aql && !aql) aql = aql_open(cfg.device);
     double aql_ms = 0.0;
     while (done < n) {
       const int chunk = std::min(n - done, info_cap);
-      int zero = 0;
-      HIPCHK(hipMemcpyAsync(&ctrl->info_slot, &zero, sizeof(int), hipMemcpyHostToDevice, stream));
-      if (use_aql) {
+      if (use_aql && async) {
+        // (the slot reset queues behind the bursts still in flight: no host wait)
         HIPCHK(hipStreamSynchronize(stream));
         aql_active = true;
+        launch_graph(g_slot0);
+        launches -= g_slot0.nlaunch;  // (not a step level)
+      } else {
+        if (use_aql) aql_drain();  // (the info slot reset below must not race levels still in flight)
+        int zero = 0;
+        HIPCHK(hipMemcpyAsync(&ctrl->info_slot, &zero, sizeof(int), hipMemcpyHostToDevice, stream));
+        if (use_aql) {
+          HIPCHK(hipStreamSynchronize(stream));
+          aql_active = true;
+        }
       }
       for (int i = 0; i < chunk; ++i) {
         if (ctrl_tape_mode_host) {
@@ -4259,7 +4345,8 @@ struct Engine {
       }
       if (use_aql) {
         aql_active = false;
-        aql_flush(*aql, &aql_ms);
+        aql_submit(*aql);
+        if (!async) aql_complete(*aql, &aql_ms);
       }
       if (info_out) {
         HIPCHK(hipMemcpyAsync(info_out + (size_t)done * kInfoMax, info, (size_t)chunk * kInfoMax * sizeof(float),
@@ -4281,6 +4368,14 @@ struct Engine {
   int ctrl_tape_mode_host = 0;
 };
 
+void Replay::drain_users() {
+  for (auto& u : users) u.first->aql_drain();
+}
+void Replay::wait_users() {
+  drain_users();
+  for (auto& u : users) HIPCHK(hipStreamWaitEvent(stream, u.second, 0));
+}
+
 }  // namespace rle
 
 // ====================================================================== C ABI
@@ -4295,6 +4390,11 @@ struct rle_replay {
 struct rle_engine {
   std::unique_ptr<Engine> e;
 };
+// The engine behind a handle, its rle_step_async burst retired first (Engine::aql_mode)
+static Engine& drained(rle_engine* h) {
+  h->e->aql_drain();
+  return *h->e;
+}
 
 template <class F>
 static int guard(F&& f) {
@@ -4357,6 +4457,10 @@ int rle_replay_create(int device, long long capacity, int state_dim, int action_
 int rle_replay_destroy(rle_replay* r) {
   return guard([&] {
     if (!r) return;
+    try {
+      r->r.drain_users();
+    } catch (const Error&) {  // (a timed-out burst: the engine's queue is closed; unbind anyway)
+    }
     for (auto& u : r->r.users) {  // engines still bound: unbind (their steps now fail: "no replay bound")
       (void)hipEventSynchronize(u.second);
       u.first->replay = nullptr;
@@ -4421,6 +4525,7 @@ int rle_replay_state(rle_replay* h, long long* ptr, long long* size, float* max_
     if (ptr) *ptr = r.ptr;
     if (size) *size = r.size;
     if (max_priority) {
+      r.drain_users();
       HIPCHK(hipDeviceSynchronize());
       HIPCHK(hipMemcpy(max_priority, r.maxp_d, 4, hipMemcpyDeviceToHost));
     }
@@ -4449,6 +4554,7 @@ int rle_replay_fill_random(rle_replay* h, long long count, unsigned long long se
 int rle_replay_get_priority(rle_replay* h, float* out, long long n) {
   return guard([&] {
     REQUIRE(n <= h->r.cap, "get_priority: n > capacity");
+    h->r.drain_users();
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, h->r.priority, n * 4, hipMemcpyDeviceToHost));
   });
@@ -4457,6 +4563,7 @@ int rle_replay_get_priority(rle_replay* h, float* out, long long n) {
 int rle_replay_set_priority(rle_replay* h, const float* p, long long n, float max_priority) {
   return guard([&] {
     REQUIRE(n <= h->r.cap, "set_priority: n > capacity");
+    h->r.drain_users();
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(h->r.priority, p, n * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->r.maxp_d, &max_priority, 4, hipMemcpyHostToDevice));
@@ -4613,6 +4720,7 @@ int rle_replay_gather(rle_replay* h, int n, const long long* ind, float* state, 
                       float* next_state, float* notdone) {
   return guard([&] {
     Replay& r = h->r;
+    r.drain_users();
     HIPCHK(hipDeviceSynchronize());
     std::vector<float> row(r.Sp);
     for (int i = 0; i < n; ++i) {
@@ -4646,6 +4754,13 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
             "create: state_dim <= 1024, action_dim <= 128, hidden <= 512");
     REQUIRE(cfg->state_dim > 0 && cfg->action_dim > 0 && cfg->hidden > 0 && cfg->hidden % 4 == 0,
             "create: bad dims (hidden must be a multiple of 4)");
+    REQUIRE(cfg->zs_dim == 0 || (cfg->algo == RLE_TD7 && cfg->zs_dim > 0 && cfg->zs_dim <= 512 && cfg->zs_dim % 4 == 0),
+            "create: zs_dim (TD7 only) must be a multiple of 4, <= 512");
+    REQUIRE(cfg->n_hidden == 0 || (cfg->algo != RLE_TD7 && cfg->n_hidden >= 2 && cfg->n_hidden <= RLE_MAX_HIDDEN),
+            "create: n_hidden (TD3 / SAC only) must be 2..6");
+    for (int i = 0; i < cfg->n_hidden; ++i)
+      REQUIRE(cfg->hidden_sizes[i] > 0 && cfg->hidden_sizes[i] <= 512 && cfg->hidden_sizes[i] % 4 == 0,
+              "create: hidden_sizes must be multiples of 4, <= 512");
     HIPCHK(hipSetDevice(cfg->device));
     auto h = std::make_unique<rle_engine>();
     h->e = std::make_unique<Engine>();
@@ -4656,8 +4771,14 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
     e.Sp = rle::r16(e.S);
     e.A = cfg->action_dim;
     e.Ap = rle::r16(e.A);
-    e.H = cfg->hidden;
+    // (TD3 / SAC: H is the LAST hidden width -- what the heads and the output layer read; each
+    // layer's own width is in HS)
+    e.HS.assign(2, cfg->hidden);
+    if (cfg->n_hidden) e.HS.assign(cfg->hidden_sizes, cfg->hidden_sizes + cfg->n_hidden);
+    e.H = e.algo == RLE_TD7 ? cfg->hidden : e.HS.back();
     e.Hp = rle::r16(e.H);
+    e.Z = cfg->zs_dim ? cfg->zs_dim : cfg->hidden;
+    e.Zp = rle::r16(e.Z);
     e.B = cfg->batch;
     e.resolve_plan();
     HIPCHK(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
@@ -4698,7 +4819,7 @@ int rle_plan_default(rle_plan* out) {
 int rle_set_plan(rle_engine* h, const rle_plan* plan) {
   return guard([&] {
     REQUIRE(h && plan, "set_plan: null");
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     REQUIRE(!e.built, "set_plan: the engine has already built its step programs (set the plan before the first step)");
     e.plan = *plan;
     e.resolve_plan();
@@ -4715,7 +4836,7 @@ int rle_get_plan(rle_engine* h, rle_plan* out) {
 int rle_destroy(rle_engine* h) {
   return guard([&] {
     if (!h) return;
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     (void)hipStreamSynchronize(e.stream);
     if (e.replay) {
       auto& us = e.replay->users;
@@ -4727,7 +4848,7 @@ int rle_destroy(rle_engine* h) {
     }
     if (e.done_ev) (void)hipEventDestroy(e.done_ev);
     for (rle::Graph* g : {&e.g_prime[0], &e.g_prime[1], &e.g_pol[0], &e.g_pol[1], &e.g_pln[0], &e.g_pln[1],
-                          &e.g_pair[0], &e.g_pair[1], &e.g_hard, &e.g_fold}) {
+                          &e.g_pair[0], &e.g_pair[1], &e.g_hard, &e.g_fold, &e.g_slot0}) {
       if (g->x) (void)hipGraphExecDestroy(g->x);
       if (g->g) (void)hipGraphDestroy(g->g);
     }
@@ -4746,7 +4867,7 @@ int rle_destroy(rle_engine* h) {
 
 int rle_bind_replay(rle_engine* h, rle_replay* r) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     REQUIRE(r, "bind: null replay");
     REQUIRE(r->r.S == e.S && r->r.A == e.A, "bind: replay dims differ from agent dims");
     if (e.replay == &r->r) return;
@@ -4770,27 +4891,27 @@ int rle_param_numel(rle_engine* h, const char* net, const char* name, long long*
   return guard([&] { *numel = h->e->numel(net, name); });
 }
 int rle_get_param(rle_engine* h, const char* net, const char* name, float* out, long long n) {
-  return guard([&] { h->e->xfer_param(net, name, out, n, false, 0); });
+  return guard([&] { drained(h).xfer_param(net, name, out, n, false, 0); });
 }
 int rle_set_param(rle_engine* h, const char* net, const char* name, const float* in, long long n) {
-  return guard([&] { h->e->xfer_param(net, name, const_cast<float*>(in), n, true, 0); });
+  return guard([&] { drained(h).xfer_param(net, name, const_cast<float*>(in), n, true, 0); });
 }
 int rle_get_adam(rle_engine* h, const char* net, const char* name, int which, float* out, long long n) {
   return guard([&] {
     REQUIRE(which == 0 || which == 1, "adam: which in {0,1}");
-    h->e->xfer_param(net, name, out, n, false, 1 + which);
+    drained(h).xfer_param(net, name, out, n, false, 1 + which);
   });
 }
 int rle_set_adam(rle_engine* h, const char* net, const char* name, int which, const float* in, long long n) {
   return guard([&] {
     REQUIRE(which == 0 || which == 1, "adam: which in {0,1}");
-    h->e->xfer_param(net, name, const_cast<float*>(in), n, true, 1 + which);
+    drained(h).xfer_param(net, name, const_cast<float*>(in), n, true, 1 + which);
   });
 }
 
 int rle_get_counters(rle_engine* h, long long* out6) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     HIPCHK(hipStreamSynchronize(e.stream));
     rle::Ctrl c;
     HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));
@@ -4810,7 +4931,7 @@ int rle_set_act_counter(rle_engine* h, unsigned long long v) {
 
 int rle_set_counters(rle_engine* h, const long long* in6) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     HIPCHK(hipStreamSynchronize(e.stream));
     rle::Ctrl c;
     HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));
@@ -4825,7 +4946,7 @@ int rle_set_counters(rle_engine* h, const long long* in6) {
 
 int rle_get_value_bounds(rle_engine* h, float* out4) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     HIPCHK(hipStreamSynchronize(e.stream));
     rle::Ctrl c;
     HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));
@@ -4838,7 +4959,7 @@ int rle_get_value_bounds(rle_engine* h, float* out4) {
 
 int rle_set_value_bounds(rle_engine* h, const float* in4) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     HIPCHK(hipStreamSynchronize(e.stream));
     rle::Ctrl c;
     HIPCHK(hipMemcpy(&c, e.ctrl, sizeof(c), hipMemcpyDeviceToHost));
@@ -4853,7 +4974,7 @@ int rle_set_value_bounds(rle_engine* h, const float* in4) {
 int rle_step(rle_engine* h, int n_steps, float* info_out) {
   return guard([&] {
     REQUIRE(n_steps >= 0, "step: n < 0");
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     HIPCHK(hipSetDevice(e.cfg.device));
     if (e.replay) HIPCHK(hipStreamSynchronize(e.replay->stream));
     e.step(n_steps, info_out);
@@ -4863,7 +4984,7 @@ int rle_step(rle_engine* h, int n_steps, float* info_out) {
 int rle_step_timed(rle_engine* h, int n_steps, float* gpu_ms) {
   return guard([&] {
     REQUIRE(n_steps >= 0 && gpu_ms, "step_timed: bad args");
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     HIPCHK(hipSetDevice(e.cfg.device));
     if (e.replay) HIPCHK(hipStreamSynchronize(e.replay->stream));
     e.step(n_steps, nullptr, gpu_ms);
@@ -4873,7 +4994,7 @@ int rle_step_timed(rle_engine* h, int n_steps, float* gpu_ms) {
 int rle_step_async(rle_engine* h, int n_steps) {
   return guard([&] {
     REQUIRE(n_steps >= 0, "step_async: n < 0");
-    Engine& e = *h->e;
+    Engine& e = *h->e;  // (its earlier bursts stay in flight: the new one queues behind them)
     HIPCHK(hipSetDevice(e.cfg.device));
     if (e.replay) HIPCHK(hipStreamSynchronize(e.replay->stream));
     e.step(n_steps, nullptr, nullptr, true);
@@ -4882,7 +5003,7 @@ int rle_step_async(rle_engine* h, int n_steps) {
 
 int rle_set_tapes(rle_engine* h, int n, const float* u, const float* eps, const float* eps_pi, const long long* ind) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     HIPCHK(hipStreamSynchronize(e.stream));
     int mode = 0;
     if (n > 0) {
@@ -4915,7 +5036,7 @@ int rle_set_tapes(rle_engine* h, int n, const float* u, const float* eps, const 
 
 int rle_last_indices(rle_engine* h, long long* out) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     HIPCHK(hipStreamSynchronize(e.stream));
     HIPCHK(hipMemcpy(out, e.bsets[e.last_set].ind, e.B * sizeof(long long), hipMemcpyDeviceToHost));
   });
@@ -4923,7 +5044,7 @@ int rle_last_indices(rle_engine* h, long long* out) {
 
 int rle_act(rle_engine* h, const float* obs, int n, float* out) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     REQUIRE(n > 0 && n <= 1024, "act: 0 < n <= 1024");
     HIPCHK(hipSetDevice(e.cfg.device));
     auto it = e.act_graphs.find(n);
@@ -4943,10 +5064,7 @@ int rle_act(rle_engine* h, const float* obs, int n, float* out) {
         rle::View p2 = e.fwd(pg, pi.layers[2], {{p1}}, M, rle::ACT_RELU, nullptr, false);
         o = e.fwd(pg, pi.layers[3], {{p2}}, M, rle::ACT_TANH, nullptr, false);
       } else {
-        rle::Net& pi = e.net("policy");
-        rle::View h0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_RELU, nullptr, false);
-        rle::View h1 = e.fwd(pg, pi.layers[1], {{h0}}, M, rle::ACT_RELU, nullptr, false);
-        o = e.fwd(pg, pi.layers[2], {{h1}}, M, rle::ACT_NONE, nullptr, false);
+        o = e.mlp_fwd(pg, e.net("policy"), {{in}}, M, rle::ACT_NONE);
       }
       rle::Graph G = e.capture(pg);
       it = e.act_graphs.emplace(n, std::make_pair(G, o)).first;
@@ -4971,7 +5089,7 @@ int rle_act(rle_engine* h, const float* obs, int n, float* out) {
 
 int rle_set_action_map(rle_engine* h, const float* scale, const float* bias, float exploration_noise) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     REQUIRE(scale && bias, "set_action_map: null scale / bias");
     HIPCHK(hipSetDevice(e.cfg.device));
     e.ensure_action_map();
@@ -4986,7 +5104,7 @@ int rle_set_action_map(rle_engine* h, const float* scale, const float* bias, flo
 
 int rle_act_sample(rle_engine* h, const float* obs, int n, int mode, const float* eps, float* out) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     REQUIRE(n > 0 && n <= 1024 && obs && out, "act_sample: 0 < n <= 1024, obs and out");
     REQUIRE(mode >= 0 && mode <= 2 && (mode != 2 || eps), "act_sample: mode 0 / 1 / 2 (2 needs eps)");
     HIPCHK(hipSetDevice(e.cfg.device));
@@ -5030,16 +5148,10 @@ int rle_act_sample(rle_engine* h, const float* obs, int n, int mode, const float
         e.fwd(pg, pi.layers[3], {{p2}}, M, rle::ACT_TANH, nullptr, false);
         tanh_act(pg);
       } else if (e.algo == RLE_TD3) {  // td3.py:114-135
-        rle::Net& pi = e.net("policy");
-        rle::View h0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_RELU, nullptr, false);
-        rle::View h1 = e.fwd(pg, pi.layers[1], {{h0}}, M, rle::ACT_RELU, nullptr, false);
-        e.fwd(pg, pi.layers[2], {{h1}}, M, rle::ACT_TANH, nullptr, false);
+        e.mlp_fwd(pg, e.net("policy"), {{in}}, M, rle::ACT_TANH);
         tanh_act(pg);
       } else {  // sac.py:132-159
-        rle::Net& pi = e.net("policy");
-        rle::View h0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_RELU, nullptr, false);
-        rle::View h1 = e.fwd(pg, pi.layers[1], {{h0}}, M, rle::ACT_RELU, nullptr, false);
-        rle::View raw = e.fwd(pg, pi.layers[2], {{h1}}, M, rle::ACT_NONE, nullptr, false);
+        rle::View raw = e.mlp_fwd(pg, e.net("policy"), {{in}}, M, rle::ACT_NONE);
         rle::Op op{};
         op.kind = rle::OP_SAC_ACTOR;
         rle::SacActorArgs& sa = op.sac;
@@ -5189,7 +5301,7 @@ int rle_launch_count(rle_engine* h, long long* n) {
 
 int rle_graph_stats(rle_engine* h, int* lp, int* lplain) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     if (!e.built) e.build();
     if (lp) *lp = e.policy_graph().levels();
     if (lplain) *lplain = e.plain_graph().levels();
@@ -5198,7 +5310,7 @@ int rle_graph_stats(rle_engine* h, int* lp, int* lplain) {
 
 int rle_graph_describe(rle_engine* h, int which, char* buf, int len) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     if (!e.built) e.build();
     const rle::Graph& G = which == 0 ? e.policy_graph()
                           : which == 1 ? e.plain_graph()
@@ -5211,7 +5323,7 @@ int rle_graph_describe(rle_engine* h, int which, char* buf, int len) {
 
 int rle_graph_trace(rle_engine* h, int which, unsigned long long* out, long long cap, long long* n_out) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     REQUIRE(n_out, "trace: null n_out");
     if (!e.built) e.build();
     const rle::Graph& G = which == 0 ? e.policy_graph()
@@ -5239,8 +5351,8 @@ int rle_aql_wait_plan(double expected_us, double elapsed_us, double timeout_s, d
 
 int rle_copy_state(rle_engine* dst, rle_engine* src) {
   return guard([&] {
-    Engine& d = *dst->e;
-    Engine& s = *src->e;
+    Engine& d = drained(dst);
+    Engine& s = drained(src);
     REQUIRE(d.nP == s.nP && d.algo == s.algo, "copy_state: config mismatch");
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(d.P, s.P, 3 * d.nP * sizeof(float), hipMemcpyDeviceToDevice));
@@ -5259,7 +5371,7 @@ int rle_eval(rle_engine* h, int what, const char* net, const char* enc, const fl
     REQUIRE(h && net && s && out && n > 0 && n <= 1024, "eval: bad args (0 < n <= 1024)");
     REQUIRE(what == RLE_EVAL_Q || what == RLE_EVAL_ZS || what == RLE_EVAL_ZSA, "eval: bad `what`");
     REQUIRE(what == RLE_EVAL_ZS || a, "eval: needs actions");
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     const bool td7 = e.algo == RLE_TD7;
     REQUIRE(what == RLE_EVAL_Q || td7, "eval: encoder outputs exist for TD7 only");
     REQUIRE(!(td7 && what == RLE_EVAL_Q) || enc, "eval: TD7 critics need the encoder of their embeddings");
@@ -5285,16 +5397,14 @@ int rle_eval(rle_engine* h, int what, const char* net, const char* enc, const fl
           eg.out = e.fwd(pg, N.layers[3], {{c2}}, M, rle::ACT_NONE, nullptr, false);
         } else {  // MLPCritic.estimate_q_value (mlp.py:98-101)
           REQUIRE(N.kind == "mlp_critic", "eval: Q needs a critic net");
-          rle::View h0 = e.fwd(pg, N.layers[0], {{eg.in0}, {eg.in1}}, M, rle::ACT_RELU, nullptr, false);
-          rle::View h1 = e.fwd(pg, N.layers[1], {{h0}}, M, rle::ACT_RELU, nullptr, false);
-          eg.out = e.fwd(pg, N.layers[2], {{h1}}, M, rle::ACT_NONE, nullptr, false);
+          eg.out = e.mlp_fwd(pg, N, {{eg.in0}, {eg.in1}}, M, rle::ACT_NONE);
         }
         eg.width = 1;
       } else {
         REQUIRE(N.kind == "sale_enc", "eval: ZS / ZSA need an encoder net");
         rle::View zs = e.enc_zs(pg, N, eg.in0, M);
         eg.out = what == RLE_EVAL_ZS ? e.normfwd(pg, zs) : e.enc_zsa(pg, N, zs, eg.in1, M);
-        eg.width = e.H;
+        eg.width = e.Z;
       }
       eg.G = e.capture(pg);
       it = e.eval_graphs.emplace(key, eg).first;
@@ -5311,7 +5421,7 @@ int rle_sac_rsample(rle_engine* h, const float* mean, const float* log_std, cons
                     float* log_pi) {
   return guard([&] {
     REQUIRE(h && mean && log_std && eps && action && log_pi && n > 0 && n <= 1024, "sac_rsample: bad args");
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     REQUIRE(e.algo == RLE_SAC, "sac_rsample: SAC engines only");
     HIPCHK(hipSetDevice(e.cfg.device));
     const int A = e.A;
@@ -5364,7 +5474,7 @@ int rle_sac_rsample(rle_engine* h, const float* mean, const float* log_std, cons
 
 int rle_get_info(rle_engine* h, int n, float* out) {
   return guard([&] {
-    Engine& e = *h->e;
+    Engine& e = drained(h);
     REQUIRE(out && n >= 0 && n <= e.info_cap, "get_info: 0 <= n <= info capacity (4096)");
     HIPCHK(hipStreamSynchronize(e.stream));
     HIPCHK(hipMemcpy(out, e.info, (size_t)n * rle::kInfoMax * sizeof(float), hipMemcpyDeviceToHost));
@@ -5372,7 +5482,7 @@ int rle_get_info(rle_engine* h, int n, float* out) {
 }
 
 int rle_synchronize(rle_engine* h) {
-  return guard([&] { HIPCHK(hipStreamSynchronize(h->e->stream)); });
+  return guard([&] { HIPCHK(hipStreamSynchronize(drained(h).stream)); });
 }
 
 }  // extern "C"

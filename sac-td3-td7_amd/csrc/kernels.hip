@@ -2901,7 +2901,7 @@ __device__ __forceinline__ void adam_scalars(long long t, float lr, GAS float* s
 // (SAC: the temperature terms, compiled into the TD3 / SAC and extended instances only)
 template <bool SAC>
 __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* smem, unsigned long long* tr) {
-  constexpr int kSums = kInfoMax + 1 + 9;  // info sums, logpi, grad-norm tensors
+  constexpr int kSums = kInfoMax + 1 + kGsqT;  // info sums, logpi, grad-norm tensors
   float* res = smem + kSums * kThreads;    // [kSums]
   float* vals = res + kSums;               // [kInfoMax]
   const float nanv = __int_as_float(0x7FC00000);
@@ -2952,7 +2952,8 @@ __device__ __forceinline__ void op_step_end(const CAS StepEndArgs& a, float* sme
   // quarters' first loads in flight together and 4 lists at once (one list at a time paid one
   // dependent round trip per list: 3-4 us of the op's ~7, the longest op of its level)
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int j = wave; j < kSums; j += 4) {
+  const int nsums = kInfoMax + 1 + (a.gsq ? a.ngsq_t : 0);  // (the lists in use)
+  for (int j = wave; j < nsums; j += 4) {
     // (mode 1 sums only the logpi list; mode 2 takes it from the scratch when there is one)
     if ((mode == 1 && j != kInfoMax) || (scr && j == kInfoMax)) continue;
     const float* p;

@@ -12,6 +12,8 @@ constexpr int kTileM = 16;      // GEMM output tile rows (v_mfma_f32_16x16x4_f32
 constexpr int kTileN = 64;      // widest GEMM output tile (GemmArgs::tn in {16, 32, 64})
 constexpr int kMaxSeg = 4;
 constexpr int kInfoMax = 8;     // floats per step in the info ring
+constexpr int kMaxHidden = 6;   // hidden layers of a TD3 / SAC MLP (rle.h RLE_MAX_HIDDEN)
+constexpr int kGsqT = 2 * (kMaxHidden + 1);  // TD3 actor tensors (weight, bias per layer) in norm/policy
 
 enum OpKind : int {
   OP_GEMM = 1,
@@ -474,7 +476,7 @@ struct StepEndArgs {
   float* log_alpha; float* la_m; float* la_v; long long* la_t; float la_lr; float target_entropy;
   float* adam_step; float* adam_bc2s; float adam_lr[4];  // (SAC autotune) slot 3: the temperature optimizer's bias corrections from this step's control op
   const float* logpi_part; int nlogpi; float inv_b;
-  const float* gsq; int gsq_off[9]; int ngsq_t;      // TD3 grad norm: tensor t = tiles [off[t], off[t+1])
+  const float* gsq; int gsq_off[kGsqT + 1]; int ngsq_t;  // TD3 grad norm: tensor t = tiles [off[t], off[t+1])
   // 0: the whole step end; 1: counters (+ the SAC temperature update, which needs the logpi sum)
   // -- what the next step depends on; 2: the info row -- what only the host reads, scheduled
   // wherever it is not the longest op.  sac_scratch: {alpha before the update, logpi sum},

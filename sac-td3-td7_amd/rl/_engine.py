@@ -39,7 +39,7 @@ class Config(ctypes.Structure):
         ("target_policy_noise", ctypes.c_float), ("noise_clip", ctypes.c_float),
         ("policy_freq", _int), ("target_update_rate", _int), ("min_log_std", ctypes.c_float),
         ("max_log_std", ctypes.c_float), ("tmp", ctypes.c_float), ("seed", ctypes.c_ulonglong),
-        ("device", _int),
+        ("device", _int), ("zs_dim", _int), ("n_hidden", _int), ("hidden_sizes", _int * 8),
     ]
 
 
@@ -501,7 +501,13 @@ class Engine:
 def make_config(algo, state_dim, action_dim, hidden, batch, use_lap=False, discount=0.99,
                 policy_lr=3e-4, critic_lr=3e-4, tau=0.005, target_policy_noise=0.2,
                 noise_clip=0.5, policy_freq=2, target_update_rate=250, min_log_std=-20.0,
-                max_log_std=2.0, tmp=-1.0, seed=0, device=0) -> Config:
-    return Config(algo, state_dim, action_dim, hidden, batch, int(use_lap), discount, policy_lr,
-                  critic_lr, tau, target_policy_noise, noise_clip, policy_freq, target_update_rate,
-                  min_log_std, max_log_std, tmp, seed, device)
+                max_log_std=2.0, tmp=-1.0, seed=0, device=0, zs_dim=0, hidden_sizes=None) -> Config:
+    """``hidden``: TD7 hdim, TD3 / SAC the width of both hidden layers; ``zs_dim`` (TD7, 0 = hidden) and
+    ``hidden_sizes`` (TD3 / SAC: make_mlp's list, 2..6 layers) give the other net shapes (include/rle.h)."""
+    hs = list(hidden_sizes) if hidden_sizes is not None else []
+    if hs and not 2 <= len(hs) <= 6:
+        raise ValueError(f"hidden_sizes {hs}: 2..6 hidden layers")
+    return Config(algo, state_dim, action_dim, hs[-1] if hs else hidden, batch, int(use_lap), discount,
+                  policy_lr, critic_lr, tau, target_policy_noise, noise_clip, policy_freq, target_update_rate,
+                  min_log_std, max_log_std, tmp, seed, device, zs_dim, len(hs),
+                  (_int * 8)(*(hs + [0] * (8 - len(hs)))))

@@ -195,6 +195,35 @@ def test_append_after_async_step_is_ordered():
         np.testing.assert_array_equal(ends[0][3][key], ends[1][3][key])
 
 
+def test_host_reads_after_async_step_see_the_whole_burst():
+    """rle_step_async leaves its levels in flight on the engine's own dispatch queue (direct AQL
+    dispatch, which no HIP stream or device synchronize covers): the replay's host reads
+    (priorities, max priority) and the engine's parameter reads issued right after it retire the
+    burst first and see the same state as after a synchronous rle_step."""
+    g = load_golden("td7_tiny")
+    alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
+    S, A, hi = spec.TASKS[env]
+    ends = []
+    for mode in ("sync", "async"):
+        eng, rep, _ = engine_from_golden(g)
+        if mode == "sync":
+            eng.step(12)
+        else:
+            eng.step_async(12)
+        prio = rep.get_priority()
+        mx = rep.state()[2]
+        eng.step_async(7)
+        params = {(n, p): eng.get_param(n, p) for n, d in spec.agent_params(alg, S, A, H, 0).items() for p in d}
+        eng.step_async(5)
+        idx = eng.last_indices()
+        ends.append((prio, mx, params, idx))
+    np.testing.assert_array_equal(ends[0][0], ends[1][0])
+    assert ends[0][1] == ends[1][1]
+    for key in ends[0][2]:
+        np.testing.assert_array_equal(ends[0][2][key], ends[1][2][key])
+    np.testing.assert_array_equal(ends[0][3], ends[1][3])
+
+
 def test_update_priority_below_one_keeps_sampling_exact():
     """Priorities < 1 written through update_priority (allowed by lap.py:66-69) recompute the
     block sums: the sampler then agrees with the searchsorted law on the new vector."""
