@@ -104,7 +104,11 @@ typedef struct rle_plan {
                                 (-1: 60, 60, SAC 16 / else 8)                                             */
   int wide;             /* 64 / 32: forward / input-gradient GEMMs over >= 64 rows as 64 x 64 / 64 x 32 tiles with
                            every W chunk staged once in LDS for the tile's four 16-row blocks (kernels.hip
-                           gemm_wide; 1 = 64; 0 off; -1: default, TD7 at batch >= 512)                     */
+                           gemm_wide; 1 = 64; 0 off; -1: default = off, slower than the 16-row tiles as
+                           measured)                                                     */
+  int lpt;              /* 1: each level's ops in its launch ordered longest first (estimated workgroup time),
+                           so a level with more workgroups than the device holds dispatches its long tiles in
+                           the first round; 0: program order; -1: default                               */
 } rle_plan;
 
 /* ---- replay memory: rl/replay_memory/{lap,simple}.py ---------------------- */
@@ -222,9 +226,9 @@ int rle_set_action_map(rle_engine* e, const float* scale, const float* bias, flo
  *                 on zs = encode_state(s), zsa = encode_state_action(zs, a) of encoder `enc`
  *                 (online critics use "fixed_encoder", target critics "fixed_encoder_target",
  *                 td7.py:175-230); TD3/SAC (MLPCritic, mlp.py:98-101) ignore `enc`.
- *   RLE_EVAL_ZS:  encoder `net`'s encode_state(s) (sale.py:41-46) -> out [n][hidden] (a unused).
+ *   RLE_EVAL_ZS:  encoder `net`'s encode_state(s) (sale.py:41-46) -> out [n][zs_dim] (a unused).
  *   RLE_EVAL_ZSA: encoder `net`'s encode_state_action(encode_state(s), a) (sale.py:48-55)
- *                 -> out [n][hidden].
+ *                 -> out [n][zs_dim].
  * Runs on the engine's stream after any enqueued step; syncs. */
 #define RLE_EVAL_Q 0
 #define RLE_EVAL_ZS 1

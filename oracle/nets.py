@@ -55,10 +55,14 @@ def sale_critic(p, s, a, zsa, zs):
 # --- MLP nets (rl/nn/mlp.py) -------------------------------------------------
 
 def mlp(p, x):
-    """make_mlp: Linear-ReLU-Linear-ReLU-Linear (mlp.py:10-35)."""
-    h = F.relu(_lin(x, p, "mlp.0"))
-    h = F.relu(_lin(h, p, "mlp.2"))
-    return _lin(h, p, "mlp.4")
+    """make_mlp: Linear-ReLU-...-Linear at nn.Sequential indices 0, 2, 4, ... (mlp.py:10-35)."""
+    n = sum(1 for k in p if k.startswith("mlp.") and k.endswith(".weight"))
+    h = x
+    for i in range(n):
+        h = _lin(h, p, f"mlp.{2 * i}")
+        if i + 1 < n:
+            h = F.relu(h)
+    return h
 
 
 def mlp_critic(p, s, a):

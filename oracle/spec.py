@@ -58,34 +58,39 @@ def sale_critic_spec(S, A, Z=256, H=256):
 
 
 def mlp_spec(inp, out, H=256):
-    """make_mlp with hidden [H, H] (rl/nn/mlp.py:10-35)."""
-    return [
-        ("mlp.0.weight", (H, inp)), ("mlp.0.bias", (H,)),
-        ("mlp.2.weight", (H, H)), ("mlp.2.bias", (H,)),
-        ("mlp.4.weight", (out, H)), ("mlp.4.bias", (out,)),
-    ]
+    """make_mlp (rl/nn/mlp.py:10-35): hidden_sizes H (an int: [H, H], mlp.py:45-47); Linear layers at
+    nn.Sequential indices 0, 2, 4, ... (a ReLU after each but the last)."""
+    hs = [H, H] if isinstance(H, int) else list(H)
+    dims = [inp] + hs + [out]
+    out_spec = []
+    for i in range(len(dims) - 1):
+        out_spec += [(f"mlp.{2 * i}.weight", (dims[i + 1], dims[i])), (f"mlp.{2 * i}.bias", (dims[i + 1],))]
+    return out_spec
 
 
-def agent_specs(alg: str, S: int, A: int, H: int = 256) -> dict:
-    """Net name -> param spec for the trainable nets of one agent."""
+def agent_specs(alg: str, S: int, A: int, H: int = 256, hidden_sizes=None, zs_dim=None) -> dict:
+    """Net name -> param spec for the trainable nets of one agent.  TD7: hdim H, zs_dim (default H,
+    sale.py:19-26); TD3 / SAC: make_mlp's hidden_sizes (default [H, H])."""
     if alg == "td7":
+        Z = H if zs_dim is None else zs_dim
         return {
-            "encoder": sale_encoder_spec(S, A, H, H),
-            "policy": sale_actor_spec(S, A, H, H),
-            "q1": sale_critic_spec(S, A, H, H),
-            "q2": sale_critic_spec(S, A, H, H),
+            "encoder": sale_encoder_spec(S, A, Z, H),
+            "policy": sale_actor_spec(S, A, Z, H),
+            "q1": sale_critic_spec(S, A, Z, H),
+            "q2": sale_critic_spec(S, A, Z, H),
         }
+    hs = [H, H] if hidden_sizes is None else list(hidden_sizes)
     if alg == "td3":
         return {
-            "policy": mlp_spec(S, A, H),
-            "q1": mlp_spec(S + A, 1, H),
-            "q2": mlp_spec(S + A, 1, H),
+            "policy": mlp_spec(S, A, hs),
+            "q1": mlp_spec(S + A, 1, hs),
+            "q2": mlp_spec(S + A, 1, hs),
         }
     if alg == "sac":
         return {
-            "policy": mlp_spec(S, 2 * A, H),
-            "q1": mlp_spec(S + A, 1, H),
-            "q2": mlp_spec(S + A, 1, H),
+            "policy": mlp_spec(S, 2 * A, hs),
+            "q1": mlp_spec(S + A, 1, hs),
+            "q2": mlp_spec(S + A, 1, hs),
         }
     raise ValueError(alg)
 
@@ -118,9 +123,9 @@ def gen_params(spec, seed: int, scale: float = 1.0) -> dict:
     return out
 
 
-def agent_params(alg: str, S: int, A: int, H: int, seed: int) -> dict:
+def agent_params(alg: str, S: int, A: int, H: int, seed: int, hidden_sizes=None, zs_dim=None) -> dict:
     """All nets (trainable + copies) of one agent: net -> {param: array}."""
-    specs = agent_specs(alg, S, A, H)
+    specs = agent_specs(alg, S, A, H, hidden_sizes, zs_dim)
     nets = {}
     for i, (name, spec) in enumerate(specs.items()):
         nets[name] = gen_params(spec, seed * 1000 + i)

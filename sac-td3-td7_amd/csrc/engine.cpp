@@ -1127,22 +1127,24 @@ struct Prog {
   int tiny_w = 30, uni_w = 60, tiny_wg = 2;
   int pl_w = 0;  // (rle_plan pl_w) added to GEMMs whose workgroups run an in-tile prologue (has_pre 3-5)
   int lap_w = 60, head_w = 60, adam_w = 8;  // (rle_plan lap_w / head_w / adam_w)
+  int lpt = 0;                              // (rle_plan lpt: longest-first op order in each level)
   int tiny_weight() const { return tiny_w ? tiny_w : 8; }
   int uniform_weight() const { return uni_w; }
   bool tiny_moves() const { return tiny_w != 0; }
+  int op_weight(const Op& op) const {
+    int x = 8;
+    if (op.kind == OP_GEMM)
+      x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? adam_w : 0) + (op.gemm.has_pre >= 3 ? pl_w : 0);
+    else if (op.kind == OP_HEAD) x = head_w;
+    else if (op.kind == OP_SAMPLE_GATHER) x = op.sample.lap ? lap_w : uniform_weight();  // (uniform: a
+                                                                                       // ~6 us gather)
+    else if (op.kind == OP_STEP_END && op.end.mode != 1) x = tiny_weight();  // (one workgroup, ~4 KB of straight-line
+                                                         // code fetched at L2 latency: 7-8 us)
+    return x;
+  }
   int item_weight(const Item& it) const {
     int w = 0;
-    for (const Op& op : it.ops) {
-      int x = 8;
-      if (op.kind == OP_GEMM)
-        x = op.gemm.R * op.gemm.tn / 1024 + (op.gemm.epi == EPI_ADAM ? adam_w : 0) + (op.gemm.has_pre >= 3 ? pl_w : 0);
-      else if (op.kind == OP_HEAD) x = head_w;
-      else if (op.kind == OP_SAMPLE_GATHER) x = op.sample.lap ? lap_w : uniform_weight();  // (uniform: a
-                                                                                         // ~6 us gather)
-      else if (op.kind == OP_STEP_END && op.end.mode != 1) x = tiny_weight();  // (one workgroup, ~4 KB of straight-line
-                                                           // code fetched at L2 latency: 7-8 us)
-      w = std::max(w, x);
-    }
+    for (const Op& op : it.ops) w = std::max(w, op_weight(op));
     return w;
   }
   // After the ASAP pass: in reverse program order, move each item with slack (every
@@ -1273,6 +1275,24 @@ struct Prog {
         owner[items[i].level].push_back((int)i);
         crit_lv[items[i].level].push_back(crit.empty() ? 0 : crit[i]);
       }
+    if (lpt)  // longest first (rle_plan lpt): a stable sort of each level by the estimated workgroup time
+      for (size_t l = 0; l < levels.size(); ++l) {
+        std::vector<int> ix(levels[l].size());
+        for (size_t k = 0; k < ix.size(); ++k) ix[k] = (int)k;
+        std::stable_sort(ix.begin(), ix.end(),
+                         [&](int a, int b) { return op_weight(levels[l][a]) > op_weight(levels[l][b]); });
+        std::vector<Op> lv;
+        std::vector<int> ow;
+        std::vector<char> cr;
+        for (int k : ix) {
+          lv.push_back(levels[l][k]);
+          ow.push_back(owner[l][k]);
+          cr.push_back(crit_lv[l][k]);
+        }
+        levels[l].swap(lv);
+        owner[l].swap(ow);
+        crit_lv[l].swap(cr);
+      }
     if (const char* hz = std::getenv("RLE_HAZARD"); hz && hz[0] == '1')
       for (size_t l = 0; l < levels.size(); ++l) level_hazards(levels[l], owner[l], (int)l);
     for (auto& lv : levels) {
@@ -1292,13 +1312,26 @@ struct Prog {
 // 2 system; default agent / agent, as HIP's own).  The first packet of a flush acquires and its
 // last releases at system scope (host-written inputs, host-read results).  tools/mbaql.cpp
 // measured the same packets at 3.83 us per level against hipGraph's 4.08.
-struct AqlQueue {
+// One HSA queue of a device, shared by the engines aql_open hands it to (at most kAqlQueuesPerDevice
+// per device and process: more user-mode queues than that oversubscribe the device's hardware queue
+// slots, and every queue's dispatches slow down -- profiles/r05_seeds_aql.txt, r05_seeds_hwq.txt).
+// mu: one burst's packets and doorbells at a time (engines driven from several threads).
+struct AqlHw {
   hsa_agent_t agent{};
   hsa_queue_t* q = nullptr;
-  hsa_signal_t sig{};
   uint64_t kobj[KS_COUNT] = {};  // rle_level<false, ks>
   uint32_t gseg[KS_COUNT] = {}, pseg[KS_COUNT] = {};
   int acq = HSA_FENCE_SCOPE_AGENT, rel = HSA_FENCE_SCOPE_AGENT;
+  std::mutex mu;
+  ~AqlHw() {
+    if (q) (void)hsa_queue_destroy(q);
+  }
+};
+constexpr int kAqlQueuesPerDevice = 4;
+// An engine's view of its queue: its own completion signal, pending packets and timing.
+struct AqlQueue {
+  std::shared_ptr<AqlHw> hw;
+  hsa_signal_t sig{};
   struct Pending {
     const void* ka;
     unsigned grid;
@@ -1310,7 +1343,6 @@ struct AqlQueue {
   size_t inflight = 0;          // packets submitted since the last aql_complete
   std::chrono::steady_clock::time_point t0{};  // first doorbell of the oldest burst in flight
   ~AqlQueue() {
-    if (q) (void)hsa_queue_destroy(q);
     if (sig.handle) (void)hsa_signal_destroy(sig);
   }
 };
@@ -1352,8 +1384,8 @@ static hsa_status_t aql_find_kernel(hsa_executable_t exe, void* data) {
 }
 
 // The queue of device `dev`, after HIP has loaded librle's code object (any rle_level launch).
-static std::unique_ptr<AqlQueue> aql_open(int dev) {
-  auto A = std::make_unique<AqlQueue>();
+static std::shared_ptr<AqlHw> aql_hw_create(int dev) {
+  auto A = std::make_shared<AqlHw>();
   HSACHK(hsa_init());
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, dev));
@@ -1375,10 +1407,33 @@ static std::unique_ptr<AqlQueue> aql_open(int dev) {
   HSACHK(hsa_agent_get_info(A->agent, HSA_AGENT_INFO_QUEUE_MAX_SIZE, &qmax));
   HSACHK(hsa_queue_create(A->agent, std::min<uint32_t>(qmax, 16384), HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
                           UINT32_MAX, UINT32_MAX, &A->q));
-  HSACHK(hsa_signal_create(0, 0, nullptr, &A->sig));  // (bursts in flight: aql_submit)
   auto scope = [](const char* v, int d) { return v ? std::max(0, std::min(2, std::atoi(v))) : d; };
   A->acq = scope(std::getenv("RLE_AQL_ACQ"), HSA_FENCE_SCOPE_AGENT);
   A->rel = scope(std::getenv("RLE_AQL_REL"), HSA_FENCE_SCOPE_AGENT);
+  return A;
+}
+// The engine's queue: a new HSA queue while the device has fewer than kAqlQueuesPerDevice live ones,
+// else the live one with the fewest engines (its bursts then run in submission order with theirs).
+static std::unique_ptr<AqlQueue> aql_open(int dev) {
+  static std::mutex pool_mu;
+  static std::map<int, std::vector<std::weak_ptr<AqlHw>>> pool;
+  auto A = std::make_unique<AqlQueue>();
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    auto& live = pool[dev];
+    live.erase(std::remove_if(live.begin(), live.end(), [](const std::weak_ptr<AqlHw>& w) { return w.expired(); }),
+               live.end());
+    if ((int)live.size() < kAqlQueuesPerDevice) {
+      A->hw = aql_hw_create(dev);
+      live.push_back(A->hw);
+    } else {
+      for (auto& w : live) {
+        auto h = w.lock();
+        if (h && (!A->hw || h.use_count() < A->hw.use_count())) A->hw = h;
+      }
+    }
+  }
+  HSACHK(hsa_signal_create(0, 0, nullptr, &A->sig));  // (bursts in flight: aql_submit)
   return A;
 }
 
@@ -1424,8 +1479,10 @@ static void aql_submit(AqlQueue& A) {
     A.pending.clear();
     throw Error{RLE_EHIP, "aql: the engine's queue is closed after a timed-out dispatch"};
   }
+  AqlHw& hw = *A.hw;
+  std::lock_guard<std::mutex> lk(hw.mu);
   hsa_signal_add_relaxed(A.sig, 1);
-  hsa_queue_t* q = A.q;
+  hsa_queue_t* q = hw.q;
   const uint64_t mask = q->size - 1;
   bool rung = false;
   for (size_t i = 0; i < n; ++i) {
@@ -1447,14 +1504,14 @@ static void aql_submit(AqlQueue& A) {
     pk->grid_size_y = 1;
     pk->grid_size_z = 1;
     const int x = A.pending[i].ks;
-    pk->private_segment_size = A.pseg[x];
-    pk->group_segment_size = A.gseg[x];
-    pk->kernel_object = A.kobj[x];
+    pk->private_segment_size = hw.pseg[x];
+    pk->group_segment_size = hw.gseg[x];
+    pk->kernel_object = hw.kobj[x];
     pk->kernarg_address = const_cast<void*>(A.pending[i].ka);
     pk->reserved2 = 0;
     const bool last = i + 1 == n;
     pk->completion_signal = last ? A.sig : hsa_signal_t{0};
-    const int a = i == 0 ? HSA_FENCE_SCOPE_SYSTEM : A.acq, r = last ? HSA_FENCE_SCOPE_SYSTEM : A.rel;
+    const int a = i == 0 ? HSA_FENCE_SCOPE_SYSTEM : hw.acq, r = last ? HSA_FENCE_SCOPE_SYSTEM : hw.rel;
     const uint16_t hdr = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
                          (a << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) | (r << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
     __atomic_store_n((uint32_t*)pk, (uint32_t)hdr | (1u << 16), __ATOMIC_RELEASE);  // header | setup (1 dim)
@@ -1471,7 +1528,7 @@ static void aql_submit(AqlQueue& A) {
 // oldest burst in flight to completion added to *ms when given).
 static void aql_complete(AqlQueue& A, double* ms) {
   if (!A.inflight) return;
-  hsa_queue_t* q = A.q;
+  hsa_queue_t* q = A.hw->q;
   // (the packets not yet retired: those behind the read index)
   const double left = (double)(hsa_queue_load_write_index_relaxed(q) - hsa_queue_load_read_index_scacquire(q));
   aql_wait(A, [&] { return hsa_signal_load_scacquire(A.sig) < 1; }, left * A.us_per_launch, "a dispatch");
@@ -1540,6 +1597,7 @@ static rle_plan plan_defaults() {
   p.pl_w = -1;
   p.lap_w = p.head_w = p.adam_w = -1;
   p.wide = -1;
+  p.lpt = -1;
   return p;
 }
 
@@ -1579,6 +1637,8 @@ struct Engine {
     // MFMAs bound the B >= 512 levels, DESIGN round 5; with them the register-blocked weight-gradient tiles, the
     // batch split over the 4 waves, where a 16 x 64 weight-gradient tile's waves would each reduce all B rows)
     if (plan.wide < 0) plan.wide = 0;  // (opt-in: slower at B = 1024 than the 16-row tiles, DESIGN round 5)
+    if (plan.lpt < 0) plan.lpt = 0;
+    plan.lpt = plan.lpt ? 1 : 0;
     plan.rb = plan.rb < 0 ? (plan.wide ? 1 : 0) : (plan.rb ? 1 : 0);
     // (A/B, 2 pairs: SAC Humanoid pl_w 0 / 8 / 16 / 24 -> 14.09k / 14.09k / 14.11k / 14.15k; TD3 HalfCheetah
     // 25.37k / 25.33k / 25.38k / 25.36k)
@@ -3898,6 +3958,7 @@ struct Engine {
     pg.lap_w = plan.lap_w;
     pg.head_w = plan.head_w;
     pg.adam_w = plan.adam_w;
+    pg.lpt = plan.lpt;
     auto levels = pg.schedule(sched_cap());
     Graph G;
     size_t total = 0;

@@ -51,7 +51,7 @@ class Plan(ctypes.Structure):
         ("level_cap", _int), ("steps_per_graph", _int), ("pre_tn", _int), ("pl_tn", _int), ("tn_min", _int),
         ("flat_div", _int), ("balance", _int), ("tiny_w", _int), ("uni_w", _int), ("tiny_wg", _int),
         ("sched_cap", _int), ("fuse_off", ctypes.c_uint), ("fuse_on", ctypes.c_uint), ("rb", _int),
-        ("pl_w", _int), ("lap_w", _int), ("head_w", _int), ("adam_w", _int), ("wide", _int),
+        ("pl_w", _int), ("lap_w", _int), ("head_w", _int), ("adam_w", _int), ("wide", _int), ("lpt", _int),
     ]
 
 
@@ -432,19 +432,19 @@ class Engine:
         return out
 
     def eval_zs(self, enc, s):
-        """encode_state of encoder `enc` (TD7) -> [n][hidden]."""
+        """encode_state of encoder `enc` (TD7) -> [n][zs_dim]."""
         s = _f32(s)
         n = s.shape[0]
-        out = np.empty((n, self.cfg.hidden), np.float32)
+        out = np.empty((n, self.cfg.zs_dim or self.cfg.hidden), np.float32)
         _check(lib().rle_eval(self.h, RLE_EVAL_ZS, enc.encode(), None, _fp(s), None, n, _fp(out)))
         return out
 
     def eval_zsa(self, enc, s, a):
-        """encode_state_action(encode_state(s), a) of encoder `enc` (TD7) -> [n][hidden]."""
+        """encode_state_action(encode_state(s), a) of encoder `enc` (TD7) -> [n][zs_dim]."""
         s = _f32(s)
         n = s.shape[0]
         a = _f32(a, (n, self.cfg.action_dim))
-        out = np.empty((n, self.cfg.hidden), np.float32)
+        out = np.empty((n, self.cfg.zs_dim or self.cfg.hidden), np.float32)
         _check(lib().rle_eval(self.h, RLE_EVAL_ZSA, enc.encode(), None, _fp(s), _fp(a), n, _fp(out)))
         return out
 

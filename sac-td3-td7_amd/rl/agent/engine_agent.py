@@ -45,22 +45,37 @@ class EngineAgent(Agent, Sampler):
 
     def _setup(self, env_id, *, hidden, batch_size, seed, device, make_nn, make_nn_kwargs, cfg):
         custom = None
+        shape = {}  # net shapes beyond the defaults: zs_dim (SALE), hidden_sizes (make_mlp)
         if make_nn is not None:  # td7.py:56-61 / td3.py:53-56 / sac.py:47-50 (rl.nn.modules nets only)
             from rl.nn.modules import nets_from_make_nn
 
             S, A = get_state_action_dims(env_id)
-            hidden, custom = nets_from_make_nn(self.ALG, make_nn, S, A, make_nn_kwargs)
+            hidden, shape, custom = nets_from_make_nn(self.ALG, make_nn, S, A, make_nn_kwargs)
             make_nn_kwargs = {}
-        hdim = make_nn_kwargs.pop("hdim", None) or make_nn_kwargs.pop("zs_dim", None)
+        hdim = make_nn_kwargs.pop("hdim", None)
+        zs = make_nn_kwargs.pop("zs_dim", None)
         hs = make_nn_kwargs.pop("hidden_sizes", None)
         if make_nn_kwargs:
             raise TypeError(f"unsupported arguments {sorted(make_nn_kwargs)}")
-        if hs is not None:
-            if len(set(hs)) != 1 or len(hs) != 2:
-                raise NotImplementedError("make_mlp with two equal hidden layers only (mlp.py:45)")
-            hidden = hs[0]
-        if hdim is not None:
-            hidden = hdim
+        if self.ALG == "td7":
+            if hs is not None:
+                raise TypeError("hidden_sizes is a make_mlp argument (TD3 / SAC); TD7 takes hdim / zs_dim")
+            if hdim is not None:
+                hidden = hdim
+            if zs is not None and int(zs) != int(hidden):
+                shape["zs_dim"] = int(zs)
+        else:
+            if hdim is not None or zs is not None:
+                raise TypeError("hdim / zs_dim are SALE arguments (TD7); TD3 / SAC take hidden_sizes")
+            if hs is not None:
+                from rl.nn.modules import _sizes
+
+                hs = _sizes(hs)
+                shape["hidden_sizes"] = [int(h) for h in hs]
+                hidden = hs[-1]
+        if shape.get("hidden_sizes") == [int(hidden)] * 2:
+            shape = {}  # (the default shape)
+        self.shape = shape
         self.env_id = env_id
         self.state_dim, self.action_dim = get_state_action_dims(env_id)
         self.action_bias, self.action_scale = get_action_bias_scale(env_id)
@@ -80,13 +95,13 @@ class EngineAgent(Agent, Sampler):
             for name, src in AGENT_COPIES[self.ALG].items():
                 nets[name] = {k: v.copy() for k, v in custom[src].items()}
         else:
-            nets = init_agent(self.ALG, self.state_dim, self.action_dim, self.hidden, self.seed)
+            nets = init_agent(self.ALG, self.state_dim, self.action_dim, self.hidden, self.seed, **self.shape)
         self._import({"params": nets})
 
     # ---- engine lifecycle ----------------------------------------------------
     def _new_engine(self, batch):
         c = E.make_config(self.ALGO, self.state_dim, self.action_dim, self.hidden, batch, seed=self.seed,
-                          device=self._device, **self._cfg)
+                          device=self._device, **self._cfg, **self.shape)
         return E.Engine(c)
 
     @property
@@ -122,7 +137,7 @@ class EngineAgent(Agent, Sampler):
         for net, kind in AGENT_NETS[self.ALG].items():
             o = 2 * self.action_dim if (self.ALG == "sac" and net == "policy") else None
             names = []
-            for prefix, fin, fout in layers(kind, self.state_dim, self.action_dim, self.hidden, o):
+            for prefix, fin, fout in layers(kind, self.state_dim, self.action_dim, self.hidden, o, **self.shape):
                 names += [(prefix + ".weight", (fout, fin)), (prefix + ".bias", (fout,))]
             out.append((net, names))
             for copy, src in AGENT_COPIES[self.ALG].items():

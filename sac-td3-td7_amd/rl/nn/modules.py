@@ -14,7 +14,7 @@ import torch
 from torch import nn
 from torch.nn import functional as F
 
-from rl.nn.layout import MLP, SALE_ACTOR, SALE_CRITIC, SALE_ENCODER, _dim
+from rl.nn.layout import SALE_ACTOR, SALE_CRITIC, SALE_ENCODER, _dim
 
 
 def avg_l1_norm(x: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
@@ -73,10 +73,13 @@ class SALECritic(_Linears):
 
 
 def _mlp(fin: int, fout: int, hidden_sizes) -> nn.Sequential:
-    """make_mlp (mlp.py:10-35): Linear-ReLU-Linear-ReLU-Linear, xavier_normal weights, zero bias."""
-    h0, h1 = hidden_sizes
-    assert len(MLP) == 3  # (the layout's nn.Sequential indices 0 / 2 / 4)
-    seq = nn.Sequential(nn.Linear(fin, h0), nn.ReLU(), nn.Linear(h0, h1), nn.ReLU(), nn.Linear(h1, fout))
+    """make_mlp (mlp.py:10-35): Linear-ReLU-...-Linear (indices 0, 2, 4, ...), xavier_normal weights,
+    zero bias."""
+    dims = [fin] + list(hidden_sizes) + [fout]
+    mods = []
+    for i in range(len(dims) - 1):
+        mods += [nn.Linear(dims[i], dims[i + 1]), nn.ReLU()]
+    seq = nn.Sequential(*mods[:-1])
     for m in seq:
         if isinstance(m, nn.Linear):
             nn.init.xavier_normal_(m.weight)
@@ -86,8 +89,8 @@ def _mlp(fin: int, fout: int, hidden_sizes) -> nn.Sequential:
 
 def _sizes(hidden_sizes):
     sizes = [hidden_sizes] * 2 if isinstance(hidden_sizes, int) else list(hidden_sizes)
-    if len(sizes) != 2:  # (make_mlp takes any depth, mlp.py:10-35; the engine's step programs have two)
-        raise NotImplementedError(f"hidden_sizes {sizes}: the engine builds MLPs of two hidden layers")
+    if not 2 <= len(sizes) <= 6:  # (make_mlp takes any depth, mlp.py:10-35; the engine builds 2..6, rle.h)
+        raise NotImplementedError(f"hidden_sizes {sizes}: the engine builds MLPs of 2 to 6 hidden layers")
     return sizes
 
 
@@ -124,9 +127,10 @@ class MLPCritic(nn.Module):
 
 def nets_from_make_nn(alg: str, make_nn, state_dim: int, action_dim: int, kwargs: dict):
     """Call a reference-style make_nn hook (state_dim / action_dim passed as keywords, as
-    annotate_make_nn does) and return (hidden width, {net name: numpy state_dict}) for the
-    engine.  Only this module's classes (the reference's default net types) are accepted, with
-    one width throughout: hdim == zs_dim (SALE), two equal hidden sizes (MLP)."""
+    annotate_make_nn does) and return (hidden width, net shape, {net name: numpy state_dict}) for
+    the engine.  Only this module's classes (the reference's default net types) are accepted, with
+    one shape across the agent's nets: (hdim, zs_dim) of the SALE nets, hidden_sizes of the MLPs
+    (the shape is {"zs_dim": ...} or {"hidden_sizes": [...]}, as rle_config takes them)."""
     import numpy as np
 
     kw = dict(kwargs)
@@ -149,13 +153,16 @@ def nets_from_make_nn(alg: str, make_nn, state_dim: int, action_dim: int, kwargs
             if m.activ is not want:
                 raise NotImplementedError(f"{name}: activation {getattr(m.activ, '__name__', m.activ)}, the engine "
                                           f"runs {want.__name__}")
-            widths.update({m.hdim, m.zs_dim})
+            widths.add((m.hdim, m.zs_dim))
         else:
-            widths.update(m.hidden_sizes)
+            widths.add(tuple(m.hidden_sizes))
         want_out = 2 * action_dim if (alg == "sac" and name == "policy") else (action_dim if name == "policy" else None)
         if want_out is not None and getattr(m, "action_dim", want_out) != want_out:
             raise ValueError(f"{name}: output width {m.action_dim}, expected {want_out}")
         nets[name] = {k: v.detach().cpu().numpy().astype(np.float32) for k, v in m.state_dict().items()}
     if len(widths) != 1:
-        raise NotImplementedError(f"one hidden width throughout (got {sorted(widths)})")
-    return widths.pop(), nets
+        raise NotImplementedError(f"one net shape across the agent's nets (got {sorted(widths)})")
+    w = widths.pop()
+    if alg == "td7":
+        return w[0], {"zs_dim": w[1]}, nets
+    return w[-1], {"hidden_sizes": list(w)}, nets

@@ -24,3 +24,14 @@ def load_golden(name):
 @pytest.fixture
 def golden():
     return load_golden
+
+
+def shape_of(g):
+    """Net shapes beyond the defaults a golden was made with (make_golden.py ``shape``): make_mlp's
+    hidden_sizes (TD3 / SAC) or SALE's zs_dim (TD7); {} for the default nets."""
+    out = {}
+    if "meta_hidden" in g:
+        out["hidden_sizes"] = [int(x) for x in g["meta_hidden"]]
+    if "meta_zs" in g:
+        out["zs_dim"] = int(g["meta_zs"])
+    return out

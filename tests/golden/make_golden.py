@@ -100,22 +100,27 @@ def dump_net(module):
     return {k: v.detach().cpu().numpy().copy() for k, v in module.state_dict().items()}
 
 
-def make_agent(alg, env_id, H, use_lap, extra):
-    S, A, _ = spec.TASKS[env_id]
+def make_agent(alg, env_id, H, use_lap, extra, shape=None):
+    """The reference agent with its nets built through its own make_nn hook (td7.py:46-61,
+    td3.py:44-58, sac.py:40-52): SALE nets with zs_dim / hdim, MLPs with make_mlp's hidden_sizes."""
+    shape = shape or {}
     if alg == "td7":
+        Z = shape.get("zs_dim", H)
+
         def mk(state_dim, action_dim, **kw):
-            return (SALEActor(state_dim, action_dim, H, H), SALECritic(state_dim, action_dim, H, H),
-                    SALECritic(state_dim, action_dim, H, H), SALEEncoder(state_dim, action_dim, H, H))
+            return (SALEActor(state_dim, action_dim, Z, H), SALECritic(state_dim, action_dim, Z, H),
+                    SALECritic(state_dim, action_dim, Z, H), SALEEncoder(state_dim, action_dim, Z, H))
         return TD7(env_id, use_lap=use_lap, make_nn=mk, **extra)
+    hs = shape.get("hidden_sizes", H)
     if alg == "td3":
         def mk(state_dim, action_dim, **kw):
-            return (MLPActor(state_dim, action_dim, H), MLPCritic(state_dim, action_dim, H),
-                    MLPCritic(state_dim, action_dim, H))
+            return (MLPActor(state_dim, action_dim, hs), MLPCritic(state_dim, action_dim, hs),
+                    MLPCritic(state_dim, action_dim, hs))
         return TD3(env_id, use_lap=use_lap, make_nn=mk, **extra)
     if alg == "sac":
         def mk(state_dim, action_dim, **kw):
-            return (MLPActor(state_dim, 2 * action_dim, H), MLPCritic(state_dim, action_dim, H),
-                    MLPCritic(state_dim, action_dim, H))
+            return (MLPActor(state_dim, 2 * action_dim, hs), MLPCritic(state_dim, action_dim, hs),
+                    MLPCritic(state_dim, action_dim, hs))
         return SAC(env_id, make_nn=mk, **extra)
     raise ValueError(alg)
 
@@ -199,13 +204,14 @@ ONLY = set(sys.argv[1:])  # optional fixture names to (re)generate; default: all
 
 
 def run_config(name, alg, env_id, H, B, N, n_fill, n_steps, use_lap, seed, extra=None,
-               full=True, sparse_prio=False, adam_steps=2):
+               full=True, sparse_prio=False, adam_steps=2, shape=None):
     if ONLY and name not in ONLY:
         return
     extra = dict(extra or {})
+    shape = dict(shape or {})
     S, A, hi = spec.TASKS[env_id]
-    nets = spec.agent_params(alg, S, A, H, seed)
-    agent = make_agent(alg, env_id, H, use_lap, extra)
+    nets = spec.agent_params(alg, S, A, H, seed, **shape)
+    agent = make_agent(alg, env_id, H, use_lap, extra, shape)
     inject(agent, alg, nets)
     lap = use_lap
     replay = (LAPReplayMemory if lap else SimpleReplayMemory)(N, env_id)
@@ -224,6 +230,10 @@ def run_config(name, alg, env_id, H, B, N, n_fill, n_steps, use_lap, seed, extra
            "meta": np.array([H, B, N, n_fill, n_steps, int(use_lap), seed]),
            "meta_extra_keys": np.array(list(extra.keys()), dtype=object).astype(str),
            "meta_extra_vals": np.array([float(v) for v in extra.values()])}
+    if "hidden_sizes" in shape:  # (net shapes beyond the defaults: tests/conftest.py shape_of)
+        res["meta_hidden"] = np.array(shape["hidden_sizes"], dtype=np.int64)
+    if "zs_dim" in shape:
+        res["meta_zs"] = np.array(shape["zs_dim"], dtype=np.int64)
     for k, v in tp.items():
         res["tape_" + k] = v
 
@@ -363,6 +373,14 @@ def main():
     run_config("sac_tiny", "sac", "Tiny-v0", 32, 16, 64, 50, 6, False, 9)
     # fixed temperature (sac.py:55-60: tmp >= 0 is a float; no temperature loss or optimizer)
     run_config("sac_tiny_fixed", "sac", "Tiny-v0", 32, 16, 64, 50, 6, False, 10, extra={"tmp": 0.2})
+    # Net shapes beyond the defaults, through make_nn: make_mlp with three hidden layers of unequal
+    # widths (mlp.py:10-35; H = the last width), SALE nets with zs_dim != hdim (sale.py:19-26)
+    run_config("td3_tiny_deep", "td3", "Tiny-v0", 32, 16, 64, 50, 6, False, 14,
+               shape={"hidden_sizes": [32, 48, 32]})
+    run_config("sac_tiny_deep", "sac", "Tiny-v0", 32, 16, 64, 50, 6, False, 15,
+               shape={"hidden_sizes": [48, 32, 32]})
+    run_config("td7_tiny_zs", "td7", "Tiny-v0", 256, 16, 64, 50, 8, True, 16,
+               extra={"target_update_rate": 4}, shape={"zs_dim": 128}, full=False)
     # Full-size digests at the BASELINE configs' shapes.
     run_config("td7_humanoid", "td7", "Humanoid-v4", 256, 256, 2048, 2048, 3, True, 41,
                full=False)

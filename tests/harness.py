@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import numpy as np
 
+from conftest import shape_of  # noqa: F401  (re-exported for the tests)
 from oracle import spec
 from rl import _engine as E
 
@@ -36,9 +37,10 @@ def engine_from_golden(g, device=0, plan=None):
         kw["target_update_rate"] = int(extra["target_update_rate"])
     if "tmp" in extra:  # SAC fixed temperature (sac.py:55-60)
         kw["tmp"] = float(extra["tmp"])
-    cfg = E.make_config(ALGO[alg], S, A, H, B, use_lap=use_lap, seed=seed, device=device, **kw)
+    shape = shape_of(g)
+    cfg = E.make_config(ALGO[alg], S, A, H, B, use_lap=use_lap, seed=seed, device=device, **kw, **shape)
     eng = E.Engine(cfg, plan)
-    for net, params in spec.agent_params(alg, S, A, H, seed).items():
+    for net, params in spec.agent_params(alg, S, A, H, seed, **shape).items():
         for name, v in params.items():
             eng.set_param(net, name, v)
     rep = E.Replay(Ncap, S, A, use_lap, device)

@@ -108,13 +108,14 @@ def _fwd_check(name):
 
 
 @pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny", "sac_tiny", "td7_humanoid", "sac_humanoid",
-                                  "td3_halfcheetah"])
+                                  "td3_halfcheetah", "td3_tiny_deep", "sac_tiny_deep", "td7_tiny_zs"])
 def test_forward_matches_reference(name):
     _fwd_check(name)
 
 
-TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed"]
-FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k"]
+TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed", "td3_tiny_deep",
+        "sac_tiny_deep"]
+FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k", "td7_tiny_zs"]
 
 
 @pytest.mark.parametrize("burst", [False, True], ids=["per_step", "burst"])

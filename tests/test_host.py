@@ -79,8 +79,9 @@ def test_train_ops_rejects_malformed_batches_and_foreign_replays():
 
 
 def test_engine_agents_reject_non_default_net_types():
-    """make_nn hooks must return the reference's default net types (rl.nn.*) of two hidden layers of one
-    width, checked before any engine exists; anything else is a clear NotImplementedError."""
+    """make_nn hooks must return the reference's default net types (rl.nn.*), one net shape across the
+    agent's nets and make_mlp depths of 2..6 (rle.h RLE_MAX_HIDDEN), checked before any engine exists;
+    anything else is a clear NotImplementedError."""
     with pytest.raises(TypeError):
         TD3("HalfCheetah-v4", make_nn=lambda **k: None)
     import torch
@@ -89,10 +90,14 @@ def test_engine_agents_reject_non_default_net_types():
 
     with pytest.raises(NotImplementedError):
         TD3("HalfCheetah-v4", make_nn=lambda state_dim, action_dim, **k: (torch.nn.Linear(1, 1),) * 3)
-    with pytest.raises(NotImplementedError, match="two hidden layers"):
+    with pytest.raises(NotImplementedError, match="one net shape"):
         TD3("HalfCheetah-v4", make_nn=lambda state_dim, action_dim, **k: (
             MLPActor(state_dim, action_dim, [64, 64, 64]), MLPCritic(state_dim, action_dim, 64),
             MLPCritic(state_dim, action_dim, 64)))
+    with pytest.raises(NotImplementedError, match="2 to 6 hidden layers"):
+        MLPActor(17, 6, [64] * 7)
+    with pytest.raises(TypeError, match="hidden_sizes"):
+        TD3("HalfCheetah-v4", zs_dim=64)
 
 
 def test_missing_library_fails_loudly(tmp_path, monkeypatch):

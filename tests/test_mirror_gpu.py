@@ -358,6 +358,64 @@ def test_make_nn_hook_with_reference_net_types():
         TD3("Tiny-v0", make_nn=other, batch_size=16, seed=1)
 
 
+def test_make_nn_hook_with_other_net_shapes():
+    """make_nn hooks with the shapes make_mlp / the SALE nets take beyond the defaults
+    (mlp.py:10-35 any depth and widths, sale.py:19-26 zs_dim != hdim): the engine builds those
+    nets with the hook's weights, acts as the hook's torch modules do, trains, and pickles back to
+    the same state (the trajectories themselves: td3_tiny_deep / sac_tiny_deep / td7_tiny_zs)."""
+    from rl.nn import MLPActor, MLPCritic, SALEActor, SALECritic, SALEEncoder
+
+    torch.manual_seed(3)
+    made = {}
+
+    def mk3(state_dim, action_dim, **kw):
+        hs = [32, 48, 32]
+        made["td3"] = (MLPActor(state_dim, action_dim, hs), MLPCritic(state_dim, action_dim, hs),
+                       MLPCritic(state_dim, action_dim, hs))
+        return made["td3"]
+
+    def mks(state_dim, action_dim, **kw):
+        hs = [48, 32, 32, 16]
+        made["sac"] = (MLPActor(state_dim, 2 * action_dim, hs), MLPCritic(state_dim, action_dim, hs),
+                       MLPCritic(state_dim, action_dim, hs))
+        return made["sac"]
+
+    def mk7(state_dim, action_dim, **kw):
+        made["td7"] = (SALEActor(state_dim, action_dim, 16, 64), SALECritic(state_dim, action_dim, 16, 64),
+                       SALECritic(state_dim, action_dim, 16, 64), SALEEncoder(state_dim, action_dim, 16, 64))
+        return made["td7"]
+
+    obs = np.linspace(-1, 1, S).astype(np.float32)
+    x = torch.from_numpy(obs)[None]
+    trans = _transitions(200, 5)
+    for cls, mk, alg in ((TD3, mk3, "td3"), (SAC, mks, "sac"), (TD7, mk7, "td7")):
+        ag = cls("Tiny-v0", make_nn=mk, batch_size=16, seed=4)
+        sd = ag.state_dict()
+        for name, m in zip(("policy", "q1", "q2", "encoder"), made[alg]):
+            for k, v in m.state_dict().items():
+                np.testing.assert_array_equal(sd[name][k], v.numpy())
+        with torch.no_grad():
+            if alg == "td7":
+                pol, enc = made["td7"][0], made["td7"][3]
+                ref = pol.inference_mean(x, enc.encode_state(x)).numpy()[0]
+            elif alg == "td3":
+                ref = torch.tanh(made["td3"][0].inference_mean(x)).numpy()[0]
+            else:
+                ref = torch.tanh(made["sac"][0].inference_mean_logvar(x)[0]).numpy()[0]
+        ref = ref * ag.action_scale + ag.action_bias
+        got = ag.sample(obs, deterministic=True)
+        assert np.abs(got - ref).max() <= 2e-6 + 1e-5 * np.abs(ref).max(), alg
+        rep = (LAPReplayMemory if alg == "td7" else SimpleReplayMemory)(256, "Tiny-v0")
+        _fill(rep, trans)
+        run_train_ops(rep, ag, 16, 5)
+        ag2 = pickle.loads(pickle.dumps(ag))
+        sd, sd2 = ag.state_dict(), ag2.state_dict()
+        for name in sd:
+            for k in sd[name]:
+                np.testing.assert_array_equal(sd[name][k], sd2[name][k])
+        assert ag2.shape == ag.shape and ag.shape
+
+
 def test_train_ops_on_a_host_batch_dict():
     """abc.py:23-28: train_ops on a plain BATCH dict (here the oracle replay's gather, as a host
     replay would hand it over) trains exactly as on the same rows drawn from a device replay, and

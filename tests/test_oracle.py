@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden
+from conftest import load_golden, shape_of
 from oracle import agents, replay, spec
 from oracle import nets as N
 
@@ -58,7 +58,7 @@ def build_from_golden(g):
     S, A, hi = spec.TASKS[env]
     extra = dict(zip([str(k) for k in g["meta_extra_keys"]], g["meta_extra_vals"].tolist()))
     extra = {k: (int(v) if k in ("target_update_rate", "policy_freq") else v) for k, v in extra.items()}
-    nets = spec.agent_params(alg, S, A, H, seed)
+    nets = spec.agent_params(alg, S, A, H, seed, **shape_of(g))
     orc = agents.make_oracle(alg, nets, A, bool(use_lap), **extra)
     scale = np.full(A, hi, np.float32)
     bias = np.zeros(A, np.float32)
@@ -76,8 +76,9 @@ def build_from_golden(g):
     return alg, orc, rep, tp, n_steps, B
 
 
-TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed"]
-FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k"]
+TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed", "td3_tiny_deep",
+        "sac_tiny_deep"]
+FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k", "td7_tiny_zs"]
 
 
 def golden_moments(g, t):

@@ -19,12 +19,12 @@ from conftest import load_golden
 pytestmark = pytest.mark.gpu
 
 E = pytest.importorskip("rl._engine")
-from harness import engine_from_golden, parse  # noqa: E402
+from harness import engine_from_golden, parse, shape_of  # noqa: E402
 from oracle import spec  # noqa: E402
 from test_oracle import expected_priorities, golden_moments  # noqa: E402
 
 ALL = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed", "td7_humanoid", "td7_ant",
-       "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k"]
+       "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k", "td3_tiny_deep", "sac_tiny_deep", "td7_tiny_zs"]
 
 
 def _fwd_close(got, ref, what):
@@ -44,7 +44,7 @@ def test_eval_matches_reference(name):
     eng, rep, _ = engine_from_golden(g)
     n = g["fwd_q1"].shape[0]
     s, a, *_ = rep.gather(np.arange(n))
-    params = spec.agent_params(alg, S, A, H, int(g["meta"][6]))
+    params = spec.agent_params(alg, S, A, H, int(g["meta"][6]), **shape_of(g))
     same = lambda x, y: all(np.array_equal(params[x][k], params[y][k]) for k in params[x])  # noqa: E731
     if alg == "td7":
         for q in ("q1", "q2"):
