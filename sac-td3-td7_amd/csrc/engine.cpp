@@ -1338,7 +1338,10 @@ struct AqlQueue {
     int ks;
   };
   std::vector<Pending> pending;
-  double us_per_launch = 10.0;  // measured mean dispatch-to-completion time per packet (EWMA over flushes)
+  // a LOWER bound on the time per packet: the fastest burst seen (>= kAqlMinBurst packets) x kAqlBoundFrac, 0 before
+  // one was timed.  The wait sleeps only through this bound's share of a burst, so it wakes before the burst ends and
+  // spins the rest: a mean-based estimate overslept short bursts (a 20-step bench burst woke 0.5 ms late, -17%).
+  double us_per_launch = 0.0;
   bool failed = false;          // a flush timed out: its packets may still be queued, the queue takes no more
   size_t inflight = 0;          // packets submitted since the last aql_complete
   std::chrono::steady_clock::time_point t0{};  // first doorbell of the oldest burst in flight
@@ -1440,8 +1443,10 @@ static std::unique_ptr<AqlQueue> aql_open(int dev) {
 // How the host waits for a flush without holding its core (MuJoCo stepping runs on the host cores beside
 // the engine, north_star): while more than kAqlSpinUs of the expected duration remain it sleeps (slices of
 // at most kAqlSliceUs, the signal checked between them), then spins on the signal; past timeout_s it gives
-// up.  expected_us = packets still to retire x the queue's measured time per packet.
+// up.  expected_us = packets still to retire x a lower bound on the queue's time per packet (AqlQueue::us_per_launch).
 constexpr double kAqlSpinUs = 150.0, kAqlSliceUs = 2000.0, kAqlTimeoutS = 60.0;
+constexpr size_t kAqlMinBurst = 32;   // bursts timed for the per-packet bound (AqlQueue::us_per_launch)
+constexpr double kAqlBoundFrac = 0.92;
 enum AqlWaitAct : int { AQL_SPIN = 0, AQL_SLEEP = 1, AQL_TIMEOUT = 2 };
 static int aql_wait_step(double expected_us, double elapsed_us, double timeout_s, double* sleep_us) {
   *sleep_us = 0.0;
@@ -1533,7 +1538,10 @@ static void aql_complete(AqlQueue& A, double* ms) {
   const double left = (double)(hsa_queue_load_write_index_relaxed(q) - hsa_queue_load_read_index_scacquire(q));
   aql_wait(A, [&] { return hsa_signal_load_scacquire(A.sig) < 1; }, left * A.us_per_launch, "a dispatch");
   const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - A.t0).count();
-  if (A.inflight >= 8) A.us_per_launch = 0.5 * A.us_per_launch + 0.5 * (wall_ms * 1e3 / (double)A.inflight);
+  if (A.inflight >= kAqlMinBurst) {
+    const double per = kAqlBoundFrac * wall_ms * 1e3 / (double)A.inflight;
+    A.us_per_launch = A.us_per_launch > 0.0 ? std::min(A.us_per_launch, per) : per;
+  }
   A.inflight = 0;
   if (ms) *ms += wall_ms;
 }
