@@ -4343,34 +4343,30 @@ struct Engine {
     if (fold_dirty && g_fold.x) launch_graph(g_fold);
     fold_dirty = false;
     int done = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    if (gpu_ms) {
-      HIPCHK(hipEventCreate(&ev0));
-      HIPCHK(hipEventCreate(&ev1));
-      HIPCHK(hipEventRecord(ev0, stream));
-    }
     // direct dispatch (RLE_AQL=1): the graphs' levels go to the engine's own queue; the HIP
     // stream is drained first and the queue after each chunk (host-side ordering between them; async:
     // the last chunk stays in flight, aql_drain)
     const bool use_aql = aql_mode() && !g_pol[0].aql.empty();
     if (use_aql && !aql) aql = aql_open(cfg.device);
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (gpu_ms && !use_aql) {  // (AQL: the levels run outside the stream; host wall time instead)
+      HIPCHK(hipEventCreate(&ev0));
+      HIPCHK(hipEventCreate(&ev1));
+      HIPCHK(hipEventRecord(ev0, stream));
+    }
     double aql_ms = 0.0;
     while (done < n) {
       const int chunk = std::min(n - done, info_cap);
-      if (use_aql && async) {
-        // (the slot reset queues behind the bursts still in flight: no host wait)
+      if (use_aql) {
+        // the info slot reset is the burst's first packet (g_slot0), in order with the bursts still in flight:
+        // no host round trip (a 4-byte H2D copy and a stream sync cost ~20 us per burst, 1% of a 20-step burst)
         HIPCHK(hipStreamSynchronize(stream));
         aql_active = true;
         launch_graph(g_slot0);
         launches -= g_slot0.nlaunch;  // (not a step level)
       } else {
-        if (use_aql) aql_drain();  // (the info slot reset below must not race levels still in flight)
         int zero = 0;
         HIPCHK(hipMemcpyAsync(&ctrl->info_slot, &zero, sizeof(int), hipMemcpyHostToDevice, stream));
-        if (use_aql) {
-          HIPCHK(hipStreamSynchronize(stream));
-          aql_active = true;
-        }
       }
       for (int i = 0; i < chunk; ++i) {
         if (ctrl_tape_mode_host) {
@@ -4425,11 +4421,12 @@ struct Engine {
       done += chunk;
     }
     HIPCHK(hipEventRecord(done_ev, stream));  // replay operations wait for this (Replay::wait_users)
-    if (gpu_ms) {
+    if (gpu_ms && use_aql) {
+      *gpu_ms = (float)aql_ms;  // (the levels ran outside the stream: host wall time)
+    } else if (gpu_ms) {
       HIPCHK(hipEventRecord(ev1, stream));
       HIPCHK(hipEventSynchronize(ev1));
       HIPCHK(hipEventElapsedTime(gpu_ms, ev0, ev1));
-      if (use_aql) *gpu_ms = (float)aql_ms;  // (the levels ran outside the stream: host wall time)
       (void)hipEventDestroy(ev0);
       (void)hipEventDestroy(ev1);
     }
