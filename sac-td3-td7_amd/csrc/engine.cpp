@@ -1688,6 +1688,10 @@ struct Engine {
   // sets keep their own Adam scalars (asc_set) so only true data dependencies order them.
   Graph g_pair[2];
   int multi_k = 0;
+  // g_rem[r][p]: kRemK[r] steps as one program (a burst's tail shorter than multi_k: the driver's 20-step bench
+  // burst is 3 x 6 + 2), built when kRemK[r] < multi_k
+  static constexpr int kRemK[2] = {4, 2};
+  Graph g_rem[2][2];
   int asc_set = 0;
   float* adamsc1 = nullptr;  // [step[4], bc2s[4]] of steps built on set 1
   float* adam_step_of(int set) { return set ? adamsc1 : ctrl->adam_step; }
@@ -4187,6 +4191,13 @@ struct Engine {
             for (int j = 0; j < multi_k; ++j) build_td7(p, j % 2 == 0, (set + j) % 2);
           });
           g_pair[set] = capture(p3);
+          for (int r = 0; r < 2; ++r) {
+            if (kRemK[r] >= multi_k) continue;
+            Prog p4 = plan_build([&](Prog& p) {
+              for (int j = 0; j < kRemK[r]; ++j) build_td7(p, j % 2 == 0, (set + j) % 2);
+            });
+            g_rem[r][set] = capture(p4);
+          }
         }
       } else {
         Prog p1 = plan_build([&](Prog& p) { build_mlp(p, true, set); });
@@ -4200,6 +4211,13 @@ struct Engine {
             for (int j = 0; j < multi_k; ++j) build_mlp(p, sac || j % 2 == 0, (set + j) % 2);
           });
           g_pair[set] = capture(p3);
+          for (int r = 0; r < 2; ++r) {
+            if (kRemK[r] >= multi_k) continue;
+            Prog p4 = plan_build([&](Prog& p) {
+              for (int j = 0; j < kRemK[r]; ++j) build_mlp(p, sac || j % 2 == 0, (set + j) % 2);
+            });
+            g_rem[r][set] = capture(p4);
+          }
         }
       }
     }
@@ -4307,11 +4325,10 @@ struct Engine {
     }
     launches += G.nlaunch;
   }
-  // The next multi_k steps may run as one multi-step program: TD7 (counter bumped first,
-  // td7.py:295) / TD3 (td3.py:231) when its first step is a policy step (and, TD7, no step
-  // of it needs a hard update); SAC any multi_k steps.
-  bool pair_window_ok() const {
-    const int K = multi_k;
+  // The next K steps (multi_k, or a remainder program's) may run as one multi-step program: TD7 (counter
+  // bumped first, td7.py:295) / TD3 (td3.py:231) when its first step is a policy step (and, TD7, no step
+  // of it needs a hard update); SAC any K steps.
+  bool pair_window_ok(int K) const {
     if (!K) return false;
     const long long k1 = algo == RLE_TD7 ? n_runs + 1 : n_runs;
     if (algo != RLE_SAC && k1 % 2) return false;
@@ -4322,15 +4339,15 @@ struct Engine {
     }
     return true;
   }
-  // host state after a multi-step program starting on batch set cur_set was enqueued
-  void pair_commit() {
+  // host state after a K-step program starting on batch set cur_set was enqueued
+  void pair_commit(int K) {
     const int p = cur_set;
-    n_runs += multi_k;
+    n_runs += K;
     pol_set = p;
     if (algo != RLE_SAC) pln_set = 1 - p;
     last_set = 1 - p;
     cur_set = p;
-    if (cfg.use_lap && algo != RLE_SAC) replay->version += multi_k;
+    if (cfg.use_lap && algo != RLE_SAC) replay->version += K;
     primed = true;
     primed_ver = replay->version;
   }
@@ -4378,13 +4395,21 @@ struct Engine {
         if (!primed || primed_ver != replay->version) launch_graph(g_prime[cur_set]);
         const int p = cur_set;
         // multi-step graph (pair_window_ok)
-        const int K = multi_k;
-        const bool pair_ok = K && i + K - 1 < chunk && (!ctrl_tape_mode_host || tape_left >= K - 1) &&
-                             pair_window_ok();
-        if (pair_ok && g_pair[p].x) {
+        // (the longest multi-step program that fits the rest of the chunk: multi_k, then the remainder ones)
+        const Graph* mg = nullptr;
+        int K = 0;
+        for (int r = -1; r < 2 && !mg; ++r) {
+          const int k = r < 0 ? multi_k : kRemK[r];
+          const Graph& g = r < 0 ? g_pair[p] : g_rem[r][p];
+          if (k && g.x && i + k - 1 < chunk && (!ctrl_tape_mode_host || tape_left >= k - 1) && pair_window_ok(k)) {
+            mg = &g;
+            K = k;
+          }
+        }
+        if (mg) {
           if (ctrl_tape_mode_host) tape_left -= K - 1;
-          launch_graph(g_pair[p]);
-          pair_commit();
+          launch_graph(*mg);
+          pair_commit(K);
           i += K - 1;
           continue;
         }
@@ -4914,7 +4939,8 @@ int rle_destroy(rle_engine* h) {
     }
     if (e.done_ev) (void)hipEventDestroy(e.done_ev);
     for (rle::Graph* g : {&e.g_prime[0], &e.g_prime[1], &e.g_pol[0], &e.g_pol[1], &e.g_pln[0], &e.g_pln[1],
-                          &e.g_pair[0], &e.g_pair[1], &e.g_hard, &e.g_fold, &e.g_slot0}) {
+                          &e.g_pair[0], &e.g_pair[1], &e.g_rem[0][0], &e.g_rem[0][1], &e.g_rem[1][0],
+                          &e.g_rem[1][1], &e.g_hard, &e.g_fold, &e.g_slot0}) {
       if (g->x) (void)hipGraphExecDestroy(g->x);
       if (g->g) (void)hipGraphDestroy(g->g);
     }
