@@ -381,9 +381,18 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
         # wall time from the first doorbell to the last packet's completion signal (rle_step_timed, rle.h);
         # with RLE_AQL=0 HIP event time on the engine's stream
         "engine_s": round(gpu_s, 6),
-        "engine_timer": ("host wall, first AQL doorbell to completion signal" if os.environ.get("RLE_AQL", "1") != "0"
+        "engine_timer": ("host wall, first AQL doorbell to completion signal" if aql_dispatch()
                          else "HIP events on the engine stream"),
     }
+
+
+def aql_dispatch():
+    """Whether the engine dispatches its step levels as direct AQL packets (engine.cpp Engine::aql_mode): RLE_AQL
+    when set, else on unless rocprofv3's kernel / HSA API tracing is on (then hipGraph replays)."""
+    if "RLE_AQL" in os.environ:
+        return os.environ["RLE_AQL"][:1] != "0"
+    return not any(os.environ.get(v, "")[:1] == "1"
+                   for v in ("ROCPROF_KERNEL_TRACE", "ROCPROF_HSA_CORE_API_TRACE", "ROCPROF_HSA_AMD_EXT_API_TRACE"))
 
 
 def multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, cuda_sync, chunk=25):

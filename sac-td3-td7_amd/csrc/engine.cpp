@@ -4299,7 +4299,15 @@ struct Engine {
   static bool aql_mode() {
     static const bool on = [] {
       const char* e = std::getenv("RLE_AQL");
-      return !(e && e[0] == '0');
+      if (e) return e[0] != '0';
+      // rocprofv3's kernel and HSA API tracing intercept HSA queue creation, and packets written into an
+      // intercepted queue crash (profiles/r05_prof_crash.txt): under those tracers (their option variables,
+      // "1" when on) the levels replay as hipGraphs -- the same rle_level dispatches, traced as usual
+      for (const char* v : {"ROCPROF_KERNEL_TRACE", "ROCPROF_HSA_CORE_API_TRACE", "ROCPROF_HSA_AMD_EXT_API_TRACE"}) {
+        const char* t = std::getenv(v);
+        if (t && t[0] == '1') return false;
+      }
+      return true;
     }();
     return on;
   }

@@ -107,6 +107,26 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
         E.Replay(16, 3, 1, False)
 
 
+def test_bench_timer_label_follows_the_dispatch_path(monkeypatch):
+    """bench.aql_dispatch mirrors engine.cpp Engine::aql_mode: RLE_AQL decides when set; otherwise direct AQL
+    dispatch unless rocprofv3's kernel / HSA API tracing is on (hipGraph replays under those tracers)."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    for v in ("RLE_AQL", "ROCPROF_KERNEL_TRACE", "ROCPROF_HSA_CORE_API_TRACE", "ROCPROF_HSA_AMD_EXT_API_TRACE"):
+        monkeypatch.delenv(v, raising=False)
+    assert bench.aql_dispatch()
+    monkeypatch.setenv("ROCPROF_KERNEL_TRACE", "0")
+    assert bench.aql_dispatch()
+    monkeypatch.setenv("ROCPROF_KERNEL_TRACE", "1")
+    assert not bench.aql_dispatch()
+    monkeypatch.setenv("RLE_AQL", "1")
+    assert bench.aql_dispatch()
+    monkeypatch.setenv("RLE_AQL", "0")
+    monkeypatch.delenv("ROCPROF_KERNEL_TRACE")
+    assert not bench.aql_dispatch()
+
+
 def test_bench_workload_figures_match_survey():
     sys.path.insert(0, REPO)
     import bench
