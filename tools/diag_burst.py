@@ -27,9 +27,21 @@ eng.bind(rep)
 eng.graph_stats()
 if last:
     rep.fill_random(bench.N_REPLAY, seed=0)
+pre = int(os.environ.get("RLE_DIAG_PREWARM", "0"))
+if pre:  # another engine on the same replay steps first (its row gathers touch the replay's pages)
+    e0 = E.Engine(E.make_config(E.RLE_TD7, S, A, 256, 256, use_lap=True, seed=7, device=0), E.parse_plan(""))
+    for net, params in init_agent("td7", S, A, 256, 5).items():
+        for name, v in params.items():
+            e0.set_param(net, name, v)
+    e0.bind(rep)
+    e0.step_timed(pre)
+    del e0
 eng.step_timed(W)
 torch.cuda.synchronize(0)
+gap = float(os.environ.get("RLE_DIAG_GAP_MS", "0"))
 for r in range(reps):
+    if gap:
+        time.sleep(gap / 1e3)
     l0 = eng.launch_count()
     t0 = time.perf_counter()
     ms = eng.step_timed(n)
