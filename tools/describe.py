@@ -1,4 +1,5 @@
-"""Print the level structure of the TD7 Humanoid step graphs (GPU box)."""
+"""Print the level structure of the step graphs (GPU box): python tools/describe.py [td7|td3|sac] [S A]
+(RLE_DESC_CRIT=1 stars the ops on a longest dependency chain)."""
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd")]
@@ -9,6 +10,8 @@ algo = sys.argv[1] if len(sys.argv) > 1 else "td7"
 code = {"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}[algo]
 if algo == "td3":
     S, A = 17, 6
+if len(sys.argv) > 3:
+    S, A = int(sys.argv[2]), int(sys.argv[3])
 eng = E.Engine(E.make_config(code, S, A, H, B, use_lap=(algo == "td7")))
 for net, params in init_agent(algo, S, A, H, 1).items():
     for k, v in params.items():
