@@ -194,7 +194,7 @@ def _cpu_run(seconds, algo, env, batch, lap, s_dim, a_dim, hi, agents, replay, s
                       f"share is 16 CPUs)",
             # the GPU boxes share their host with other jobs: the same oracle run measured 34.5-53.9 steps/s
             # (TD7 Humanoid B=256) on different boxes in rounds 3-4, i.e. about 1.5x box to box
-            "box_to_box_spread": "about 1.5x (TD7 Humanoid B=256: 34.5-53.9 steps/s across GPU boxes, rounds 3-4)",
+            "box_to_box_spread": "about 2x (TD7 Humanoid B=256: 28.5-53.9 steps/s across GPU boxes and runs, rounds 3-5)",
             "host": hc}
 
 
