@@ -122,50 +122,59 @@ def socket_cores():
     return sock, cpus, len(cores)
 
 
-def cpu_baseline(seconds=12.0, algo="td7", env="Humanoid-v4", batch=B, lap=True, pin=True):
+def cpu_baseline(seconds=12.0, algo="td7", env="Humanoid-v4", batch=B, lap=True, pin=True, cpus=None,
+                 n_replay=N_REPLAY):
     """Oracle (torch-CPU restatement of train_ops + replay sample) on host cores, same
     synthetic workload as the GPU run (full 1M replay).  SURVEY §8(d): torch threads = the
-    physical cores of one socket, the process pinned to one logical CPU of each (restored after)."""
+    physical cores of one socket, the process pinned to one logical CPU of each (restored after).
+    cpus: pin to exactly these CPUs instead, one torch thread each (the N-process figure of
+    BASELINE.md: one process per rank, each on its own slice of the host, cpu_baseline_ranks)."""
     import torch
 
     from oracle import agents, replay, spec
 
     s_dim, a_dim, hi = TASKS[env]
     old_aff, old_threads = os.sched_getaffinity(0), torch.get_num_threads()
-    sock, cpus, ncore = socket_cores()
-    # the GPU box is a one-GPU share of an 8-GPU host: 16 of its CPUs are this box's (more threads
-    # contend with other tenants and measure less); RLE_CPU_THREADS overrides
-    cpus = cpus[:int(os.environ.get("RLE_CPU_THREADS", "16"))]
+    if cpus is not None:
+        sock, ncore = -1, len(cpus)
+    else:
+        sock, cpus, ncore = socket_cores()
+        # the GPU box is a one-GPU share of an 8-GPU host: 16 of its CPUs are this box's (more threads
+        # contend with other tenants and measure less); RLE_CPU_THREADS overrides
+        cpus = cpus[:int(os.environ.get("RLE_CPU_THREADS", "16"))]
     if pin and cpus:
         os.sched_setaffinity(0, cpus)
         torch.set_num_threads(len(cpus))
     try:
         return _cpu_run(seconds, algo, env, batch, lap, s_dim, a_dim, hi, agents, replay, spec, torch,
-                        {"socket": sock, "physical_cores_socket": ncore, "pinned_cpus": len(cpus) if pin else 0})
+                        {"socket": sock, "physical_cores_socket": ncore, "pinned_cpus": len(cpus) if pin else 0},
+                        n_replay)
     finally:
         if pin and cpus:
             os.sched_setaffinity(0, old_aff)
             torch.set_num_threads(old_threads)
 
 
-def _cpu_run(seconds, algo, env, batch, lap, s_dim, a_dim, hi, agents, replay, spec, torch, pinning):
+def _cpu_run(seconds, algo, env, batch, lap, s_dim, a_dim, hi, agents, replay, spec, torch, pinning,
+             n_replay=N_REPLAY):
     threads = torch.get_num_threads()
     rng = np.random.default_rng(0)
     nets = spec.agent_params(algo, s_dim, a_dim, H, 123)
     orc = agents.make_oracle(algo, nets, a_dim, lap)
-    rep = replay.Replay(N_REPLAY, s_dim, a_dim, np.full(a_dim, hi, np.float32), np.zeros(a_dim, np.float32), lap)
+    N = n_replay
+    rep = replay.Replay(N, s_dim, a_dim, np.full(a_dim, hi, np.float32), np.zeros(a_dim, np.float32), lap)
     blk = 4096
     base_s = rng.standard_normal((blk, s_dim), dtype=np.float32)
     base_s2 = rng.standard_normal((blk, s_dim), dtype=np.float32)
-    for i in range(0, N_REPLAY, blk):
-        n = min(blk, N_REPLAY - i)
+    for i in range(0, N, blk):
+        n = min(blk, N - i)
         rep.state[i:i + n] = base_s[:n]
         rep.next_state[i:i + n] = base_s2[:n]
-    rep.action[:] = rng.uniform(-1, 1, (N_REPLAY, a_dim)).astype(np.float32)
-    rep.reward[:, 0] = rng.standard_normal(N_REPLAY).astype(np.float32)
-    rep.done[:, 0] = (rng.random(N_REPLAY) < 0.99).astype(np.float32)
+    rep.action[:] = rng.uniform(-1, 1, (N, a_dim)).astype(np.float32)
+    rep.reward[:, 0] = rng.standard_normal(N).astype(np.float32)
+    rep.done[:, 0] = (rng.random(N) < 0.99).astype(np.float32)
     rep.priority[:] = 1.0
-    rep.size, rep.ptr = N_REPLAY, 0
+    rep.size, rep.ptr = N, 0
 
     def one():
         u = rng.random(batch, dtype=np.float32)
@@ -188,10 +197,11 @@ def _cpu_run(seconds, algo, env, batch, lap, s_dim, a_dim, hi, agents, replay, s
     hc.update(pinning)
     return {"value": round(n / dt, 3), "unit": "gradient-steps/s", "cores": threads, "threads": threads,
             "kind": "port",
-            "sample": f"{n} {algo.upper()} {env} B={batch} steps ({'LAP' if lap else 'uniform'} over a 1M replay) "
-                      f"of the torch-CPU oracle, {dt:.1f} s, torch threads={threads} pinned one per physical core "
-                      f"of socket {pinning['socket']} ({pinning['physical_cores_socket']} physical cores; the box's "
-                      f"share is 16 CPUs)",
+            "sample": f"{n} {algo.upper()} {env} B={batch} steps ({'LAP' if lap else 'uniform'} over a "
+                      f"{N // 1000}K replay) of the torch-CPU oracle, {dt:.1f} s, torch threads={threads} "
+                      + (f"pinned one per physical core of socket {pinning['socket']} "
+                         f"({pinning['physical_cores_socket']} physical cores; the box's share is 16 CPUs)"
+                         if pinning["socket"] >= 0 else "pinned to the rank's own CPU slice"),
             # the GPU boxes share their host with other jobs: the same oracle run measured 34.5-53.9 steps/s
             # (TD7 Humanoid B=256) on different boxes in rounds 3-4, i.e. about 1.5x box to box
             "box_to_box_spread": "about 2x (TD7 Humanoid B=256: 28.5-53.9 steps/s across GPU boxes and runs, rounds 3-5)",
@@ -319,8 +329,9 @@ def gather_evidence(s_dim, a_dim, batch, n_replay, lap):
 
 
 def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7", env="Humanoid-v4",
-              batch=B, lap=True, launches=None):
-    """The bench JSON line (everything but cpu_baseline) from the max-over-ranks timings."""
+              batch=B, lap=True, launches=None, dispatch=1):
+    """The bench JSON line (everything but cpu_baseline) from the max-over-ranks timings.  dispatch: the
+    engine's rle_plan.dispatch (1 direct AQL, 0 hipGraph replays, 2 launches on the stream)."""
     value = n_gpus * steps / wall
     headline = (algo, env, batch) == ("td7", "Humanoid-v4", B)
     if headline:
@@ -379,20 +390,14 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
         "roofline": roofline,
         # the engine's own elapsed time over the timed steps: under the default direct AQL dispatch it is host
         # wall time from the first doorbell to the last packet's completion signal (rle_step_timed, rle.h);
-        # with RLE_AQL=0 HIP event time on the engine's stream
+        # with rle_plan dispatch 0 / 2 HIP event time on the engine's stream
         "engine_s": round(gpu_s, 6),
-        "engine_timer": ("host wall, first AQL doorbell to completion signal" if aql_dispatch()
-                         else "HIP events on the engine stream"),
+        "engine_timer": ENGINE_TIMERS[dispatch],
     }
 
 
-def aql_dispatch():
-    """Whether the engine dispatches its step levels as direct AQL packets (engine.cpp Engine::aql_mode): RLE_AQL
-    when set, else on unless rocprofv3's kernel / HSA API tracing is on (then hipGraph replays)."""
-    if "RLE_AQL" in os.environ:
-        return os.environ["RLE_AQL"][:1] != "0"
-    return not any(os.environ.get(v, "")[:1] == "1"
-                   for v in ("ROCPROF_KERNEL_TRACE", "ROCPROF_HSA_CORE_API_TRACE", "ROCPROF_HSA_AMD_EXT_API_TRACE"))
+ENGINE_TIMERS = {1: "host wall, first AQL doorbell to completion signal", 0: "HIP events on the engine stream",
+                 2: "HIP events on the engine stream"}
 
 
 def multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, cuda_sync, chunk=25):
@@ -477,6 +482,125 @@ def kfd_gpu_count(root="/sys/class/kfd/kfd/topology/nodes"):
     return n
 
 
+def parse_cpulist(text):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11] (sysfs cpulist format)."""
+    out = []
+    for part in filter(None, (t.strip() for t in text.split(","))):
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def kfd_gpu_nodes(root="/sys/class/kfd/kfd/topology/nodes"):
+    """The KFD topology's GPU nodes (those with SIMDs) in node order -- the order HIP numbers the devices
+    in -- narrowed by *_VISIBLE_DEVICES (integer lists) when set: [(node, properties dict)]."""
+    import glob
+
+    nodes = []
+    for f in glob.glob(os.path.join(root, "*", "properties")):
+        try:
+            props = dict(line.split() for line in open(f) if len(line.split()) == 2)
+            node = int(os.path.basename(os.path.dirname(f)))
+        except (OSError, ValueError):
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            nodes.append((node, props))
+    nodes.sort(key=lambda t: t[0])
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            try:
+                idx = [int(x) for x in v.split(",") if x.strip() != ""]
+            except ValueError:
+                continue
+            nodes = [nodes[i] for i in idx if 0 <= i < len(nodes)]
+    return nodes
+
+
+def gpu_local_cpus(local, n_local, kfd_root="/sys/class/kfd/kfd/topology/nodes", pci_root="/sys/bus/pci/devices",
+                   allowed=None):
+    """The host CPUs rank `local` (of n_local ranks on this node, one GPU each) is pinned to, without any
+    HIP / HSA call (bench.py pins its ranks before they touch a GPU): the CPUs NUMA-local to its GPU (the
+    PCI device's local_cpulist, found from the KFD node's domain / location_id) among this process's
+    allowed CPUs, split evenly among the ranks whose GPUs share them -- where MuJoCo stepping for that
+    seed would run.  Returns (cpus, info); the allowed CPUs split by rank when the GPU's
+    locality cannot be read or none of its local CPUs is allowed."""
+    allowed = sorted(os.sched_getaffinity(0) if allowed is None else allowed)
+    nodes = kfd_gpu_nodes(kfd_root)
+
+    def local_set(i):
+        if i >= len(nodes):
+            return None, None
+        props = nodes[i][1]
+        loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
+        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 31:02x}.{loc & 7:x}"
+        try:
+            with open(os.path.join(pci_root, bdf, "local_cpulist")) as f:
+                cpus = [c for c in parse_cpulist(f.read()) if c in set(allowed)]
+            with open(os.path.join(pci_root, bdf, "numa_node")) as f:
+                numa = int(f.read().strip())
+        except (OSError, ValueError):
+            return bdf, None
+        return bdf, (numa, tuple(cpus)) if cpus else None
+
+    sets = [local_set(i) for i in range(n_local)]
+    bdf, mine = sets[local] if local < len(sets) else (None, None)
+    if mine is None:  # (no locality: an even split of the allowed CPUs by rank)
+        k = max(1, len(allowed) // max(1, n_local))
+        cpus = allowed[local * k:(local + 1) * k] or allowed
+        return cpus, {"gpu_bdf": bdf, "numa_node": None, "numa_local": False, "cpus": len(cpus)}
+    sharers = [i for i, t in enumerate(sets) if t[1] is not None and t[1][1] == mine[1]]
+    k = max(1, len(mine[1]) // len(sharers))
+    j = sharers.index(local)
+    cpus = list(mine[1][j * k:(j + 1) * k]) or list(mine[1])
+    return cpus, {"gpu_bdf": bdf, "numa_node": mine[0], "numa_local": True, "cpus": len(cpus)}
+
+
+def physical_core_cpus(cpus):
+    """One logical CPU per physical core among `cpus` (/proc/cpuinfo physical id / core id)."""
+    by_cpu, cur = {}, {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if not k:
+                    if "processor" in cur:
+                        by_cpu[cur["processor"]] = cur
+                    cur = {}
+                elif k in ("processor", "physical id", "core id"):
+                    cur[k] = int(v)
+        if "processor" in cur:
+            by_cpu[cur["processor"]] = cur
+    except OSError:
+        return list(cpus)
+    seen, out = set(), []
+    for c in cpus:
+        e = by_cpu.get(c, {})
+        key = (e.get("physical id", 0), e.get("core id", ("cpu", c)))
+        if key not in seen:
+            seen.add(key)
+            out.append(c)
+    return out
+
+
+def cpu_baseline_ranks(dist, rank, world, cpus, seconds, algo, env, batch, lap, n_replay=N_REPLAY):
+    """BASELINE.md's N-process CPU figure for an N-GPU line: every rank runs the torch-CPU oracle at the
+    same time, pinned to its own CPU slice (gpu_local_cpus: cores/N of the host, one thread per physical
+    core), after the GPU timing; rank 0 gets the sum.  None on ranks other than 0."""
+    dist.barrier()
+    r = cpu_baseline(seconds, algo, env, batch, lap, cpus=physical_core_cpus(cpus), n_replay=n_replay)
+    rows = [None] * world
+    dist.all_gather_object(rows, r)
+    if rank != 0:
+        return None
+    return {"value": round(sum(x["value"] for x in rows), 3), "unit": "gradient-steps/s",
+            "cores": sum(x["cores"] for x in rows), "kind": "port", "procs": world,
+            "threads_per_proc": [x["threads"] for x in rows], "per_proc": [x["value"] for x in rows],
+            "sample": f"{world} concurrent processes (one per rank), each: {rows[0]['sample']}",
+            "host": rows[0]["host"]}
+
+
 def launch_ranks(n, argv, device_count):
     """``--gpus N`` without a launcher (WORLD_SIZE unset): start N fresh rank processes of this
     script, one per GPU, each with RANK / LOCAL_RANK / WORLD_SIZE and a local rendezvous.  The
@@ -529,6 +653,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-replay", type=int, default=N_REPLAY,
+                    help="replay rows of the CPU baseline's oracle (default the GPU run's 1M; tests use fewer)")
     ap.add_argument("--algo", choices=("td7", "td3", "sac"), default="td7")
     ap.add_argument("--env", choices=tuple(TASKS), default="Humanoid-v4")
     ap.add_argument("--batch", type=int, default=B)
@@ -557,7 +683,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    pin_cpus, pinning = None, None
     if world > 1:
+        # each rank on its GPU's NUMA-local cores (its share of them), before anything touches a GPU
+        n_local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        pin_cpus, pinning = gpu_local_cpus(local, n_local)
+        os.sched_setaffinity(0, pin_cpus)
         import torch.distributed as dist  # gloo: start barrier + timing reduction only
         dist.init_process_group("gloo")
 
@@ -607,18 +738,31 @@ def main():
     wall = t1 - t0
     wall, gpu_s = max_over_ranks([wall, gpu_ms / 1e3], dist)
 
+    cb = None
+    if world > 1 and not args.no_cpu_baseline:  # (every rank: the N concurrent CPU processes)
+        cb = cpu_baseline_ranks(dist, rank, world, pin_cpus, args.cpu_seconds, args.algo, args.env, args.batch, lap,
+                                args.cpu_replay)
+    pins = [None] * world
+    if dist:
+        dist.all_gather_object(pins, pinning)
     if rank != 0:
         if dist:
             dist.barrier()
         return
+    plan = eng.plan()
     out = summarize(world, args.steps, args.warmup, wall, gpu_s, lv_policy, lv_plain, args.algo, args.env,
-                    args.batch, lap, launches)
-    out["config"]["plan"] = eng.plan()
+                    args.batch, lap, launches, plan.get("dispatch", 1))
+    out["config"]["plan"] = plan
     # share of the timed region the stepping thread spent on a host core (the AQL wait sleeps: engine.cpp
     # aql_wait_step), i.e. what is left for MuJoCo stepping beside the engine (north_star)
     out["host_thread_busy_frac"] = round((c1 - c0) / max(wall, 1e-9), 4)
+    if world > 1:
+        out["config"]["rank_pinning"] = pins
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.algo, args.env, args.batch, lap)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.algo, args.env, args.batch, lap,
+                                           n_replay=args.cpu_replay)
+    elif cb is not None:
+        out["cpu_baseline"] = cb
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

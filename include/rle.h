@@ -109,6 +109,14 @@ typedef struct rle_plan {
   int lpt;              /* 1: each level's ops in its launch ordered longest first (estimated workgroup time),
                            so a level with more workgroups than the device holds dispatches its long tiles in
                            the first round; 0: program order; -1: default                               */
+  /* Launch choices (they change no result: the same ops, tiles and summation order either way) */
+  int dispatch;         /* how the step programs' level launches reach the device: 1 direct AQL kernel-dispatch
+                           packets in the engine's own HSA queue; 0 hipGraph replays on the engine's HIP stream;
+                           2 level launches on the stream without a graph (A/B); -1: default = 1            */
+  int dpf;              /* 1: each launch leads with one workgroup per XCD that loads the next launch's op
+                           descriptors into that XCD's L2; 0 off (A/B); -1: default = 1                     */
+  int xcd;              /* 1: XCD-aware tile order (each XCD a compact band of a GEMM's tiles); 0 row-major
+                           (A/B); -1: default = 1                                                          */
 } rle_plan;
 
 /* ---- replay memory: rl/replay_memory/{lap,simple}.py ---------------------- */
@@ -180,10 +188,10 @@ int rle_set_value_bounds(rle_engine* e, const float* in4);
  * key order; NaN = None).  One host sync per call. */
 int rle_step(rle_engine* e, int n_steps, float* info_out);
 /* Benchmark form of rle_step: n_steps without info readback; *gpu_ms = the engine's elapsed time.
- * Under the default direct AQL dispatch (RLE_AQL unset or 1; the levels go to the engine's own HSA
- * queue, opened at its first synchronous step) that is HOST WALL time from the first doorbell to the
- * last packet's completion signal; with RLE_AQL=0 (hipGraph replays) it is HIP event time on the
- * engine's stream.  The host thread sleeps while the expected remainder of the burst exceeds 150 us
+ * Under the default direct AQL dispatch (rle_plan.dispatch 1; the levels go to the engine's own HSA
+ * queue, opened at its first step) that is HOST WALL time from the first doorbell to the last
+ * packet's completion signal; with dispatch 0 / 2 (hipGraph replays / launches on the stream) it is
+ * HIP event time on the engine's stream.  The host thread sleeps while the expected remainder of the burst exceeds 150 us
  * and spins only for the tail (rle_aql_wait_plan); a burst that does not complete within 60 s closes
  * the engine's queue (every later step fails).  Syncs once at the end. */
 int rle_step_timed(rle_engine* e, int n_steps, float* gpu_ms);
@@ -265,6 +273,10 @@ int rle_trace_stride(void);
  * outstanding and the time waited so far, returns 0 spin on the completion signal, 1 sleep *sleep_us
  * then check again, 2 time out (the engine's queue is then closed). */
 int rle_aql_wait_plan(double expected_us, double elapsed_us, double timeout_s, double* sleep_us);
+/* Self-test of the AQL queue's failure handling (no GPU, no HSA call): a queue closed by a timed-out
+ * burst refuses new bursts and completes at once, also for other engines sharing its hardware queue,
+ * and no doorbell publishes a run of packets that straddles the ring's end.  0 when every check holds. */
+int rle_aql_selftest(void);
 /* Copy all weights/optimizer state/counters of src into dst (checkpoint agent,
  * ckpt_agent.load_state_dict(agent), run_w_checkpoint.py:140). Same config required. */
 int rle_copy_state(rle_engine* dst, rle_engine* src);

@@ -304,7 +304,7 @@ static void check_gemm(const GemmArgs& g) {
   REQUIRE(g.R <= 16 * 1024, "gemm: reduction too long");
 }
 
-static void xcd_plan(GemmArgs& g);
+static void xcd_plan(GemmArgs& g, bool xcd);
 
 // (ks < 0: in any kernel set)
 static bool gemm_variant_compiled(int vid, int ks = -1) {
@@ -316,7 +316,7 @@ static bool gemm_variant_compiled(int vid, int ks = -1) {
 
 // Device-side dispatch fields of a GEMM op: compiled variant, split count, tile-row
 // reciprocal (kernels.hip gemm_v).
-static void gemm_finalize(GemmArgs& g) {
+static void gemm_finalize(GemmArgs& g, bool xcd = true) {
   int norm = 0;
   for (int q = 0; q < g.A.nseg; ++q) norm |= g.A.seg[q].norm.part != nullptr;
   for (int q = 0; q < g.B.nseg; ++q) norm |= g.B.seg[q].norm.part != nullptr;
@@ -422,18 +422,17 @@ static void gemm_finalize(GemmArgs& g) {
   h.b0p = g.B.seg[0].p;
   h.bias = g.epi == EPI_ADAM ? nullptr : g.bias;
   h.tiles = (g.hot.wide ? g.tiles_m / 4 : g.tiles_m) * g.tiles_n;
-  xcd_plan(g);
+  xcd_plan(g, xcd);
 }
 
 // XCD-aware tile order of a GEMM (GemmHot::xb): each of the 8 XCDs takes ~tiles/8 tiles as
 // a band-ordered run.  Band width b (in tiles) minimises the operand blocks one XCD reads:
 // ceil(share / b) A row-blocks of 16 rows plus b B column-blocks of tn columns (both x R).
-// RLE_XCD=0 keeps the plain row-major tile order.
-static void xcd_plan(GemmArgs& g) {
+// rle_plan.xcd 0 keeps the plain row-major tile order.
+static void xcd_plan(GemmArgs& g, bool xcd) {
   GemmHot& h = g.hot;
   h.xb = 0;
-  const char* e = std::getenv("RLE_XCD");
-  if (e && e[0] == '0') return;
+  if (!xcd) return;
   const int tm = g.hot.wide ? g.tiles_m / 4 : g.tiles_m, rh = g.hot.wide ? 64 : 16;  // tile rows, rows per tile
   const int T = tm * g.tiles_n;
   if (T < 16 || g.tiles_n < 2) return;
@@ -1091,6 +1090,7 @@ struct Prog {
   static constexpr int max_ops = kLevelOps;
   // register-blocked wide weight-gradient tiles (rle_plan rb)
   int rb = 0;
+  int xcd = 1;  // XCD-aware tile order (rle_plan xcd)
   // (Engine::norm_fin) the finalized AvgL1Norm row means of this program: producer partials -> (means, resource)
   std::map<const float*, std::pair<float*, int>> norm_fins;
   static bool rb_eligible(const GemmArgs& g) {
@@ -1103,7 +1103,7 @@ struct Prog {
     for (Op& op : ops)
       if (op.kind == OP_GEMM) {
         op.gemm.hot.rb = rb && rb_eligible(op.gemm) ? 1 : 0;
-        gemm_finalize(op.gemm);
+        gemm_finalize(op.gemm, xcd != 0);
         check_gemm(op.gemm);
         if (std::getenv("RLE_AUDIT")) audit_gemm(op.gemm);  // (read per op: tests set it per engine)
       }
@@ -1306,12 +1306,11 @@ struct Prog {
   }
 };
 
-// ---- Direct AQL dispatch (default; RLE_AQL=0 for the hipGraph path): the step graphs' level
-// launches written as kernel-dispatch packets into the engine's own HSA queue instead of
-// hipGraph replays, with chosen fence scopes (RLE_AQL_ACQ / RLE_AQL_REL: 0 none, 1 agent,
-// 2 system; default agent / agent, as HIP's own).  The first packet of a flush acquires and its
-// last releases at system scope (host-written inputs, host-read results).  tools/mbaql.cpp
-// measured the same packets at 3.83 us per level against hipGraph's 4.08.
+// ---- Direct AQL dispatch (default; rle_plan.dispatch 0 for the hipGraph path): the step graphs' level
+// launches written as kernel-dispatch packets into the engine's own HSA queue instead of hipGraph
+// replays.  Fences as HIP's own: agent-scope acquire and release between dependent levels; the first
+// packet of a flush acquires and its last releases at system scope (host-written inputs, host-read
+// results).  tools/mbaql.cpp measured the same packets at 3.83 us per level against hipGraph's 4.08.
 // One HSA queue of a device, shared by the engines aql_open hands it to (at most kAqlQueuesPerDevice
 // per device and process: more user-mode queues than that oversubscribe the device's hardware queue
 // slots, and every queue's dispatches slow down -- profiles/r05_seeds_aql.txt, r05_seeds_hwq.txt).
@@ -1321,7 +1320,7 @@ struct AqlHw {
   hsa_queue_t* q = nullptr;
   uint64_t kobj[KS_COUNT] = {};  // rle_level<false, ks>
   uint32_t gseg[KS_COUNT] = {}, pseg[KS_COUNT] = {};
-  int acq = HSA_FENCE_SCOPE_AGENT, rel = HSA_FENCE_SCOPE_AGENT;
+  std::atomic<bool> failed{false};  // a burst on this queue timed out: every engine sharing it fails fast
   std::mutex mu;
   ~AqlHw() {
     if (q) (void)hsa_queue_destroy(q);
@@ -1344,7 +1343,10 @@ struct AqlQueue {
   double us_per_launch = 0.0;
   bool failed = false;          // a flush timed out: its packets may still be queued, the queue takes no more
   size_t inflight = 0;          // packets submitted since the last aql_complete
+  uint64_t last_idx = 0;        // queue index of the last packet this engine submitted
+  bool timed_idle = false;      // the oldest burst in flight started on an idle queue (its wall time is its own)
   std::chrono::steady_clock::time_point t0{};  // first doorbell of the oldest burst in flight
+  bool closed() const { return failed || (hw && hw->failed.load(std::memory_order_relaxed)); }
   ~AqlQueue() {
     if (sig.handle) (void)hsa_signal_destroy(sig);
   }
@@ -1410,9 +1412,6 @@ static std::shared_ptr<AqlHw> aql_hw_create(int dev) {
   HSACHK(hsa_agent_get_info(A->agent, HSA_AGENT_INFO_QUEUE_MAX_SIZE, &qmax));
   HSACHK(hsa_queue_create(A->agent, std::min<uint32_t>(qmax, 16384), HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
                           UINT32_MAX, UINT32_MAX, &A->q));
-  auto scope = [](const char* v, int d) { return v ? std::max(0, std::min(2, std::atoi(v))) : d; };
-  A->acq = scope(std::getenv("RLE_AQL_ACQ"), HSA_FENCE_SCOPE_AGENT);
-  A->rel = scope(std::getenv("RLE_AQL_REL"), HSA_FENCE_SCOPE_AGENT);
   return A;
 }
 // The engine's queue: a new HSA queue while the device has fewer than kAqlQueuesPerDevice live ones,
@@ -1456,7 +1455,8 @@ static int aql_wait_step(double expected_us, double elapsed_us, double timeout_s
   *sleep_us = std::min(left, kAqlSliceUs);
   return AQL_SLEEP;
 }
-// Waits until pred() holds, by aql_wait_step's policy; on timeout the queue is marked failed.
+// Waits until pred() holds, by aql_wait_step's policy; on timeout the engine's queue and the shared
+// hardware queue are marked failed (every engine on it then fails fast instead of waiting 60 s again).
 template <class Pred>
 static void aql_wait(AqlQueue& A, Pred pred, double expected_us, const char* what) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -1466,40 +1466,71 @@ static void aql_wait(AqlQueue& A, Pred pred, double expected_us, const char* wha
     const int act = aql_wait_step(expected_us, el, kAqlTimeoutS, &sl);
     if (act == AQL_TIMEOUT) {
       A.failed = true;
+      if (A.hw) A.hw->failed = true;
       A.pending.clear();
+      A.inflight = 0;
       throw Error{RLE_EHIP, std::string("aql: ") + what + " did not complete within 60 s; the engine's queue is "
                             "closed (every later step fails; destroy the engine)"};
     }
     if (act == AQL_SLEEP) std::this_thread::sleep_for(std::chrono::duration<double, std::micro>(sl));
   }
 }
+static Error aql_closed_error() { return Error{RLE_EHIP, "aql: the engine's queue is closed after a timed-out dispatch"}; }
+
+// Doorbell batching: the doorbell is rung after a packet whose queue index is the last of an aligned
+// group of kAqlDoorbellEvery (and after a burst's last packet).  The groups are aligned to the ABSOLUTE
+// index, so the packets one doorbell publishes never straddle the end of the ring (its size is a power
+// of two >= kAqlDoorbellEvery).  Queue interceptors (rocprofv3's kernel tracing wraps the queue) copy
+// the packets of one doorbell as one contiguous run of the ring: a run that crossed the ring's end read
+// past it (profiles/r05_prof_crash.txt: SIGSEGV at the 1 MB ring's end, 16384 x 64 B).
+constexpr uint64_t kAqlDoorbellEvery = 64;
+static bool aql_doorbell_after(uint64_t idx, bool last) { return last || (idx & (kAqlDoorbellEvery - 1)) == kAqlDoorbellEvery - 1; }
 
 // Writes every pending packet and rings the doorbell; the completion signal counts the submitted bursts
 // still in flight (each burst's last packet decrements it), so bursts may be submitted back to back
-// (rle_step_async) and aql_complete waits for all of them.
+// (rle_step_async) and aql_complete waits for all of them.  A slot is reserved only once the ring has
+// room for it (the wait happens before hsa_queue_add_write_index, under hw.mu, so a timed-out wait never
+// leaves a reserved slot unwritten for the packet processor to stall on).
 static void aql_submit(AqlQueue& A) {
   const size_t n = A.pending.size();
   if (!n) return;
-  if (A.failed) {
+  if (A.closed()) {
     A.pending.clear();
-    throw Error{RLE_EHIP, "aql: the engine's queue is closed after a timed-out dispatch"};
+    throw aql_closed_error();
   }
   AqlHw& hw = *A.hw;
   std::lock_guard<std::mutex> lk(hw.mu);
-  hsa_signal_add_relaxed(A.sig, 1);
   hsa_queue_t* q = hw.q;
   const uint64_t mask = q->size - 1;
+  if (!A.inflight) {
+    A.timed_idle = hsa_queue_load_read_index_scacquire(q) == hsa_queue_load_write_index_relaxed(q);
+  }
+  hsa_signal_add_relaxed(A.sig, 1);
   bool rung = false;
+  uint64_t since_bell = 0;  // packets written since the last doorbell
+  auto bell = [&](uint64_t idx) {
+    hsa_signal_store_screlease(q->doorbell_signal, idx);
+    since_bell = 0;
+    if (!A.inflight && !rung) A.t0 = std::chrono::steady_clock::now();
+    rung = true;
+  };
   for (size_t i = 0; i < n; ++i) {
-    const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
-    if (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
-      // (bursts of > q->size packets) wait until half the queue has drained, then write on: the host
-      // sleeps through most of it instead of tracking the device one retired packet at a time
+    const uint64_t next = hsa_queue_load_write_index_relaxed(q);
+    if (next - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+      // (bursts of > q->size packets) publish what is written, wait until half the queue has drained, then
+      // write on: the host sleeps through most of it instead of tracking the device one packet at a time
+      if (since_bell) bell(next - 1);
       const uint64_t half = q->size / 2;
-      const double ahead = (double)(idx - hsa_queue_load_read_index_scacquire(q) - half + 1);
-      aql_wait(A, [&] { return idx - hsa_queue_load_read_index_scacquire(q) < half; }, ahead * A.us_per_launch,
-               "a queue slot");
+      const double ahead = (double)(next - hsa_queue_load_read_index_scacquire(q) - half + 1);
+      try {
+        aql_wait(A, [&] { return next - hsa_queue_load_read_index_scacquire(q) < half; }, ahead * A.us_per_launch,
+                 "a queue slot");
+      } catch (...) {
+        hsa_signal_subtract_relaxed(A.sig, 1);  // (this burst's last packet will never be written)
+        throw;
+      }
     }
+    const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
     auto* pk = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx & mask);
     pk->workgroup_size_x = kThreads;
     pk->workgroup_size_y = 1;
@@ -1516,29 +1547,34 @@ static void aql_submit(AqlQueue& A) {
     pk->reserved2 = 0;
     const bool last = i + 1 == n;
     pk->completion_signal = last ? A.sig : hsa_signal_t{0};
-    const int a = i == 0 ? HSA_FENCE_SCOPE_SYSTEM : hw.acq, r = last ? HSA_FENCE_SCOPE_SYSTEM : hw.rel;
+    const int a = i == 0 ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+    const int r = last ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
     const uint16_t hdr = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
                          (a << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) | (r << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
     __atomic_store_n((uint32_t*)pk, (uint32_t)hdr | (1u << 16), __ATOMIC_RELEASE);  // header | setup (1 dim)
-    if (last || (i & 63) == 63) {
-      hsa_signal_store_screlease(q->doorbell_signal, idx);
-      if (!A.inflight && !rung) A.t0 = std::chrono::steady_clock::now();
-      rung = true;
-    }
+    ++since_bell;
+    if (last) A.last_idx = idx;
+    if (aql_doorbell_after(idx, last)) bell(idx);
   }
   A.inflight += n;
   A.pending.clear();
 }
 // Waits until every submitted burst has retired (host-side wall time from the first doorbell of the
-// oldest burst in flight to completion added to *ms when given).
+// oldest burst in flight to completion added to *ms when given).  The sleep estimate counts only the
+// packets up to this engine's last one (other engines' later bursts on a pooled queue are not its
+// wait), and the per-packet bound is refreshed only from bursts that started on an idle queue.
 static void aql_complete(AqlQueue& A, double* ms) {
   if (!A.inflight) return;
+  if (A.closed()) {
+    A.inflight = 0;
+    throw aql_closed_error();
+  }
   hsa_queue_t* q = A.hw->q;
-  // (the packets not yet retired: those behind the read index)
-  const double left = (double)(hsa_queue_load_write_index_relaxed(q) - hsa_queue_load_read_index_scacquire(q));
+  const uint64_t rd = hsa_queue_load_read_index_scacquire(q);
+  const double left = A.last_idx + 1 > rd ? (double)(A.last_idx + 1 - rd) : 0.0;
   aql_wait(A, [&] { return hsa_signal_load_scacquire(A.sig) < 1; }, left * A.us_per_launch, "a dispatch");
   const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - A.t0).count();
-  if (A.inflight >= kAqlMinBurst) {
+  if (A.inflight >= kAqlMinBurst && A.timed_idle) {
     const double per = kAqlBoundFrac * wall_ms * 1e3 / (double)A.inflight;
     A.us_per_launch = A.us_per_launch > 0.0 ? std::min(A.us_per_launch, per) : per;
   }
@@ -1559,8 +1595,8 @@ struct Graph {
   std::vector<int> nops, nwg, off;
   std::string desc;
   int nlaunch = 0;  // rle_level dispatches per replay (a level of > kLevelOps ops takes several)
-  std::vector<std::vector<Op>> host_levels;  // the launches' host op tables (RLE_EAGER replays)
-  std::vector<LevelLaunch> aql;               // (RLE_AQL) the dispatches' kernel arguments ...
+  std::vector<std::vector<Op>> host_levels;  // the launches' host op tables (rle_plan dispatch 2)
+  std::vector<LevelLaunch> aql;               // (rle_plan dispatch 1) the dispatches' kernel arguments ...
   unsigned char* aql_ka = nullptr;            // ... in device memory, 128 B apart
   int levels() const { return (int)nops.size(); }
 };
@@ -1606,6 +1642,7 @@ static rle_plan plan_defaults() {
   p.lap_w = p.head_w = p.adam_w = -1;
   p.wide = -1;
   p.lpt = -1;
+  p.dispatch = p.dpf = p.xcd = -1;
   return p;
 }
 
@@ -1659,6 +1696,9 @@ struct Engine {
     if (plan.adam_w < 0) plan.adam_w = algo == RLE_SAC ? 16 : 8;
     if (plan.level_cap < 0) plan.level_cap = 0;
     plan.wide = plan.wide == 32 || plan.wide == 0 ? plan.wide : 64;  // (the tile width; 1 = 64)
+    plan.dispatch = plan.dispatch < 0 ? 1 : std::min(plan.dispatch, 2);
+    plan.dpf = plan.dpf < 0 ? 1 : (plan.dpf ? 1 : 0);
+    plan.xcd = plan.xcd < 0 ? 1 : (plan.xcd ? 1 : 0);
   }
   int S, Sp, A, Ap, H, Hp, B;
   int Z = 0, Zp = 0;    // TD7: SALE embedding width zs_dim (sale.py:23), padded
@@ -4034,13 +4074,10 @@ struct Engine {
       for (int w : G.nwg) G.trace_n += w;
       G.trace = mem.make<unsigned long long>((size_t)G.trace_n * trace_stride());
     }
-    if (aql_mode() && !G.trace) g_level_rec = &G.aql;
+    if (plan.dispatch == 1 && !G.trace) g_level_rec = &G.aql;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     long long tr_off = 0;
-    static const bool dpf = [] {
-      const char* e = std::getenv("RLE_NO_DPF");  // A/B: no next-level descriptor prefetch
-      return !(e && e[0] == '1');
-    }();
+    const bool dpf = plan.dpf != 0;  // (rle_plan dpf: the next level's descriptor prefetch workgroups)
     for (size_t l = 0; l < levels.size(); ++l) {
       // (after the last level: this graph's first, as the next replay is usually of the same graph)
       const size_t ln = l + 1 < levels.size() ? l + 1 : 0;
@@ -4107,6 +4144,7 @@ struct Engine {
     tn_seq = 0;
     Prog p0;
     p0.rb = plan.rb;
+    p0.xcd = plan.xcd;
     f(p0);
     std::vector<int> tplan(tn_seq, 16);
     auto at = [&](int seq) -> int& { return tplan[seq]; };
@@ -4155,6 +4193,7 @@ struct Engine {
     tn_seq = 0;
     Prog p;
     p.rb = plan.rb;
+    p.xcd = plan.xcd;
     f(p);
     tn_plan.clear();
     return p;
@@ -4179,6 +4218,7 @@ struct Engine {
     multi_k = pair_k();
     for (int set = 0; set < 2; ++set) {
       Prog pp;
+      pp.xcd = plan.xcd;
       build_prime(pp, sac, set);
       g_prime[set] = capture(pp);
       if (algo == RLE_TD7) {
@@ -4223,10 +4263,12 @@ struct Engine {
     }
     if (algo == RLE_TD7) {
       Prog ph;
+      ph.xcd = plan.xcd;
       build_td7_hard(ph);
       g_hard = capture(ph);
       if (td7_fold()) {
         Prog pf;
+        pf.xcd = plan.xcd;
         add_target_fold(pf);
         g_fold = capture(pf);
       }
@@ -4289,36 +4331,19 @@ struct Engine {
 
   // ---------------------------------------------------------------- run
   long long launches = 0;  // rle_level dispatches enqueued by step graphs (rle_launch_count)
-  std::unique_ptr<AqlQueue> aql;  // (RLE_AQL=1) direct dispatch of the step graphs
+  std::unique_ptr<AqlQueue> aql;  // (rle_plan dispatch 1) direct dispatch of the step graphs
   bool aql_active = false;        // inside step(): graphs go to the AQL queue
   // Direct AQL dispatch of the step graphs (rle_step / rle_step_timed wait for their bursts; rle_step_async
   // leaves its burst in flight on the engine's own queue -- each seed on a queue of its own, where hipGraph
   // replays on HIP streams share GPU_MAX_HW_QUEUES hardware queues -- and every other entry point, and
-  // every replay operation on a replay the engine is bound to, drains it first: aql_drain).  RLE_AQL=0:
-  // hipGraph everywhere (A/B; the launch path does not change any result).
-  static bool aql_mode() {
-    static const bool on = [] {
-      const char* e = std::getenv("RLE_AQL");
-      if (e) return e[0] != '0';
-      // rocprofv3's kernel and HSA API tracing intercept HSA queue creation, and packets written into an
-      // intercepted queue crash (profiles/r05_prof_crash.txt): under those tracers (their option variables,
-      // "1" when on) the levels replay as hipGraphs -- the same rle_level dispatches, traced as usual
-      for (const char* v : {"ROCPROF_KERNEL_TRACE", "ROCPROF_HSA_CORE_API_TRACE", "ROCPROF_HSA_AMD_EXT_API_TRACE"}) {
-        const char* t = std::getenv(v);
-        if (t && t[0] == '1') return false;
-      }
-      return true;
-    }();
-    return on;
-  }
+  // every replay operation on a replay the engine is bound to, drains it first: aql_drain).  rle_plan
+  // dispatch 0 / 2: hipGraph replays / launches on the stream (A/B; the launch path changes no result).
+  bool aql_mode() const { return plan.dispatch == 1; }
   void aql_drain(double* ms = nullptr) {
     if (aql) aql_complete(*aql, ms);
   }
   void launch_graph(const Graph& G) {
-    static const bool eager = [] {
-      const char* e = std::getenv("RLE_EAGER");  // A/B: level launches on the stream, no graph
-      return e && e[0] == '1';
-    }();
+    const bool eager = plan.dispatch == 2;  // (A/B: level launches on the stream, no graph)
     if (aql_active && !G.aql.empty()) {
       for (size_t i = 0; i < G.aql.size(); ++i) aql->pending.push_back({G.aql_ka + i * 128, G.aql[i].grid, G.aql[i].ks});
       launches += G.nlaunch;
@@ -4368,7 +4393,7 @@ struct Engine {
     if (fold_dirty && g_fold.x) launch_graph(g_fold);
     fold_dirty = false;
     int done = 0;
-    // direct dispatch (RLE_AQL=1): the graphs' levels go to the engine's own queue; the HIP
+    // direct dispatch (rle_plan dispatch 1): the graphs' levels go to the engine's own queue; the HIP
     // stream is drained first and the queue after each chunk (host-side ordering between them; async:
     // the last chunk stays in flight, aql_drain)
     const bool use_aql = aql_mode() && !g_pol[0].aql.empty();
@@ -4935,7 +4960,11 @@ int rle_get_plan(rle_engine* h, rle_plan* out) {
 int rle_destroy(rle_engine* h) {
   return guard([&] {
     if (!h) return;
-    Engine& e = drained(h);
+    Engine& e = *h->e;
+    try {
+      e.aql_drain();
+    } catch (const Error&) {  // (a timed-out burst closed the engine's queue: destroy anyway)
+    }
     (void)hipStreamSynchronize(e.stream);
     if (e.replay) {
       auto& us = e.replay->users;
@@ -5441,6 +5470,59 @@ int rle_graph_trace(rle_engine* h, int which, unsigned long long* out, long long
 }
 
 int rle_trace_stride(void) { return rle::trace_stride(); }
+
+// The failed-queue state machine of the AQL path without a device (no HSA call is reached): a closed
+// queue refuses new bursts and completes at once, for the engine that timed out and for every engine
+// sharing its hardware queue; doorbell groups never straddle the ring's end.
+int rle_aql_selftest(void) {
+  return guard([&] {
+    using namespace rle;
+    auto hw = std::make_shared<AqlHw>();
+    AqlQueue a, b;
+    a.hw = hw;
+    b.hw = hw;
+    REQUIRE(!a.closed() && !b.closed(), "selftest: fresh queues closed");
+    a.failed = true;
+    hw->failed = true;  // (as aql_wait's timeout leaves them)
+    a.pending.push_back({nullptr, 1, 0});
+    a.inflight = 7;
+    int refused = 0;
+    try {
+      aql_submit(a);
+    } catch (const Error&) {
+      ++refused;
+    }
+    REQUIRE(refused == 1 && a.pending.empty(), "selftest: a closed queue took a burst");
+    try {
+      aql_complete(a, nullptr);
+    } catch (const Error&) {
+      ++refused;
+    }
+    REQUIRE(refused == 2 && a.inflight == 0, "selftest: a closed queue waited for its burst");
+    aql_complete(a, nullptr);  // (nothing in flight: returns)
+    b.pending.push_back({nullptr, 1, 0});
+    try {
+      aql_submit(b);
+    } catch (const Error&) {
+      ++refused;
+    }
+    REQUIRE(refused == 3, "selftest: an engine sharing a failed hardware queue took a burst");
+    // doorbell groups: for every start index, the packets between two doorbells lie in one pass of the ring
+    for (uint64_t size : {64ull, 1024ull, 16384ull})
+      for (uint64_t start = size - 130; start < size + 130; ++start)
+        for (uint64_t n : {1ull, 5ull, 64ull, 200ull}) {
+          uint64_t first = start;
+          for (uint64_t i = start; i < start + n; ++i)
+            if (aql_doorbell_after(i, i + 1 == start + n)) {
+              REQUIRE(first / size == i / size, "selftest: a doorbell group straddles the ring's end");
+              first = i + 1;
+            }
+          REQUIRE(first == start + n, "selftest: packets left without a doorbell");
+        }
+    a.hw.reset();
+    b.hw.reset();
+  });
+}
 
 int rle_aql_wait_plan(double expected_us, double elapsed_us, double timeout_s, double* sleep_us) {
   double sl = 0.0;

@@ -2036,7 +2036,9 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       mat_st4(g.out, ib, j, make_float4(dz[0], dz[1], dz[2], dz[3]));
     }
     ls = wg_sum(ls, red);
-    if (tid == 0) GW(g.loss_part)[t] = t == 0 ? ls + (float)g.M * sload(g.qb) : ls;
+    // (partials by tile, not by workgroup: the sum's order does not follow the XCD tile order)
+    const int tix = it * tiles_n + jt;
+    if (tid == 0) GW(g.loss_part)[tix] = tix == 0 ? ls + (float)g.M * sload(g.qb) : ls;
   } else if constexpr (EPI == EPI_NBDOT) {  // sale.py:11-13 backward, first half (the rest: kDwNb)
     auto epi_nbdot = [&](const f32x4 acc, const int i0, const int ib, const float4 nbxv, float* red) {
       float rd[4] = {0.f, 0.f, 0.f, 0.f};
@@ -2101,7 +2103,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       mat_st4(g.out, ib, j, make_float4(gr[0], gr[1], gr[2], gr[3]));
     }
     d2 = wg_sum(d2, red);
-    if (tid == 0) GW(g.loss_part)[t] = d2;
+    if (tid == 0) GW(g.loss_part)[it * tiles_n + jt] = d2;  // (by tile: see EPI_QHEAD)
   } else {  // EPI_ADAM (torch.optim.Adam single-tensor law, see oracle/agents.py)
     const CAS AdamArgs& ad = g.adam;
     float gg = 0.f;

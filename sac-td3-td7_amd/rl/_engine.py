@@ -52,6 +52,7 @@ class Plan(ctypes.Structure):
         ("flat_div", _int), ("balance", _int), ("tiny_w", _int), ("uni_w", _int), ("tiny_wg", _int),
         ("sched_cap", _int), ("fuse_off", ctypes.c_uint), ("fuse_on", ctypes.c_uint), ("rb", _int),
         ("pl_w", _int), ("lap_w", _int), ("head_w", _int), ("adam_w", _int), ("wide", _int), ("lpt", _int),
+        ("dispatch", _int), ("dpf", _int), ("xcd", _int),
     ]
 
 
@@ -147,6 +148,7 @@ SIGNATURES = {
     "rle_graph_trace": (_int, [_vp, _int, ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)]),
     "rle_trace_stride": (_int, []),
     "rle_aql_wait_plan": (_int, [ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
+    "rle_aql_selftest": (_int, []),
     "rle_eval": (_int, [_vp, _int, _cs, _cs, _f32p, _f32p, _int, _f32p]),
     "rle_sac_rsample": (_int, [_vp, _f32p, _f32p, _f32p, _int, _f32p, _f32p]),
     "rle_get_info": (_int, [_vp, _int, _f32p]),

@@ -67,3 +67,14 @@ def test_aql_wait_policy_releases_the_host_core():
     assert plan(250_000.0, 400_000.0)[0] == 0           # overran the estimate: spin, no more sleeping
     assert plan(250_000.0, 61e6)[0] == 2                # past 60 s: time out
     assert plan(250_000.0, 1.5e6, timeout=1.0)[0] == 2
+
+
+def test_aql_failed_queue_fails_fast_and_doorbells_stay_in_one_ring_pass():
+    """A queue closed by a timed-out burst refuses new bursts and completes at once (so rle_destroy and every
+    later entry point return instead of waiting another 60 s), also for engines sharing its hardware queue;
+    doorbell groups never straddle the ring's end (engine.cpp aql_doorbell_after, the rocprofv3 crash of
+    profiles/r05_prof_crash.txt).  No GPU: rle_aql_selftest reaches no HSA call."""
+    from rl import _engine
+
+    lib = _engine.lib()
+    assert lib.rle_aql_selftest() == 0, lib.rle_last_error()

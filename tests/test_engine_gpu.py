@@ -589,7 +589,9 @@ def test_plan_is_explicit_and_env_free(name, monkeypatch):
 
     base = run()
     for var, val in (("RLE_LEVEL_CAP", "512"), ("RLE_PL_TN", "16"), ("RLE_PRE_TN", "16"), ("RLE_PAIR", "2"),
-                     ("RLE_NO_HEADDX", "1"), ("RLE_FLAT_DIV", "1"), ("RLE_TN_MIN", "64")):
+                     ("RLE_NO_HEADDX", "1"), ("RLE_FLAT_DIV", "1"), ("RLE_TN_MIN", "64"), ("RLE_AQL", "0"),
+                     ("RLE_AQL_ACQ", "0"), ("RLE_AQL_REL", "0"), ("RLE_EAGER", "1"), ("RLE_NO_DPF", "1"),
+                     ("RLE_XCD", "0")):
         monkeypatch.setenv(var, val)
     env = run()
     assert env[0].plan() == base[0].plan()
@@ -600,6 +602,11 @@ def test_plan_is_explicit_and_env_free(name, monkeypatch):
     assert fields[0].plan()["level_cap"] == 512 and fields[0].plan() == text[0].plan()
     same(fields, text)
     assert fields[0].describe(0) != base[0].describe(0)  # (a narrower level capacity widens other tiles)
+    # the launch choices (rle_plan dispatch / dpf / xcd) change how the levels reach the device, not a float
+    for launch in (dict(dispatch=0, dpf=0, xcd=0), dict(dispatch=2)):
+        other = run(E.make_plan(**launch))
+        assert all(other[0].plan()[k] == v for k, v in launch.items())
+        same(base, other)
 
 
 def _alg_dims(g):

@@ -107,24 +107,15 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
         E.Replay(16, 3, 1, False)
 
 
-def test_bench_timer_label_follows_the_dispatch_path(monkeypatch):
-    """bench.aql_dispatch mirrors engine.cpp Engine::aql_mode: RLE_AQL decides when set; otherwise direct AQL
-    dispatch unless rocprofv3's kernel / HSA API tracing is on (hipGraph replays under those tracers)."""
+def test_bench_timer_label_follows_the_dispatch_path():
+    """The line's engine_timer names the clock of the engine's rle_plan.dispatch (no environment variable
+    chooses the dispatch path: it is a plan field, rle.h)."""
     sys.path.insert(0, REPO)
     import bench
 
-    for v in ("RLE_AQL", "ROCPROF_KERNEL_TRACE", "ROCPROF_HSA_CORE_API_TRACE", "ROCPROF_HSA_AMD_EXT_API_TRACE"):
-        monkeypatch.delenv(v, raising=False)
-    assert bench.aql_dispatch()
-    monkeypatch.setenv("ROCPROF_KERNEL_TRACE", "0")
-    assert bench.aql_dispatch()
-    monkeypatch.setenv("ROCPROF_KERNEL_TRACE", "1")
-    assert not bench.aql_dispatch()
-    monkeypatch.setenv("RLE_AQL", "1")
-    assert bench.aql_dispatch()
-    monkeypatch.setenv("RLE_AQL", "0")
-    monkeypatch.delenv("ROCPROF_KERNEL_TRACE")
-    assert not bench.aql_dispatch()
+    kw = dict(wall=0.5, gpu_s=0.45, lv_policy=30, lv_plain=20)
+    assert bench.summarize(1, 1000, 10, **kw)["engine_timer"].startswith("host wall, first AQL doorbell")
+    assert bench.summarize(1, 1000, 10, dispatch=0, **kw)["engine_timer"] == "HIP events on the engine stream"
 
 
 def test_bench_workload_figures_match_survey():
@@ -175,14 +166,60 @@ def test_bench_gpus_n_launches_its_own_ranks():
     env = dict(os.environ, RLE_BENCH_STUB=os.path.join(REPO, "tests", "bench_stub.py"))
     env.pop("WORLD_SIZE", None)
     res = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "40",
-                          "--warmup", "2", "--no-cpu-baseline"], capture_output=True, text=True, timeout=240,
-                         env=env)
+                          "--warmup", "2", "--cpu-seconds", "0.5", "--cpu-replay", "8192"], capture_output=True,
+                         text=True, timeout=240, env=env)
     assert res.returncode == 0, res.stderr[-2000:]
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, res.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 40 and out["scaling"] == "weak"
     assert out["value"] > 0
+    # BASELINE.md's N-process CPU figure: both ranks ran the oracle concurrently, each on its own CPU slice
+    cb = out["cpu_baseline"]
+    assert cb["procs"] == 2 and len(cb["per_proc"]) == 2 and all(v > 0 for v in cb["per_proc"])
+    assert cb["kind"] == "port" and abs(cb["value"] - sum(cb["per_proc"])) < 1e-2
+    assert cb["cores"] == sum(cb["threads_per_proc"]) >= 2
+    # each rank pinned (here: no KFD topology, so an even split of the allowed CPUs)
+    pins = out["config"]["rank_pinning"]
+    assert len(pins) == 2 and all(p["cpus"] >= 1 for p in pins)
+
+
+def test_rank_pinning_follows_gpu_numa_locality(tmp_path, monkeypatch):
+    """bench.gpu_local_cpus: a rank is pinned to the CPUs NUMA-local to its GPU (the PCI device's
+    local_cpulist, found from the KFD node's domain / location_id), split among the ranks whose GPUs share
+    them, without a HIP call; the allowed CPUs split by rank when the locality cannot be read."""
+    import bench
+
+    kfd, pci = tmp_path / "kfd", tmp_path / "pci"
+    # node 0: CPU; nodes 1-4: GPUs at buses 0x11, 0x21 (NUMA 0: CPUs 0-7) and 0x81, 0x91 (NUMA 1: CPUs 8-15)
+    for node, bus in ((0, None), (1, 0x11), (2, 0x21), (3, 0x81), (4, 0x91)):
+        d = kfd / str(node)
+        d.mkdir(parents=True)
+        props = "simd_count 0\n" if bus is None else f"simd_count 1024\nlocation_id {bus << 8}\ndomain 0\n"
+        d.joinpath("properties").write_text(props)
+        if bus is not None:
+            p = pci / f"0000:{bus:02x}:00.0"
+            p.mkdir(parents=True)
+            p.joinpath("local_cpulist").write_text("0-7\n" if bus < 0x80 else "8-15\n")
+            p.joinpath("numa_node").write_text("0\n" if bus < 0x80 else "1\n")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    allowed = list(range(16))
+    got = [bench.gpu_local_cpus(r, 4, str(kfd), str(pci), allowed) for r in range(4)]
+    assert [c for c, _ in got] == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9, 10, 11], [12, 13, 14, 15]]
+    assert [i["numa_node"] for _, i in got] == [0, 0, 1, 1] and all(i["numa_local"] for _, i in got)
+    assert got[2][1]["gpu_bdf"] == "0000:81:00.0"
+    # two ranks on GPUs of different NUMA nodes each get their node's CPUs
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1,2")
+    got = [bench.gpu_local_cpus(r, 2, str(kfd), str(pci), allowed)[0] for r in range(2)]
+    assert got == [list(range(0, 8)), list(range(8, 16))]
+    # a box whose allowed CPUs are all off the GPU's node, or no topology: an even split of the allowed CPUs
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    cpus, info = bench.gpu_local_cpus(1, 2, str(kfd), str(pci), [20, 21, 22, 23])
+    assert cpus == [22, 23] and not info["numa_local"]
+    cpus, info = bench.gpu_local_cpus(0, 2, str(tmp_path / "none"), str(pci), allowed)
+    assert cpus == list(range(8)) and info["gpu_bdf"] is None
+    assert bench.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
 
 
 def test_bench_seeds_per_gpu_line():

@@ -11,8 +11,8 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out
 mkdir -p $OUT
 cd $ROOT
-if [ -x sac-td3-td7_amd/lib/mbcoh ]; then
-  timeout -k 10 120 sac-td3-td7_amd/lib/mbcoh 200 20 | tee $OUT/${TAG}_mbcoh.txt || exit 1
+if [ -x build/mbcoh ]; then
+  timeout -k 10 120 build/mbcoh 200 20 | tee $OUT/${TAG}_mbcoh.txt || exit 1
 fi
 # BITCMP_BURST=6 (env): compare after whole 6-step graph replays instead of single steps
 for run in 1 2; do

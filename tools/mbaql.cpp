@@ -8,8 +8,8 @@
 // buffers (level l reads buf[l & 1], writes buf[(l + 1) & 1]): a cache that is not refreshed
 // across levels returns stale values, and the final buffer differs from the hipGraph run.
 // Build: hipcc --offload-arch=gfx950 --offload-device-only --no-gpu-bundle-output -O3 -c
-//   tools/mbaql_k.hip -o sac-td3-td7_amd/lib/mbaql_k.co &&
-//   hipcc -O2 tools/mbaql.cpp -o sac-td3-td7_amd/lib/mbaql -lhsa-runtime64
+//   tools/mbaql_k.hip -o build/mbaql_k.co &&
+//   hipcc -O2 tools/mbaql.cpp -o build/mbaql -lhsa-runtime64
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -68,7 +68,7 @@ static hsa_status_t find_exe(hsa_executable_t e, void*) {
 }
 
 int main(int argc, char** argv) {
-  const char* path = argc > 1 ? argv[1] : "sac-td3-td7_amd/lib/mbaql_k.co";
+  const char* path = argc > 1 ? argv[1] : "build/mbaql_k.co";
   std::ifstream f(path, std::ios::binary);
   std::vector<char> co((std::istreambuf_iterator<char>(f)), {});
   if (co.empty()) { printf("no code object %s\n", path); return 1; }

@@ -6,7 +6,7 @@
 // previous level (rows owned by its team; sc1 buffer loads), does a little math, writes
 // a 16 x 64 tile (sc1 stores), then a sharded team barrier (agent atomics, sc1 poll).
 // Output is checked against the host.  Compared with the same per-level body as one
-// kernel launch per level.  Build: hipcc --offload-arch=gfx950 -O3 tools/mbchain.hip -o sac-td3-td7_amd/lib/mbchain
+// kernel launch per level.  Build: hipcc --offload-arch=gfx950 -O3 tools/mbchain.hip -o build/mbchain
 #include <hip/hip_runtime.h>
 
 #include <cmath>

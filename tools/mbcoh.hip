@@ -7,7 +7,7 @@
 //   -> read  (every workgroup loads it: scalar load, or vector load)
 // repeated `iters` times per graph with a new value each time, the graph replayed `reps` times.
 // A cache that a kernel-node boundary does not refresh returns the previous iteration's value.
-// Build: hipcc --offload-arch=gfx950 -O3 tools/mbcoh.hip -o sac-td3-td7_amd/lib/mbcoh
+// Build: hipcc --offload-arch=gfx950 -O3 tools/mbcoh.hip -o build/mbcoh
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

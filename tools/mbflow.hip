@@ -8,7 +8,7 @@
 //             its consumers is dispatched: a wait always ends.  Each wait is bounded anyway (err counts
 //             the waits that gave up; the result is then wrong, never a hang).
 //   nowait:   the same single launch without the waits (the stages' work alone, overlapped)
-// Prints microseconds per stage.  Build: hipcc --offload-arch=gfx950 -O3 tools/mbflow.hip -o sac-td3-td7_amd/lib/mbflow
+// Prints microseconds per stage.  Build: hipcc --offload-arch=gfx950 -O3 tools/mbflow.hip -o build/mbflow
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

@@ -1,5 +1,5 @@
 // Instruction-fetch cost probe: straight-line code of N bytes per wave (GPU box).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mbic.hip -o sac-td3-td7_amd/lib/mbic
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mbic.hip -o build/mbic
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

@@ -1,5 +1,5 @@
 // Main-loop variants on one workgroup, to separate MFMA, load and loop costs (GPU box).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mbk.hip -o sac-td3-td7_amd/lib/mbk
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mbk.hip -o build/mbk
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

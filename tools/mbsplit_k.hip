@@ -1,0 +1,111 @@
+// Device code of tools/mbsplit.cpp (a raw gfx950 code object loaded through HSA): one dependency level
+// of N GEMM ops, dispatched either as ONE dispatch-kernel launch (`mega`: the op found from a preloaded
+// 12-entry table by straight-line selects, its 64-byte descriptor loaded, a switch to the op's
+// variant -- rle_level's structure) or as N launches of specialised kernels (`spec<V>`: operands as
+// preloaded kernel arguments, no decode, no switch, no descriptor; `specd<V>`: the same with the
+// descriptor loaded from memory).  Op body: a 16 x 64 output tile of a [M x 256] x [256 x 256] fp32
+// GEMM in 16 x 16 fragment images (ops.h layout), 4 waves = 4 column blocks, a 4-chunk register ring,
+// v_mfma_f32_16x16x4_f32, a bias + per-variant bounded activation epilogue (six variants so the six
+// bodies are six code paths, as the engine's GEMM variants are).
+// Build: hipcc --offload-arch=gfx950 --offload-device-only --no-gpu-bundle-output -O3
+//   -mllvm -amdgpu-kernarg-preload-count=14 -c tools/mbsplit_k.hip -o build/mbsplit_k.co
+#include <hip/hip_runtime.h>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+struct Desc {  // 64 B, one scalar line
+  const float* a;
+  const float* w;
+  float* out;
+  const float* bias;
+  unsigned long long pad[4];
+};
+
+template <int V>
+__device__ __forceinline__ float act(float x) {
+  if constexpr (V == 0) return tanhf(x);
+  if constexpr (V == 1) return x / (1.f + fabsf(x));
+  if constexpr (V == 2) return fminf(fmaxf(x, -1.f), 1.f);
+  if constexpr (V == 3) return 0.5f * tanhf(x);
+  if constexpr (V == 4) return x / (1.f + x * x);
+  return 0.9f * tanhf(x);
+}
+
+// tile t of an [M x 256] output: row block t / 4, column blocks 4 (t % 4) + wave
+template <int V>
+__device__ __forceinline__ void body(const float* A, const float* W, float* out, const float* bias, int t) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rb = t >> 2, cb = (t & 3) * 4 + wave;
+  const float* pa = A + (size_t)rb * 16 * 256 + lane * 4;  // [rb][16 chunks][256]
+  const float* pw = W + (size_t)cb * 16 * 256 + lane * 4;  // [cb][16 chunks][256]
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  f4 ra[4], rw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    ra[i] = *(const f4*)(pa + i * 256);
+    rw[i] = *(const f4*)(pw + i * 256);
+  }
+#pragma unroll
+  for (int kc = 0; kc < 16; ++kc) {
+    const f4 a = ra[kc & 3], w = rw[kc & 3];
+    if (kc + 4 < 16) {
+      ra[kc & 3] = *(const f4*)(pa + (kc + 4) * 256);
+      rw[kc & 3] = *(const f4*)(pw + (kc + 4) * 256);
+    }
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, w.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, w.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, w.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, w.w, acc, 0, 0, 0);
+  }
+  const float b = bias[cb * 16 + (lane & 15)];
+  f4 o;
+  o.x = act<V>(acc.x + b);
+  o.y = act<V>(acc.y + b);
+  o.z = act<V>(acc.z + b);
+  o.w = act<V>(acc.w + b);
+  *(f4*)(out + ((size_t)rb * 16 + cb) * 256 + lane * 4) = o;
+}
+
+#define SPEC(V)                                                                                              \
+  extern "C" __global__ __launch_bounds__(256, 4) void spec##V(const float* a, const float* w, float* out,   \
+                                                               const float* bias) {                          \
+    body<V>(a, w, out, bias, blockIdx.x);                                                                    \
+  }                                                                                                          \
+  extern "C" __global__ __launch_bounds__(256, 4) void specd##V(const Desc* d) {                            \
+    body<V>(d->a, d->w, d->out, d->bias, blockIdx.x);                                                        \
+  }
+SPEC(0)
+SPEC(1)
+SPEC(2)
+SPEC(3)
+SPEC(4)
+SPEC(5)
+
+// entry q = first workgroup (bits 0-15) | variant (bits 20-23)
+extern "C" __global__ __launch_bounds__(256, 4) void mega(unsigned e0, unsigned e1, unsigned e2, unsigned e3,
+                                                         unsigned e4, unsigned e5, unsigned e6, unsigned e7,
+                                                         unsigned e8, unsigned e9, unsigned e10, unsigned e11,
+                                                         const Desc* ops) {
+  const unsigned entry[12] = {e0, e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11};
+  const int wg = (int)blockIdx.x;
+  int k = 0;
+  unsigned e = entry[0];
+#pragma unroll
+  for (int q = 1; q < 12; ++q) {
+    const unsigned x = entry[q];
+    const bool in = (int)(x & 0xffffu) <= wg;
+    e = in ? x : e;
+    k = in ? q : k;
+  }
+  const int vid = (e >> 20) & 0xf, t = wg - (int)(e & 0xffffu);
+  const Desc& d = ops[k];
+  switch (vid) {
+    case 0: body<0>(d.a, d.w, d.out, d.bias, t); break;
+    case 1: body<1>(d.a, d.w, d.out, d.bias, t); break;
+    case 2: body<2>(d.a, d.w, d.out, d.bias, t); break;
+    case 3: body<3>(d.a, d.w, d.out, d.bias, t); break;
+    case 4: body<4>(d.a, d.w, d.out, d.bias, t); break;
+    default: body<5>(d.a, d.w, d.out, d.bias, t); break;
+  }
+}
+extern "C" __global__ __launch_bounds__(256, 4) void empty(const float*, const float*, float*, const float*) {}
