@@ -1547,8 +1547,12 @@ static void aql_submit(AqlQueue& A) {
     pk->reserved2 = 0;
     const bool last = i + 1 == n;
     pk->completion_signal = last ? A.sig : hsa_signal_t{0};
-    const int a = i == 0 ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
-    const int r = last ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+#ifndef RLE_EXP_ACQ  // (timing-only variant builds: make variant-engine; the product uses agent / agent)
+#define RLE_EXP_ACQ HSA_FENCE_SCOPE_AGENT
+#define RLE_EXP_REL HSA_FENCE_SCOPE_AGENT
+#endif
+    const int a = i == 0 ? HSA_FENCE_SCOPE_SYSTEM : RLE_EXP_ACQ;
+    const int r = last ? HSA_FENCE_SCOPE_SYSTEM : RLE_EXP_REL;
     const uint16_t hdr = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
                          (a << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) | (r << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
     __atomic_store_n((uint32_t*)pk, (uint32_t)hdr | (1u << 16), __ATOMIC_RELEASE);  // header | setup (1 dim)

@@ -67,6 +67,13 @@ __device__ __forceinline__ void st4g(GAS float* p, const float4& v) {
   w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
   *(GAS f32x4*)p = w;
 }
+// Write-through store (sc1): the bytes leave the XCD's L2 during the kernel instead of staying dirty for the
+// launch's end-of-kernel release (its L2 write-back costs ~bytes / 6 TB/s at every level boundary).  For data
+// nothing reads again soon (Adam moments, the weights' T image).  (s_nop 1: the asm store's data registers
+// must not be overwritten right behind it.)
+__device__ __forceinline__ void st4wt(GAS float* p, const f32x4& w) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+}
 
 // Cross-lane reductions through DPP (register-to-register, a few cycles per step)
 // instead of ds_bpermute shuffles (an LDS round trip each).  Fixed order:
@@ -2132,7 +2139,11 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       {  // the weights' T image (+ bias) too: +0.3% over 3 A/B pairs
         f32x4 w;
         w.x = po[0]; w.y = po[1]; w.z = po[2]; w.w = po[3];
+#ifdef RLE_EXP_ADAM_WT
+        st4wt(pw, w);
+#else
         __builtin_nontemporal_store(w, (GAS f32x4*)pw);
+#endif
       }
       // Adam moments: read again only by the next step's Adam of this tile, so streaming
       // (nontemporal) stores -- measured +0.45% (3 A/B pairs, tools/ablib.sh); the T image above
@@ -2140,9 +2151,15 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
       {
         f32x4 w;
         w.x = mo[0]; w.y = mo[1]; w.z = mo[2]; w.w = mo[3];
+#ifdef RLE_EXP_ADAM_WT
+        st4wt(pw + ad.mo, w);
+        w.x = vo[0]; w.y = vo[1]; w.z = vo[2]; w.w = vo[3];
+        st4wt(pw + ad.vo, w);
+#else
         __builtin_nontemporal_store(w, (GAS f32x4*)(pw + ad.mo));
         w.x = vo[0]; w.y = vo[1]; w.z = vo[2]; w.w = vo[3];
         __builtin_nontemporal_store(w, (GAS f32x4*)(pw + ad.vo));
+#endif
       }
       if (!bias_tile) {
         GAS float* qn = GW(ad.w.n) + nidx(ad.w.cbn, ib, j);

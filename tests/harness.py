@@ -9,6 +9,8 @@ from oracle import spec
 from rl import _engine as E
 
 ALGO = {"td7": E.RLE_TD7, "td3": E.RLE_TD3, "sac": E.RLE_SAC}
+# Per-step losses / info columns against the reference or the oracle (rel 1e-3 for <= 10-step losses)
+LOSS_RTOL = 1e-3
 
 
 def parse(g):

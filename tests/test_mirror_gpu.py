@@ -16,6 +16,7 @@ import torch
 
 from oracle import agents as OA
 from oracle import replay as OR
+from harness import LOSS_RTOL  # noqa: E402
 from rl.agent import SAC, TD3, TD7
 from rl.replay_memory import LAPReplayMemory, SimpleReplayMemory
 from rl.runner.run import run_train_ops
@@ -78,7 +79,7 @@ def test_train_ops_on_sampled_batches_matches_oracle(alg, lap):
         ref = orc.step(ob, orep, np.zeros((B, A), np.float32))
         assert list(info) == list(ref)
         for k in ref:
-            _close(info[k], ref[k], 2e-3)
+            _close(info[k], ref[k], LOSS_RTOL)
         if lap:
             np.testing.assert_allclose(rep.priority.numpy()[:300], orep.priority[:300], rtol=1e-4, atol=1e-5)
             assert abs(rep.max_priority - orep.max_priority) <= 1e-4 * orep.max_priority

@@ -19,7 +19,7 @@ from conftest import load_golden
 pytestmark = pytest.mark.gpu
 
 E = pytest.importorskip("rl._engine")
-from harness import engine_from_golden, parse, shape_of  # noqa: E402
+from harness import LOSS_RTOL, engine_from_golden, parse, shape_of  # noqa: E402
 from oracle import spec  # noqa: E402
 from test_oracle import expected_priorities, golden_moments  # noqa: E402
 
@@ -129,7 +129,7 @@ def test_many_block_lap_trajectory_per_step():
         np.testing.assert_allclose(rep.get_priority(Ncap), expected_priorities(g, Ncap, t), rtol=1e-4, atol=1e-5)
         assert rep.state()[2] == pytest.approx(float(g[f"maxprio_{t}"]), rel=1e-4)
         np.testing.assert_allclose(eng.value_bounds(), g[f"vbounds_{t}"].astype(np.float32), rtol=1e-4, atol=1e-4)
-        np.testing.assert_allclose(info[:3], g["info"][t], rtol=2e-3, atol=1e-4, equal_nan=True)
+        np.testing.assert_allclose(info[:3], g["info"][t], rtol=LOSS_RTOL, atol=1e-4, equal_nan=True)
     eng.set_tapes()
 
 
@@ -137,7 +137,7 @@ def _tiny_end_state_matches(eng, rep, g, infos):
     alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
     np.testing.assert_array_equal(eng.last_indices(), g["ind"][n_steps - 1])
     ref = g["info"]
-    np.testing.assert_allclose(infos[:, :ref.shape[1]], ref, rtol=2e-3, atol=1e-4, equal_nan=True)
+    np.testing.assert_allclose(infos[:, :ref.shape[1]], ref, rtol=LOSS_RTOL, atol=1e-4, equal_nan=True)
     if use_lap:
         np.testing.assert_allclose(rep.get_priority(Ncap), g[f"prio_{n_steps - 1}"], rtol=1e-4, atol=1e-5)
     for key in g:
