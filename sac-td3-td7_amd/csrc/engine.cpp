@@ -477,15 +477,17 @@ struct Access {
   uintptr_t lo, hi;
   int w;  // 1: the op stores (or atomically updates) these bytes
   const char* what;
+  int t = -1;  // (GEMM ranges) the op's workgroup that touches them; -1: the op as a whole
 };
 static thread_local std::vector<Access>* g_sink = nullptr;
+static thread_local int g_tile = -1;  // (audit_gemm: the workgroup whose ranges g_sink receives)
 
 static void audit_range(const void* base, long long lo, long long bytes, const char* what, const GemmArgs& g,
                         int w = 0) {
   if (bytes <= 0) return;
   const uintptr_t a = (uintptr_t)base + (uintptr_t)lo, b = a + (uintptr_t)bytes;
   if (g_sink) {
-    g_sink->push_back({a, b, w, what});
+    g_sink->push_back({a, b, w, what, g_tile});
     return;
   }
   std::lock_guard<std::mutex> lk(live_mu());
@@ -538,6 +540,7 @@ static void audit_gemm(const GemmArgs& g0) {
   const int NB = g.tn / 16, T = g.tiles_m * g.tiles_n, ks = 1 << g.ks_log;
   const int nch = g.R / 16, per = (nch + ks - 1) / ks;
   for (int t = 0; t < T; ++t) {
+    g_tile = g0.hot.wide ? -1 : t;
     int it, jt;
     if (h.xb) xcd_tile(t, h.tiles, h.tiles_n, h.xb, h.tmb, h.nfull, h.inv_tmb, h.inv_xb, h.inv_blast, it, jt);
     else {
@@ -793,6 +796,7 @@ static void op_accesses(const Op& op, std::vector<Access>& v) {
       g_sink = &v;
       audit_gemm(op.gemm);
       g_sink = nullptr;
+      g_tile = -1;
       break;
     }
     case OP_NORMBWD: {
@@ -1011,6 +1015,10 @@ static void level_hazards(const std::vector<Op>& ops, const std::vector<int>& it
 // sets it against the PMC counters: traffic above these bytes is re-reads, e.g. one copy per XCD).
 struct LevelTraffic {
   double act_r = 0, act_w = 0, w_r = 0, adam = 0, other = 0;
+  // Per-XCD read model: every XCD's L2 fetches its own copy of what its workgroups read (round-robin dispatch:
+  // workgroup w of a launch runs on XCD w mod 8, the 8 descriptor-prefetch workgroups first), so a GEMM
+  // operand that tiles on several XCDs read is fetched once per XCD; reads of non-GEMM ops count once.
+  double xcd_r = 0, adam_w = 0;  // (adam_w: the Adam stores alone -- adam counts its reads and stores)
 };
 static double union_bytes(std::vector<std::pair<uintptr_t, uintptr_t>>& v) {
   std::sort(v.begin(), v.end());
@@ -1033,13 +1041,15 @@ static double union_bytes(std::vector<std::pair<uintptr_t, uintptr_t>>& v) {
 static LevelTraffic level_traffic(const std::vector<Op>& ops, const float* P, size_t nP) {
   LevelTraffic t;
   std::vector<std::pair<uintptr_t, uintptr_t>> ar, aw, wr, ad;
+  std::vector<std::pair<uintptr_t, uintptr_t>> xr[8], once;  // (per-XCD model: GEMM reads by XCD, other reads)
   const uintptr_t p0 = (uintptr_t)P, p1 = p0 + 3 * nP * 4;
   std::vector<Access> v;
   for (const Op& op : ops) {
     v.clear();
     if (op.kind == OP_SAMPLE_GATHER) {  // rows of the batch + one path down the LAP sum tree per query
       const SampleArgs& s = op.sample;
-      t.other += (double)s.B * (2.0 * s.Sp + s.Ap + 2) * 4 + (s.lap ? s.B * (64.0 * 8 + 64 * 4) + s.nblk * 8.0 : 0);
+      t.other += (double)s.B * (2.0 * s.Sp + s.Ap + 2) * 4 +
+                 (s.lap ? (s.pend_n ? s.B * (64.0 * 8 + 64 * 4) : s.B * 4096.0 * 4) + s.nblk * 8.0 : 0);
       t.act_w += (double)s.B * ((s.ss.n != nullptr) + (s.ss.t != nullptr)) * 2 * s.Sp * 4 +
                  (double)s.B * ((s.a.n != nullptr) + (s.a.t != nullptr)) * s.Ap * 4 + s.B * 20.0;
       continue;
@@ -1057,7 +1067,13 @@ static LevelTraffic level_traffic(const std::vector<Op>& ops, const float* P, si
       const std::string what = a.what ? a.what : "";
       if (what.rfind("tape", 0) == 0) continue;  // (declared whole; read only in tape mode, one row)
       const bool in_p = a.lo >= p0 && a.hi <= p1;
+      // (reads: every range not stored, and Adam's T-image / bias ranges, which hold p, m, v read and then written)
+      if (!a.w || what == "adam w.t" || what == "adam bias") {
+        if (op.kind == OP_GEMM && a.t >= 0) xr[(op.wg_begin + a.t) & 7].push_back({a.lo, a.hi});
+        else once.push_back({a.lo, a.hi});
+      }
       if (what.rfind("adam", 0) == 0) {
+        if (a.w) t.adam_w += (double)(a.hi - a.lo);
         ad.push_back({a.lo, a.hi});
         if (what == "adam w.t" || what == "adam bias") ad.push_back({a.lo, a.hi});  // (read and written)
       } else if (a.w) {
@@ -1076,6 +1092,9 @@ static LevelTraffic level_traffic(const std::vector<Op>& ops, const float* P, si
   double adam = 0;
   for (auto& r : ad) adam += (double)(r.second - r.first);
   t.adam = adam;
+  double xb = union_bytes(once);
+  for (auto& r : xr) xb += union_bytes(r);
+  t.xcd_r = xb;
   return t;
 }
 
@@ -4039,9 +4058,10 @@ struct Engine {
       G.desc += "L" + std::to_string(l) + " wg=" + std::to_string(G.nwg[l]) + ":";
       if (traffic) {
         const LevelTraffic t = level_traffic(levels[l], P, nP);
-        char buf[160];
-        snprintf(buf, sizeof buf, " [KB act_r %.0f act_w %.0f w_r %.0f adam %.0f other %.0f]", t.act_r / 1024,
-                 t.act_w / 1024, t.w_r / 1024, t.adam / 1024, t.other / 1024);
+        char buf[220];
+        snprintf(buf, sizeof buf, " [KB act_r %.0f act_w %.0f w_r %.0f adam %.0f other %.0f xcd_r %.0f adam_w %.0f]",
+                 t.act_r / 1024, t.act_w / 1024, t.w_r / 1024, t.adam / 1024, t.other / 1024, t.xcd_r / 1024,
+                 t.adam_w / 1024);
         G.desc += buf;
       }
       for (size_t k = 0; k < levels[l].size(); ++k) {
@@ -4564,7 +4584,8 @@ int rle_replay_create(int device, long long capacity, int state_dim, int action_
       r.action = r.mem.make<float>((size_t)capacity * r.Ap);
       r.reward = r.mem.make<float>(capacity);
       r.notdone = r.mem.make<float>(capacity);
-      r.priority = r.mem.make<float>(capacity);
+      r.priority = r.mem.make<float>((size_t)(capacity + 4095) / 4096 * 4096);  // (whole blocks: the sampler's
+                                                                                  // two-tier search loads them)
       r.size_d = r.mem.make<long long>(1);
       r.maxp_d = r.mem.make<float>(1);
       const float one = 1.f;  // lap.py:29 max_priority = 1

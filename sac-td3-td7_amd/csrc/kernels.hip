@@ -2669,18 +2669,56 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t,
       FINE_MARK(2);
       // level 2: the block's 64 sub-blocks, one per lane
       const int nsub = (int)min((long long)(kBlk / kSub), (size - (long long)blk * kBlk + kSub - 1) / kSub);
-      double sv = lane < nsub ? G(s.ssum)[(size_t)blk * (kBlk / kSub) + lane] : 0.0;
+      double sv;
+      float* subp = smem + wave * kSub;  // (two-tier search: the chosen sub-block's priorities, one per lane)
+      if (!pend) {
+        // Two tiers after the block sums (round 6): the chosen block's 4096 priorities in ONE round trip, lane l
+        // holding sub-block l as 16 float4 (the replay pads the array to whole blocks; elements past the replay
+        // size count 0), its fp64 sum formed in op_sample_reduce's order -- 4 runs of 16 summed in sequence,
+        // then (r0 + r1) + (r2 + r3) -- so sv is the kept sub-block sum bit for bit (and exact, Q8), instead of
+        // loading the sub-block sums and then, a round trip later, the sub-block's priorities.
+        const long long e0 = (long long)blk * kBlk + (long long)lane * kSub;
+        const GAS f32x4* pp = (const GAS f32x4*)(G(s.priority) + e0);
+        f32x4 pr[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) pr[q] = pp[q];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) pr[q][c] = e0 + 4 * q + c < size ? pr[q][c] : 0.f;
+        double r4[4];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          double acc = 0.0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc += (double)pr[4 * g4 + q][c];
+          r4[g4] = acc;
+        }
+        sv = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+        inc = wave_scan_incl_d(sv);
+        const int l2 = first_lane(lane < nsub && ((float)(base + inc) >= v || lane == nsub - 1));
+        const int sub2 = max(l2, 0);
+        if (lane == sub2) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) *(f32x4*)(subp + 4 * q) = pr[q];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (one wave: its LDS write, then its reads)
+      } else {
+        sv = lane < nsub ? G(s.ssum)[(size_t)blk * (kBlk / kSub) + lane] : 0.0;
+      }
       const int pj0 = pend ? pt.bhead[blk] : -1;
       for (int j = pj0; j >= 0; j = pt.wnext[j])  // (the update's rows in this block: ~B / blocks of them)
         if (((pt.wkey[j] & (kBlk - 1)) >> 6) == lane) sv += pt.wdel[j];
-      inc = wave_scan_incl_d(sv);
+      if (pend) inc = wave_scan_incl_d(sv);
       const int l2 = first_lane(lane < nsub && ((float)(base + inc) >= v || lane == nsub - 1));
       const int sub = max(l2, 0);
       base += readlane_d(inc - sv, sub);
       FINE_MARK(3);
-      // level 3: the sub-block's 64 priorities, one per lane
+      // level 3: the sub-block's 64 priorities, one per lane (two-tier: from LDS)
       const long long e = (long long)blk * kBlk + (long long)sub * kSub + lane;
-      float pv = e < size ? G(s.priority)[e] : 0.f;
+      float pv = !pend ? subp[lane] : e < size ? G(s.priority)[e] : 0.f;
       for (int j = pj0; j >= 0; j = pt.wnext[j])
         if (pt.wkey[j] == (int)e) pv = pt.wnew[j];
       inc = wave_scan_incl_d((double)pv);

@@ -1,5 +1,6 @@
 """Print the level structure of the step graphs (GPU box): python tools/describe.py [td7|td3|sac] [S A]
-(RLE_DESC_CRIT=1 stars the ops on a longest dependency chain)."""
+(RLE_DESC_CRIT=1 stars the ops on a longest dependency chain; RLE_DESC_ONLY=3 prints the multi-step graph
+alone, as tools/pmc_levels.py takes it; RLE_TRAFFIC=1 adds each level's traffic model)."""
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd")]
@@ -19,6 +20,8 @@ for net, params in init_agent(algo, S, A, H, 1).items():
 rep = E.Replay(1000000, S, A, algo == "td7")
 rep.fill_random(1000000, 1)
 eng.bind(rep)
-for w in (0, 1, 3):
-    print(f"=== graph {w}")
+only = os.environ.get("RLE_DESC_ONLY")
+for w in ((int(only),) if only else (0, 1, 3)):
+    if not only:
+        print(f"=== graph {w}")
     print(eng.describe(w))

@@ -67,9 +67,10 @@ import re
 
 MODEL = {}  # level -> {kind: KB} from RLE_TRAFFIC=1 descriptions
 for k, d in DESC.items():
-    m = re.search(r"\[KB act_r (\d+) act_w (\d+) w_r (\d+) adam (\d+) other (\d+)\]", d)
+    m = re.search(r"\[KB act_r (\d+) act_w (\d+) w_r (\d+) adam (\d+) other (\d+)(?: xcd_r (\d+) adam_w (\d+))?\]", d)
     if m:
-        MODEL[k] = dict(zip(("act_r", "act_w", "w_r", "adam", "other"), map(float, m.groups())))
+        MODEL[k] = dict(zip(("act_r", "act_w", "w_r", "adam", "other", "xcd_r", "adam_w"),
+                            (float(x) if x is not None else None for x in m.groups())))
 cols = [c for c in ("FETCH_SIZE", "WRITE_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY",
                     "SQ_WAVE_CYCLES", "TCC_HIT_sum", "TCC_MISS_sum") if any(c in r for r in merged.values())]
 print("per level of the multi-step graph (means over its replays); traffic KB = 2 x FETCH_SIZE + WRITE_SIZE "
@@ -97,12 +98,32 @@ if MODEL:
             continue
         r = merged[q]
         tr = 2 * r.get("FETCH_SIZE", 0) + r.get("WRITE_SIZE", 0)
-        tot_m = sum(m.values())
+        tot_m = sum(m[kk] for kk in ("act_r", "act_w", "w_r", "adam", "other"))
         for kk, vv in m.items():
-            mt[kk] += vv
+            mt[kk] += vv or 0.0
         mt["pmc"] += tr
         print(f"{q:3d} " + " ".join(f"{m[kk]:7.0f}" for kk in ("act_r", "act_w", "w_r", "adam", "other")) +
               f" {tot_m:8.0f} {tr:8.0f} {tr / max(tot_m, 1):5.2f}")
     tm = sum(mt[kk] for kk in ("act_r", "act_w", "w_r", "adam", "other"))
     print("sum " + " ".join(f"{mt[kk]:7.0f}" for kk in ("act_r", "act_w", "w_r", "adam", "other")) +
           f" {tm:8.0f} {mt['pmc']:8.0f} {mt['pmc'] / max(tm, 1):5.2f}")
+    if all(m.get("xcd_r") is not None for m in MODEL.values()):
+        # per-XCD model: every XCD's L2 fetches its own copy of what its workgroups read (engine.cpp LevelTraffic)
+        # + the unique bytes stored (activations, Adam's stores) + the sampler / priority / reductions' bytes
+        print("\nper-XCD read model against the counters, KB: reads (2 x FETCH_SIZE) and stores (WRITE_SIZE) apart")
+        print(f"{'lvl':>3} {'xcd_r':>8} {'2xFETCH':>8} {'x':>5} {'stores':>8} {'WRITE':>8} {'x':>5} {'model':>8} {'pmc':>8} {'cover':>6}")
+        xt = defaultdict(float)
+        for q in sorted(merged):
+            m = MODEL.get(q)
+            if not m:
+                continue
+            r = merged[q]
+            rd, wr = 2 * r.get("FETCH_SIZE", 0), r.get("WRITE_SIZE", 0)
+            mr, mw = m["xcd_r"] + m["other"], m["act_w"] + m["adam_w"]
+            for kk, vv in (("mr", mr), ("mw", mw), ("rd", rd), ("wr", wr)):
+                xt[kk] += vv
+            print(f"{q:3d} {mr:8.0f} {rd:8.0f} {rd / max(mr, 1):5.2f} {mw:8.0f} {wr:8.0f} {wr / max(mw, 1):5.2f} "
+                  f"{mr + mw:8.0f} {rd + wr:8.0f} {(mr + mw) / max(rd + wr, 1):6.2f}")
+        print(f"sum {xt['mr']:8.0f} {xt['rd']:8.0f} {xt['rd'] / max(xt['mr'], 1):5.2f} {xt['mw']:8.0f} {xt['wr']:8.0f} "
+              f"{xt['wr'] / max(xt['mw'], 1):5.2f} {xt['mr'] + xt['mw']:8.0f} {xt['rd'] + xt['wr']:8.0f} "
+              f"{(xt['mr'] + xt['mw']) / max(xt['rd'] + xt['wr'], 1):6.2f}")
