@@ -345,7 +345,8 @@ static void gemm_finalize(GemmArgs& g, bool xcd = true) {
     REQUIRE(g.has_pre != 2 || (g.mode == GEMM_DX && g.epi == EPI_STORE && (act == ACT_ELU || act == ACT_RELU) &&
                                !norm && g.A.nseg == 1 && modes && parts && h.dact == act && (!h.sac || h.logpi) &&
                                (!h.lap || h.prio) && h.H <= 256 && h.H % 4 == 0 && g.R == r16(h.H) &&
-                               g.M % 16 == 0 && h.rows == g.M && (g.head_n == 0 || g.head_n == 1)),
+                               g.M % 16 == 0 && h.rows == h.nvalid && h.rows <= g.M && g.M - h.rows < 16 &&
+                               (g.head_n == 0 || g.head_n == 1)),
             "gemm: fused loss head layout");
   }
   REQUIRE(g.epi != EPI_SACFWD || (g.mode == GEMM_FWD && act == ACT_NONE && !norm && g.has_pre == 0 && g.tn == 64 &&
@@ -1724,6 +1725,8 @@ struct Engine {
     plan.xcd = plan.xcd < 0 ? 1 : (plan.xcd ? 1 : 0);
   }
   int S, Sp, A, Ap, H, Hp, B;
+  int Bv = 0;  // batch rows (rle_config.batch, any 1..1024); B = Bv padded to 16: the padded rows are zero and
+               // every mean, loss, priority and value bound counts the Bv batch rows only
   int Z = 0, Zp = 0;    // TD7: SALE embedding width zs_dim (sale.py:23), padded
   std::vector<int> HS;  // TD3 / SAC: hidden widths of make_mlp (mlp.py:10-35), input side first
   int algo;
@@ -2883,13 +2886,13 @@ struct Engine {
     op.kind = OP_SAMPLE_GATHER;
     fill_sample_args(op.sample, sac);
     op.sample.ahead = ahead;
-    op.wg_count = cdiv(B, 4);  // one wave per query
+    op.wg_count = cdiv(Bv, 4);  // one wave per query
     // reads the RNG step / tape position counters -> ordered before STEP_END (WAR)
     std::vector<int> rd{bsum_id, R_PRIO, R_REPLAY, R_CNT};
     if (pu) {
       op.sample.pend_ind = pu->ind;
       op.sample.pend_p = pu->p;
-      op.sample.pend_n = B;
+      op.sample.pend_n = Bv;
       rd.push_back(pu->ind_id);
       rd.push_back(pu->p_id);
     }
@@ -2898,7 +2901,7 @@ struct Engine {
     nz.kind = OP_NOISE;
     fill_sample_args(nz.sample, sac);
     nz.sample.ahead = ahead;
-    nz.wg_count = cdiv(B * A, kThreads);
+    nz.wg_count = cdiv(Bv * A, kThreads);
     pg.add(nz, {R_CNT}, {eps.id, sac ? eps2.id : -1});
   }
   int bsum_id = -1, ind_id = -1;
@@ -2919,6 +2922,7 @@ struct Engine {
     s.cap = rp.cap;
     s.lap = rp.lap;
     s.B = B;
+    s.nq = Bv;
     s.bsum = rp.bsum;
     s.ssum = rp.ssum;
     s.nblk = rp.nblk;
@@ -2948,7 +2952,8 @@ struct Engine {
     h.rows = rows;
     h.H = H;
     h.gamma = cfg.discount;
-    h.inv_b = 1.f / (float)B;
+    h.inv_b = 1.f / (float)Bv;
+    h.nvalid = Bv;
     h.tgt_mode = -1;
     op.wg_count = cdiv(rows, 4);
     return op;
@@ -2985,7 +2990,7 @@ struct Engine {
     a.info_slot = &ctrl->info_slot;
     a.info = info;
     a.info_cap = info_cap;
-    a.inv_b = 1.f / (float)B;
+    a.inv_b = 1.f / (float)Bv;
     op.wg_count = 1;
     return op;
   }
@@ -3062,7 +3067,7 @@ struct Engine {
     op.prio.priority = replay->priority;
     op.prio.ind = ind;
     op.prio.p = prio.p;
-    op.prio.B = B;
+    op.prio.B = Bv;
     op.prio.max_priority = replay->maxp_d;
     op.prio.bsum = replay->lap ? replay->bsum : nullptr;
     op.prio.ssum = replay->ssum;
@@ -3146,7 +3151,8 @@ struct Engine {
       enc_tiles = g.tiles_m * g.tiles_n;
       enc_loss = mem.make<float>(enc_tiles);
       g.loss_part = enc_loss;
-      g.mse_scale = 1.f / (float)((long long)B * Z);  // (mean over the B x zs_dim zsa, td7.py:253)
+      g.mse_scale = 1.f / (float)((long long)Bv * Z);  // (mean over the B x zs_dim zsa, td7.py:253)
+      g.mvalid = Bv;
       op.wg_count = (wide ? g.tiles_m / 4 : g.tiles_m) * g.tiles_n;
       pg.add(op, {ea2.id, L.res, ezs2.id, ezs2.norm_id}, {ed3.id, loss_id_enc = next_id++});
     }
@@ -3241,7 +3247,7 @@ struct Engine {
     View d1f[2];  // (hdx) dZ of each critic's first hidden layer from the fused head + DX
     {
       // target head (td7.py:211-218) fused: y per row from the target twins, then the loss
-      Op op = head_op(HEAD_TD7_LOSS, B);
+      Op op = head_op(HEAD_TD7_LOSS, Bv);
       HeadArgs& h = op.head;
       set_head_twin(h, c2[0], c2[1], q[0]->layers[3], q[1]->layers[3]);
       set_head_target(h, HEAD_TD7_TARGET, th[0], th[1], tq[0]->layers[3], tq[1]->layers[3]);
@@ -3333,7 +3339,7 @@ struct Engine {
       ploss_n = 0;
       for (int n = 0; n < 2; ++n) {
         int nt = 0;
-        dzp2[n] = fwd_qhead(pg, q[n]->layers[2], q[n]->layers[3], p1[n], B, -0.5f / (float)B, ploss_part + ploss_n,
+        dzp2[n] = fwd_qhead(pg, q[n]->layers[2], q[n]->layers[3], p1[n], B, -0.5f / (float)Bv, ploss_part + ploss_n,
                             &nt, n ? ploss_id2 : ploss_id);
         ploss_n += nt;
       }
@@ -3389,9 +3395,9 @@ struct Engine {
     // ---- step end: info row [encoder, q_fn, policy]
     Op op = step_end_op();
     StepEndArgs& a = op.end;
-    info_sum(a, 0, enc_loss, enc_tiles, 1, 1.f / (float)((long long)B * Z));
-    info_sum(a, 1, qloss_part, hw * 4, 1, (lap ? 1.f : 0.5f) / (float)B);
-    if (policy) info_sum(a, 2, ploss_part, ploss_n, 1, -0.5f / (float)B);
+    info_sum(a, 0, enc_loss, enc_tiles, 1, 1.f / (float)((long long)Bv * Z));
+    info_sum(a, 1, qloss_part, hw * 4, 1, (lap ? 1.f : 0.5f) / (float)Bv);
+    if (policy) info_sum(a, 2, ploss_part, ploss_n, 1, -0.5f / (float)Bv);
     else a.kind[2] = INFO_NAN;
     a.ninfo = 3;
     std::vector<int> rd{loss_id_enc, qloss_id};
@@ -3447,6 +3453,7 @@ struct Engine {
     g.qw_cbn = Lq.cb;
     g.qb = bias(Lq);
     g.qscale = dq;
+    g.mvalid = Bv;
     op.wg_count = (wide ? g.tiles_m / 4 : g.tiles_m) * g.tiles_n;
     pg.add(op, {x.id, L.res, Lq.res}, {dz.id, loss_id});
     return dz;
@@ -3728,7 +3735,7 @@ struct Engine {
     qloss_part = mem.make<float>((size_t)hw * 4);
     {
       // target head (td3.py:160-164, sac.py:188-193) fused: y per row, then the loss
-      Op op = head_op(HEAD_MLP_LOSS, B);
+      Op op = head_op(HEAD_MLP_LOSS, Bv);
       HeadArgs& h = op.head;
       set_head_twin(h, c1[0], c1[1], *qo[0], *qo[1]);
       set_head_target(h, HEAD_MLP_TARGET, th1[0], th1[1], *tqo[0], *tqo[1]);
@@ -3794,7 +3801,7 @@ struct Engine {
       ploss_part = mem.make<float>((size_t)hw * 4);
       View dzp0[2];
       if (hdx) {  // the objective's head inside the DX of each critic's last hidden layer
-        Op op = head_op(HEAD_MLP_POLICY, B);
+        Op op = head_op(HEAD_MLP_POLICY, Bv);
         HeadArgs& h = op.head;
         set_head_twin(h, p1[0], p1[1], *qo[0], *qo[1]);
         h.dact = ACT_RELU;
@@ -3819,7 +3826,7 @@ struct Engine {
         }
         out_t = true;
       } else {
-        Op op = head_op(HEAD_MLP_POLICY, B);
+        Op op = head_op(HEAD_MLP_POLICY, Bv);
         HeadArgs& h = op.head;
         set_head_twin(h, p1[0], p1[1], *qo[0], *qo[1]);
         h.dsrc[0] = p1[0].m;
@@ -3863,7 +3870,8 @@ struct Engine {
           a.dout = dout.m;
           a.log_alpha = alpha_src();
           a.alpha_lin = cfg.tmp >= 0.f;
-          a.inv_b = 1.f / (float)B;
+          a.inv_b = 1.f / (float)Bv;
+          a.nvalid = Bv;
           a.min_log_std = cfg.min_log_std;
           a.max_log_std = cfg.max_log_std;
           a.mean_off = 0;
@@ -3882,7 +3890,7 @@ struct Engine {
         SacActorArgs& a = op.sac;
         a.out = raw.m;
         a.A = A;
-        a.rows = B;
+        a.rows = Bv;  // (rows of the padded batch past it keep a zero gradient)
         a.eps2 = eps2.m;
         a.min_log_std = cfg.min_log_std;
         a.max_log_std = cfg.max_log_std;
@@ -3892,8 +3900,8 @@ struct Engine {
         a.dout = dout.m;
         a.log_alpha = alpha_src();
         a.alpha_lin = cfg.tmp >= 0.f;
-        a.inv_b = 1.f / (float)B;
-        op.wg_count = cdiv(B, kThreads);
+        a.inv_b = 1.f / (float)Bv;
+        op.wg_count = cdiv(Bv, kThreads);
         pg.add(op, {raw.id, eps2.id, da.id, R_LA}, {dout.id});
       }
       if (!sac) {
@@ -3964,9 +3972,9 @@ struct Engine {
     std::vector<int> rd{qloss_id};
     if (policy) rd.push_back(ploss_id);
     if (!sac) {  // [train/q_fn, train/policy, norm/policy]
-      info_sum(a, 0, qloss_part, hw * 4, 1, (lap ? 1.f : 0.5f) / (float)B);
+      info_sum(a, 0, qloss_part, hw * 4, 1, (lap ? 1.f : 0.5f) / (float)Bv);
       if (policy) {
-        info_sum(a, 1, ploss_part, hw, 4, -1.f / (float)B);
+        info_sum(a, 1, ploss_part, hw, 4, -1.f / (float)Bv);
         a.kind[2] = INFO_GNORM;
         a.gsq = gsq;
         a.ngsq_t = (int)gsq_offs.size() - 1;
@@ -3978,10 +3986,10 @@ struct Engine {
       }
       a.ninfo = 3;
     } else if (cfg.tmp < 0.f) {  // [train/q_fn, tmp, norm/tmp, train/policy, train/tmp, entropy]
-      info_sum(a, 0, qloss_part, hw * 4, 1, 0.5f / (float)B);
+      info_sum(a, 0, qloss_part, hw * 4, 1, 0.5f / (float)Bv);
       a.kind[1] = INFO_SAC_TMP;
       a.kind[2] = INFO_SAC_NTMP;
-      info_sum(a, 3, ploss_part, hw, 4, 1.f / (float)B);
+      info_sum(a, 3, ploss_part, hw, 4, 1.f / (float)Bv);
       a.kind[3] = INFO_SAC_POL;
       a.kind[4] = INFO_SAC_TMPL;
       a.kind[5] = INFO_SAC_ENT;
@@ -3998,8 +4006,8 @@ struct Engine {
       a.logpi_part = ploss_part;
       a.nlogpi = hw;
     } else {  // fixed temperature: [train/q_fn, train/policy, entropy]
-      info_sum(a, 0, qloss_part, hw * 4, 1, 0.5f / (float)B);
-      info_sum(a, 1, ploss_part, hw, 4, 1.f / (float)B);
+      info_sum(a, 0, qloss_part, hw * 4, 1, 0.5f / (float)Bv);
+      info_sum(a, 1, ploss_part, hw, 4, 1.f / (float)Bv);
       a.kind[2] = INFO_SAC_ENT;
       a.ninfo = 3;
       a.logpi_part = ploss_part;
@@ -4772,6 +4780,7 @@ int rle_replay_sample_indices(rle_replay* h, int n, const float* u, long long* i
     s.cap = r.cap;
     s.lap = r.lap;
     s.B = n;
+    s.nq = n;
     s.bsum = r.bsum;
     s.ssum = r.ssum;
     s.nblk = r.nblk;
@@ -4897,8 +4906,7 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
   return guard([&] {
     REQUIRE(cfg && out, "create: null");
     REQUIRE(cfg->algo >= 0 && cfg->algo <= 2, "create: bad algo");
-    REQUIRE(cfg->batch > 0 && cfg->batch % 16 == 0 && cfg->batch <= 1024,
-            "create: batch must be a multiple of 16, <= 1024");
+    REQUIRE(cfg->batch > 0 && cfg->batch <= 1024, "create: batch must be in 1..1024");
     REQUIRE(cfg->state_dim <= 1024 && cfg->action_dim <= 128 && cfg->hidden <= 512,
             "create: state_dim <= 1024, action_dim <= 128, hidden <= 512");
     REQUIRE(cfg->state_dim > 0 && cfg->action_dim > 0 && cfg->hidden > 0 && cfg->hidden % 4 == 0,
@@ -4928,7 +4936,8 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
     e.Hp = rle::r16(e.H);
     e.Z = cfg->zs_dim ? cfg->zs_dim : cfg->hidden;
     e.Zp = rle::r16(e.Z);
-    e.B = cfg->batch;
+    e.Bv = cfg->batch;
+    e.B = (cfg->batch + 15) / 16 * 16;  // (padded rows: zero, masked out of every mean, loss and priority)
     e.resolve_plan();
     HIPCHK(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
     if (e.algo == RLE_TD7) {
@@ -5163,7 +5172,7 @@ int rle_set_tapes(rle_engine* h, int n, const float* u, const float* eps, const 
     if (n > 0) {
       REQUIRE(n <= 1024, "set_tapes: at most 1024 steps per tape");
       e.ensure_tapes(n);
-      const size_t nb = (size_t)n * e.B, na = nb * e.A;
+      const size_t nb = (size_t)n * e.Bv, na = nb * e.A;  // (host tapes: [n][batch rows])
       if (u) HIPCHK(hipMemcpy(e.t_u, u, nb * 4, hipMemcpyHostToDevice));
       if (eps) HIPCHK(hipMemcpy(e.t_eps, eps, na * 4, hipMemcpyHostToDevice));
       if (eps_pi) HIPCHK(hipMemcpy(e.t_eps2, eps_pi, na * 4, hipMemcpyHostToDevice));
@@ -5192,7 +5201,7 @@ int rle_last_indices(rle_engine* h, long long* out) {
   return guard([&] {
     Engine& e = drained(h);
     HIPCHK(hipStreamSynchronize(e.stream));
-    HIPCHK(hipMemcpy(out, e.bsets[e.last_set].ind, e.B * sizeof(long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, e.bsets[e.last_set].ind, e.Bv * sizeof(long long), hipMemcpyDeviceToHost));
   });
 }
 

@@ -1052,6 +1052,7 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
   __syncthreads();
   if (wave == 0 && lane < 16) {  // one row per lane (op_head_t, target fused)
     const int b = i0 + lane;
+    const bool ok = b < h.nvalid;  // (rows of the padded batch past it: no loss, no gradient, no priority)
     const float q[2] = {qv[lane], qv[16 + lane]};
     float dq[2], ac[2] = {0.f, 0.f}, dmax = 0.f;
     if (pol) {  // HEAD_MLP_POLICY: td3.py:191, sac.py:227-229
@@ -1086,9 +1087,10 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
           dq[n] = -e * h.inv_b;
         }
       }
-      if (own_wg && hn == 0 && h.lap) GW(h.prio)[b] = lap_priority(dmax);
+      if (own_wg && hn == 0 && h.lap && ok) GW(h.prio)[b] = lap_priority(dmax);
       kq[lane] = fkey(yv);
     }
+    if (!ok) dq[0] = dq[1] = ac[0] = ac[1] = 0.f;
     const float dqn = hn ? dq[1] : dq[0];
     if (own_wg && h.dq[hn].t) GW(h.dq[hn].t)[tidx(h.dq[hn].rbs, b, 0)] = dqn;
     dqs[lane] = dqn;
@@ -1107,7 +1109,8 @@ __device__ __forceinline__ f32x4 headdx_reduce(const CAS GemmArgs& g, int i0, in
     }
     if (lane == 0 && td7) {  // value_max / value_min (td7.py:217-218)
       int kmax = kq[0], kmin = kq[0];
-      for (int r = 1; r < 16; ++r) {
+      const int nr = min(16, h.nvalid - i0);  // (>= 1: the batch pads fewer than 16 rows)
+      for (int r = 1; r < nr; ++r) {
         kmax = max(kmax, kq[r]);
         kmin = min(kmin, kq[r]);
       }
@@ -1373,8 +1376,9 @@ __device__ __forceinline__ void gemm_wide(const CAS GemmArgs& g, int t, float* s
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           const float z = acc[qq] + pb[c], y = act_f<ACT>(z);
-          lv += y * qwj[c];
-          dz[qq] = (g.qscale * qwj[c]) * act_b<ACT>(ACT == ACT_RELU ? y : z);
+          const bool rv = ib + qq < g.mvalid;  // (rows of the padded batch past it add nothing)
+          lv += rv ? y * qwj[c] : 0.f;
+          dz[qq] = rv ? (g.qscale * qwj[c]) * act_b<ACT>(ACT == ACT_RELU ? y : z) : 0.f;
         }
         mat_st4(g.out, ib, j, make_float4(dz[0], dz[1], dz[2], dz[3]));
       }
@@ -1393,7 +1397,7 @@ __device__ __forceinline__ void gemm_wide(const CAS GemmArgs& g, int t, float* s
           } else {
             iv = norm_inv(nr, ib + qq);
           }
-          const float d = (acc[qq] + pb[c]) - e4[qq] * iv;
+          const float d = ib + qq < g.mvalid ? (acc[qq] + pb[c]) - e4[qq] * iv : 0.f;  // (padded rows: 0)
           gr[qq] = (2.f * d) * g.mse_scale;
           lv += d * d;
         }
@@ -1431,7 +1435,7 @@ __device__ __forceinline__ void gemm_wide(const CAS GemmArgs& g, int t, float* s
     if (lane == 0) {
       const int t16 = (i0 >> 4) * tiles_n + jt;  // (the 16-row tile's row-major index: the partial count is unchanged)
       float v = NBW == 4 ? lsa + lsb : lsa;
-      if constexpr (EPI == EPI_QHEAD) v = t16 == 0 ? v + (float)g.M * sload(g.qb) : v;
+      if constexpr (EPI == EPI_QHEAD) v = t16 == 0 ? v + (float)g.mvalid * sload(g.qb) : v;
       GW(g.loss_part)[t16] = v;
     }
   }
@@ -2024,8 +2028,9 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         gsd += gu * ej;
         float gls = gsd * sd;
         if (!(lsr >= s.min_log_std && lsr <= s.max_log_std)) gls = 0.f;
-        gm[q] = gmu;
-        gl[q] = gls;
+        const bool rv = ib + q < s.nvalid;  // (rows of the padded batch past it: no gradient)
+        gm[q] = rv ? gmu : 0.f;
+        gl[q] = rv ? gls : 0.f;
       }
       mat_st4(s.dout, ib, s.mean_off + j, make_float4(gm[0], gm[1], gm[2], gm[3]));
       mat_st4(s.dout, ib, s.ls_off + j, make_float4(gl[0], gl[1], gl[2], gl[3]));
@@ -2037,15 +2042,16 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float z = acc[q] + pre_b, y = act_f<ACT>(z);
-        ls += y * qwj;
-        dz[q] = (g.qscale * qwj) * act_b<ACT>(ACT == ACT_RELU ? y : z);
+        const bool rv = ib + q < g.mvalid;  // (rows of the padded batch past it add nothing)
+        ls += rv ? y * qwj : 0.f;
+        dz[q] = rv ? (g.qscale * qwj) * act_b<ACT>(ACT == ACT_RELU ? y : z) : 0.f;
       }
       mat_st4(g.out, ib, j, make_float4(dz[0], dz[1], dz[2], dz[3]));
     }
     ls = wg_sum(ls, red);
     // (partials by tile, not by workgroup: the sum's order does not follow the XCD tile order)
     const int tix = it * tiles_n + jt;
-    if (tid == 0) GW(g.loss_part)[tix] = tix == 0 ? ls + (float)g.M * sload(g.qb) : ls;
+    if (tid == 0) GW(g.loss_part)[tix] = tix == 0 ? ls + (float)g.mvalid * sload(g.qb) : ls;
   } else if constexpr (EPI == EPI_NBDOT) {  // sale.py:11-13 backward, first half (the rest: kDwNb)
     auto epi_nbdot = [&](const f32x4 acc, const int i0, const int ib, const float4 nbxv, float* red) {
       float rd[4] = {0.f, 0.f, 0.f, 0.f};
@@ -2103,7 +2109,7 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         } else {
           inv = norm_inv(nr, ib + q);
         }
-        const float d = (acc[q] + pre_b) - tq[q] * inv;
+        const float d = ib + q < g.mvalid ? (acc[q] + pre_b) - tq[q] * inv : 0.f;  // (padded rows: 0)
         gr[q] = (2.f * d) * g.mse_scale;  // mse_scale = 1/n
         d2 += d * d;
       }
@@ -2471,15 +2477,15 @@ __device__ __forceinline__ double wg_scan_excl_d(double v, double* wtot, double&
 // SAC next-state rsample noise, and the SAC policy rsample noise in eps2.
 __device__ __forceinline__ void op_noise(const CAS SampleArgs& s, int t) {
   const int e = t * kThreads + threadIdx.x;
-  if (e >= s.B * s.A) return;
+  if (e >= s.nq * s.A) return;  // (rows of the padded batch past nq keep zero noise)
   const int b = e / s.A, j = e - b * s.A;
   const int tape = sload(s.tape_mode);
   const long long pos = sload(s.tape_pos) + s.ahead;
   const unsigned long long step = (unsigned long long)sload(s.ctrl_rng) + s.ahead;
   float v, v2 = 0.f;
   if (tape & kTapeEps) {
-    v = G(s.tape_eps)[(size_t)pos * s.B * s.A + e];
-    if (s.eps2.t) v2 = G(s.tape_eps2)[(size_t)pos * s.B * s.A + e];
+    v = G(s.tape_eps)[(size_t)pos * s.nq * s.A + e];
+    if (s.eps2.t) v2 = G(s.tape_eps2)[(size_t)pos * s.nq * s.A + e];
   } else {
     const uint2 key = make_uint2((unsigned)s.seed, (unsigned)(s.seed >> 32));
     const uint4 r = philox(key, make_uint4((unsigned)e, 1u, (unsigned)step, (unsigned)(step >> 32)));
@@ -2594,8 +2600,8 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t,
   const int tape = sload(s.tape_mode);
   // (uniform over the workgroup: every wave takes part in the fused update's LDS phases)
   const bool pend = EXT && s.pend_n > 0 && s.lap && !(tape & kTapeInd);
-  if (!pend && b >= s.B) return;
-  const bool live = b < s.B;  // (wave-uniform; a wave past the batch only helps with the update)
+  if (!pend && b >= s.nq) return;
+  const bool live = b < s.nq;  // (wave-uniform; a wave past the batch only helps with the update)
   const long long size = sload(s.size);
   const long long pos = sload(s.tape_pos) + s.ahead;
   const uint2 key = make_uint2((unsigned)s.seed, (unsigned)(s.seed >> 32));
@@ -2614,7 +2620,7 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t,
   }
   float u = 0.f;
   if (!tind && live) {
-    if (tape & kTapeU) u = sload(s.tape_u + (size_t)pos * s.B + b);
+    if (tape & kTapeU) u = sload(s.tape_u + (size_t)pos * s.nq + b);
     else u = u01(philox(key, make_uint4((unsigned)b, 0u, (unsigned)step, (unsigned)(step >> 32))).x);
   }
   PendTab pt{};
@@ -2629,7 +2635,7 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t,
   if (tind) {
     // (host-checked in range; the clamp only guards a prefetch past a tape's end, whose batch
     // the host discards)
-    ind = sload(s.tape_ind + (size_t)pos * s.B + b);
+    ind = sload(s.tape_ind + (size_t)pos * s.nq + b);
     ind = ind < 0 ? 0 : (ind > size - 1 ? size - 1 : ind);
   } else {
     if (lane == 0) GW(s.u_out)[b] = u;
@@ -2753,7 +2759,7 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t,
   // whole float4s, instead of every wave storing its row as four scattered floats per column quad.
   // A/B: TD7 Humanoid +0.4%, SAC Humanoid +0.4%, TD7 B = 1024 +0.8%; rows of <= 64 floats (TD3
   // HalfCheetah) -0.3%: they keep the per-wave stores.)
-  const bool quad = (s.B & 3) == 0 && s.Sp >= 128;  // (uniform)
+  const bool quad = (s.nq & 3) == 0 && s.Sp >= 128;  // (uniform; a partial last quad of queries: per-wave stores)
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const int c = 4 * lane + 256 * p;

@@ -285,6 +285,7 @@ struct HeadArgs {                   // 4 rows per workgroup (1 per wave)
   Mat h[2];                          // last hidden (post-activation) of each twin, N image
   Mat dsrc[2];                       // derivative source (Z for ELU, H for ReLU), N image
   int dact;
+  int nvalid;                        // batch rows: rows past it (the batch padded to 16) add nothing (fused heads)
   const float* w[2];                 // last-layer weight row: N image of a [1][H] matrix
   int w_cbn;                         // its column blocks
   const float* b[2];                 // last-layer bias [1]
@@ -326,6 +327,7 @@ struct SacBwdArgs {
   const float* log_alpha;            // log alpha, or alpha itself (alpha_lin)
   float inv_b, min_log_std, max_log_std;
   int alpha_lin, mean_off, ls_off;
+  int nvalid;                        // batch rows (rows past it: no gradient)
 };
 
 // EPI_SACFWD operands (sac.py:132-152 rsample of both row halves: policy rows < eps_row_split)
@@ -383,6 +385,7 @@ struct GemmArgs {
   };
   union {
     int head_n;    // has_pre 2: the critic whose DX this is
+    int mvalid;    // EPI_QHEAD / EPI_MSE: batch rows of M (rows past it, the batch padded to 16, add nothing)
     int nb_width;  // kDwNb with nbm finalized (nparts 1, width 1; engine.cpp norm_fin): x's width for the sign term
   };
   AdamArgs adam;
@@ -418,7 +421,8 @@ struct SampleArgs {
   int S, Sp, A, Ap;
   const long long* size;             // device replay size
   long long cap;                     // replay capacity (priority array length)
-  int lap, B;
+  int lap, B;                        // B: the padded batch (ss row offset of next_state)
+  int nq;                            // queries = batch rows (<= B; rows past it stay zero)
   double* bsum; int nblk;            // LAP block sums (fp64), 4096 priorities per block
   double* ssum;                      // LAP sub-block sums (fp64), 64 priorities each (64 per block)
   // outputs

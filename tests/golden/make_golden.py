@@ -381,6 +381,11 @@ def main():
                shape={"hidden_sizes": [48, 32, 32]})
     run_config("td7_tiny_zs", "td7", "Tiny-v0", 256, 16, 64, 50, 8, True, 16,
                extra={"target_update_rate": 4}, shape={"zs_dim": 128}, full=False)
+    # A batch that is not a multiple of 16 (the reference's --batch-size takes any int, cli_utils.py:83):
+    # B = 100, the engine pads it to 112 rows and counts 100
+    run_config("td7_tiny_b100", "td7", "Tiny-v0", 32, 100, 256, 200, 8, True, 17, extra={"target_update_rate": 4})
+    run_config("td3_tiny_b100", "td3", "Tiny-v0", 32, 100, 256, 200, 6, False, 18)
+    run_config("sac_tiny_b100", "sac", "Tiny-v0", 32, 100, 256, 200, 6, False, 19)
     # Full-size digests at the BASELINE configs' shapes.
     run_config("td7_humanoid", "td7", "Humanoid-v4", 256, 256, 2048, 2048, 3, True, 41,
                full=False)
