@@ -296,8 +296,8 @@ def gather_evidence(s_dim, a_dim, batch, n_replay, lap):
     1M-row TD7 Humanoid replay, one rle_level launch each; mean duration after warm-up).
 
     Bytes per query are what the kernel issues: the block sums its lanes load (64 lanes x
-    ceil(blocks / 64) x 8 B), the 4096 priorities of the chosen block (round 6: one round trip; the
-    sub-block sums are formed from them), the row (2 Sp + Ap floats + reward + notdone) and its stores into the
+    ceil(blocks / 64) x 8 B), the 64 sub-block sums (8 B) and 64 priorities (4 B) of the chosen
+    block / sub-block, the row (2 Sp + Ap floats + reward + notdone) and its stores into the
     batch's T images (+ reward, notdone, index, uniform).  The PMC traffic of the same dispatches
     (2 x FETCH_SIZE + WRITE_SIZE, profiles/rNN_sampler_pmc.json) is reported beside it."""
     path = _latest_profile("sampler.csv")
@@ -310,7 +310,7 @@ def gather_evidence(s_dim, a_dim, batch, n_replay, lap):
     sp = (s_dim + 15) // 16 * 16
     ap = (a_dim + 15) // 16 * 16
     nblk = math.ceil(n_replay / 4096)
-    search = (64 * math.ceil(nblk / 64) * 8 + 4096 * 4) if lap else 0  # (block sums, then the chosen block)
+    search = (64 * math.ceil(nblk / 64) * 8 + 64 * 8 + 64 * 4) if lap else 0
     row_rd = (2 * sp + ap) * 4 + 8
     row_wr = (2 * sp + ap) * 4 + 4 + 4 + 8 + 4
     q = search + row_rd + row_wr

@@ -1049,8 +1049,7 @@ static LevelTraffic level_traffic(const std::vector<Op>& ops, const float* P, si
     v.clear();
     if (op.kind == OP_SAMPLE_GATHER) {  // rows of the batch + one path down the LAP sum tree per query
       const SampleArgs& s = op.sample;
-      t.other += (double)s.B * (2.0 * s.Sp + s.Ap + 2) * 4 +
-                 (s.lap ? (s.pend_n ? s.B * (64.0 * 8 + 64 * 4) : s.B * 4096.0 * 4) + s.nblk * 8.0 : 0);
+      t.other += (double)s.nq * (2.0 * s.Sp + s.Ap + 2) * 4 + (s.lap ? s.nq * (64.0 * 8 + 64 * 4) + s.nblk * 8.0 : 0);
       t.act_w += (double)s.B * ((s.ss.n != nullptr) + (s.ss.t != nullptr)) * 2 * s.Sp * 4 +
                  (double)s.B * ((s.a.n != nullptr) + (s.a.t != nullptr)) * s.Ap * 4 + s.B * 20.0;
       continue;
@@ -4592,8 +4591,7 @@ int rle_replay_create(int device, long long capacity, int state_dim, int action_
       r.action = r.mem.make<float>((size_t)capacity * r.Ap);
       r.reward = r.mem.make<float>(capacity);
       r.notdone = r.mem.make<float>(capacity);
-      r.priority = r.mem.make<float>((size_t)(capacity + 4095) / 4096 * 4096);  // (whole blocks: the sampler's
-                                                                                  // two-tier search loads them)
+      r.priority = r.mem.make<float>(capacity);
       r.size_d = r.mem.make<long long>(1);
       r.maxp_d = r.mem.make<float>(1);
       const float one = 1.f;  // lap.py:29 max_priority = 1

@@ -2142,30 +2142,19 @@ __device__ __forceinline__ void gemm_v(const CAS GemmArgs& g, int t, float* smem
         for (int q = 0; q < 4; ++q) po[q] = __fadd_rn(__fmul_rn(ad.ptau, po[q]), __fmul_rn(po[q], omt));
       }
       GAS float* pw = bias_tile ? GW(ad.b) + ib : GW(ad.w.t) + wt;
-      {  // the weights' T image (+ bias) too: +0.3% over 3 A/B pairs
-        f32x4 w;
-        w.x = po[0]; w.y = po[1]; w.z = po[2]; w.w = po[3];
-#ifdef RLE_EXP_ADAM_WT
-        st4wt(pw, w);
-#else
-        __builtin_nontemporal_store(w, (GAS f32x4*)pw);
-#endif
-      }
-      // Adam moments: read again only by the next step's Adam of this tile, so streaming
-      // (nontemporal) stores -- measured +0.45% (3 A/B pairs, tools/ablib.sh); the T image above
-      // is read by the next step's input-gradient GEMMs, long after
+      // The weights' T image (+ bias) and the Adam moments: read again only a step later (the moments by this
+      // tile's next Adam, the T image by the next step's input-gradient GEMMs), so write-through stores (round 6;
+      // they were nontemporal stores, +0.45% / +0.3% over plain in round 3): the bytes leave the XCD's L2 during
+      // the kernel instead of waiting dirty for the launch's release.  A/B against the nontemporal stores: TD7
+      // Humanoid B = 256 8,341 / 8,338 steps/s (3 pairs), B = 1024 3,809 / 3,789 (2 pairs)
       {
         f32x4 w;
+        w.x = po[0]; w.y = po[1]; w.z = po[2]; w.w = po[3];
+        st4wt(pw, w);
         w.x = mo[0]; w.y = mo[1]; w.z = mo[2]; w.w = mo[3];
-#ifdef RLE_EXP_ADAM_WT
         st4wt(pw + ad.mo, w);
         w.x = vo[0]; w.y = vo[1]; w.z = vo[2]; w.w = vo[3];
         st4wt(pw + ad.vo, w);
-#else
-        __builtin_nontemporal_store(w, (GAS f32x4*)(pw + ad.mo));
-        w.x = vo[0]; w.y = vo[1]; w.z = vo[2]; w.w = vo[3];
-        __builtin_nontemporal_store(w, (GAS f32x4*)(pw + ad.vo));
-#endif
       }
       if (!bias_tile) {
         GAS float* qn = GW(ad.w.n) + nidx(ad.w.cbn, ib, j);
@@ -2675,56 +2664,20 @@ __device__ __forceinline__ void op_sample_gather(const CAS SampleArgs& s, int t,
       FINE_MARK(2);
       // level 2: the block's 64 sub-blocks, one per lane
       const int nsub = (int)min((long long)(kBlk / kSub), (size - (long long)blk * kBlk + kSub - 1) / kSub);
-      double sv;
-      float* subp = smem + wave * kSub;  // (two-tier search: the chosen sub-block's priorities, one per lane)
-      if (!pend) {
-        // Two tiers after the block sums (round 6): the chosen block's 4096 priorities in ONE round trip, lane l
-        // holding sub-block l as 16 float4 (the replay pads the array to whole blocks; elements past the replay
-        // size count 0), its fp64 sum formed in op_sample_reduce's order -- 4 runs of 16 summed in sequence,
-        // then (r0 + r1) + (r2 + r3) -- so sv is the kept sub-block sum bit for bit (and exact, Q8), instead of
-        // loading the sub-block sums and then, a round trip later, the sub-block's priorities.
-        const long long e0 = (long long)blk * kBlk + (long long)lane * kSub;
-        const GAS f32x4* pp = (const GAS f32x4*)(G(s.priority) + e0);
-        f32x4 pr[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) pr[q] = pp[q];
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) pr[q][c] = e0 + 4 * q + c < size ? pr[q][c] : 0.f;
-        double r4[4];
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          double acc = 0.0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc += (double)pr[4 * g4 + q][c];
-          r4[g4] = acc;
-        }
-        sv = (r4[0] + r4[1]) + (r4[2] + r4[3]);
-        inc = wave_scan_incl_d(sv);
-        const int l2 = first_lane(lane < nsub && ((float)(base + inc) >= v || lane == nsub - 1));
-        const int sub2 = max(l2, 0);
-        if (lane == sub2) {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) *(f32x4*)(subp + 4 * q) = pr[q];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (one wave: its LDS write, then its reads)
-      } else {
-        sv = lane < nsub ? G(s.ssum)[(size_t)blk * (kBlk / kSub) + lane] : 0.0;
-      }
+      double sv = lane < nsub ? G(s.ssum)[(size_t)blk * (kBlk / kSub) + lane] : 0.0;
       const int pj0 = pend ? pt.bhead[blk] : -1;
       for (int j = pj0; j >= 0; j = pt.wnext[j])  // (the update's rows in this block: ~B / blocks of them)
         if (((pt.wkey[j] & (kBlk - 1)) >> 6) == lane) sv += pt.wdel[j];
-      if (pend) inc = wave_scan_incl_d(sv);
+      inc = wave_scan_incl_d(sv);
       const int l2 = first_lane(lane < nsub && ((float)(base + inc) >= v || lane == nsub - 1));
       const int sub = max(l2, 0);
       base += readlane_d(inc - sv, sub);
       FINE_MARK(3);
-      // level 3: the sub-block's 64 priorities, one per lane (two-tier: from LDS)
+      // level 3: the sub-block's 64 priorities, one per lane
+      // (a two-tier search -- the chosen block's 4096 priorities in one round trip, the sub-block sums formed
+      // from them -- measured slower in round 6: standalone 9.6 against 7.1 us, TD7 Humanoid -1.7%)
       const long long e = (long long)blk * kBlk + (long long)sub * kSub + lane;
-      float pv = !pend ? subp[lane] : e < size ? G(s.priority)[e] : 0.f;
+      float pv = e < size ? G(s.priority)[e] : 0.f;
       for (int j = pj0; j >= 0; j = pt.wnext[j])
         if (pt.wkey[j] == (int)e) pv = pt.wnew[j];
       inc = wave_scan_incl_d((double)pv);
