@@ -25,6 +25,7 @@
 #include <fstream>
 #include <iterator>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #define CK(x)                                                                       \
@@ -220,6 +221,44 @@ int main(int argc, char** argv) {
       fflush(stdout);
     }
   }
-  printf("('!' = final buffers differ from A's)\ndone\n");
+  printf("('!' = final buffers differ from A's)\n");
+
+  // ---- F: row-block fused chains (P chains x L layers in ONE launch, 16 workgroups per chain, the activations in
+  // LDS) against the same work as L dependent `mega` levels of P ops (M = 256: 64 workgroups of 16 x 64 tiles each)
+  Kern kchain = kern("chain");
+  float *cx, *cw, *cout;
+  CK(hipMalloc(&cx, 12 * 65536 * 4));
+  CK(hipMalloc(&cw, 12 * 8 * 65536 * 4));
+  CK(hipMalloc(&cout, 12 * 65536 * 4));
+  CK(hipMemset(cx, 0, 12 * 65536 * 4));
+  CK(hipMemset(cw, 0, 12 * 8 * 65536 * 4));
+  char* cka;
+  CK(hipMalloc(&cka, 128));
+  printf("\nfused chains: us per chain pass (median of 5 bursts of 48) vs L x the level time of mode A (N = P, M = 256)\n");
+  printf("%3s %3s %9s %9s %9s\n", "P", "L", "F fused", "L x A", "F / LxA");
+  for (int P : {1, 2, 4, 6, 12}) {
+    setup(P, 256);
+    std::vector<double> ta;
+    for (int r = 0; r < 5; ++r) ta.push_back(burst('A', P, 256, L * 4) / (L * 4));
+    std::sort(ta.begin(), ta.end());
+    for (int Lc : {2, 3, 4, 8}) {
+      struct { const float *x, *w; float* o; const float* b; int L; } a{cx, cw, cout, bias, Lc};
+      CK(hipMemcpy(cka, &a, sizeof(a), hipMemcpyHostToDevice));
+      std::vector<double> tf;
+      for (int r = 0; r < 5; ++r) {
+        hsa_signal_store_relaxed(sig, 1);
+        const int nb = 48;
+        for (int i = 0; i < nb; ++i) dispatch(kchain, P * 16, cka, true, i == 0 ? SY : AG, i == nb - 1 ? SY : AG, i == nb - 1);
+        auto t0 = std::chrono::steady_clock::now();
+        hsa_signal_store_screlease(q->doorbell_signal, wi - 1);
+        while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 1000000000ull, HSA_WAIT_STATE_ACTIVE) >= 1) {}
+        tf.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / nb);
+      }
+      std::sort(tf.begin(), tf.end());
+      printf("%3d %3d %9.3f %9.3f %9.3f\n", P, Lc, tf[2], Lc * ta[2], tf[2] / (Lc * ta[2]));
+      fflush(stdout);
+    }
+  }
+  printf("done\n");
   return 0;
 }
