@@ -38,7 +38,7 @@ typedef struct rle_config {
   int algo;                 /* RLE_TD7 / RLE_TD3 / RLE_SAC */
   int state_dim, action_dim;
   int hidden;               /* hidden width (TD7: hdim; TD3/SAC: every hidden layer unless n_hidden is set) */
-  int batch;                /* B (multiple of 16, <= 1024) */
+  int batch;                /* B, 1..1024 (padded to 16 rows inside; the padded rows count in nothing) */
   int use_lap;              /* TD7/TD3: LAP Huber + priority update */
   float discount;           /* td7.py:37 / td3.py:36 / sac.py:30 */
   float policy_lr, critic_lr;

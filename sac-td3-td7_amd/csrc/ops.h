@@ -611,7 +611,7 @@ struct LevelArgs {
 };
 constexpr int kMaxLevelWG = 0xfffe;  // workgroups per launch (16-bit entry field)
 
-// One rle_level dispatch as an AQL packet needs it (engine.cpp direct dispatch, RLE_AQL): the
+// One rle_level dispatch as an AQL packet needs it (engine.cpp direct dispatch, rle_plan.dispatch 1): the
 // kernel-argument bytes (rle_level<false>'s 76-byte segment: no hidden arguments) and the
 // workgroup count.  launch_level appends one per dispatch while g_level_rec is set.
 struct LevelLaunch {
