@@ -53,9 +53,10 @@ def _close(a, b, tol):
         assert abs(a - b) <= tol * (1 + abs(b)), (a, b)
 
 
-@pytest.mark.parametrize("alg,lap", [("td7", True), ("td7", False), ("td3", False), ("td3", True)])
-def test_train_ops_on_sampled_batches_matches_oracle(alg, lap):
-    cap, B, H, steps = 512, 32, 32, 6
+@pytest.mark.parametrize("alg,lap,B", [("td7", True, 32), ("td7", False, 32), ("td3", False, 32), ("td3", True, 32),
+                                       ("td7", True, 20), ("td3", False, 20)])  # (B = 20: padded to 32 inside)
+def test_train_ops_on_sampled_batches_matches_oracle(alg, lap, B):
+    cap, H, steps = 512, 32, 6
     trans = _transitions(300, 1)
     Agent = TD7 if alg == "td7" else TD3
     ag = Agent("Tiny-v0", use_lap=lap, target_policy_noise=0.0, hidden=H, batch_size=B, seed=5)
