@@ -281,6 +281,28 @@ def pmc_evidence(cfg=("td7", "Humanoid-v4", 256)):
     return out
 
 
+def traffic_model_evidence():
+    """How much of the measured per-level HBM traffic the per-XCD traffic model explains (tools/pmc_levels.py on
+    the committed per-level PMC passes of the 6-step TD7 graph: every XCD's L2 fetches its own copy of what its
+    workgroups read; engine.cpp LevelTraffic).  {} when no such table is committed."""
+    path = _latest_profile("pmc_levels.txt")
+    if path is None:
+        return {}
+    last = None
+    with open(path) as f:
+        for line in f:
+            parts = line.split()
+            if parts and parts[0] == "sum" and len(parts) == 10:
+                last = parts
+    if last is None:
+        return {}
+    model, pmc = float(last[7]), float(last[8])
+    return {"traffic_model_xcd": {"model_KB_per_graph": model, "pmc_KB_per_graph": pmc,
+                                  "explained_frac": round(model / pmc, 4),
+                                  "reads_pmc_over_model": float(last[3]), "stores_pmc_over_model": float(last[6]),
+                                  "source": f"profiles/{os.path.basename(path)} (per level of the 6-step graph)"}}
+
+
 def _pmc_value(key, cfg=("td7", "Humanoid-v4", 256)):
     path = _latest_profile(PMC_FILES[cfg])
     if path is None:
@@ -365,6 +387,7 @@ def summarize(n_gpus, steps, warmup, wall, gpu_s, lv_policy, lv_plain, algo="td7
     }
     if headline:
         roofline.update(gather_evidence(s_dim, a_dim, batch, N_REPLAY, lap))
+        roofline.update(traffic_model_evidence())
     busy = _pmc_value("SQ_VALU_MFMA_BUSY_CYCLES", (algo, env, batch))
     if busy is not None:  # the same counter over this run's measured launch duration, 2.4 GHz
         roofline["mfma_busy_vs_launch_time"] = round(busy / (1024 * 2.4e9 * per_launch_s), 5)
