@@ -55,8 +55,18 @@ typedef struct rle_config {
   int n_hidden;             /* TD3/SAC: hidden layers of make_mlp (mlp.py:10-35), 2..RLE_MAX_HIDDEN; 0 = two
                                layers of `hidden` (mlp.py:45-47) */
   int hidden_sizes[8];      /* TD3/SAC: their widths, input side first (each a multiple of 4, <= 512) */
+  /* Hidden-layer activations (RLE_ACT_*; 0 = the reference default of that net).  TD7: SALEActor / SALECritic /
+     SALEEncoder `activ` (sale.py:25,67,97: ReLU / ELU / ELU); TD3/SAC: make_mlp's action_fn of the policy and of the
+     critics (mlp.py:13, default ReLU; act_encoder must be 0).  A non-default activation runs its programs without
+     the activation-specific fusions (RLE_FUSE_PRELAYER, PRE, QDOT, HEADDX, TWOSTAGE, SACPRE) on the extended kernel
+     instance. */
+  int act_actor, act_critic, act_encoder;
 } rle_config;
 #define RLE_MAX_HIDDEN 6
+#define RLE_ACT_DEFAULT 0
+#define RLE_ACT_RELU 1
+#define RLE_ACT_ELU 2       /* alpha = 1 (F.elu / nn.ELU defaults) */
+#define RLE_ACT_IDENTITY 3  /* make_mlp(action_fn=None): no activation between the Linear layers */
 
 /* Step-program plan: the schedule and tile-plan choices that decide how the step's reductions are
  * split (so its fp32 summation order) and how its ops are fused.  Every engine starts from the

@@ -68,10 +68,19 @@ def _tt(x):
     return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32))
 
 
+def _acts(acts, defaults):
+    """{"actor", "critic", "encoder"} -> activation functions (nets.ACTS names; missing: the reference
+    defaults, sale.py:25,67,97 / mlp.py:13)."""
+    acts = dict(acts or {})
+    return {k: N.ACTS[acts.get(k) or d] for k, d in defaults.items()}
+
+
 class TD7Oracle:
     def __init__(self, nets, discount=0.99, policy_lr=3e-4, critic_lr=3e-4,
                  target_update_rate=250, target_policy_noise=0.2, noise_clip=0.5,
-                 policy_freq=2, use_lap=True):
+                 policy_freq=2, use_lap=True, acts=None):
+        a = _acts(acts, {"actor": "relu", "critic": "elu", "encoder": "elu"})
+        self.ap, self.ac, self.ae = a["actor"], a["critic"], a["encoder"]
         self.enc = _params(nets["encoder"])
         self.pi = _params(nets["policy"])
         self.q1 = _params(nets["q1"])
@@ -96,28 +105,29 @@ class TD7Oracle:
         s, a, s2 = _tt(batch["state"]), _tt(batch["action"]), _tt(batch["next_state"])
         r, nd = _tt(batch["reward"]), _tt(batch["done"])
         # encoder (td7.py:246-257, 299-303)
+        zs_, zsa_, actor, critic = self._fns()
         with torch.no_grad():
-            zs_next = N.sale_zs(self.enc, s2)
-        zsa = N.sale_zsa(self.enc, N.sale_zs(self.enc, s), a)
+            zs_next = zs_(self.enc, s2)
+        zsa = zsa_(self.enc, zs_(self.enc, s), a)
         loss_e = (zsa - zs_next).pow(2.0).mean()
         self.opt_enc.step(_grads(loss_e, self.enc))
         info["train/encoder"] = float(loss_e.detach())
         # critics (td7.py:175-244)
         with torch.no_grad():
-            zs2 = N.sale_zs(self.fet, s2)
+            zs2 = zs_(self.fet, s2)
             noise = (_tt(eps) * self.noise).clamp(-self.clip, self.clip)
-            a2 = (N.sale_actor(self.pi, s2, zs2) + noise).clamp(-1.0, 1.0)
-            zsa2 = N.sale_zsa(self.fet, zs2, a2)
-            nq1 = N.sale_critic(self.tq1, s2, a2, zsa2, zs2)
-            nq2 = N.sale_critic(self.tq2, s2, a2, zsa2, zs2)
+            a2 = (actor(self.pi, s2, zs2) + noise).clamp(-1.0, 1.0)
+            zsa2 = zsa_(self.fet, zs2, a2)
+            nq1 = critic(self.tq1, s2, a2, zsa2, zs2)
+            nq2 = critic(self.tq2, s2, a2, zsa2, zs2)
             nv = torch.cat([nq1, nq2], -1).min(1, keepdim=True)[0].clamp(self.vt_min, self.vt_max)
             y = r + self.gamma * nv * nd
             self.value_max = max(self.value_max, float(y.max()))
             self.value_min = min(self.value_min, float(y.min()))
-            zs = N.sale_zs(self.fe, s)
-            zsa_f = N.sale_zsa(self.fe, zs, a)
-        q1 = N.sale_critic(self.q1, s, a, zsa_f, zs)
-        q2 = N.sale_critic(self.q2, s, a, zsa_f, zs)
+            zs = zs_(self.fe, s)
+            zsa_f = zsa_(self.fe, zs, a)
+        q1 = critic(self.q1, s, a, zsa_f, zs)
+        q2 = critic(self.q2, s, a, zsa_f, zs)
         if self.lap:
             td = torch.cat([(q1 - y).abs(), (q2 - y).abs()], 1)
             loss_q = torch.where(td < 1.0, 0.5 * td.pow(2), 1.0 * td).sum(1).mean()
@@ -132,11 +142,11 @@ class TD7Oracle:
         # policy (td7.py:259-276, 319-324)
         info["train/policy"] = None
         if self.n_runs % self.pf == 0:
-            zs = N.sale_zs(self.fe, s)
-            act = N.sale_actor(self.pi, s, zs)
-            zsa_p = N.sale_zsa(self.fe, zs, act)
-            qa = N.sale_critic(self.q1, s, act, zsa_p, zs)
-            qb = N.sale_critic(self.q2, s, act, zsa_p, zs)
+            zs = zs_(self.fe, s)
+            act = actor(self.pi, s, zs)
+            zsa_p = zsa_(self.fe, zs, act)
+            qa = critic(self.q1, s, act, zsa_p, zs)
+            qb = critic(self.q2, s, act, zsa_p, zs)
             loss_p = -torch.cat([qa, qb], -1).mean()
             self.opt_pi.step(_grads(loss_p, self.pi))
             info["train/policy"] = float(loss_p.detach())
@@ -152,11 +162,20 @@ class TD7Oracle:
                 replay.reset_max_priority()
         return info
 
+    def _fns(self):
+        """The four SALE forwards with this agent's activations."""
+        ae, ap, ac = self.ae, self.ap, self.ac
+        return (lambda p, s: N.sale_zs(p, s, ae), lambda p, zs, a: N.sale_zsa(p, zs, a, ae),
+                lambda p, s, zs: N.sale_actor(p, s, zs, ap),
+                lambda p, s, a, zsa, zs: N.sale_critic(p, s, a, zsa, zs, ac))
+
 
 class TD3Oracle:
     def __init__(self, nets, discount=0.99, policy_lr=3e-4, critic_lr=3e-4,
                  target_policy_noise=0.2, noise_clip=0.5, policy_freq=2, tau=0.005,
-                 use_lap=False):
+                 use_lap=False, acts=None):
+        a = _acts(acts, {"actor": "relu", "critic": "relu"})
+        self.ap, self.ac = a["actor"], a["critic"]
         self.pi = _params(nets["policy"])
         self.q1 = _params(nets["q1"])
         self.q2 = _params(nets["q2"])
@@ -176,10 +195,10 @@ class TD3Oracle:
         r, nd = _tt(batch["reward"]), _tt(batch["done"])
         with torch.no_grad():
             noise = (_tt(eps) * self.noise).clamp(-self.clip, self.clip)
-            a2 = (torch.tanh(N.mlp(self.pi, s2)) + noise).clamp(-1.0, 1.0)
-            nv = torch.min(N.mlp_critic(self.tq1, s2, a2), N.mlp_critic(self.tq2, s2, a2))
+            a2 = (torch.tanh(N.mlp(self.pi, s2, self.ap)) + noise).clamp(-1.0, 1.0)
+            nv = torch.min(N.mlp_critic(self.tq1, s2, a2, self.ac), N.mlp_critic(self.tq2, s2, a2, self.ac))
             y = r + self.gamma * nv * nd
-        q1, q2 = N.mlp_critic(self.q1, s, a), N.mlp_critic(self.q2, s, a)
+        q1, q2 = N.mlp_critic(self.q1, s, a, self.ac), N.mlp_critic(self.q2, s, a, self.ac)
         if self.lap:
             d1, d2 = (q1 - y).abs(), (q2 - y).abs()
 
@@ -198,8 +217,8 @@ class TD3Oracle:
         info["train/policy"] = None
         info["norm/policy"] = None
         if self.n_runs % self.pf == 0:
-            act = torch.tanh(N.mlp(self.pi, s))
-            loss_p = -torch.min(N.mlp_critic(self.q1, s, act), N.mlp_critic(self.q2, s, act)).mean()
+            act = torch.tanh(N.mlp(self.pi, s, self.ap))
+            loss_p = -torch.min(N.mlp_critic(self.q1, s, act, self.ac), N.mlp_critic(self.q2, s, act, self.ac)).mean()
             gp = _grads(loss_p, self.pi)
             info["train/policy"] = float(loss_p.detach())
             tot = 0.0
@@ -217,7 +236,9 @@ class TD3Oracle:
 
 class SACOracle:
     def __init__(self, nets, A, discount=0.99, policy_lr=3e-4, critic_lr=3e-4, tau=0.005,
-                 min_log_std=-20.0, max_log_std=2.0, tmp=-1.0):
+                 min_log_std=-20.0, max_log_std=2.0, tmp=-1.0, acts=None):
+        a = _acts(acts, {"actor": "relu", "critic": "relu"})
+        self.ap, self.ac = a["actor"], a["critic"]
         self.pi = _params(nets["policy"])
         self.q1 = _params(nets["q1"])
         self.q2 = _params(nets["q2"])
@@ -238,7 +259,7 @@ class SACOracle:
         self.n_runs = 0
 
     def _dist(self, s, eps):
-        out = N.mlp(self.pi, s)
+        out = N.mlp(self.pi, s, self.ap)
         mean, log_std = out.chunk(2, -1)
         return N.gaussian_tanh(mean, log_std, _tt(eps), self.lo, self.hi)
 
@@ -249,17 +270,17 @@ class SACOracle:
         r, nd = _tt(batch["reward"]), _tt(batch["done"])
         with torch.no_grad():
             a2, lp2 = self._dist(s2, eps)
-            nq = torch.min(N.mlp_critic(self.tq1, s2, a2), N.mlp_critic(self.tq2, s2, a2))
+            nq = torch.min(N.mlp_critic(self.tq1, s2, a2, self.ac), N.mlp_critic(self.tq2, s2, a2, self.ac))
             alpha = self.log_alpha.exp() if self.auto else self.tmp  # sac.py:189
             y = r + self.gamma * (nq - alpha * lp2) * nd
-        q1, q2 = N.mlp_critic(self.q1, s, a), N.mlp_critic(self.q2, s, a)
+        q1, q2 = N.mlp_critic(self.q1, s, a, self.ac), N.mlp_critic(self.q2, s, a, self.ac)
         loss_q = torch.mean((y - q1) ** 2.0) * 0.5 + torch.mean((y - q2) ** 2.0) * 0.5
         g = _grads(loss_q, {**{"a" + k: v for k, v in self.q1.items()},
                             **{"b" + k: v for k, v in self.q2.items()}})
         self.opt_q.step(g)
         info["train/q_fn"] = float(loss_q.detach())
         act, lp = self._dist(s, eps_pi)
-        qv = torch.min(N.mlp_critic(self.q1, s, act), N.mlp_critic(self.q2, s, act))
+        qv = torch.min(N.mlp_critic(self.q1, s, act, self.ac), N.mlp_critic(self.q2, s, act, self.ac))
         alpha_d = self.log_alpha.exp().detach() if self.auto else self.tmp  # sac.py:227-228
         policy_obj = torch.mean(-qv + lp * alpha_d)
         entropy = -(lp.mean().detach())
@@ -336,12 +357,13 @@ def moments(oracle):
     return out
 
 
-def make_oracle(alg, nets, A, use_lap, **hp):
+def make_oracle(alg, nets, A, use_lap, acts=None, **hp):
+    """acts: hidden activations {"actor", "critic", "encoder" (TD7)} by nets.ACTS name (None: defaults)."""
     if alg == "td7":
-        return TD7Oracle(nets, use_lap=use_lap, **hp)
+        return TD7Oracle(nets, use_lap=use_lap, acts=acts, **hp)
     if alg == "td3":
-        return TD3Oracle(nets, use_lap=use_lap, **hp)
-    return SACOracle(nets, A, **hp)
+        return TD3Oracle(nets, use_lap=use_lap, acts=acts, **hp)
+    return SACOracle(nets, A, acts=acts, **hp)
 
 
 def run_steps(oracle, alg, replay, tapes, n_steps, B):

@@ -1678,6 +1678,7 @@ struct Engine {
   // the rle_level instance this engine's programs run on (ops.h KernelSet): the agent's own set, or the
   // extended instance when the plan asks for its opt-in paths
   int kernel_set() const {
+    if (!acts_default) return KS_EXT;  // (the activation variants outside the agent's own set)
     if (algo == RLE_TD7 && plan.wide && !(plan.fuse_on & RLE_FUSE_PRIOSAMPLE)) return KS_TD7W;  // (rb compiled in)
     if (plan.rb || (plan.fuse_on & RLE_FUSE_PRIOSAMPLE) || plan.wide) return KS_EXT;
     return algo == RLE_TD7 ? KS_TD7 : KS_MLP;
@@ -1728,6 +1729,14 @@ struct Engine {
                // every mean, loss, priority and value bound counts the Bv batch rows only
   int Z = 0, Zp = 0;    // TD7: SALE embedding width zs_dim (sale.py:23), padded
   std::vector<int> HS;  // TD3 / SAC: hidden widths of make_mlp (mlp.py:10-35), input side first
+  // hidden activations (ops.h Act) of the actor, the critics and TD7's encoders (rle_config act_*)
+  int actP = ACT_RELU, actC = ACT_ELU, actE = ACT_ELU;
+  bool acts_default = true;
+  // The derivative source of a hidden activation for an input-gradient GEMM: ELU' = exp(z) reads the pre-activation
+  // z (as autograd's elu_backward does), ReLU' the output, identity none.
+  static const View* dsrc_of(int act, const View& y, const View& z) {
+    return act == ACT_ELU ? &z : act == ACT_RELU ? &y : nullptr;
+  }
   int algo;
   hipStream_t stream = nullptr;
   DevMem mem;
@@ -1846,17 +1855,17 @@ struct Engine {
     if (algo == RLE_TD7) {  // td7.py:158-162: zs = fixed_encoder(s); policy(s, zs)
       Net& fe = net("fixed_encoder");
       Net& pi = net("policy");
-      ok &= layer(fe.layers[0], ACT_ELU, 0, -1, 0, 1, 0);
+      ok &= layer(fe.layers[0], actE, 0, -1, 0, 1, 0);
       ok &= layer(pi.layers[0], ACT_NONE, 0, -1, 1, 2, 1);
-      ok &= layer(fe.layers[1], ACT_ELU, 1, -1, 0, 3, 1);
+      ok &= layer(fe.layers[1], actE, 1, -1, 0, 3, 1);
       ok &= layer(fe.layers[2], ACT_NONE, 3, -1, 1, 4, 1);
-      ok &= layer(pi.layers[1], ACT_RELU, 2, 4, 0, 5, 1);
-      ok &= layer(pi.layers[2], ACT_RELU, 5, -1, 0, 6, 1);
+      ok &= layer(pi.layers[1], actP, 2, 4, 0, 5, 1);
+      ok &= layer(pi.layers[2], actP, 5, -1, 0, 6, 1);
       ok &= layer(pi.layers[3], ACT_TANH, 6, -1, 0, 7, 0);
     } else {  // mlp.py:55-68
       Net& pi = net("policy");
       const int D = (int)HS.size();  // (hidden layer i -> slot i + 1; the output -> slot 7)
-      for (int i = 0; i < D; ++i) ok &= layer(pi.layers[i], ACT_RELU, i, -1, 0, i + 1, 1);
+      for (int i = 0; i < D; ++i) ok &= layer(pi.layers[i], actP, i, -1, 0, i + 1, 1);
       ok &= layer(pi.layers[D], algo == RLE_SAC ? ACT_NONE : ACT_TANH, D, -1, 0, 7, 0);
       c.sac = algo == RLE_SAC;
     }
@@ -2237,7 +2246,11 @@ struct Engine {
   // 23.37k / 23.79k / 23.91k, TD7 Humanoid 8069 / 8094 / 8060 steps/s)
   int pre_tn() const { return plan.pre_tn; }
   int pl_tn() const { return plan.pl_tn; }
+  // (fusions whose in-tile recomputation or fused head is written for the default activations)
+  static constexpr unsigned kActFusions = RLE_FUSE_PRELAYER | RLE_FUSE_PRE | RLE_FUSE_QDOT | RLE_FUSE_HEADDX |
+                                          RLE_FUSE_TWOSTAGE | RLE_FUSE_SACPRE;
   bool fused(unsigned bit) const {
+    if (!acts_default && (bit & kActFusions)) return false;
     return (bit & RLE_FUSE_OPT_IN) ? (plan.fuse_on & bit) != 0 : !(plan.fuse_off & bit);
   }
   bool prelayer_shape(const Layer& L0, const Layer& L1) const {
@@ -2792,23 +2805,23 @@ struct Engine {
 
   // SALEEncoder.encode_state (sale.py:41-46): a normed view (consumers apply the norm).
   View enc_zs(Prog& pg, Net& E, const View& s, int M) {
-    View h1 = fwd(pg, E.layers[0], {{s}}, M, ACT_ELU, nullptr, false);
-    View h2 = fwd(pg, E.layers[1], {{h1}}, M, ACT_ELU, nullptr, false);
+    View h1 = fwd(pg, E.layers[0], {{s}}, M, actE, nullptr, false);
+    View h2 = fwd(pg, E.layers[1], {{h1}}, M, actE, nullptr, false);
     return fwd(pg, E.layers[2], {{h2}}, M, ACT_NONE, nullptr, true);
   }
   // SALEEncoder.encode_state_action (sale.py:48-55).
   View enc_zsa(Prog& pg, Net& E, const View& zs, const View& a, int M) {
-    View a1 = fwd(pg, E.layers[3], {{zs}, {a}}, M, ACT_ELU, nullptr, false);
-    View a2 = fwd(pg, E.layers[4], {{a1}}, M, ACT_ELU, nullptr, false);
+    View a1 = fwd(pg, E.layers[3], {{zs}, {a}}, M, actE, nullptr, false);
+    View a2 = fwd(pg, E.layers[4], {{a1}}, M, actE, nullptr, false);
     return fwd(pg, E.layers[5], {{a2}}, M, ACT_NONE, nullptr, false);
   }
 
-  // make_mlp forward (mlp.py:24-35): ReLU after every hidden layer, `last` after the output layer.
-  View mlp_fwd(Prog& pg, Net& N, const std::vector<std::vector<View>>& in, int M, int last) {
+  // make_mlp forward (mlp.py:24-35): `act` (action_fn) after every hidden layer, `last` after the output layer.
+  View mlp_fwd(Prog& pg, Net& N, const std::vector<std::vector<View>>& in, int M, int last, int act) {
     View h;
     for (size_t i = 0; i < N.layers.size(); ++i)
       h = fwd(pg, N.layers[i], i ? std::vector<std::vector<View>>{{h}} : in, M,
-              i + 1 == N.layers.size() ? last : ACT_RELU, nullptr, false);
+              i + 1 == N.layers.size() ? last : act, nullptr, false);
     return h;
   }
 
@@ -3105,13 +3118,13 @@ struct Engine {
     View s = ss.sub(0, B), s2 = ss.sub(B, B);
     // ---- encoder phase (td7.py:246-257): online encoder on [s; s'] (one GEMM per layer)
     View ez1, ez2;
-    View eh1 = fwd(pg, enc.layers[0], {{ss}}, B2, ACT_ELU, &ez1, false);
-    View eh2 = fwd(pg, enc.layers[1], {{eh1}}, B2, ACT_ELU, &ez2, false);
+    View eh1 = fwd(pg, enc.layers[0], {{ss}}, B2, actE, &ez1, false);
+    View eh2 = fwd(pg, enc.layers[1], {{eh1}}, B2, actE, &ez2, false);
     View ex3 = fwd(pg, enc.layers[2], {{eh2}}, B2, ACT_NONE, nullptr, true);
     View ezs = ex3.sub(0, B), ezs2 = ex3.sub(B, B);
     View ea1z, ea2z;
-    View ea1 = fwd(pg, enc.layers[3], {{ezs}, {act_in}}, B, ACT_ELU, &ea1z, false);
-    View ea2 = fwd(pg, enc.layers[4], {{ea1}}, B, ACT_ELU, &ea2z, false);
+    View ea1 = fwd(pg, enc.layers[3], {{ezs}, {act_in}}, B, actE, &ea1z, false);
+    View ea2 = fwd(pg, enc.layers[4], {{ea1}}, B, actE, &ea2z, false);
     // zsa3 + MSE gradient vs zs_next (normed) fused
     View ed3;
     float* enc_loss = nullptr;
@@ -3157,9 +3170,9 @@ struct Engine {
     }
     // encoder backward + Adam (optim_encoder, lr = policy_lr)
     {
-      View d2 = dx(pg, {{ed3, &enc.layers[5], 0}}, H, B, ACT_ELU, &ea2z);
+      View d2 = dx(pg, {{ed3, &enc.layers[5], 0}}, H, B, actE, &ea2z);
       dw(pg, enc.layers[5], ed3, {ea2}, B, CNT_ADAM_ENC, cfg.policy_lr);
-      View d1 = dx(pg, {{d2, &enc.layers[4], 0}}, H, B, ACT_ELU, &ea1z);
+      View d1 = dx(pg, {{d2, &enc.layers[4], 0}}, H, B, actE, &ea1z);
       dw(pg, enc.layers[4], d2, {ea1}, B, CNT_ADAM_ENC, cfg.policy_lr);
       out_t = false;  // (read by the norm backward only)
       View gzs = dx(pg, {{d1, &enc.layers[3], 0}}, Z, B, ACT_NONE, nullptr);
@@ -3167,30 +3180,32 @@ struct Engine {
       dw(pg, enc.layers[3], d1, {ezs, act_in}, B, CNT_ADAM_ENC, cfg.policy_lr);
       View dx3 = normbwd(pg, gzs, ex3.sub(0, B));
       View ez2s = ez2.sub(0, B), ez1s = ez1.sub(0, B);
-      View dh2 = dx(pg, {{dx3, &enc.layers[2], 0}}, H, B, ACT_ELU, &ez2s);
+      View dh2 = dx(pg, {{dx3, &enc.layers[2], 0}}, H, B, actE, &ez2s);
       dw(pg, enc.layers[2], dx3, {eh2.sub(0, B)}, B, CNT_ADAM_ENC, cfg.policy_lr);
-      View dh1 = dx(pg, {{dh2, &enc.layers[1], 0}}, H, B, ACT_ELU, &ez1s);
+      View dh1 = dx(pg, {{dh2, &enc.layers[1], 0}}, H, B, actE, &ez1s);
       dw(pg, enc.layers[1], dh2, {eh1.sub(0, B)}, B, CNT_ADAM_ENC, cfg.policy_lr);
       dw(pg, enc.layers[0], dh1, {s}, B, CNT_ADAM_ENC, cfg.policy_lr);
     }
     // ---- fixed encoder on s, fixed target encoder on s'
     out_t = false;  // forward-only outputs (no weight gradient reads them)
-    View fh1 = fwd(pg, fe.layers[0], {{s}}, B, ACT_ELU, nullptr, false);
-    View fh2 = fwd(pg, fe.layers[1], {{fh1}}, B, ACT_ELU, nullptr, false);
+    View fh1 = fwd(pg, fe.layers[0], {{s}}, B, actE, nullptr, false);
+    View fh2 = fwd(pg, fe.layers[1], {{fh1}}, B, actE, nullptr, false);
     out_t = true;
     View fzs = fwd(pg, fe.layers[2], {{fh2}}, B, ACT_NONE, nullptr, true);
     out_t = false;
-    View th1 = fwd(pg, fet.layers[0], {{s2}}, B, ACT_ELU, nullptr, false);
-    View th2 = fwd(pg, fet.layers[1], {{th1}}, B, ACT_ELU, nullptr, false);
+    View th1 = fwd(pg, fet.layers[0], {{s2}}, B, actE, nullptr, false);
+    View th2 = fwd(pg, fet.layers[1], {{th1}}, B, actE, nullptr, false);
     View tzs = fwd(pg, fet.layers[2], {{th2}}, B, ACT_NONE, nullptr, true);
-    View fa1 = fwd(pg, fe.layers[3], {{fzs}, {act_in}}, B, ACT_ELU, nullptr, false);
-    View fa2 = fwd(pg, fe.layers[4], {{fa1}}, B, ACT_ELU, nullptr, false);
+    View fa1 = fwd(pg, fe.layers[3], {{fzs}, {act_in}}, B, actE, nullptr, false);
+    View fa2 = fwd(pg, fe.layers[4], {{fa1}}, B, actE, nullptr, false);
     out_t = true;
     View fzsa = fwd(pg, fe.layers[5], {{fa2}}, B, ACT_NONE, nullptr, false);
     // ---- actor on [s; s'] (target policy aliases the policy, Q1)
     View ap0 = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_NONE, nullptr, true);
-    View ap1 = fwd(pg, pi.layers[1], {{ap0}, {fzs, tzs}}, B2, ACT_RELU, nullptr, false);
-    View ap2 = fwd(pg, pi.layers[2], {{ap1}}, B2, ACT_RELU, nullptr, false);
+    // (an ELU actor keeps its pre-activations for the policy backward: ELU' = exp(z))
+    View ap1z, ap2z;
+    View ap1 = fwd(pg, pi.layers[1], {{ap0}, {fzs, tzs}}, B2, actP, actP == ACT_ELU ? &ap1z : nullptr, false);
+    View ap2 = fwd(pg, pi.layers[2], {{ap1}}, B2, actP, actP == ACT_ELU ? &ap2z : nullptr, false);
     // a' = clamp(pi(s', zs') + noise) only feeds the target branch's first layers, which
     // recompute it in-tile (pre-GEMM): the actor output layer runs on the s rows alone
     const bool prea = actor_pre();
@@ -3202,8 +3217,8 @@ struct Engine {
     const PreUse* pnext = prea ? &pn1 : nullptr;
     // ---- target: zsa' and target critics (forward only)
     out_t = false;
-    View ta1 = fwd(pg, fet.layers[3], {{tzs}, {a_next}}, B, ACT_ELU, nullptr, false, nullptr, 0, nullptr, nullptr, pnext);
-    View ta2 = fwd(pg, fet.layers[4], {{ta1}}, B, ACT_ELU, nullptr, false);
+    View ta1 = fwd(pg, fet.layers[3], {{tzs}, {a_next}}, B, actE, nullptr, false, nullptr, 0, nullptr, nullptr, pnext);
+    View ta2 = fwd(pg, fet.layers[4], {{ta1}}, B, actE, nullptr, false);
     // zsa' = zsa3(ta2) only feeds the target critics' first hidden layer, a linear map:
     // with `fold`, tq.q1[:, zsa block] x fet.zsa3 is precomputed (add_target_fold) and the
     // target critics read ta2 directly (one dependent level fewer)
@@ -3219,11 +3234,11 @@ struct Engine {
         const Layer& L1 = tq[n]->layers[1];
         const std::vector<WSeg> ws{wblock(L1, 0), {tfold_w[n].m.n, tfold_w[n].m.cbn, tfold_w[n].id},
                                    wblock(L1, L1.seg_p[0] + L1.seg_p[1])};
-        t1 = fwd(pg, L1, {{t01}, {ta2}, {tzs}}, B, ACT_ELU, nullptr, false, nullptr, 0, &ws, &tfold_b[n]);
+        t1 = fwd(pg, L1, {{t01}, {ta2}, {tzs}}, B, actC, nullptr, false, nullptr, 0, &ws, &tfold_b[n]);
       } else {
-        t1 = fwd(pg, tq[n]->layers[1], {{t01}, {tzsa}, {tzs}}, B, ACT_ELU, nullptr, false);
+        t1 = fwd(pg, tq[n]->layers[1], {{t01}, {tzsa}, {tzs}}, B, actC, nullptr, false);
       }
-      th[n] = fwd(pg, tq[n]->layers[2], {{t1}}, B, ACT_ELU, nullptr, false, nullptr, 0, nullptr, nullptr, nullptr,
+      th[n] = fwd(pg, tq[n]->layers[2], {{t1}}, B, actC, nullptr, false, nullptr, 0, nullptr, nullptr, nullptr,
                   qpart ? &tq[n]->layers[3] : nullptr);
     }
     out_t = true;
@@ -3231,8 +3246,8 @@ struct Engine {
     View c01[2], c1[2], c2[2], c1z[2], c2z[2];
     for (int n = 0; n < 2; ++n) {
       c01[n] = fwd(pg, q[n]->layers[0], {{s}, {act_in}}, B, ACT_NONE, nullptr, true);
-      c1[n] = fwd(pg, q[n]->layers[1], {{c01[n]}, {fzsa}, {fzs}}, B, ACT_ELU, &c1z[n], false);
-      c2[n] = fwd(pg, q[n]->layers[2], {{c1[n]}}, B, ACT_ELU, &c2z[n], false, nullptr, 0, nullptr, nullptr, nullptr,
+      c1[n] = fwd(pg, q[n]->layers[1], {{c01[n]}, {fzsa}, {fzs}}, B, actC, &c1z[n], false);
+      c2[n] = fwd(pg, q[n]->layers[2], {{c1[n]}}, B, actC, &c2z[n], false, nullptr, 0, nullptr, nullptr, nullptr,
                   qpart ? &q[n]->layers[3] : nullptr, true);
     }
     const bool hdx = td7_headdx() && qpart;  // (the fused head reads q partials only)
@@ -3257,7 +3272,7 @@ struct Engine {
       h.vt = ctrl->vt;
       h.dsrc[0] = c2z[0].m;
       h.dsrc[1] = c2z[1].m;
-      h.dact = ACT_ELU;
+      h.dact = actC;
       h.lap = lap;
       h.dz[0] = dz2[0].m;
       h.dz[1] = dz2[1].m;
@@ -3297,7 +3312,7 @@ struct Engine {
                      {dz2[n].id, dq[n].id}};
           if (n == 0) hu.wr.insert(hu.wr.end(), {prio.id, qloss_id, R_VKEYS});
           hu.rd.insert(hu.rd.end(), qrd.begin(), qrd.end());
-          d1f[n] = dx(pg, {{c2z[n], &q[n]->layers[2], 0}}, H, B, ACT_ELU, &c1z[n], nullptr, nullptr, nullptr, &hu);
+          d1f[n] = dx(pg, {{c2z[n], &q[n]->layers[2], 0}}, H, B, actC, &c1z[n], nullptr, nullptr, nullptr, &hu);
         }
       }
     }
@@ -3305,7 +3320,7 @@ struct Engine {
     for (int n = 0; n < 2; ++n) {  // critic backward + Adam (optim_q_fns spans q1 + q2)
       Net& Q = *q[n];
       dw(pg, Q.layers[3], dq[n], {c2[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
-      View d1 = hdx ? d1f[n] : dx(pg, {{dz2[n], &Q.layers[2], 0}}, H, B, ACT_ELU, &c1z[n]);
+      View d1 = hdx ? d1f[n] : dx(pg, {{dz2[n], &Q.layers[2], 0}}, H, B, actC, &c1z[n]);
       dw(pg, Q.layers[2], dz2[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
       (nbd ? out_n : out_t) = false;  // (read by the weight gradient / the norm backward only)
       View g01 = dx(pg, {{d1, &Q.layers[1], 0}}, H, B, ACT_NONE, nullptr, nullptr, nbd ? &c01[n] : nullptr);
@@ -3322,13 +3337,13 @@ struct Engine {
     if (policy) {  // td7.py:259-276 with the updated critics (no weight gradient of these layers)
       View pa1z, pa2z;
       out_t = false;
-      View pa1 = fwd(pg, fe.layers[3], {{fzs}, {a_pi}}, B, ACT_ELU, &pa1z, false);
-      View pa2 = fwd(pg, fe.layers[4], {{pa1}}, B, ACT_ELU, &pa2z, false);
+      View pa1 = fwd(pg, fe.layers[3], {{fzs}, {a_pi}}, B, actE, &pa1z, false);
+      View pa2 = fwd(pg, fe.layers[4], {{pa1}}, B, actE, &pa2z, false);
       View pzsa = fwd(pg, fe.layers[5], {{pa2}}, B, ACT_NONE, nullptr, false);
       View p01[2], p1[2], p1z[2], dzp2[2];
       for (int n = 0; n < 2; ++n) {
         p01[n] = fwd(pg, q[n]->layers[0], {{s}, {a_pi}}, B, ACT_NONE, nullptr, true);
-        p1[n] = fwd(pg, q[n]->layers[1], {{p01[n]}, {pzsa}, {fzs}}, B, ACT_ELU, &p1z[n], false);
+        p1[n] = fwd(pg, q[n]->layers[1], {{p01[n]}, {pzsa}, {fzs}}, B, actC, &p1z[n], false);
       }
       out_t = true;
       // q2 + q3 + dL/dQ = -1/(2B) fused (EPI_QHEAD): dZ of q2 straight from the GEMM
@@ -3345,7 +3360,7 @@ struct Engine {
       View dzp1[2], dxp01[2];
       out_t = false;  // (no weight gradient of the critics or the fixed encoder in the policy pass)
       for (int n = 0; n < 2; ++n) {
-        dzp1[n] = dx(pg, {{dzp2[n], &q[n]->layers[2], 0}}, H, B, ACT_ELU, &p1z[n]);
+        dzp1[n] = dx(pg, {{dzp2[n], &q[n]->layers[2], 0}}, H, B, actC, &p1z[n]);
         View g = dx(pg, {{dzp1[n], &q[n]->layers[1], 0}}, H, B, ACT_NONE, nullptr);
         dxp01[n] = normbwd(pg, g, p01[n]);
       }
@@ -3357,15 +3372,15 @@ struct Engine {
         for (int n = 0; n < 2; ++n)
           G[n] = dx(pg, {{wview_n(q[n]->layers[1], Hp, H), &fe.layers[5], 0}}, H, H, ACT_NONE, nullptr);
         out_t = false;
-        dpa2 = dx(pg, {{dzp1[0], nullptr, 0, &G[0]}, {dzp1[1], nullptr, 0, &G[1]}}, H, B, ACT_ELU, &pa2z);
+        dpa2 = dx(pg, {{dzp1[0], nullptr, 0, &G[0]}, {dzp1[1], nullptr, 0, &G[1]}}, H, B, actE, &pa2z);
         out_t = true;
       } else {
         View gzsa = dx(pg, {{dzp1[0], &q[0]->layers[1], Hp}, {dzp1[1], &q[1]->layers[1], Hp}}, Z, B, ACT_NONE,
                        nullptr);
-        dpa2 = dx(pg, {{gzsa, &fe.layers[5], 0}}, H, B, ACT_ELU, &pa2z);
+        dpa2 = dx(pg, {{gzsa, &fe.layers[5], 0}}, H, B, actE, &pa2z);
       }
       out_t = false;
-      View dpa1 = dx(pg, {{dpa2, &fe.layers[4], 0}}, H, B, ACT_ELU, &pa1z);
+      View dpa1 = dx(pg, {{dpa2, &fe.layers[4], 0}}, H, B, actE, &pa1z);
       out_t = true;
       // d action = sum of three paths, then tanh' (actor output)
       const std::vector<DxTerm> t3{
@@ -3375,9 +3390,11 @@ struct Engine {
       // input-grads through a layer are emitted BEFORE its Adam update so the
       // scheduler orders them against the pre-update weights (as autograd does)
       View ap2s = ap2.sub(0, B), ap1s = ap1.sub(0, B);
-      View dl2 = dx(pg, {{dl3, &pi.layers[3], 0}}, H, B, ACT_RELU, &ap2s, nullptr, nullptr, prea ? &p3 : nullptr);
+      const View ap2zs = actP == ACT_ELU ? ap2z.sub(0, B) : View{}, ap1zs = actP == ACT_ELU ? ap1z.sub(0, B) : View{};
+      View dl2 = dx(pg, {{dl3, &pi.layers[3], 0}}, H, B, actP, dsrc_of(actP, ap2s, ap2zs), nullptr, nullptr,
+                    prea ? &p3 : nullptr);
       dw(pg, pi.layers[3], dl3, {ap2s}, B, CNT_ADAM_PI, cfg.policy_lr);
-      View dl1 = dx(pg, {{dl2, &pi.layers[2], 0}}, H, B, ACT_RELU, &ap1s);
+      View dl1 = dx(pg, {{dl2, &pi.layers[2], 0}}, H, B, actP, dsrc_of(actP, ap1s, ap1zs));
       dw(pg, pi.layers[2], dl2, {ap1s}, B, CNT_ADAM_PI, cfg.policy_lr);
       const View ap0s = ap0.sub(0, B);
       (nbd ? out_n : out_t) = false;
@@ -3443,7 +3460,7 @@ struct Engine {
     g.tiles_n = cdiv(L.out, g.tn);
     *ntiles = g.tiles_m * g.tiles_n;  // (wide: one loss partial per 16-row block too)
     g.epi = EPI_QHEAD;
-    g.act = ACT_ELU;
+    g.act = actC;
     g.bias = bias(L);
     View dz = buf(M, L.out, true, false);  // (read by the input-gradient GEMM only: no weight update here)
     g.out = dz.m;
@@ -3562,10 +3579,14 @@ struct Engine {
   // GemmArgs::has_pre 4, whose epilogue is the q partials: two hidden layers only): the target branch's
   // first layer costs no level of its own.  Without the fusion it is its own level, in at most 32-wide
   // tiles (pl_src), so both give the same floats.
+  // hz: the pre-activations too when the backward needs them (ELU critics; the last layer's with an N image,
+  // for the loss head's rows)
   void mlp_critic_fwd(Prog& pg, Net& Q, const View& sv, const View& av, std::vector<View>& hs,
-                      const PreUse* pre = nullptr, bool last_t = true, bool qd = false) {
+                      const PreUse* pre = nullptr, bool last_t = true, bool qd = false, std::vector<View>* hz = nullptr) {
     const int D = (int)Q.layers.size() - 1;
     hs.assign(D, View{});
+    if (hz) hz->assign(D, View{});
+    auto zp = [&](int i) { return hz && actC == ACT_ELU ? &(*hz)[i] : nullptr; };
     const bool shape = prelayer_shape(Q.layers[0], Q.layers[1]);
     // (the pre-GEMM's a' segment is one column block, kernels.hip PK 4 / gemm_finalize's two-stage REQUIRE)
     const bool two = pre && pre->kind == 1 && pre->a.mode == GEMM_FWD && pre->a.N <= 32 && r16(A) <= 16 && qd &&
@@ -3576,7 +3597,8 @@ struct Engine {
       hs[0] = buf(B, Q.layers[0].out, true, false);  // (layout of the consumer's A operand only: never stored)
     } else {
       pl_src = use_pl || (pre && shape);
-      hs[0] = fwd(pg, Q.layers[0], {{sv}, {av}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr, pre);
+      hs[0] = fwd(pg, Q.layers[0], {{sv}, {av}}, B, actC, zp(0), false, nullptr, 0, nullptr, nullptr, pre, nullptr,
+                  D == 1);
       pl_src = false;
     }
     const bool keep = out_t;
@@ -3589,8 +3611,8 @@ struct Engine {
         pl.a2 = pre->a;
         pl.rd.insert(pl.rd.end(), pre->rd.begin(), pre->rd.end());
       }
-      hs[i] = fwd(pg, Q.layers[i], {{hs[i - 1]}}, B, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr,
-                  pl.kind >= 3 ? &pl : nullptr, last && qd ? &Q.layers[D] : nullptr);
+      hs[i] = fwd(pg, Q.layers[i], {{hs[i - 1]}}, B, actC, zp(i), false, nullptr, 0, nullptr, nullptr,
+                  pl.kind >= 3 ? &pl : nullptr, last && qd ? &Q.layers[D] : nullptr, last);
     }
     out_t = keep;
   }
@@ -3651,12 +3673,13 @@ struct Engine {
     const Layer& Lout = pi.layers[D];
     // actor on [s; s'] (target policy aliases the policy, Q1; SAC policy unchanged until its step)
     pl_src = prelayer_ok(pi.layers[0], pi.layers[1]);
-    std::vector<View> h(D);
-    h[0] = fwd(pg, pi.layers[0], {{ss}}, B2, ACT_RELU, nullptr, false);
+    std::vector<View> h(D), hz(D);  // (hz: an ELU actor's pre-activations, for the policy backward)
+    const bool pz = actP == ACT_ELU;
+    h[0] = fwd(pg, pi.layers[0], {{ss}}, B2, actP, pz ? &hz[0] : nullptr, false);
     pl_src = false;
     const PreUse pl0 = prelayer_ok(pi.layers[0], pi.layers[1]) ? pre_layer(pi.layers[0], {ss}) : PreUse{};
     for (int i = 1; i < D; ++i)
-      h[i] = fwd(pg, pi.layers[i], {{h[i - 1]}}, B2, ACT_RELU, nullptr, false, nullptr, 0, nullptr, nullptr,
+      h[i] = fwd(pg, pi.layers[i], {{h[i - 1]}}, B2, actP, pz ? &hz[i] : nullptr, false, nullptr, 0, nullptr, nullptr,
                  i == 1 && pl0.kind == 3 ? &pl0 : nullptr);
     const View hl = h[D - 1];  // the last hidden layer's output
     View actv, raw, logpi;
@@ -3719,8 +3742,10 @@ struct Engine {
     for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *tq[n], s2, a_next, th[n], tpre, true, hdx);
     out_t = true;
     // online critics
-    std::vector<View> c[2];
-    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c[n], nullptr, true, hdx);
+    std::vector<View> c[2], cz[2];
+    for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, act_in, c[n], nullptr, true, hdx, &cz[n]);
+    // (the loss heads' derivative rows: ELU' reads the pre-activation; ReLU' / identity the output)
+    const bool cze = actC == ACT_ELU;
     // (the last hidden layers and the heads' layers)
     const View c1[2] = {c[0][D - 1], c[1][D - 1]}, th1[2] = {th[0][D - 1], th[1][D - 1]};
     const Layer *qo[2] = {&q[0]->layers[D], &q[1]->layers[D]}, *tqo[2] = {&tq[0]->layers[D], &tq[1]->layers[D]};
@@ -3750,9 +3775,10 @@ struct Engine {
         rd.push_back(logpi.id);
         rd.push_back(R_LA);
       }
-      h.dsrc[0] = c1[0].m;
-      h.dsrc[1] = c1[1].m;
-      h.dact = ACT_RELU;
+      h.dsrc[0] = (cze ? cz[0][D - 1] : c1[0]).m;
+      h.dsrc[1] = (cze ? cz[1][D - 1] : c1[1]).m;
+      if (cze) rd.insert(rd.end(), {cz[0][D - 1].id, cz[1][D - 1].id});
+      h.dact = actC;
       h.lap = lap;
       h.dz[0] = dz1[0].m;
       h.dz[1] = dz1[1].m;
@@ -3770,8 +3796,8 @@ struct Engine {
         for (int n = 0; n < 2; ++n) {
           HeadUse hu{h, n, rd, {dz1[n].id, dq[n].id}};
           if (n == 0) hu.wr.insert(hu.wr.end(), {prio.id, qloss_id});
-          d0f[n] = dx(pg, {{c1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &c[n][D - 2], nullptr, nullptr,
-                      nullptr, &hu);
+          d0f[n] = dx(pg, {{c1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, actC, dsrc_of(actC, c[n][D - 2], cz[n][D - 2]),
+                      nullptr, nullptr, nullptr, &hu);
         }
       }
     }
@@ -3781,7 +3807,9 @@ struct Engine {
       dw(pg, Q.layers[D], dq[n], {c1[n]}, B, CNT_ADAM_Q, cfg.critic_lr);
       View d = dz1[n];  // dZ of hidden layer i, from i = D - 1 down
       for (int i = D - 1; i >= 1; --i) {
-        const View dp = hdx && i == D - 1 ? d0f[n] : dx(pg, {{d, &Q.layers[i], 0}}, HS[i - 1], B, ACT_RELU, &c[n][i - 1]);
+        const View dp = hdx && i == D - 1 ? d0f[n]
+                                           : dx(pg, {{d, &Q.layers[i], 0}}, HS[i - 1], B, actC,
+                                                dsrc_of(actC, c[n][i - 1], cz[n][i - 1]));
         dw(pg, Q.layers[i], d, {c[n][i - 1]}, B, CNT_ADAM_Q, cfg.critic_lr);
         d = dp;
       }
@@ -3791,8 +3819,8 @@ struct Engine {
     float* gsq = nullptr;
     int ngsq = 0;
     if (policy) {
-      std::vector<View> pc[2];
-      for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, a_pi, pc[n], nullptr, false, hdx);
+      std::vector<View> pc[2], pcz[2];
+      for (int n = 0; n < 2; ++n) mlp_critic_fwd(pg, *q[n], s, a_pi, pc[n], nullptr, false, hdx, &pcz[n]);
       const View p1[2] = {pc[0][D - 1], pc[1][D - 1]};
       // (no weight gradient of the critics in the policy pass: the gradients keep N images only)
       View dzp1[2];
@@ -3803,7 +3831,7 @@ struct Engine {
         Op op = head_op(HEAD_MLP_POLICY, Bv);
         HeadArgs& h = op.head;
         set_head_twin(h, p1[0], p1[1], *qo[0], *qo[1]);
-        h.dact = ACT_RELU;
+        h.dact = actC;
         h.loss_part = ploss_part;
         std::vector<int> rd{p1[0].id, p1[1].id, qo[0]->res, qo[1]->res};
         if (sac) {
@@ -3820,21 +3848,22 @@ struct Engine {
         for (int n = 0; n < 2; ++n) {
           HeadUse hu{h, n, rd, {}};
           if (n == 0) hu.wr.push_back(ploss_id);
-          dzp0[n] = dx(pg, {{p1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &pc[n][D - 2], nullptr, nullptr,
-                       nullptr, &hu);
+          dzp0[n] = dx(pg, {{p1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, actC,
+                       dsrc_of(actC, pc[n][D - 2], pcz[n][D - 2]), nullptr, nullptr, nullptr, &hu);
         }
         out_t = true;
       } else {
         Op op = head_op(HEAD_MLP_POLICY, Bv);
         HeadArgs& h = op.head;
         set_head_twin(h, p1[0], p1[1], *qo[0], *qo[1]);
-        h.dsrc[0] = p1[0].m;
-        h.dsrc[1] = p1[1].m;
-        h.dact = ACT_RELU;
+        h.dsrc[0] = (cze ? pcz[0][D - 1] : p1[0]).m;
+        h.dsrc[1] = (cze ? pcz[1][D - 1] : p1[1]).m;
+        h.dact = actC;
         h.dz[0] = dzp1[0].m;
         h.dz[1] = dzp1[1].m;
         h.loss_part = ploss_part;
         std::vector<int> rd{p1[0].id, p1[1].id, qo[0]->res, qo[1]->res};
+        if (cze) rd.insert(rd.end(), {pcz[0][D - 1].id, pcz[1][D - 1].id});
         if (sac) {
           h.sac = 1;
           h.logpi = logpi.p;
@@ -3846,13 +3875,15 @@ struct Engine {
         pg.add(op, rd, {dzp1[0].id, dzp1[1].id, ploss_id = next_id++});
         out_t = false;
         for (int n = 0; n < 2; ++n)
-          dzp0[n] = dx(pg, {{dzp1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &pc[n][D - 2]);
+          dzp0[n] = dx(pg, {{dzp1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, actC,
+                       dsrc_of(actC, pc[n][D - 2], pcz[n][D - 2]));
         out_t = true;
       }
       // (deeper critics: on down to the first hidden layer; no weight gradient reads these)
       out_t = false;
       for (int i = D - 2; i >= 1; --i)
-        for (int n = 0; n < 2; ++n) dzp0[n] = dx(pg, {{dzp0[n], &q[n]->layers[i], 0}}, HS[i - 1], B, ACT_RELU, &pc[n][i - 1]);
+        for (int n = 0; n < 2; ++n)
+          dzp0[n] = dx(pg, {{dzp0[n], &q[n]->layers[i], 0}}, HS[i - 1], B, actC, dsrc_of(actC, pc[n][i - 1], pcz[n][i - 1]));
       out_t = true;
       View dout;
       PreUse pdout{};  // TD3: d1 recomputes dout in-tile
@@ -3923,26 +3954,29 @@ struct Engine {
       // actor backward: tensors in parameters() order mlp.0.w, mlp.0.b, mlp.2.w, ...
       std::vector<std::pair<float*, float*>> gl;
       for (int i = 0; i <= D; ++i) gl.push_back(gsq_for(pi.layers[i], 2 * i, 2 * i + 1));
-      std::vector<View> hsub(D);
+      std::vector<View> hsub(D), hzsub(D);
       for (int i = 0; i < D; ++i) hsub[i] = h[i].sub(0, B);
+      if (pz)
+        for (int i = 0; i < D; ++i) hzsub[i] = hz[i].sub(0, B);
       // TD3: the aliased target policy's Polyak (td3.py:200-204) in the Adam epilogues: one level
       // fewer between the actor update and the next step's target action
       adam_ptau = !sac && pi_polyak_fused() ? cfg.tau : 0.f;
       // SAC: d1 (the gradient through the raw head, K = 2A <= 48) recomputed in-tile by d0's DX
       const bool pld = sac && sac_bwd_fused() && prelayer_ok_dx(Lout, pi.layers[D - 1]);
       pl_src = pld;
-      View d = dx(pg, {{dout, &Lout, 0}}, HS[D - 1], B, ACT_RELU, &hsub[D - 1], nullptr, nullptr, prea ? &pdout : nullptr);
+      View d = dx(pg, {{dout, &Lout, 0}}, HS[D - 1], B, actP, dsrc_of(actP, hsub[D - 1], hzsub[D - 1]), nullptr, nullptr,
+                  prea ? &pdout : nullptr);
       pl_src = false;
       // (d0 reads the raw head's pre-update weights when it recomputes d1: emitted before that Adam)
       const PreUse pd1 = pld ? pre_layer_dx(Lout, dout, hsub[D - 1]) : PreUse{};
       View dp;
-      if (pld) dp = dx(pg, {{d, &pi.layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &hsub[D - 2], nullptr, nullptr, &pd1);
+      if (pld) dp = dx(pg, {{d, &pi.layers[D - 1], 0}}, HS[D - 2], B, actP, &hsub[D - 2], nullptr, nullptr, &pd1);
       dw(pg, Lout, dout, {hsub[D - 1]}, B, CNT_ADAM_PI, cfg.policy_lr, gl[D].first, gl[D].second);
-      if (!pld) dp = dx(pg, {{d, &pi.layers[D - 1], 0}}, HS[D - 2], B, ACT_RELU, &hsub[D - 2]);
+      if (!pld) dp = dx(pg, {{d, &pi.layers[D - 1], 0}}, HS[D - 2], B, actP, dsrc_of(actP, hsub[D - 2], hzsub[D - 2]));
       dw(pg, pi.layers[D - 1], d, {hsub[D - 2]}, B, CNT_ADAM_PI, cfg.policy_lr, gl[D - 1].first, gl[D - 1].second);
       d = dp;
       for (int i = D - 2; i >= 1; --i) {  // (deeper actors)
-        dp = dx(pg, {{d, &pi.layers[i], 0}}, HS[i - 1], B, ACT_RELU, &hsub[i - 1]);
+        dp = dx(pg, {{d, &pi.layers[i], 0}}, HS[i - 1], B, actP, dsrc_of(actP, hsub[i - 1], hzsub[i - 1]));
         dw(pg, pi.layers[i], d, {hsub[i - 1]}, B, CNT_ADAM_PI, cfg.policy_lr, gl[i].first, gl[i].second);
         d = dp;
       }
@@ -4916,6 +4950,9 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
     for (int i = 0; i < cfg->n_hidden; ++i)
       REQUIRE(cfg->hidden_sizes[i] > 0 && cfg->hidden_sizes[i] <= 512 && cfg->hidden_sizes[i] % 4 == 0,
               "create: hidden_sizes must be multiples of 4, <= 512");
+    for (int a : {cfg->act_actor, cfg->act_critic, cfg->act_encoder})
+      REQUIRE(a >= RLE_ACT_DEFAULT && a <= RLE_ACT_IDENTITY, "create: activation must be an RLE_ACT_* code");
+    REQUIRE(cfg->algo == RLE_TD7 || cfg->act_encoder == RLE_ACT_DEFAULT, "create: act_encoder is TD7's (SALEEncoder)");
     HIPCHK(hipSetDevice(cfg->device));
     auto h = std::make_unique<rle_engine>();
     h->e = std::make_unique<Engine>();
@@ -4936,6 +4973,18 @@ int rle_create(const rle_config* cfg, rle_engine** out) {
     e.Zp = rle::r16(e.Z);
     e.Bv = cfg->batch;
     e.B = (cfg->batch + 15) / 16 * 16;  // (padded rows: zero, masked out of every mean, loss and priority)
+    // hidden activations (sale.py:25,67,97; mlp.py:13): the reference defaults unless the config names one
+    auto act_of = [](int code, int dflt) {
+      return code == RLE_ACT_RELU ? rle::ACT_RELU
+             : code == RLE_ACT_ELU ? rle::ACT_ELU
+             : code == RLE_ACT_IDENTITY ? rle::ACT_NONE
+                                        : dflt;
+    };
+    const bool td7 = e.algo == RLE_TD7;
+    e.actP = act_of(cfg->act_actor, rle::ACT_RELU);
+    e.actC = act_of(cfg->act_critic, td7 ? rle::ACT_ELU : rle::ACT_RELU);
+    e.actE = act_of(cfg->act_encoder, rle::ACT_ELU);
+    e.acts_default = e.actP == rle::ACT_RELU && e.actC == (td7 ? rle::ACT_ELU : rle::ACT_RELU) && e.actE == rle::ACT_ELU;
     e.resolve_plan();
     HIPCHK(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
     if (e.algo == RLE_TD7) {
@@ -5217,15 +5266,15 @@ int rle_act(rle_engine* h, const float* obs, int n, float* out) {
       if (e.algo == RLE_TD7) {  // td7.py:158-162
         rle::Net& fe = e.net("fixed_encoder");
         rle::Net& pi = e.net("policy");
-        rle::View h1 = e.fwd(pg, fe.layers[0], {{in}}, M, rle::ACT_ELU, nullptr, false);
-        rle::View h2 = e.fwd(pg, fe.layers[1], {{h1}}, M, rle::ACT_ELU, nullptr, false);
+        rle::View h1 = e.fwd(pg, fe.layers[0], {{in}}, M, e.actE, nullptr, false);
+        rle::View h2 = e.fwd(pg, fe.layers[1], {{h1}}, M, e.actE, nullptr, false);
         rle::View zs = e.fwd(pg, fe.layers[2], {{h2}}, M, rle::ACT_NONE, nullptr, true);
         rle::View p0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_NONE, nullptr, true);
-        rle::View p1 = e.fwd(pg, pi.layers[1], {{p0}, {zs}}, M, rle::ACT_RELU, nullptr, false);
-        rle::View p2 = e.fwd(pg, pi.layers[2], {{p1}}, M, rle::ACT_RELU, nullptr, false);
+        rle::View p1 = e.fwd(pg, pi.layers[1], {{p0}, {zs}}, M, e.actP, nullptr, false);
+        rle::View p2 = e.fwd(pg, pi.layers[2], {{p1}}, M, e.actP, nullptr, false);
         o = e.fwd(pg, pi.layers[3], {{p2}}, M, rle::ACT_TANH, nullptr, false);
       } else {
-        o = e.mlp_fwd(pg, e.net("policy"), {{in}}, M, rle::ACT_NONE);
+        o = e.mlp_fwd(pg, e.net("policy"), {{in}}, M, rle::ACT_NONE, e.actP);
       }
       rle::Graph G = e.capture(pg);
       it = e.act_graphs.emplace(n, std::make_pair(G, o)).first;
@@ -5300,19 +5349,19 @@ int rle_act_sample(rle_engine* h, const float* obs, int n, int mode, const float
       if (e.algo == RLE_TD7) {  // td7.py:141-162
         rle::Net& fe = e.net("fixed_encoder");
         rle::Net& pi = e.net("policy");
-        rle::View h1 = e.fwd(pg, fe.layers[0], {{in}}, M, rle::ACT_ELU, nullptr, false);
-        rle::View h2 = e.fwd(pg, fe.layers[1], {{h1}}, M, rle::ACT_ELU, nullptr, false);
+        rle::View h1 = e.fwd(pg, fe.layers[0], {{in}}, M, e.actE, nullptr, false);
+        rle::View h2 = e.fwd(pg, fe.layers[1], {{h1}}, M, e.actE, nullptr, false);
         rle::View zs = e.fwd(pg, fe.layers[2], {{h2}}, M, rle::ACT_NONE, nullptr, true);
         rle::View p0 = e.fwd(pg, pi.layers[0], {{in}}, M, rle::ACT_NONE, nullptr, true);
-        rle::View p1 = e.fwd(pg, pi.layers[1], {{p0}, {zs}}, M, rle::ACT_RELU, nullptr, false);
-        rle::View p2 = e.fwd(pg, pi.layers[2], {{p1}}, M, rle::ACT_RELU, nullptr, false);
+        rle::View p1 = e.fwd(pg, pi.layers[1], {{p0}, {zs}}, M, e.actP, nullptr, false);
+        rle::View p2 = e.fwd(pg, pi.layers[2], {{p1}}, M, e.actP, nullptr, false);
         e.fwd(pg, pi.layers[3], {{p2}}, M, rle::ACT_TANH, nullptr, false);
         tanh_act(pg);
       } else if (e.algo == RLE_TD3) {  // td3.py:114-135
-        e.mlp_fwd(pg, e.net("policy"), {{in}}, M, rle::ACT_TANH);
+        e.mlp_fwd(pg, e.net("policy"), {{in}}, M, rle::ACT_TANH, e.actP);
         tanh_act(pg);
       } else {  // sac.py:132-159
-        rle::View raw = e.mlp_fwd(pg, e.net("policy"), {{in}}, M, rle::ACT_NONE);
+        rle::View raw = e.mlp_fwd(pg, e.net("policy"), {{in}}, M, rle::ACT_NONE, e.actP);
         rle::Op op{};
         op.kind = rle::OP_SAC_ACTOR;
         rle::SacActorArgs& sa = op.sac;
@@ -5606,12 +5655,12 @@ int rle_eval(rle_engine* h, int what, const char* net, const char* enc, const fl
           rle::View zs = e.enc_zs(pg, E, eg.in0, M);
           rle::View zsa = e.enc_zsa(pg, E, zs, eg.in1, M);
           rle::View c01 = e.fwd(pg, N.layers[0], {{eg.in0}, {eg.in1}}, M, rle::ACT_NONE, nullptr, true);
-          rle::View c1 = e.fwd(pg, N.layers[1], {{c01}, {zsa}, {zs}}, M, rle::ACT_ELU, nullptr, false);
-          rle::View c2 = e.fwd(pg, N.layers[2], {{c1}}, M, rle::ACT_ELU, nullptr, false);
+          rle::View c1 = e.fwd(pg, N.layers[1], {{c01}, {zsa}, {zs}}, M, e.actC, nullptr, false);
+          rle::View c2 = e.fwd(pg, N.layers[2], {{c1}}, M, e.actC, nullptr, false);
           eg.out = e.fwd(pg, N.layers[3], {{c2}}, M, rle::ACT_NONE, nullptr, false);
         } else {  // MLPCritic.estimate_q_value (mlp.py:98-101)
           REQUIRE(N.kind == "mlp_critic", "eval: Q needs a critic net");
-          eg.out = e.mlp_fwd(pg, N, {{eg.in0}, {eg.in1}}, M, rle::ACT_NONE);
+          eg.out = e.mlp_fwd(pg, N, {{eg.in0}, {eg.in1}}, M, rle::ACT_NONE, e.actC);
         }
         eg.width = 1;
       } else {

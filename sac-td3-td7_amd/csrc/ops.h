@@ -149,7 +149,8 @@ static_assert(gemm_vid(2, 8, 15, 1, 3) < 2048, "GEMM variant ids fit 11 bits");
 // (gemm_vid), gemm_v's path (PK: 0 plain, 1 pre-GEMM, 2 fused loss head, 3 pre-layer, 4 pre-layer behind a
 // pre-GEMM, 5 SAC raw head pre-GEMM) and the kernel sets that hold it (bit 0: TD7, bit 1: TD3 / SAC; the
 // extended instance holds all).  kernels.hip op_gemm dispatches exactly these, and the engine refuses a
-// program with an op whose id is not in its kernel set.
+// program with an op whose id is not in its kernel set.  (sets 0: the extended instance only -- the TD7 policy
+// pass's q-head under a non-default critic activation, rle_config act_critic)
 #define RLE_GEMM_VARIANTS(X)                        \
   X(GEMM_FWD, EPI_STORE, ACT_NONE, 0, 0, 0, 3)      \
   X(GEMM_FWD, EPI_STORE, ACT_NONE, 1, 0, 0, 1)      \
@@ -160,6 +161,8 @@ static_assert(gemm_vid(2, 8, 15, 1, 3) < 2048, "GEMM variant ids fit 11 bits");
   X(GEMM_FWD, EPI_STORE, ACT_TANH, 0, 0, 0, 3)      \
   X(GEMM_FWD, EPI_STORE, ACT_TANH, 1, 0, 0, 1)      \
   X(GEMM_FWD, EPI_QHEAD, ACT_ELU, 0, 0, 0, 1)       \
+  X(GEMM_FWD, EPI_QHEAD, ACT_RELU, 0, 0, 0, 0)      \
+  X(GEMM_FWD, EPI_QHEAD, ACT_NONE, 0, 0, 0, 0)      \
   X(GEMM_FWD, EPI_MSE, ACT_NONE, 0, 0, 0, 1)        \
   X(GEMM_FWD, EPI_MSE, ACT_NONE, 1, 0, 0, 1)        \
   X(GEMM_FWD, EPI_ACT, ACT_TANH, 0, 0, 0, 3)        \

@@ -40,7 +40,12 @@ class Config(ctypes.Structure):
         ("policy_freq", _int), ("target_update_rate", _int), ("min_log_std", ctypes.c_float),
         ("max_log_std", ctypes.c_float), ("tmp", ctypes.c_float), ("seed", ctypes.c_ulonglong),
         ("device", _int), ("zs_dim", _int), ("n_hidden", _int), ("hidden_sizes", _int * 8),
+        ("act_actor", _int), ("act_critic", _int), ("act_encoder", _int),
     ]
+
+
+# rle_config act_* codes (include/rle.h RLE_ACT_*): 0 = the reference default of that net
+ACT_CODES = {"default": 0, "relu": 1, "elu": 2, "identity": 3}
 
 
 class Plan(ctypes.Structure):
@@ -503,13 +508,20 @@ class Engine:
 def make_config(algo, state_dim, action_dim, hidden, batch, use_lap=False, discount=0.99,
                 policy_lr=3e-4, critic_lr=3e-4, tau=0.005, target_policy_noise=0.2,
                 noise_clip=0.5, policy_freq=2, target_update_rate=250, min_log_std=-20.0,
-                max_log_std=2.0, tmp=-1.0, seed=0, device=0, zs_dim=0, hidden_sizes=None) -> Config:
+                max_log_std=2.0, tmp=-1.0, seed=0, device=0, zs_dim=0, hidden_sizes=None,
+                act_actor="default", act_critic="default", act_encoder="default") -> Config:
     """``hidden``: TD7 hdim, TD3 / SAC the width of both hidden layers; ``zs_dim`` (TD7, 0 = hidden) and
-    ``hidden_sizes`` (TD3 / SAC: make_mlp's list, 2..6 layers) give the other net shapes (include/rle.h)."""
+    ``hidden_sizes`` (TD3 / SAC: make_mlp's list, 2..6 layers) give the other net shapes (include/rle.h).
+    ``act_*``: hidden activations, "relu" / "elu" / "identity" (make_mlp action_fn=None) or "default"."""
     hs = list(hidden_sizes) if hidden_sizes is not None else []
     if hs and not 2 <= len(hs) <= 6:
         raise ValueError(f"hidden_sizes {hs}: 2..6 hidden layers")
+    acts = []
+    for a in (act_actor, act_critic, act_encoder):
+        if a not in ACT_CODES:
+            raise ValueError(f"activation {a!r}: one of {sorted(ACT_CODES)}")
+        acts.append(ACT_CODES[a])
     return Config(algo, state_dim, action_dim, hs[-1] if hs else hidden, batch, int(use_lap), discount,
                   policy_lr, critic_lr, tau, target_policy_noise, noise_clip, policy_freq, target_update_rate,
                   min_log_std, max_log_std, tmp, seed, device, zs_dim, len(hs),
-                  (_int * 8)(*(hs + [0] * (8 - len(hs)))))
+                  (_int * 8)(*(hs + [0] * (8 - len(hs)))), *acts)

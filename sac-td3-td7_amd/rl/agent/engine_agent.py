@@ -46,11 +46,12 @@ class EngineAgent(Agent, Sampler):
     def _setup(self, env_id, *, hidden, batch_size, seed, device, make_nn, make_nn_kwargs, cfg):
         custom = None
         shape = {}  # net shapes beyond the defaults: zs_dim (SALE), hidden_sizes (make_mlp)
+        acts = {}  # hidden activations of the make_nn nets (make_config act_*)
         if make_nn is not None:  # td7.py:56-61 / td3.py:53-56 / sac.py:47-50 (rl.nn.modules nets only)
             from rl.nn.modules import nets_from_make_nn
 
             S, A = get_state_action_dims(env_id)
-            hidden, shape, custom = nets_from_make_nn(self.ALG, make_nn, S, A, make_nn_kwargs)
+            hidden, shape, custom, acts = nets_from_make_nn(self.ALG, make_nn, S, A, make_nn_kwargs)
             make_nn_kwargs = {}
         hdim = make_nn_kwargs.pop("hdim", None)
         zs = make_nn_kwargs.pop("zs_dim", None)
@@ -76,6 +77,7 @@ class EngineAgent(Agent, Sampler):
         if shape.get("hidden_sizes") == [int(hidden)] * 2:
             shape = {}  # (the default shape)
         self.shape = shape
+        self.acts = acts
         self.env_id = env_id
         self.state_dim, self.action_dim = get_state_action_dims(env_id)
         self.action_bias, self.action_scale = get_action_bias_scale(env_id)
@@ -101,7 +103,7 @@ class EngineAgent(Agent, Sampler):
     # ---- engine lifecycle ----------------------------------------------------
     def _new_engine(self, batch):
         c = E.make_config(self.ALGO, self.state_dim, self.action_dim, self.hidden, batch, seed=self.seed,
-                          device=self._device, **self._cfg, **self.shape)
+                          device=self._device, **self._cfg, **self.shape, **getattr(self, "acts", {}))
         return E.Engine(c)
 
     @property

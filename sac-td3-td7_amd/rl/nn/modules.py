@@ -31,6 +31,20 @@ class _Linears(nn.Module):
             self.add_module(name, nn.Linear(_dim(fin, env), _dim(fout, env)))
 
 
+# hidden activations the engine runs (rle_config act_*, include/rle.h RLE_ACT_*), by name
+def _act_name(fn) -> str:
+    """A SALE `activ` callable (sale.py:25,67,97) or a make_mlp action_fn module (mlp.py:23) -> "relu" /
+    "elu" / "identity"; NotImplementedError for anything the engine does not run."""
+    if fn in (F.relu, torch.relu) or isinstance(fn, nn.ReLU):
+        return "relu"
+    if fn is F.elu or (isinstance(fn, nn.ELU) and fn.alpha == 1.0):
+        return "elu"
+    if isinstance(fn, nn.Identity):
+        return "identity"
+    raise NotImplementedError(f"activation {getattr(fn, '__name__', fn)!r}: the engine runs ReLU, ELU (alpha 1) "
+                              "and Identity")
+
+
 class SALEEncoder(_Linears):
     """sale.py:16-55: zs = AvgL1Norm(zs3(elu(zs2(elu(zs1(s)))))), zsa = zsa3(elu(zsa2(elu(zsa1([zs, a])))))."""
 
@@ -72,19 +86,25 @@ class SALECritic(_Linears):
         return self.q3(self.activ(self.q2(self.activ(self.q1(h)))))
 
 
-def _mlp(fin: int, fout: int, hidden_sizes) -> nn.Sequential:
-    """make_mlp (mlp.py:10-35): Linear-ReLU-...-Linear (indices 0, 2, 4, ...), xavier_normal weights,
-    zero bias."""
+def _mlp(fin: int, fout: int, hidden_sizes, action_fn="ReLU", init_weight=None, init_bias=None):
+    """make_mlp (mlp.py:10-35): Linear-act-...-Linear (indices 0, 2, 4, ...); weights by nn.init.<init_weight>
+    (default xavier_normal_), biases by nn.init.<init_bias> (default zeros_).  Returns (Sequential, activation
+    name).  action_fn=None is refused: make_mlp then pops the output Linear (mlp.py:34), not an activation."""
+    if action_fn is None:
+        raise NotImplementedError("make_mlp(action_fn=None) drops the output layer (mlp.py:34 pops the last Linear); "
+                                  "use action_fn='Identity' for a net without activations")
+    act = getattr(nn, action_fn)() if isinstance(action_fn, str) else action_fn
+    name = _act_name(act)
+    init_w = nn.init.xavier_normal_ if init_weight is None else getattr(nn.init, init_weight)
+    init_b = nn.init.zeros_ if init_bias is None else getattr(nn.init, init_bias)
     dims = [fin] + list(hidden_sizes) + [fout]
     mods = []
     for i in range(len(dims) - 1):
-        mods += [nn.Linear(dims[i], dims[i + 1]), nn.ReLU()]
-    seq = nn.Sequential(*mods[:-1])
-    for m in seq:
-        if isinstance(m, nn.Linear):
-            nn.init.xavier_normal_(m.weight)
-            nn.init.zeros_(m.bias)
-    return seq
+        lin = nn.Linear(dims[i], dims[i + 1])
+        init_w(lin.weight.data)
+        init_b(lin.bias.data)
+        mods += [lin, act]
+    return nn.Sequential(*mods[:-1]), name
 
 
 def _sizes(hidden_sizes):
@@ -99,10 +119,8 @@ class MLPActor(nn.Module):
 
     def __init__(self, state_dim: int, action_dim: int, hidden_sizes=256, **mlp_kwargs):
         super().__init__()
-        if mlp_kwargs:
-            raise NotImplementedError(f"make_mlp options {sorted(mlp_kwargs)} (the engine builds ReLU MLPs)")
         self.state_dim, self.action_dim, self.hidden_sizes = state_dim, action_dim, _sizes(hidden_sizes)
-        self.mlp = _mlp(state_dim, action_dim, self.hidden_sizes)
+        self.mlp, self.act = _mlp(state_dim, action_dim, self.hidden_sizes, **mlp_kwargs)
 
     def inference_mean(self, state):
         return self.mlp(state)
@@ -116,10 +134,8 @@ class MLPCritic(nn.Module):
 
     def __init__(self, state_dim: int, action_dim: int, hidden_sizes=256, **mlp_kwargs):
         super().__init__()
-        if mlp_kwargs:
-            raise NotImplementedError(f"make_mlp options {sorted(mlp_kwargs)} (the engine builds ReLU MLPs)")
         self.state_dim, self.action_dim, self.hidden_sizes = state_dim, action_dim, _sizes(hidden_sizes)
-        self.mlp = _mlp(state_dim + action_dim, 1, self.hidden_sizes)
+        self.mlp, self.act = _mlp(state_dim + action_dim, 1, self.hidden_sizes, **mlp_kwargs)
 
     def estimate_q_value(self, state, action):
         return self.mlp(torch.cat([state, action], -1))
@@ -127,10 +143,12 @@ class MLPCritic(nn.Module):
 
 def nets_from_make_nn(alg: str, make_nn, state_dim: int, action_dim: int, kwargs: dict):
     """Call a reference-style make_nn hook (state_dim / action_dim passed as keywords, as
-    annotate_make_nn does) and return (hidden width, net shape, {net name: numpy state_dict}) for
+    annotate_make_nn does) and return (hidden width, net shape, {net name: numpy state_dict}, activations) for
     the engine.  Only this module's classes (the reference's default net types) are accepted, with
     one shape across the agent's nets: (hdim, zs_dim) of the SALE nets, hidden_sizes of the MLPs
-    (the shape is {"zs_dim": ...} or {"hidden_sizes": [...]}, as rle_config takes them)."""
+    (the shape is {"zs_dim": ...} or {"hidden_sizes": [...]}, as rle_config takes them).  The
+    activations are make_config's act_actor / act_critic / act_encoder ("relu" / "elu" / "identity"):
+    the SALE nets' `activ`, make_mlp's action_fn; the two critics must agree."""
     import numpy as np
 
     kw = dict(kwargs)
@@ -144,15 +162,16 @@ def nets_from_make_nn(alg: str, make_nn, state_dim: int, action_dim: int, kwargs
         raise TypeError(f"make_nn must return {len(names)} nets {names}")
     widths = set()
     nets = {}
+    acts = {}
     for name, kind, m in zip(names, kinds, out):
         if type(m) is not kind:
             raise NotImplementedError(f"make_nn returned {type(m).__name__} for {name}; the engine builds "
                                       f"rl.nn.{kind.__name__} nets only")
+        role = "act_actor" if name == "policy" else "act_encoder" if name == "encoder" else "act_critic"
+        act = _act_name(m.activ) if isinstance(m, (SALEActor, SALECritic, SALEEncoder)) else m.act
+        if acts.setdefault(role, act) != act:
+            raise NotImplementedError(f"one activation for both critics (got {acts[role]} and {act})")
         if isinstance(m, (SALEActor, SALECritic, SALEEncoder)):
-            want = F.relu if isinstance(m, SALEActor) else F.elu  # (the engine's fixed activations)
-            if m.activ is not want:
-                raise NotImplementedError(f"{name}: activation {getattr(m.activ, '__name__', m.activ)}, the engine "
-                                          f"runs {want.__name__}")
             widths.add((m.hdim, m.zs_dim))
         else:
             widths.add(tuple(m.hidden_sizes))
@@ -164,5 +183,5 @@ def nets_from_make_nn(alg: str, make_nn, state_dim: int, action_dim: int, kwargs
         raise NotImplementedError(f"one net shape across the agent's nets (got {sorted(widths)})")
     w = widths.pop()
     if alg == "td7":
-        return w[0], {"zs_dim": w[1]}, nets
-    return w[-1], {"hidden_sizes": list(w)}, nets
+        return w[0], {"zs_dim": w[1]}, nets, acts
+    return w[-1], {"hidden_sizes": list(w)}, nets, acts

@@ -35,3 +35,11 @@ def shape_of(g):
     if "meta_zs" in g:
         out["zs_dim"] = int(g["meta_zs"])
     return out
+
+
+def acts_of(g):
+    """Hidden activations beyond the defaults a golden was made with (make_golden.py ``acts``):
+    {"actor", "critic", "encoder"} -> "relu" / "elu" / "identity"; {} for the default nets."""
+    if "meta_acts" not in g:
+        return {}
+    return {k: str(v) for k, v in zip(("actor", "critic", "encoder"), g["meta_acts"]) if str(v) != "default"}

@@ -100,27 +100,37 @@ def dump_net(module):
     return {k: v.detach().cpu().numpy().copy() for k, v in module.state_dict().items()}
 
 
-def make_agent(alg, env_id, H, use_lap, extra, shape=None):
+# hidden activations by name (oracle/nets.py ACTS): SALE `activ` callables (sale.py:25,67,97) and make_mlp's
+# action_fn names (mlp.py:13,23 getattr(nn, action_fn)())
+SALE_ACTIV = {"relu": torch.nn.functional.relu, "elu": torch.nn.functional.elu}
+MLP_ACTION_FN = {"relu": "ReLU", "elu": "ELU", "identity": "Identity"}
+
+
+def make_agent(alg, env_id, H, use_lap, extra, shape=None, acts=None):
     """The reference agent with its nets built through its own make_nn hook (td7.py:46-61,
-    td3.py:44-58, sac.py:40-52): SALE nets with zs_dim / hdim, MLPs with make_mlp's hidden_sizes."""
+    td3.py:44-58, sac.py:40-52): SALE nets with zs_dim / hdim and `activ`, MLPs with make_mlp's hidden_sizes
+    and action_fn.  acts: {"actor", "critic", "encoder"} activation names (missing: the defaults)."""
     shape = shape or {}
+    acts = acts or {}
     if alg == "td7":
         Z = shape.get("zs_dim", H)
+        kw_a, kw_c, kw_e = ({"activ": SALE_ACTIV[acts[k]]} if k in acts else {} for k in ("actor", "critic", "encoder"))
 
         def mk(state_dim, action_dim, **kw):
-            return (SALEActor(state_dim, action_dim, Z, H), SALECritic(state_dim, action_dim, Z, H),
-                    SALECritic(state_dim, action_dim, Z, H), SALEEncoder(state_dim, action_dim, Z, H))
+            return (SALEActor(state_dim, action_dim, Z, H, **kw_a), SALECritic(state_dim, action_dim, Z, H, **kw_c),
+                    SALECritic(state_dim, action_dim, Z, H, **kw_c), SALEEncoder(state_dim, action_dim, Z, H, **kw_e))
         return TD7(env_id, use_lap=use_lap, make_nn=mk, **extra)
     hs = shape.get("hidden_sizes", H)
+    kw_a, kw_c = ({"action_fn": MLP_ACTION_FN[acts[k]]} if k in acts else {} for k in ("actor", "critic"))
     if alg == "td3":
         def mk(state_dim, action_dim, **kw):
-            return (MLPActor(state_dim, action_dim, hs), MLPCritic(state_dim, action_dim, hs),
-                    MLPCritic(state_dim, action_dim, hs))
+            return (MLPActor(state_dim, action_dim, hs, **kw_a), MLPCritic(state_dim, action_dim, hs, **kw_c),
+                    MLPCritic(state_dim, action_dim, hs, **kw_c))
         return TD3(env_id, use_lap=use_lap, make_nn=mk, **extra)
     if alg == "sac":
         def mk(state_dim, action_dim, **kw):
-            return (MLPActor(state_dim, 2 * action_dim, hs), MLPCritic(state_dim, action_dim, hs),
-                    MLPCritic(state_dim, action_dim, hs))
+            return (MLPActor(state_dim, 2 * action_dim, hs, **kw_a), MLPCritic(state_dim, action_dim, hs, **kw_c),
+                    MLPCritic(state_dim, action_dim, hs, **kw_c))
         return SAC(env_id, make_nn=mk, **extra)
     raise ValueError(alg)
 
@@ -204,14 +214,14 @@ ONLY = set(sys.argv[1:])  # optional fixture names to (re)generate; default: all
 
 
 def run_config(name, alg, env_id, H, B, N, n_fill, n_steps, use_lap, seed, extra=None,
-               full=True, sparse_prio=False, adam_steps=2, shape=None):
+               full=True, sparse_prio=False, adam_steps=2, shape=None, acts=None):
     if ONLY and name not in ONLY:
         return
     extra = dict(extra or {})
     shape = dict(shape or {})
     S, A, hi = spec.TASKS[env_id]
     nets = spec.agent_params(alg, S, A, H, seed, **shape)
-    agent = make_agent(alg, env_id, H, use_lap, extra, shape)
+    agent = make_agent(alg, env_id, H, use_lap, extra, shape, acts)
     inject(agent, alg, nets)
     lap = use_lap
     replay = (LAPReplayMemory if lap else SimpleReplayMemory)(N, env_id)
@@ -234,6 +244,8 @@ def run_config(name, alg, env_id, H, B, N, n_fill, n_steps, use_lap, seed, extra
         res["meta_hidden"] = np.array(shape["hidden_sizes"], dtype=np.int64)
     if "zs_dim" in shape:
         res["meta_zs"] = np.array(shape["zs_dim"], dtype=np.int64)
+    if acts:  # (hidden activations beyond the defaults: tests/conftest.py acts_of)
+        res["meta_acts"] = np.array([acts.get(k, "default") for k in ("actor", "critic", "encoder")])
     for k, v in tp.items():
         res["tape_" + k] = v
 
@@ -386,6 +398,14 @@ def main():
     run_config("td7_tiny_b100", "td7", "Tiny-v0", 32, 100, 256, 200, 8, True, 17, extra={"target_update_rate": 4})
     run_config("td3_tiny_b100", "td3", "Tiny-v0", 32, 100, 256, 200, 6, False, 18)
     run_config("sac_tiny_b100", "sac", "Tiny-v0", 32, 100, 256, 200, 6, False, 19)
+    # Hidden activations beyond the defaults, through make_nn: SALE nets' `activ` (sale.py:25,67,97) swapped
+    # (actor ELU, critics and encoder ReLU), make_mlp's action_fn (mlp.py:13,23) as ELU / Identity
+    run_config("td7_tiny_act", "td7", "Tiny-v0", 32, 16, 64, 50, 8, True, 20, extra={"target_update_rate": 4},
+               acts={"actor": "elu", "critic": "relu", "encoder": "relu"})
+    run_config("td3_tiny_act", "td3", "Tiny-v0", 32, 16, 64, 50, 6, True, 21,
+               acts={"actor": "elu", "critic": "identity"})
+    run_config("sac_tiny_act", "sac", "Tiny-v0", 32, 16, 64, 50, 6, False, 22,
+               acts={"actor": "identity", "critic": "elu"}, shape={"hidden_sizes": [32, 48, 32]})
     # Full-size digests at the BASELINE configs' shapes.
     run_config("td7_humanoid", "td7", "Humanoid-v4", 256, 256, 2048, 2048, 3, True, 41,
                full=False)

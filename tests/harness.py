@@ -4,7 +4,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from conftest import shape_of  # noqa: F401  (re-exported for the tests)
+from conftest import acts_of, shape_of  # noqa: F401  (re-exported for the tests)
 from oracle import spec
 from rl import _engine as E
 
@@ -40,7 +40,8 @@ def engine_from_golden(g, device=0, plan=None):
     if "tmp" in extra:  # SAC fixed temperature (sac.py:55-60)
         kw["tmp"] = float(extra["tmp"])
     shape = shape_of(g)
-    cfg = E.make_config(ALGO[alg], S, A, H, B, use_lap=use_lap, seed=seed, device=device, **kw, **shape)
+    acts = {f"act_{k}": v for k, v in acts_of(g).items()}  # (hidden activations beyond the defaults)
+    cfg = E.make_config(ALGO[alg], S, A, H, B, use_lap=use_lap, seed=seed, device=device, **kw, **shape, **acts)
     eng = E.Engine(cfg, plan)
     for net, params in spec.agent_params(alg, S, A, H, seed, **shape).items():
         for name, v in params.items():

@@ -78,3 +78,32 @@ def test_aql_failed_queue_fails_fast_and_doorbells_stay_in_one_ring_pass():
 
     lib = _engine.lib()
     assert lib.rle_aql_selftest() == 0, lib.rle_last_error()
+
+
+def test_ctypes_structs_match_the_header_layout(tmp_path):
+    """rl/_engine.py Config / Plan mirror rle_config / rle_plan field by field: a C program compiled against
+    include/rle.h prints each struct's size and every field's offset (gcc on the host, no GPU)."""
+    import ctypes
+    import shutil
+    import subprocess
+
+    from rl import _engine
+
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    lines = []
+    for cname, cls in (("rle_config", _engine.Config), ("rle_plan", _engine.Plan)):
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, *_ in cls._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "rle.h"\nint main(void) {\n'
+                   + "\n".join(lines) + "\nreturn 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(ln.split() for ln in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                    text=True).stdout.splitlines())
+    for cname, cls in (("rle_config", _engine.Config), ("rle_plan", _engine.Plan)):
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f, *_ in cls._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)

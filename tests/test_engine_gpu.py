@@ -108,13 +108,15 @@ def _fwd_check(name):
 
 
 @pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny", "sac_tiny", "td7_humanoid", "sac_humanoid",
-                                  "td3_halfcheetah", "td3_tiny_deep", "sac_tiny_deep", "td7_tiny_zs"])
+                                  "td3_halfcheetah", "td3_tiny_deep", "sac_tiny_deep", "td7_tiny_zs", "td7_tiny_act",
+                                  "td3_tiny_act", "sac_tiny_act"])
 def test_forward_matches_reference(name):
     _fwd_check(name)
 
 
 TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed", "td3_tiny_deep",
-        "sac_tiny_deep", "td7_tiny_b100", "td3_tiny_b100", "sac_tiny_b100"]  # (b100: a batch of 100, padded to 112)
+        "sac_tiny_deep", "td7_tiny_b100", "td3_tiny_b100", "sac_tiny_b100",  # (b100: a batch of 100, padded to 112)
+        "td7_tiny_act", "td3_tiny_act", "sac_tiny_act"]  # (act: hidden activations beyond the defaults)
 FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k", "td7_tiny_zs"]
 
 

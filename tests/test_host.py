@@ -78,6 +78,66 @@ def test_train_ops_rejects_malformed_batches_and_foreign_replays():
         td7.train_ops(batch, rep_b)
 
 
+def test_make_nn_activation_and_init_options():
+    """make_mlp's action_fn / init_weight / init_bias (mlp.py:10-35) and the SALE nets' `activ` (sale.py:25,67,97)
+    reach the engine as rle_config act_* names (nets_from_make_nn, no engine needed): ReLU, ELU (alpha 1) and
+    Identity, as strings or modules; the init functions are nn.init's, applied in make_mlp's order.  Refused:
+    action_fn=None (make_mlp then pops the output Linear, mlp.py:34), other activations, critics that disagree."""
+    import torch
+    from torch.nn import functional as F
+
+    from rl.nn import MLPActor, MLPCritic, SALEActor, SALECritic, SALEEncoder
+    from rl.nn.modules import nets_from_make_nn
+
+    torch.manual_seed(0)
+    m = MLPActor(5, 2, [8, 8], action_fn="ELU", init_weight="orthogonal_", init_bias="normal_")
+    torch.manual_seed(0)  # make_mlp's own order: Linear(), init_weight(w), init_bias(b), layer by layer
+    ref = []
+    for fin, fout in ((5, 8), (8, 8), (8, 2)):
+        lin = torch.nn.Linear(fin, fout)
+        torch.nn.init.orthogonal_(lin.weight.data)
+        torch.nn.init.normal_(lin.bias.data)
+        ref.append(lin)
+    for i, lin in enumerate(ref):
+        np.testing.assert_array_equal(m.mlp[2 * i].weight.detach().numpy(), lin.weight.detach().numpy())
+        np.testing.assert_array_equal(m.mlp[2 * i].bias.detach().numpy(), lin.bias.detach().numpy())
+    assert m.act == "elu" and isinstance(m.mlp[1], torch.nn.ELU)
+    assert MLPCritic(5, 2, 8, action_fn=torch.nn.Identity()).act == "identity"
+    assert MLPCritic(5, 2, 8).act == "relu"
+    with pytest.raises(NotImplementedError, match="output layer"):
+        MLPActor(5, 2, 8, action_fn=None)
+    with pytest.raises(NotImplementedError, match="ReLU, ELU"):
+        MLPActor(5, 2, 8, action_fn="Tanh")
+    with pytest.raises(NotImplementedError, match="ReLU, ELU"):
+        MLPActor(5, 2, 8, action_fn=torch.nn.ELU(alpha=0.5))
+
+    def mk3(state_dim, action_dim, **kw):
+        return (MLPActor(state_dim, action_dim, 16, action_fn="ELU"), MLPCritic(state_dim, action_dim, 16),
+                MLPCritic(state_dim, action_dim, 16))
+
+    assert nets_from_make_nn("td3", mk3, 3, 2, {})[3] == {"act_actor": "elu", "act_critic": "relu"}
+
+    def mk7(state_dim, action_dim, **kw):
+        return (SALEActor(state_dim, action_dim, 16, 16, activ=F.elu), SALECritic(state_dim, action_dim, 16, 16, activ=F.relu),
+                SALECritic(state_dim, action_dim, 16, 16, activ=torch.relu), SALEEncoder(state_dim, action_dim, 16, 16))
+
+    assert nets_from_make_nn("td7", mk7, 3, 2, {})[3] == {"act_actor": "elu", "act_critic": "relu", "act_encoder": "elu"}
+
+    def mixed(state_dim, action_dim, **kw):
+        return (MLPActor(state_dim, action_dim, 16), MLPCritic(state_dim, action_dim, 16, action_fn="ELU"),
+                MLPCritic(state_dim, action_dim, 16))
+
+    with pytest.raises(NotImplementedError, match="both critics"):
+        nets_from_make_nn("td3", mixed, 3, 2, {})
+
+    def tanh7(state_dim, action_dim, **kw):
+        return (SALEActor(state_dim, action_dim, 16, 16, activ=torch.tanh), SALECritic(state_dim, action_dim, 16, 16),
+                SALECritic(state_dim, action_dim, 16, 16), SALEEncoder(state_dim, action_dim, 16, 16))
+
+    with pytest.raises(NotImplementedError, match="ReLU, ELU"):
+        nets_from_make_nn("td7", tanh7, 3, 2, {})
+
+
 def test_engine_agents_reject_non_default_net_types():
     """make_nn hooks must return the reference's default net types (rl.nn.*), one net shape across the
     agent's nets and make_mlp depths of 2..6 (rle.h RLE_MAX_HIDDEN), checked before any engine exists;

@@ -17,6 +17,7 @@ import torch
 from oracle import agents as OA
 from oracle import replay as OR
 from harness import LOSS_RTOL  # noqa: E402
+from rl import _engine as E
 from rl.agent import SAC, TD3, TD7
 from rl.replay_memory import LAPReplayMemory, SimpleReplayMemory
 from rl.runner.run import run_train_ops
@@ -54,7 +55,8 @@ def _close(a, b, tol):
 
 
 @pytest.mark.parametrize("alg,lap,B", [("td7", True, 32), ("td7", False, 32), ("td3", False, 32), ("td3", True, 32),
-                                       ("td7", True, 20), ("td3", False, 20)])  # (B = 20: padded to 32 inside)
+                                       ("td7", True, 20), ("td3", False, 20), ("td7", True, 1), ("td3", True, 17)])
+# (B = 20 / 1 / 17: padded to 32 / 16 / 32 rows inside; the padded rows count in nothing)
 def test_train_ops_on_sampled_batches_matches_oracle(alg, lap, B):
     cap, H, steps = 512, 32, 6
     trans = _transitions(300, 1)
@@ -416,6 +418,74 @@ def test_make_nn_hook_with_other_net_shapes():
             for k in sd[name]:
                 np.testing.assert_array_equal(sd[name][k], sd2[name][k])
         assert ag2.shape == ag.shape and ag.shape
+
+
+def test_make_nn_hook_with_other_activations():
+    """make_nn hooks whose nets use other hidden activations (sale.py:25,67,97 `activ`; mlp.py:13,23 action_fn,
+    with make_mlp's init_weight / init_bias): the engine runs them (rle_config act_*), acts as the hook's torch
+    modules do, trains, and pickles back with the same activations (the trajectories themselves: the
+    td7_tiny_act / td3_tiny_act / sac_tiny_act goldens)."""
+    from torch.nn import functional as F
+
+    from rl.nn import MLPActor, MLPCritic, SALEActor, SALECritic, SALEEncoder
+
+    torch.manual_seed(5)
+    made = {}
+
+    def mk3(state_dim, action_dim, **kw):
+        made["td3"] = (MLPActor(state_dim, action_dim, 32, action_fn="ELU", init_weight="orthogonal_"),
+                       MLPCritic(state_dim, action_dim, 32, action_fn="Identity", init_bias="normal_"),
+                       MLPCritic(state_dim, action_dim, 32, action_fn="Identity", init_bias="normal_"))
+        return made["td3"]
+
+    def mks(state_dim, action_dim, **kw):
+        made["sac"] = (MLPActor(state_dim, 2 * action_dim, [48, 32], action_fn=torch.nn.Identity()),
+                       MLPCritic(state_dim, action_dim, [48, 32], action_fn=torch.nn.ELU()),
+                       MLPCritic(state_dim, action_dim, [48, 32], action_fn=torch.nn.ELU()))
+        return made["sac"]
+
+    def mk7(state_dim, action_dim, **kw):
+        made["td7"] = (SALEActor(state_dim, action_dim, 32, 32, activ=F.elu),
+                       SALECritic(state_dim, action_dim, 32, 32, activ=F.relu),
+                       SALECritic(state_dim, action_dim, 32, 32, activ=F.relu),
+                       SALEEncoder(state_dim, action_dim, 32, 32, activ=F.relu))
+        return made["td7"]
+
+    want = {"td3": {"act_actor": "elu", "act_critic": "identity"}, "sac": {"act_actor": "identity", "act_critic": "elu"},
+            "td7": {"act_actor": "elu", "act_critic": "relu", "act_encoder": "relu"}}
+    obs = np.linspace(-1, 1, S).astype(np.float32)
+    x = torch.from_numpy(obs)[None]
+    trans = _transitions(200, 6)
+    for cls, mk, alg in ((TD3, mk3, "td3"), (SAC, mks, "sac"), (TD7, mk7, "td7")):
+        ag = cls("Tiny-v0", make_nn=mk, batch_size=16, seed=4)
+        assert {k: v for k, v in ag.acts.items() if k in want[alg]} == want[alg], ag.acts
+        codes = {k: getattr(ag.engine.cfg, k) for k in want[alg]}
+        assert codes == {k: E.ACT_CODES[v] for k, v in want[alg].items()}
+        sd = ag.state_dict()
+        for name, m in zip(("policy", "q1", "q2", "encoder"), made[alg]):
+            for k, v in m.state_dict().items():
+                np.testing.assert_array_equal(sd[name][k], v.numpy())
+        with torch.no_grad():
+            if alg == "td7":
+                pol, enc = made["td7"][0], made["td7"][3]
+                ref = pol.inference_mean(x, enc.encode_state(x)).numpy()[0]
+            elif alg == "td3":
+                ref = torch.tanh(made["td3"][0].inference_mean(x)).numpy()[0]
+            else:
+                ref = torch.tanh(made["sac"][0].inference_mean_logvar(x)[0]).numpy()[0]
+        ref = ref * ag.action_scale + ag.action_bias
+        got = ag.sample(obs, deterministic=True)
+        assert np.abs(got - ref).max() <= 2e-6 + 1e-5 * np.abs(ref).max(), alg
+        rep = (LAPReplayMemory if alg == "td7" else SimpleReplayMemory)(256, "Tiny-v0")
+        _fill(rep, trans)
+        run_train_ops(rep, ag, 16, 5)
+        ag2 = pickle.loads(pickle.dumps(ag))
+        assert ag2.acts == ag.acts
+        assert {k: getattr(ag2.engine.cfg, k) for k in want[alg]} == codes
+        sd, sd2 = ag.state_dict(), ag2.state_dict()
+        for name in sd:
+            for k in sd[name]:
+                np.testing.assert_array_equal(sd[name][k], sd2[name][k])
 
 
 def test_train_ops_on_a_host_batch_dict():

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden, shape_of
+from conftest import acts_of, load_golden, shape_of
 from oracle import agents, replay, spec
 from oracle import nets as N
 
@@ -59,7 +59,7 @@ def build_from_golden(g):
     extra = dict(zip([str(k) for k in g["meta_extra_keys"]], g["meta_extra_vals"].tolist()))
     extra = {k: (int(v) if k in ("target_update_rate", "policy_freq") else v) for k, v in extra.items()}
     nets = spec.agent_params(alg, S, A, H, seed, **shape_of(g))
-    orc = agents.make_oracle(alg, nets, A, bool(use_lap), **extra)
+    orc = agents.make_oracle(alg, nets, A, bool(use_lap), acts=acts_of(g), **extra)
     scale = np.full(A, hi, np.float32)
     bias = np.zeros(A, np.float32)
     rep = replay.Replay(Ncap, S, A, (scale - (-scale)) / 2.0, bias, bool(use_lap))
@@ -77,7 +77,8 @@ def build_from_golden(g):
 
 
 TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed", "td3_tiny_deep",
-        "sac_tiny_deep", "td7_tiny_b100", "td3_tiny_b100", "sac_tiny_b100"]  # (b100: a batch of 100, padded to 112)
+        "sac_tiny_deep", "td7_tiny_b100", "td3_tiny_b100", "sac_tiny_b100",  # (b100: a batch of 100, padded to 112)
+        "td7_tiny_act", "td3_tiny_act", "sac_tiny_act"]  # (act: hidden activations beyond the defaults)
 FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k", "td7_tiny_zs"]
 
 
