@@ -139,7 +139,7 @@ def test_td7_head_variants_match_reference(name, variant):
 
 
 @pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah",
-                                  "sac_humanoid"])
+                                  "sac_humanoid", "td7_tiny_act", "td3_tiny_act", "sac_tiny_act"])
 def test_level_hazards(name, monkeypatch):
     """RLE_HAZARD=1: no byte that one op of a level stores is read or stored by another op of the
     same level (engine.cpp level_hazards: each op's accesses replayed from its descriptor) in any
@@ -151,7 +151,8 @@ def test_level_hazards(name, monkeypatch):
     run_with_tapes(eng, tp, 1, lambda t: None)
 
 
-@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah", "sac_humanoid"])
+@pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah", "sac_humanoid",
+                                  "td7_tiny_act", "td3_tiny_act", "sac_tiny_act"])
 def test_gemm_address_audit(name, monkeypatch):
     """RLE_AUDIT=1: every byte range each GEMM op's workgroups can load or store (the kernel's
     address arithmetic replayed on the host, engine.cpp audit_gemm) lies inside one live device
