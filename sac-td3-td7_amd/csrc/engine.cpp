@@ -2246,11 +2246,13 @@ struct Engine {
   // 23.37k / 23.79k / 23.91k, TD7 Humanoid 8069 / 8094 / 8060 steps/s)
   int pre_tn() const { return plan.pre_tn; }
   int pl_tn() const { return plan.pl_tn; }
-  // (fusions whose in-tile recomputation or fused head is written for the default activations)
-  static constexpr unsigned kActFusions = RLE_FUSE_PRELAYER | RLE_FUSE_PRE | RLE_FUSE_QDOT | RLE_FUSE_HEADDX |
-                                          RLE_FUSE_TWOSTAGE | RLE_FUSE_SACPRE;
+  // (fusions whose in-tile recomputations are compiled for the default activations only; the q-dot partials and the
+  // loss head fused into the DX also for ReLU / ELU critics -- the extended instance holds both -- not for identity)
+  static constexpr unsigned kActFusions = RLE_FUSE_PRELAYER | RLE_FUSE_PRE | RLE_FUSE_TWOSTAGE | RLE_FUSE_SACPRE;
+  static constexpr unsigned kCriticActFusions = RLE_FUSE_QDOT | RLE_FUSE_HEADDX;
   bool fused(unsigned bit) const {
     if (!acts_default && (bit & kActFusions)) return false;
+    if (!acts_default && actC == ACT_NONE && (bit & kCriticActFusions)) return false;
     return (bit & RLE_FUSE_OPT_IN) ? (plan.fuse_on & bit) != 0 : !(plan.fuse_off & bit);
   }
   bool prelayer_shape(const Layer& L0, const Layer& L1) const {
@@ -3796,8 +3798,9 @@ struct Engine {
         for (int n = 0; n < 2; ++n) {
           HeadUse hu{h, n, rd, {dz1[n].id, dq[n].id}};
           if (n == 0) hu.wr.insert(hu.wr.end(), {prio.id, qloss_id});
-          d0f[n] = dx(pg, {{c1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, actC, dsrc_of(actC, c[n][D - 2], cz[n][D - 2]),
-                      nullptr, nullptr, nullptr, &hu);
+          // (the head forms dZ = dq w act'(segment 0): an ELU critic's pre-activations, a ReLU critic's outputs)
+          d0f[n] = dx(pg, {{cze ? cz[n][D - 1] : c1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, actC,
+                      dsrc_of(actC, c[n][D - 2], cz[n][D - 2]), nullptr, nullptr, nullptr, &hu);
         }
       }
     }
@@ -3848,7 +3851,7 @@ struct Engine {
         for (int n = 0; n < 2; ++n) {
           HeadUse hu{h, n, rd, {}};
           if (n == 0) hu.wr.push_back(ploss_id);
-          dzp0[n] = dx(pg, {{p1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, actC,
+          dzp0[n] = dx(pg, {{cze ? pcz[n][D - 1] : p1[n], &q[n]->layers[D - 1], 0}}, HS[D - 2], B, actC,
                        dsrc_of(actC, pc[n][D - 2], pcz[n][D - 2]), nullptr, nullptr, nullptr, &hu);
         }
         out_t = true;
