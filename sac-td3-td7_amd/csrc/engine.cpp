@@ -2536,6 +2536,7 @@ struct Engine {
   View dx(Prog& pg, const std::vector<DxTerm>& terms, int ncols, int M, int dact, const View* saved,
           const View* into = nullptr, const View* nb_x = nullptr, const PreUse* pre = nullptr,
           const HeadUse* head = nullptr, const SacBwdUse* sbu = nullptr) {
+    if (dact == ACT_NONE && !pre && !head) saved = nullptr;  // (an identity layer's backward reads no derivative)
     Op op{};
     op.kind = OP_GEMM;
     GemmArgs& g = op.gemm;

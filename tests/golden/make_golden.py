@@ -102,7 +102,7 @@ def dump_net(module):
 
 # hidden activations by name (oracle/nets.py ACTS): SALE `activ` callables (sale.py:25,67,97) and make_mlp's
 # action_fn names (mlp.py:13,23 getattr(nn, action_fn)())
-SALE_ACTIV = {"relu": torch.nn.functional.relu, "elu": torch.nn.functional.elu}
+SALE_ACTIV = {"relu": torch.nn.functional.relu, "elu": torch.nn.functional.elu, "identity": torch.nn.Identity()}
 MLP_ACTION_FN = {"relu": "ReLU", "elu": "ELU", "identity": "Identity"}
 
 
@@ -402,6 +402,8 @@ def main():
     # (actor ELU, critics and encoder ReLU), make_mlp's action_fn (mlp.py:13,23) as ELU / Identity
     run_config("td7_tiny_act", "td7", "Tiny-v0", 32, 16, 64, 50, 8, True, 20, extra={"target_update_rate": 4},
                acts={"actor": "elu", "critic": "relu", "encoder": "relu"})
+    run_config("td7_tiny_act_id", "td7", "Tiny-v0", 32, 16, 64, 50, 6, False, 23, extra={"target_update_rate": 3},
+               acts={"critic": "identity"})
     run_config("td3_tiny_act", "td3", "Tiny-v0", 32, 16, 64, 50, 6, True, 21,
                acts={"actor": "elu", "critic": "identity"})
     run_config("sac_tiny_act", "sac", "Tiny-v0", 32, 16, 64, 50, 6, False, 22,

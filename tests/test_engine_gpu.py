@@ -109,14 +109,14 @@ def _fwd_check(name):
 
 @pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny", "sac_tiny", "td7_humanoid", "sac_humanoid",
                                   "td3_halfcheetah", "td3_tiny_deep", "sac_tiny_deep", "td7_tiny_zs", "td7_tiny_act",
-                                  "td3_tiny_act", "sac_tiny_act"])
+                                  "td7_tiny_act_id", "td3_tiny_act", "sac_tiny_act"])
 def test_forward_matches_reference(name):
     _fwd_check(name)
 
 
 TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed", "td3_tiny_deep",
         "sac_tiny_deep", "td7_tiny_b100", "td3_tiny_b100", "sac_tiny_b100",  # (b100: a batch of 100, padded to 112)
-        "td7_tiny_act", "td3_tiny_act", "sac_tiny_act"]  # (act: hidden activations beyond the defaults)
+        "td7_tiny_act", "td7_tiny_act_id", "td3_tiny_act", "sac_tiny_act"]  # (act: hidden activations beyond the defaults)
 FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k", "td7_tiny_zs"]
 
 
@@ -139,7 +139,7 @@ def test_td7_head_variants_match_reference(name, variant):
 
 
 @pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah",
-                                  "sac_humanoid", "td7_tiny_act", "td3_tiny_act", "sac_tiny_act"])
+                                  "sac_humanoid", "td7_tiny_act", "td7_tiny_act_id", "td3_tiny_act", "sac_tiny_act"])
 def test_level_hazards(name, monkeypatch):
     """RLE_HAZARD=1: no byte that one op of a level stores is read or stored by another op of the
     same level (engine.cpp level_hazards: each op's accesses replayed from its descriptor) in any
@@ -152,7 +152,7 @@ def test_level_hazards(name, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["td7_tiny", "td3_tiny_lap", "sac_tiny", "td7_humanoid", "td3_halfcheetah", "sac_humanoid",
-                                  "td7_tiny_act", "td3_tiny_act", "sac_tiny_act"])
+                                  "td7_tiny_act", "td7_tiny_act_id", "td3_tiny_act", "sac_tiny_act"])
 def test_gemm_address_audit(name, monkeypatch):
     """RLE_AUDIT=1: every byte range each GEMM op's workgroups can load or store (the kernel's
     address arithmetic replayed on the host, engine.cpp audit_gemm) lies inside one live device
