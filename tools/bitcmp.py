@@ -17,14 +17,16 @@ sys.path[:0] = [REPO, os.path.join(REPO, "sac-td3-td7_amd"), os.path.join(REPO, 
 
 def dump(name, steps, out):
     from conftest import load_golden
-    from harness import engine_from_golden, parse
+    from harness import engine_from_golden, parse, shape_of
     from oracle import spec
 
     g = load_golden(name)
     alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
+    steps = min(steps, n_steps)  # (the golden's tapes cover n_steps)
     S, A, hi = spec.TASKS[env]
     eng, rep, tp = engine_from_golden(g)
-    shapes = {net: {k: np.shape(v) for k, v in p.items()} for net, p in spec.agent_params(alg, S, A, H, seed).items()}
+    shapes = {net: {k: np.shape(v) for k, v in p.items()}
+              for net, p in spec.agent_params(alg, S, A, H, seed, **shape_of(g)).items()}
     names = {net: list(p.keys()) for net, p in shapes.items()}
     keep = os.environ.get("BITCMP_NETS")  # comma-separated nets to dump (default: all)
     if keep:
