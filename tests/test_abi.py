@@ -107,3 +107,23 @@ def test_ctypes_structs_match_the_header_layout(tmp_path):
         assert int(got[cname]) == ctypes.sizeof(cls), cname
         for f, *_ in cls._fields_:
             assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
+
+
+def test_create_rejects_bad_activation_codes_before_any_hip_call():
+    """rle_create validates rle_config.act_* (RLE_ACT_DEFAULT..RLE_ACT_IDENTITY; act_encoder is TD7's) before it
+    touches a device, so the errors come back through the ABI on a host without a GPU."""
+    import ctypes
+
+    from rl import _engine as E
+
+    lib = E.lib()
+    out = ctypes.c_void_p()
+    cfg = E.make_config(E.RLE_TD7, 17, 6, 32, 16)
+    cfg.act_actor = 7
+    assert lib.rle_create(ctypes.byref(cfg), ctypes.byref(out)) == -1
+    assert b"activation" in lib.rle_last_error()
+    cfg = E.make_config(E.RLE_TD3, 17, 6, 32, 16, act_encoder="elu")
+    assert lib.rle_create(ctypes.byref(cfg), ctypes.byref(out)) == -1
+    assert b"act_encoder" in lib.rle_last_error()
+    with pytest.raises(ValueError, match="activation"):
+        E.make_config(E.RLE_SAC, 17, 6, 32, 16, act_critic="tanh")
