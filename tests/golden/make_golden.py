@@ -400,6 +400,17 @@ def main():
     run_config("sac_tiny_b100", "sac", "Tiny-v0", 32, 100, 256, 200, 6, False, 19)
     # Hidden activations beyond the defaults, through make_nn: SALE nets' `activ` (sale.py:25,67,97) swapped
     # (actor ELU, critics and encoder ReLU), make_mlp's action_fn (mlp.py:13,23) as ELU / Identity
+    # Hyper-parameters beyond the defaults (the agents' constructor arguments, td7.py:34-43, td3.py:33-43,
+    # sac.py:27-37): policy_freq 3 (single-step graphs), discount, learning rates, smoothing noise, tau, log-std bounds
+    run_config("td7_tiny_hp", "td7", "Tiny-v0", 32, 16, 64, 50, 9, True, 24,
+               extra={"target_update_rate": 4, "policy_freq": 3, "discount_factor": 0.95, "policy_lr": 1e-3,
+                      "critic_lr": 5e-4, "target_policy_noise": 0.3, "noise_clip": 0.4})
+    run_config("td3_tiny_hp", "td3", "Tiny-v0", 32, 16, 64, 50, 7, False, 25,
+               extra={"policy_freq": 3, "discount_factor": 0.9, "policy_lr": 1e-3, "critic_lr": 5e-4,
+                      "target_policy_noise": 0.1, "noise_clip": 0.25, "tau": 0.02})
+    run_config("sac_tiny_hp", "sac", "Tiny-v0", 32, 16, 64, 50, 6, False, 26,
+               extra={"discount_factor": 0.9, "policy_lr": 1e-3, "critic_lr": 5e-4, "tau": 0.02, "min_log_std": -5.0,
+                      "max_log_std": 1.0})
     run_config("td7_tiny_act", "td7", "Tiny-v0", 32, 16, 64, 50, 8, True, 20, extra={"target_update_rate": 4},
                acts={"actor": "elu", "critic": "relu", "encoder": "relu"})
     run_config("td7_tiny_act_id", "td7", "Tiny-v0", 32, 16, 64, 50, 6, False, 23, extra={"target_update_rate": 3},

@@ -35,10 +35,17 @@ def engine_from_golden(g, device=0, plan=None):
     alg, env, H, B, Ncap, n_fill, n_steps, use_lap, seed, extra = parse(g)
     S, A, hi = spec.TASKS[env]
     kw = {}
-    if "target_update_rate" in extra:
-        kw["target_update_rate"] = int(extra["target_update_rate"])
-    if "tmp" in extra:  # SAC fixed temperature (sac.py:55-60)
-        kw["tmp"] = float(extra["tmp"])
+    # the reference's constructor arguments (td7.py:34-43, td3.py:33-43, sac.py:27-37) -> rle_config fields
+    for k, v in extra.items():
+        if k in ("target_update_rate", "policy_freq"):
+            kw[k] = int(v)
+        elif k == "discount_factor":
+            kw["discount"] = float(v)
+        elif k in ("tmp", "policy_lr", "critic_lr", "tau", "target_policy_noise", "noise_clip", "min_log_std",
+                   "max_log_std"):  # (tmp: SAC fixed temperature, sac.py:55-60)
+            kw[k] = float(v)
+        else:
+            raise KeyError(f"golden hyper-parameter {k} has no rle_config field")
     shape = shape_of(g)
     acts = {f"act_{k}": v for k, v in acts_of(g).items()}  # (hidden activations beyond the defaults)
     cfg = E.make_config(ALGO[alg], S, A, H, B, use_lap=use_lap, seed=seed, device=device, **kw, **shape, **acts)

@@ -116,7 +116,8 @@ def test_forward_matches_reference(name):
 
 TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed", "td3_tiny_deep",
         "sac_tiny_deep", "td7_tiny_b100", "td3_tiny_b100", "sac_tiny_b100",  # (b100: a batch of 100, padded to 112)
-        "td7_tiny_act", "td7_tiny_act_id", "td3_tiny_act", "sac_tiny_act"]  # (act: hidden activations beyond the defaults)
+        "td7_tiny_act", "td7_tiny_act_id", "td3_tiny_act", "sac_tiny_act",  # (act: hidden activations beyond the defaults)
+        "td7_tiny_hp", "td3_tiny_hp", "sac_tiny_hp"]  # (hp: constructor hyper-parameters beyond the defaults)
 FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k", "td7_tiny_zs"]
 
 

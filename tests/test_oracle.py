@@ -57,7 +57,8 @@ def build_from_golden(g):
     H, B, Ncap, n_fill, n_steps, use_lap, seed = (int(x) for x in g["meta"])
     S, A, hi = spec.TASKS[env]
     extra = dict(zip([str(k) for k in g["meta_extra_keys"]], g["meta_extra_vals"].tolist()))
-    extra = {k: (int(v) if k in ("target_update_rate", "policy_freq") else v) for k, v in extra.items()}
+    extra = {("discount" if k == "discount_factor" else k): (int(v) if k in ("target_update_rate", "policy_freq") else v)
+             for k, v in extra.items()}  # (the reference's constructor names -> the oracle's)
     nets = spec.agent_params(alg, S, A, H, seed, **shape_of(g))
     orc = agents.make_oracle(alg, nets, A, bool(use_lap), acts=acts_of(g), **extra)
     scale = np.full(A, hi, np.float32)
@@ -78,7 +79,8 @@ def build_from_golden(g):
 
 TINY = ["td7_tiny", "td7_tiny_nolap", "td3_tiny", "td3_tiny_lap", "sac_tiny", "sac_tiny_fixed", "td3_tiny_deep",
         "sac_tiny_deep", "td7_tiny_b100", "td3_tiny_b100", "sac_tiny_b100",  # (b100: a batch of 100, padded to 112)
-        "td7_tiny_act", "td7_tiny_act_id", "td3_tiny_act", "sac_tiny_act"]  # (act: hidden activations beyond the defaults)
+        "td7_tiny_act", "td7_tiny_act_id", "td3_tiny_act", "sac_tiny_act",  # (act: hidden activations beyond the defaults)
+        "td7_tiny_hp", "td3_tiny_hp", "sac_tiny_hp"]  # (hp: constructor hyper-parameters beyond the defaults)
 FULL = ["td7_humanoid", "td7_ant", "td3_halfcheetah", "sac_humanoid", "td7_humanoid_64k", "td7_tiny_zs"]
 
 
