@@ -57,16 +57,16 @@ typedef struct rle_config {
   int hidden_sizes[8];      /* TD3/SAC: their widths, input side first (each a multiple of 4, <= 512) */
   /* Hidden-layer activations (RLE_ACT_*; 0 = the reference default of that net).  TD7: SALEActor / SALECritic /
      SALEEncoder `activ` (sale.py:25,67,97: ReLU / ELU / ELU); TD3/SAC: make_mlp's action_fn of the policy and of the
-     critics (mlp.py:13, default ReLU; act_encoder must be 0).  A non-default activation runs its programs without
-     the activation-specific fusions (RLE_FUSE_PRELAYER, PRE, QDOT, HEADDX, TWOSTAGE, SACPRE) on the extended kernel
-     instance. */
+     critics (mlp.py:13, default ReLU; act_encoder must be 0).  A non-default activation runs its programs on the
+     extended kernel instance without RLE_FUSE_PRELAYER, PRE, TWOSTAGE and SACPRE (and, for identity critics, without
+     QDOT and HEADDX). */
   int act_actor, act_critic, act_encoder;
 } rle_config;
 #define RLE_MAX_HIDDEN 6
 #define RLE_ACT_DEFAULT 0
 #define RLE_ACT_RELU 1
 #define RLE_ACT_ELU 2       /* alpha = 1 (F.elu / nn.ELU defaults) */
-#define RLE_ACT_IDENTITY 3  /* make_mlp(action_fn=None): no activation between the Linear layers */
+#define RLE_ACT_IDENTITY 3  /* action_fn "Identity" / nn.Identity(): no activation between the Linear layers */
 
 /* Step-program plan: the schedule and tile-plan choices that decide how the step's reductions are
  * split (so its fp32 summation order) and how its ops are fused.  Every engine starts from the
@@ -100,7 +100,8 @@ typedef struct rle_plan {
   int pl_tn;            /* tile width of pre-layer consumers (0: SAC 32, else 64)                        */
   int tn_min;           /* narrowest GEMM tile (0: 16)                                                   */
   int flat_div;         /* Polyak / copy workgroups count 1 / flat_div in the planner (0: 4)            */
-  int balance;          /* rebalance pass (-1: 1 = on; 0 off)                                            */
+  int balance;          /* rebalance pass: 0 off, 1 any item, 2 no Adam items, 3 no Adam items and only under a
+                           twice-longer op (-1: TD7 3, else 1)                                              */
   int tiny_w, uni_w, tiny_wg;  /* rebalance weights: step end, uniform sampler, tiny-op bound (-1: 30,
                                   SAC 30 / TD3 8 / TD7 60, 2) */
   int sched_cap;        /* 1: the scheduler defers ops past level_cap workgroups to a later level       */

@@ -1694,7 +1694,10 @@ struct Engine {
     plan.pl_tn = plan.pl_tn == 16 || plan.pl_tn == 32 ? plan.pl_tn : 64;
     plan.tn_min = plan.tn_min == 32 || plan.tn_min == 64 ? plan.tn_min : 16;
     if (plan.flat_div <= 0) plan.flat_div = 4;
-    if (plan.balance < 0) plan.balance = 1;
+    // (TD7: mode 3, no Adam items moved and only under a twice-longer op -- interleaved A/B, 4 pairs: TD7 Humanoid
+    // 8,295-8,306 -> 8,328-8,341 steps/s, Ant +0.1%, B = 1024 +-0; TD3 -5%, SAC -2% at 3, so they keep 1;
+    // profiles/r06_ab_balance.txt)
+    if (plan.balance < 0) plan.balance = algo == RLE_TD7 ? 3 : 1;
     if (plan.tiny_w < 0) plan.tiny_w = 30;
     // (uniform sampler weight, A/B 2 pairs, SAC Humanoid uni_w 60 / 45 / 30 / 15 -> 14.10k / 14.13k / 14.40k /
     // 14.39k; TD3 HalfCheetah 60 / 30 / 20 / 15 / 8 / 1 -> 25.40k / 25.42k / 25.30k / 25.81k / 25.84k / 25.76k: a
