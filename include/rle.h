@@ -119,7 +119,7 @@ typedef struct rle_plan {
                            measured)                                                     */
   int lpt;              /* 1: each level's ops in its launch ordered longest first (estimated workgroup time),
                            so a level with more workgroups than the device holds dispatches its long tiles in
-                           the first round; 0: program order; -1: default                               */
+                           the first round and its long workgroups start first; 0: program order; -1: default = 1) */
   /* Launch choices (they change no result: the same ops, tiles and summation order either way) */
   int dispatch;         /* how the step programs' level launches reach the device: 1 direct AQL kernel-dispatch
                            packets in the engine's own HSA queue; 0 hipGraph replays on the engine's HIP stream;

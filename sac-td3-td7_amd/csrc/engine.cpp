@@ -1709,7 +1709,9 @@ struct Engine {
     // MFMAs bound the B >= 512 levels, DESIGN round 5; with them the register-blocked weight-gradient tiles, the
     // batch split over the 4 waves, where a 16 x 64 weight-gradient tile's waves would each reduce all B rows)
     if (plan.wide < 0) plan.wide = 0;  // (opt-in: slower at B = 1024 than the 16-row tiles, DESIGN round 5)
-    if (plan.lpt < 0) plan.lpt = 0;
+    // (longest first: interleaved A/B on the round-6 tree, TD7 Humanoid +0.5% (4 pairs), Ant +1.1%, B = 1024 +0.2%,
+    // TD3 HalfCheetah +1.9%, SAC Humanoid +0.9%; profiles/r06_ab_lpt.txt.  Round 5 measured it at +-0)
+    if (plan.lpt < 0) plan.lpt = 1;
     plan.lpt = plan.lpt ? 1 : 0;
     plan.rb = plan.rb < 0 ? (plan.wide ? 1 : 0) : (plan.rb ? 1 : 0);
     // (A/B, 2 pairs: SAC Humanoid pl_w 0 / 8 / 16 / 24 -> 14.09k / 14.09k / 14.11k / 14.15k; TD3 HalfCheetah
