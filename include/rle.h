@@ -94,14 +94,15 @@ typedef struct rle_config {
                                         their producer) for the weight gradients' per-row tables      */
 #define RLE_FUSE_OPT_IN RLE_FUSE_PRIOSAMPLE  /* fusions off unless set in fuse_on                      */
 typedef struct rle_plan {
-  int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity; TD3 7/8, TD7 at B >= 1024 3/2) */
+  int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity; TD7 at B >= 1024 3/2;
+                           TD3 7/8 when lpt is 0) */
   int steps_per_graph;  /* steps per multi-step graph (-1: TD7 6, SAC 8, TD3 16; 0: single-step only)  */
   int pre_tn;           /* tile width of pre-GEMM consumers (0: TD3 64, else 32)                         */
   int pl_tn;            /* tile width of pre-layer consumers (0: SAC 32, else 64)                        */
   int tn_min;           /* narrowest GEMM tile (0: 16)                                                   */
   int flat_div;         /* Polyak / copy workgroups count 1 / flat_div in the planner (0: 4)            */
   int balance;          /* rebalance pass: 0 off, 1 any item, 2 no Adam items, 3 no Adam items and only under a
-                           twice-longer op (-1: TD7 3, else 1)                                              */
+                           twice-longer op (-1: TD7 3, SAC 2, TD3 1)                                        */
   int tiny_w, uni_w, tiny_wg;  /* rebalance weights: step end, uniform sampler, tiny-op bound (-1: 30,
                                   SAC 30 / TD3 8 / TD7 60, 2) */
   int sched_cap;        /* 1: the scheduler defers ops past level_cap workgroups to a later level       */

@@ -1697,7 +1697,8 @@ struct Engine {
     // (TD7: mode 3, no Adam items moved and only under a twice-longer op -- interleaved A/B, 4 pairs: TD7 Humanoid
     // 8,295-8,306 -> 8,328-8,341 steps/s, Ant +0.1%, B = 1024 +-0; TD3 -5%, SAC -2% at 3, so they keep 1;
     // profiles/r06_ab_balance.txt)
-    if (plan.balance < 0) plan.balance = algo == RLE_TD7 ? 3 : 1;
+    // (SAC: mode 2, 4 pairs 14.75k -> 14.78k, profiles/r06_ab_plan_mlp.txt; TD3 keeps 1)
+    if (plan.balance < 0) plan.balance = algo == RLE_TD7 ? 3 : algo == RLE_SAC ? 2 : 1;
     if (plan.tiny_w < 0) plan.tiny_w = 30;
     // (uniform sampler weight, A/B 2 pairs, SAC Humanoid uni_w 60 / 45 / 30 / 15 -> 14.10k / 14.13k / 14.40k /
     // 14.39k; TD3 HalfCheetah 60 / 30 / 20 / 15 / 8 / 1 -> 25.40k / 25.42k / 25.30k / 25.81k / 25.84k / 25.76k: a
@@ -4233,8 +4234,9 @@ struct Engine {
     // (round 4, 2 pairs) 1024 / 896 / 768 / 640 -> 25.22k / 25.33k / 25.23k / 24.94k.  TD7 at
     // B >= 1024 plans for 3/2 of them (its levels are over capacity anyway; 2 pairs at B = 1024:
     // 1024 / 1536 / 2048 -> 3564 / 3598 / 3529).  (TD7 B = 256: 1024 best, 896 -1.2%; SAC: 1024 best,
-    // 768 -0.8%.)
-    if (algo == RLE_TD3) cap = cap * 7 / 8;
+    // 768 -0.8%.)  Round 6, with each level's ops longest first (plan lpt): TD3 at the full capacity again, 4 pairs
+    // 896 (7/8) / 960 / 1024 -> 26.53k / 26.55k / 26.62k (profiles/r06_ab_plan_mlp.txt).
+    if (algo == RLE_TD3 && !plan.lpt) cap = cap * 7 / 8;
     if (algo == RLE_TD7 && B >= 1024) cap = cap * 3 / 2;
     // (plan.level_cap: tuning experiments, and seeds per GPU on streams -- bench.py)
     if (plan.level_cap > 0) cap = plan.level_cap;
