@@ -732,9 +732,11 @@ def main():
     if K > 1:
         # K seeds on streams: the tile planner sizes each seed's levels for 512 resident workgroups
         # (half the device) so two seeds' levels co-reside (A/B, 3 seeds: 13.1k default, 14.1k at 512,
-        # 13.9k at 384; profiles/r03_ab.txt "multiseed_cap").  --plan overrides.
+        # 13.9k at 384; profiles/r03_ab.txt "multiseed_cap"), 384 from 4 seeds on (round 6, 2 pairs each:
+        # 4 seeds 15.46k at 512 / 15.59k at 384, 2 and 3 seeds 6% / 3% slower at 384;
+        # profiles/r06_ab_multiseed_cap.txt).  --plan overrides.
         if "level_cap" not in args.plan:
-            args.plan = ",".join(filter(None, [args.plan, "level_cap=512"]))
+            args.plan = ",".join(filter(None, [args.plan, f"level_cap={512 if K < 4 else 384}"]))
         return multi_seed(args, K, world, rank, local, dist, algo_id, lap, E, init_agent, cuda_sync)
     cfg = E.make_config(algo_id, s_dim, a_dim, H, args.batch, use_lap=lap, seed=111 * (rank + 1), device=local)
     eng = E.Engine(cfg, E.parse_plan(args.plan))
