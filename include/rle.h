@@ -94,8 +94,8 @@ typedef struct rle_config {
                                         their producer) for the weight gradients' per-row tables      */
 #define RLE_FUSE_OPT_IN RLE_FUSE_PRIOSAMPLE  /* fusions off unless set in fuse_on                      */
 typedef struct rle_plan {
-  int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity; TD7 at B >= 1024 3/2;
-                           TD3 7/8 when lpt is 0) */
+  int level_cap;        /* workgroups per level the tile planner targets (0: resident capacity; TD7 at B >= 1024 5/4
+                           (3/2 when lpt is 0); TD3 7/8 when lpt is 0) */
   int steps_per_graph;  /* steps per multi-step graph (-1: TD7 6, SAC 8, TD3 16; 0: single-step only)  */
   int pre_tn;           /* tile width of pre-GEMM consumers (0: TD3 64, else 32)                         */
   int pl_tn;            /* tile width of pre-layer consumers (0: SAC 32, else 64)                        */

@@ -4237,7 +4237,9 @@ struct Engine {
     // 768 -0.8%.)  Round 6, with each level's ops longest first (plan lpt): TD3 at the full capacity again, 4 pairs
     // 896 (7/8) / 960 / 1024 -> 26.53k / 26.55k / 26.62k (profiles/r06_ab_plan_mlp.txt).
     if (algo == RLE_TD3 && !plan.lpt) cap = cap * 7 / 8;
-    if (algo == RLE_TD7 && B >= 1024) cap = cap * 3 / 2;
+    // (round 6, longest first: TD7 B = 1024 at 5/4, 4 pairs 1,536 / 1,152 / 1,280 / 1,408 -> 3.79k / 3.81k / 3.83k / 3.79k,
+    // profiles/r06_ab_b1024_cap.txt)
+    if (algo == RLE_TD7 && B >= 1024) cap = plan.lpt ? cap * 5 / 4 : cap * 3 / 2;
     // (plan.level_cap: tuning experiments, and seeds per GPU on streams -- bench.py)
     if (plan.level_cap > 0) cap = plan.level_cap;
     // elementwise ops (Polyak, copies) are short: they free their slots long before the level's
